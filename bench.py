@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Headline benchmark: stencil Gpoints/s (whole node) on the reference's own
+benchmark configuration — fortran/hip/input.dat = `32768 0.25 0.05 1.0 25000 0`:
+a 32768 x 32768 fp64 grid (ghost-frame convention, T=2 inside, Dirichlet T=1
+frame, fortran/hip/heat.F90:274-282), slab-decomposed over N GPUs (strong
+scaling: the grid is fixed), RCCL halo exchange over xGMI.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+W untimed warm-up steps, then exactly K FTCS time steps, bracketed by a
+barrier + device synchronisation on both sides; the time is the MAX over
+ranks. One "step" = one full time step of every grid point (temporal blocking
+fuses up to --tb steps per HBM pass; every point is still updated every step).
+Rank 0 prints one JSON line.
+
+vs_baseline: the reference publishes no numbers. We divide by the
+derived reference ceiling of BASELINE.md — 50 Gpts/s per MI250X GCD for its
+kernel + per-step D2D copy (>= 32 B/pt/step at 1.6 TB/s) — times N ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+_ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, _ROOT)
+
+REF_GPTS_PER_RANK = 50.0  # BASELINE.md derived ceiling, 1 MI250X GCD, fp64
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=48)
+    ap.add_argument("--n", type=int, default=32768)
+    ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+    ap.add_argument("--tb", type=int, default=8, help="time steps fused per HBM pass")
+    ap.add_argument("--tile-rows", type=int, default=0)
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--check", action="store_true", help="print field statistics after the run")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import heat2d
+    from heat2d.models.heat2d import HeatSolver
+    from heat2d.parallel.transport import RcclTransport, SelfTransport
+
+    inp = heat2d.InputDat(n=args.n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
+    prob = heat2d.make_problem(inp, "ghost", "uniform")
+    tr = RcclTransport(rank, world, local) if world > 1 else SelfTransport()
+    s = HeatSolver(prob, dtype=args.dtype, backend="hip", tb=args.tb, overlap=not args.no_overlap,
+                   tile_rows=args.tile_rows, transport=tr, device=local)
+
+    def barrier():
+        if world > 1:
+            tr_vals = torch.zeros(1, device="cuda")
+            dist.all_reduce(tr_vals)
+        torch.cuda.synchronize()
+
+    s.step(args.warmup)
+    s.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    s.step(args.steps)
+    s.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    pts = float(prob.n_owned) ** 2
+    gpts = pts * args.steps / elapsed / 1e9
+    es = 8 if args.dtype == "fp64" else 4
+    info = s.info()
+    tb = info["tb"]
+    # model HBM traffic: one read + one write of the field per HBM pass (tb steps)
+    model_gbps = gpts * (2.0 * es / tb)
+    stats = s.stats() if args.check else None
+    if rank == 0:
+        out = {
+            "metric": "stencil Gpoints/sec (whole node)",
+            "value": round(gpts, 3),
+            "unit": "Gpts/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 6),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(gpts / (REF_GPTS_PER_RANK * world), 3),
+            "dtype": args.dtype,
+            "data": "synthetic (reference benchmark IC: T=2 interior, Dirichlet T=1 frame)",
+            "config": {
+                "model": "heat2d FTCS 5-point, fortran/hip/input.dat (32768 0.25 0.05 1.0 25000 0)",
+                "grid": [prob.n_owned, prob.n_owned],
+                "global_batch": 1,
+                "seq_len": prob.n_owned,
+                "parallelism": f"slab{world}",
+                "temporal_block": tb,
+                "overlap": not args.no_overlap,
+            },
+            "hbm_gb_per_s_model": round(model_gbps, 1),
+            "baseline_basis": "BASELINE.md derived ceiling 50 Gpts/s per MI250X GCD x n_gpus",
+        }
+        if stats:
+            out["field_stats"] = stats
+        print(json.dumps(out), flush=True)
+    s.close()
+    tr.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

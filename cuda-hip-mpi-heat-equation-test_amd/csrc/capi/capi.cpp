@@ -1,0 +1,250 @@
+// C ABI over the native runtime (see heat2d/capi.h).
+#include "heat2d/capi.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "heat2d/runtime.hpp"
+
+extern "C" int heat2d_io_write_xyz_impl(const char*, int, const void*, int64_t, int64_t, int64_t,
+                                        const double*, const double*, int);
+extern "C" int heat2d_io_write_npy_impl(const char*, int, const void*, int64_t, int64_t, int64_t);
+
+using namespace heat2d;
+
+namespace {
+thread_local std::string g_err;
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+  } catch (...) {
+    g_err = "unknown error";
+  }
+  return 1;
+}
+
+SlabLayout to_layout(const heat2d_layout* l) {
+  SlabLayout L{};
+  static_assert(sizeof(heat2d_layout) == sizeof(SlabLayout), "layout ABI");
+  std::memcpy(&L, l, sizeof(L));
+  return L;
+}
+kern::IcParams to_ic(const heat2d_ic* ic) {
+  static_assert(sizeof(heat2d_ic) == sizeof(kern::IcParams), "ic ABI");
+  kern::IcParams p{};
+  std::memcpy(&p, ic, sizeof(p));
+  return p;
+}
+SolverConfig to_cfg(const heat2d_config* c) {
+  static_assert(sizeof(heat2d_config) == sizeof(SolverConfig), "config ABI");
+  SolverConfig s{};
+  std::memcpy(&s, c, sizeof(s));
+  return s;
+}
+hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+struct TransportHandle {
+  std::shared_ptr<Transport> t;
+};
+}  // namespace
+
+extern "C" {
+
+const char* heat2d_last_error(void) { return g_err.c_str(); }
+int heat2d_version(void) { return 100; }
+int heat2d_max_tb(void) { return kMaxTB; }
+
+int heat2d_device_count(int* n) {
+  return guarded([&] {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+  });
+}
+
+int heat2d_make_layout(int64_t nrows, int64_t ncols, int64_t halo, int64_t row0, int64_t nrows_global,
+                       heat2d_layout* out) {
+  return guarded([&] {
+    SlabLayout L = make_layout(nrows, ncols, halo, row0, nrows_global);
+    std::memcpy(out, &L, sizeof(L));
+  });
+}
+
+int heat2d_decompose(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nrows) {
+  return guarded([&] {
+    SlabRange r = decompose(n, nranks, rank);
+    *row0 = r.row0;
+    *nrows = r.nrows;
+  });
+}
+
+int heat2d_plan_tb(int dtype, const heat2d_layout* L, int64_t rb, int64_t re, int k, int64_t tile_rows,
+                   heat2d_tb_plan* out) {
+  return guarded([&] {
+    kern::TbPlan p = kern::plan_tb((DType)dtype, to_layout(L), rb, re, k, tile_rows);
+    static_assert(sizeof(heat2d_tb_plan) == sizeof(kern::TbPlan), "plan ABI");
+    std::memcpy(out, &p, sizeof(p));
+  });
+}
+
+int heat2d_tb(int dtype, const void* src, void* dst, const heat2d_layout* L, int64_t rb, int64_t re, int k,
+              double r, void* stream, int64_t tile_rows) {
+  return guarded([&] { kern::launch_tb((DType)dtype, src, dst, to_layout(L), rb, re, k, r, as_stream(stream), tile_rows); });
+}
+
+int heat2d_init_field(int dtype, void* field, const heat2d_layout* L, const heat2d_ic* ic,
+                      const double* xc, const double* yc, void* stream) {
+  return guarded([&] { kern::launch_init((DType)dtype, field, to_layout(L), to_ic(ic), xc, yc, as_stream(stream)); });
+}
+
+int heat2d_stats(int dtype, const void* field, const void* other, const heat2d_layout* L, double* work,
+                 double* out, void* stream) {
+  return guarded([&] { kern::launch_stats((DType)dtype, field, other, to_layout(L), work, out, as_stream(stream)); });
+}
+
+int64_t heat2d_stats_work_elems(void) { return kern::stats_work_elems(); }
+
+int heat2d_pack_rows(int dtype, const void* field, const heat2d_layout* L, int64_t row, int64_t nrows,
+                     void* buf, void* stream) {
+  return guarded([&] { kern::launch_pack_rows((DType)dtype, field, to_layout(L), row, nrows, buf, as_stream(stream)); });
+}
+
+int heat2d_unpack_rows(int dtype, void* field, const heat2d_layout* L, int64_t row, int64_t nrows,
+                       const void* buf, void* stream) {
+  return guarded([&] { kern::launch_unpack_rows((DType)dtype, field, to_layout(L), row, nrows, buf, as_stream(stream)); });
+}
+
+int heat2d_cpu_tb(int dtype, const void* src, void* dst, const heat2d_layout* L, int64_t rb, int64_t re, int k,
+                  double r) {
+  return guarded([&] { cpu::tb((DType)dtype, src, dst, to_layout(L), rb, re, k, r); });
+}
+
+int heat2d_cpu_init_field(int dtype, void* field, const heat2d_layout* L, const heat2d_ic* ic, const double* xc,
+                          const double* yc) {
+  return guarded([&] { cpu::init((DType)dtype, field, to_layout(L), to_ic(ic), xc, yc); });
+}
+
+int heat2d_cpu_stats(int dtype, const void* field, const void* other, const heat2d_layout* L, double* out6) {
+  return guarded([&] { cpu::stats((DType)dtype, field, other, to_layout(L), out6); });
+}
+
+int heat2d_rccl_unique_id(void* out128) {
+  return guarded([&] { rccl_unique_id(out128); });
+}
+
+int heat2d_transport_self(void** out) {
+  return guarded([&] { *out = new TransportHandle{make_self_transport()}; });
+}
+
+int heat2d_transport_rccl(const void* uid128, int rank, int size, int device, void** out) {
+  return guarded([&] { *out = new TransportHandle{make_rccl_transport(uid128, rank, size, device)}; });
+}
+
+int heat2d_transport_callback(heat2d_exchange_fn ex, heat2d_allreduce_fn ar, heat2d_barrier_fn br, void* ctx,
+                              int rank, int size, void** out) {
+  return guarded([&] {
+    CallbackOps ops{ctx, ex, ar, br};
+    *out = new TransportHandle{make_callback_transport(ops, rank, size)};
+  });
+}
+
+int heat2d_transport_free(void* t) {
+  return guarded([&] { delete static_cast<TransportHandle*>(t); });
+}
+
+int heat2d_solver_create(const heat2d_config* cfg, void* transport, void** out) {
+  return guarded([&] {
+    std::shared_ptr<Transport> t =
+        transport ? static_cast<TransportHandle*>(transport)->t : make_self_transport();
+    *out = new Solver(to_cfg(cfg), t);
+  });
+}
+
+int heat2d_solver_free(void* s) {
+  return guarded([&] { delete static_cast<Solver*>(s); });
+}
+
+int heat2d_solver_init(void* s, const heat2d_ic* ic, const double* xg, const double* yg) {
+  return guarded([&] { static_cast<Solver*>(s)->init(to_ic(ic), xg, yg); });
+}
+
+int heat2d_solver_step(void* s, int64_t n) {
+  return guarded([&] { static_cast<Solver*>(s)->step(n); });
+}
+
+int heat2d_solver_sync(void* s) {
+  return guarded([&] { static_cast<Solver*>(s)->synchronize(); });
+}
+
+int heat2d_solver_stats(void* s, double* out6, int residual) {
+  return guarded([&] { static_cast<Solver*>(s)->stats(out6, residual != 0); });
+}
+
+int heat2d_solver_download(void* s, void* host, int64_t ld) {
+  return guarded([&] { static_cast<Solver*>(s)->download(host, ld); });
+}
+
+int heat2d_solver_upload(void* s, const void* host, int64_t ld) {
+  return guarded([&] { static_cast<Solver*>(s)->upload(host, ld); });
+}
+
+int heat2d_solver_layout(void* s, heat2d_layout* out) {
+  return guarded([&] {
+    const SlabLayout& L = static_cast<Solver*>(s)->layout();
+    std::memcpy(out, &L, sizeof(L));
+  });
+}
+
+int heat2d_solver_info(void* s, int32_t* tb, int64_t* band, int64_t* steps, void** field, void** stream) {
+  return guarded([&] {
+    Solver* so = static_cast<Solver*>(s);
+    if (tb) *tb = so->config().tb;
+    if (band) *band = so->band();
+    if (steps) *steps = so->steps_done();
+    if (field) *field = so->field();
+    if (stream) *stream = reinterpret_cast<void*>(so->stream());
+  });
+}
+
+int heat2d_group_create(const heat2d_config* cfg, int nranks, void** out) {
+  return guarded([&] { *out = new LoopbackGroup(to_cfg(cfg), nranks); });
+}
+
+int heat2d_group_free(void* g) {
+  return guarded([&] { delete static_cast<LoopbackGroup*>(g); });
+}
+
+int heat2d_group_init(void* g, const heat2d_ic* ic, const double* xg, const double* yg) {
+  return guarded([&] { static_cast<LoopbackGroup*>(g)->init(to_ic(ic), xg, yg); });
+}
+
+int heat2d_group_step(void* g, int64_t n) {
+  return guarded([&] { static_cast<LoopbackGroup*>(g)->step(n); });
+}
+
+int heat2d_group_download(void* g, void* host, int64_t ld) {
+  return guarded([&] {
+    auto* gr = static_cast<LoopbackGroup*>(g);
+    gr->synchronize();
+    gr->download(host, ld);
+  });
+}
+
+int heat2d_write_xyz(const char* path, int dtype, const void* host, int64_t nrows, int64_t ncols, int64_t ld,
+                     const double* x, const double* y, int append) {
+  return guarded([&] { heat2d_io_write_xyz_impl(path, dtype, host, nrows, ncols, ld, x, y, append); });
+}
+
+int heat2d_write_npy(const char* path, int dtype, const void* host, int64_t nrows, int64_t ncols, int64_t ld) {
+  return guarded([&] { heat2d_io_write_npy_impl(path, dtype, host, nrows, ncols, ld); });
+}
+
+}  // extern "C"

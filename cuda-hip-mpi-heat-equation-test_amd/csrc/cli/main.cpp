@@ -1,0 +1,303 @@
+// heat2d — native command-line driver.
+//
+// `heat2d [input.dat] [flags]` reproduces the run behaviour of every
+// reference program (reads ./input.dat by default, prints the same progress /
+// completion / timing lines, writes int.dat / soln.dat / soln%05d.dat):
+//   --variant mpi     fortran/hip + fortran/mpi+cuda (6-field input; ghost frame,
+//                     uniform IC, per-rank soln%05d.dat, "Average time:")
+//   --variant serial  fortran/serial (5-field input; boundary-inclusive grid,
+//                     hat IC, int.dat + soln.dat, "total time:")
+//   --variant cuda    fortran/cuda_cuf + fortran/cuda_kernel (hat on y in [0.5,1.0])
+//   --managed         fortran/cuda_kernel/heat_managed.F90 (hipMallocManaged fields)
+//   --cpu             native CPU path (replaces the gfortran serial build)
+// Multi-GPU is one host thread per GPU (hipSetDevice(rank), the reference's
+// node-local rank -> device binding, fortran/hip/heat.F90:119-125) with RCCL
+// communicators; the halo exchange is RCCL send/recv over xGMI.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "heat2d/capi.h"
+#include "heat2d/config.hpp"
+#include "heat2d/runtime.hpp"
+
+using namespace heat2d;
+
+namespace {
+
+struct Args {
+  std::string input = "input.dat";
+  std::string variant;  // mpi | serial | cuda (default: by number of input fields)
+  std::string ic;       // override IC
+  std::string dtype = "fp64";
+  std::string output = "ascii";  // ascii | npy | none
+  std::string json;
+  int gpus = -1;  // -1: 1 if a GPU exists
+  bool cpu = false;
+  int tb = 8;
+  bool overlap = true;
+  bool copy_swap = false;
+  bool managed = false;
+  bool graph = false;
+  int64_t print_every = 0;
+  int64_t check_every = 0;
+  int64_t ntime = -1;  // override
+  int64_t n = -1;      // override
+  bool quiet = false;
+};
+
+void usage() {
+  std::printf(
+      "usage: heat2d [input.dat] [--variant mpi|serial|cuda] [--gpus N | --cpu] [--dtype fp64|fp32]\n"
+      "              [--tb K] [--no-overlap] [--copy-swap] [--managed] [--graph] [--ic NAME]\n"
+      "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
+      "              [--n N] [--ntime N] [--quiet]\n");
+}
+
+Args parse_args(int argc, char** argv) {
+  Args a;
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    auto need = [&](const char* what) -> std::string {
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "missing value for %s\n", what);
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (s == "-h" || s == "--help") { usage(); std::exit(0); }
+    else if (s == "--variant") a.variant = need("--variant");
+    else if (s == "--ic") a.ic = need("--ic");
+    else if (s == "--dtype") a.dtype = need("--dtype");
+    else if (s == "--output") a.output = need("--output");
+    else if (s == "--json") a.json = need("--json");
+    else if (s == "--gpus" || s == "-np") a.gpus = std::atoi(need("--gpus").c_str());
+    else if (s == "--cpu") a.cpu = true;
+    else if (s == "--tb") a.tb = std::atoi(need("--tb").c_str());
+    else if (s == "--no-overlap") a.overlap = false;
+    else if (s == "--copy-swap") a.copy_swap = true;
+    else if (s == "--managed") a.managed = true;
+    else if (s == "--graph") a.graph = true;
+    else if (s == "--print-every") a.print_every = std::atoll(need("--print-every").c_str());
+    else if (s == "--check-every") a.check_every = std::atoll(need("--check-every").c_str());
+    else if (s == "--ntime") a.ntime = std::atoll(need("--ntime").c_str());
+    else if (s == "--n") a.n = std::atoll(need("--n").c_str());
+    else if (s == "--quiet") a.quiet = true;
+    else if (!s.empty() && s[0] != '-') a.input = s;
+    else { std::fprintf(stderr, "unknown flag %s\n", s.c_str()); usage(); std::exit(2); }
+  }
+  return a;
+}
+
+struct Shared {
+  Args args;
+  InputDat in;
+  Problem prob;
+  int nranks = 1;
+  unsigned char uid[128];
+  std::vector<double> t_elapsed;
+  std::atomic<int> failed{0};
+  std::string err;
+  double final_stats[6] = {0};
+};
+
+std::string rank_file(int rank) {
+  char b[32];
+  std::snprintf(b, sizeof(b), "soln%05d.dat", rank);
+  return b;
+}
+
+void write_inclusive(Solver& s, const Problem& p, const char* path, bool first_rank, bool last_rank, bool append) {
+  // full frame-inclusive rows of this slab: x outer, y inner (fortran/serial/heat.f90:77-83)
+  const SlabLayout& L = s.layout();
+  const int64_t r0 = first_rank ? -1 : 0, r1 = last_rank ? L.nrows + 1 : L.nrows;
+  const int64_t w = L.ncols + 2;
+  std::vector<char> host((size_t)((r1 - r0) * w) * dtype_size(s.dtype()));
+  s.download_region(r0, r1, -1, L.ncols + 1, host.data(), w);
+  std::vector<double> xs((size_t)(r1 - r0));
+  for (int64_t i = r0; i < r1; ++i) xs[(size_t)(i - r0)] = p.x[(size_t)(L.row0 + i + 1)];
+  if (heat2d_write_xyz(path, (int)s.dtype(), host.data(), r1 - r0, w, w, xs.data(), p.x.data(), append ? 1 : 0))
+    fail(__FILE__, __LINE__, heat2d_last_error());
+}
+
+void run_rank(Shared& sh, int rank) {
+  const Args& a = sh.args;
+  const int P = sh.nranks;
+  const bool root = rank == 0;
+  try {
+    std::shared_ptr<Transport> tr;
+    if (!a.cpu) {
+      if (hipSetDevice(rank) != hipSuccess) fail(__FILE__, __LINE__, "hipSetDevice failed");
+      if (!a.quiet && (root || P > 1)) std::printf(" MPI rank %12d using GPU %12d\n", rank, rank);
+    }
+    tr = P > 1 ? make_rccl_transport(sh.uid, rank, P, a.cpu ? -1 : rank) : make_self_transport();
+
+    SolverConfig cfg{};
+    cfg.n_rows = sh.prob.n_owned;
+    cfg.n_cols = sh.prob.n_owned;
+    cfg.dtype = a.dtype == "fp32" ? 0 : 1;
+    cfg.backend = a.cpu ? 1 : 0;
+    cfg.r = sh.prob.r;
+    cfg.tb = a.tb;
+    cfg.overlap = a.overlap ? 1 : 0;
+    cfg.copy_swap = a.copy_swap ? 1 : 0;
+    cfg.managed = a.managed ? 1 : 0;
+    cfg.device = a.cpu ? -1 : rank;
+    cfg.use_graph = a.graph ? 1 : 0;
+    Solver s(cfg, tr);
+    s.init(sh.prob.ic, sh.prob.x.data(), sh.prob.x.data());
+    const bool inclusive = sh.prob.conv == Convention::Inclusive;
+    if (root && !a.quiet) {
+      if (P > 1 || sh.args.variant == "mpi") std::printf(" Automatic MPI decomposition: %12d  x 1\n", P);
+      std::printf(" nx: %12lld\n", (long long)s.layout().nrows);
+      std::printf(" ny: %12lld\n", (long long)s.layout().ncols);
+      std::fflush(stdout);
+    }
+    if (inclusive && a.output == "ascii") {  // int.dat: the IC (fortran/serial/heat.f90:50-55)
+      for (int turn = 0; turn < P; ++turn) {
+        if (turn == rank) write_inclusive(s, sh.prob, "int.dat", rank == 0, rank == P - 1, rank > 0);
+        tr->barrier();
+      }
+    }
+
+    const int64_t ntime = sh.in.ntime;
+    tr->barrier();
+    s.synchronize();
+    const auto t0 = std::chrono::steady_clock::now();
+    int64_t done = 0;
+    const int64_t chunk_every = std::max<int64_t>(a.print_every, a.check_every);
+    while (done < ntime) {
+      int64_t chunk = ntime - done;
+      if (a.print_every > 0) chunk = std::min(chunk, a.print_every - (done % a.print_every));
+      if (a.check_every > 0) chunk = std::min(chunk, a.check_every - (done % a.check_every));
+      (void)chunk_every;
+      s.step(chunk);
+      done += chunk;
+      if (root && a.print_every > 0 && done % a.print_every == 0) std::printf(" time_it: %12lld\n", (long long)done);
+      if (a.check_every > 0 && done % a.check_every == 0) {
+        double st[6];
+        s.stats(st, true);
+        if (root)
+          std::printf(" step %lld: sum=%.17g min=%.6g max=%.6g residual_l2=%.6e\n", (long long)done, st[0], st[2],
+                      st[3], std::sqrt(st[4]));
+        if (!std::isfinite(st[0])) fail(__FILE__, __LINE__, "non-finite temperature at step " + std::to_string(done));
+      }
+    }
+    s.synchronize();
+    tr->barrier();
+    const auto t1 = std::chrono::steady_clock::now();
+    sh.t_elapsed[(size_t)rank] = std::chrono::duration<double>(t1 - t0).count();
+
+    // outputs
+    if (a.output != "none") {
+      if (inclusive) {
+        if (a.output == "ascii") {
+          for (int turn = 0; turn < P; ++turn) {
+            if (turn == rank) write_inclusive(s, sh.prob, "soln.dat", rank == 0, rank == P - 1, rank > 0);
+            tr->barrier();
+          }
+        }
+      } else if (sh.in.soln == 1 || a.output == "npy") {
+        const SlabLayout& L = s.layout();
+        std::vector<char> host((size_t)(L.nrows * L.ncols) * dtype_size(s.dtype()));
+        s.download(host.data(), L.ncols);
+        if (a.output == "npy") {
+          char b[32];
+          std::snprintf(b, sizeof(b), "soln%05d.npy", rank);
+          if (heat2d_write_npy(b, (int)s.dtype(), host.data(), L.nrows, L.ncols, L.ncols)) fail(__FILE__, __LINE__, heat2d_last_error());
+        } else {
+          // soln%05d.dat: x(i), y(j), T(i,j) for owned points (fortran/hip/heat.F90:308-319)
+          const double* xs = sh.prob.x.data() + 1 + L.row0;
+          if (heat2d_write_xyz(rank_file(rank).c_str(), (int)s.dtype(), host.data(), L.nrows, L.ncols, L.ncols, xs,
+                               sh.prob.x.data() + 1, 0))
+            fail(__FILE__, __LINE__, heat2d_last_error());
+        }
+      }
+    }
+    double st[6];
+    s.stats(st, false);
+    if (root) std::memcpy(sh.final_stats, st, sizeof(st));
+  } catch (const std::exception& e) {
+    sh.failed = 1;
+    if (sh.err.empty()) sh.err = e.what();
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Shared sh;
+  sh.args = parse_args(argc, argv);
+  Args& a = sh.args;
+  try {
+    sh.in = read_input_file(a.input);
+    if (a.n > 0) sh.in.n = a.n;
+    if (a.ntime >= 0) sh.in.ntime = a.ntime;
+    if (a.variant.empty()) a.variant = sh.in.nfields >= 6 ? "mpi" : "serial";
+    Convention conv = a.variant == "mpi" ? Convention::Ghost : Convention::Inclusive;
+    std::string ic = a.ic.empty() ? (a.variant == "mpi" ? "uniform" : a.variant == "cuda" ? "hat-cuda" : "hat") : a.ic;
+    sh.prob = make_problem(sh.in, conv, ic);
+    if (sh.prob.r > 0.25 + 1e-12 && !a.quiet)
+      std::fprintf(stderr, "warning: r = %.6g > 0.25: FTCS is unstable in 2-D\n", sh.prob.r);
+    int ndev = 0;
+    if (!a.cpu && hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    if (!a.cpu && ndev == 0) {
+      if (!a.quiet) std::fprintf(stderr, "no GPU found: running the CPU path\n");
+      a.cpu = true;
+    }
+    sh.nranks = a.cpu ? std::max(1, a.gpus) : (a.gpus > 0 ? a.gpus : 1);
+    if (!a.cpu && sh.nranks > ndev) fail(__FILE__, __LINE__, "more GPUs requested than present");
+    if (a.cpu && sh.nranks > 1) fail(__FILE__, __LINE__, "--cpu runs one rank (use the Python launcher for CPU multi-rank)");
+    if (sh.nranks > 1) rccl_unique_id(sh.uid);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "heat2d: %s\n", e.what());
+    return 1;
+  }
+  sh.t_elapsed.assign((size_t)sh.nranks, 0.0);
+  std::vector<std::thread> th;
+  for (int r = 1; r < sh.nranks; ++r) th.emplace_back(run_rank, std::ref(sh), r);
+  run_rank(sh, 0);
+  for (auto& t : th) t.join();
+  if (sh.failed) {
+    std::fprintf(stderr, "heat2d: %s\n", sh.err.c_str());
+    return 1;
+  }
+  double tmax = 0;
+  for (double t : sh.t_elapsed) tmax = std::max(tmax, t);
+  const int64_t ntime = sh.in.ntime;
+  const double pts = (double)sh.prob.n_owned * (double)sh.prob.n_owned;
+  const double gpts = ntime > 0 && tmax > 0 ? pts * (double)ntime / tmax / 1e9 : 0.0;
+  const int es = a.dtype == "fp32" ? 4 : 8;
+  const int K = a.copy_swap ? 1 : std::max(1, std::min(a.tb, kMaxTB));
+  // model bytes/pt/step: one read + one write per HBM pass (K steps); copy mode adds the copy
+  const double bpp = a.copy_swap ? 4.0 * es : 2.0 * es / K;
+  std::printf(" simulation completed!!!!\n");
+  if (a.variant == "mpi")
+    std::printf(" Average time: %24.16g\n", ntime > 0 ? tmax / (double)ntime : 0.0);
+  else
+    std::printf(" total time: %24.16g\n", tmax);
+  if (!a.quiet)
+    std::printf(" heat2d: n=%lld P=%d %s K=%d steps=%lld wall=%.6f s  %.3f Gpts/s  %.1f GB/s(model)  sum(T)=%.17g\n",
+                (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, (long long)ntime, tmax, gpts,
+                gpts * bpp, sh.final_stats[0]);
+  if (!a.json.empty()) {
+    FILE* f = std::fopen(a.json.c_str(), "w");
+    if (f) {
+      std::fprintf(f,
+                   "{\"n\": %lld, \"nranks\": %d, \"dtype\": \"%s\", \"tb\": %d, \"steps\": %lld, \"wall_s\": %.9g, "
+                   "\"gpts_per_s\": %.9g, \"model_gb_per_s\": %.9g, \"sum\": %.17g, \"min\": %.17g, \"max\": %.17g, "
+                   "\"backend\": \"%s\", \"variant\": \"%s\"}\n",
+                   (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, (long long)ntime, tmax, gpts, gpts * bpp,
+                   sh.final_stats[0], sh.final_stats[2], sh.final_stats[3], a.cpu ? "cpu" : "hip", a.variant.c_str());
+      std::fclose(f);
+    }
+  }
+  return 0;
+}

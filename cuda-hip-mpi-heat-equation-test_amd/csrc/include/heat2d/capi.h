@@ -1,0 +1,116 @@
+/* heat2d C ABI — consumed by the Python package through ctypes and by any
+ * other host language. Replaces the reference's Fortran<->C++ `bind(c)`
+ * launcher interface (fortran/hip/heat.F90:48-102 -> heat_kernel.cpp:48-150)
+ * with a complete engine API. Every function returns 0 on success, non-zero on
+ * error; heat2d_last_error() gives the message (thread-local). */
+#ifndef HEAT2D_CAPI_H
+#define HEAT2D_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct heat2d_layout {
+  int64_t nrows, ncols, halo, cpad, pitch, row0, nrows_global;
+} heat2d_layout;
+
+typedef struct heat2d_ic {
+  int32_t kind;
+  double a, b;
+  double x0, x1, y0, y1;
+  int64_t i0, i1, j0, j1;
+  double kx, ky;
+  double pad;
+} heat2d_ic;
+
+typedef struct heat2d_config {
+  int64_t n_rows, n_cols;
+  int32_t dtype, backend;
+  double r;
+  int32_t tb, overlap, copy_swap, managed, device, use_graph;
+  int64_t tile_rows, halo;
+} heat2d_config;
+
+typedef struct heat2d_tb_plan {
+  int32_t k, vec, strip_w, useful_w;
+  int64_t tile_rows, nstrips, ntiles, nwaves, nblocks;
+} heat2d_tb_plan;
+
+typedef int (*heat2d_exchange_fn)(void* ctx, void* send_lo, void* send_hi, void* recv_lo,
+                                  void* recv_hi, int64_t count, int32_t dtype);
+typedef int (*heat2d_allreduce_fn)(void* ctx, double* vals, int32_t n, int32_t op);
+typedef int (*heat2d_barrier_fn)(void* ctx);
+
+const char* heat2d_last_error(void);
+int heat2d_version(void);
+int heat2d_max_tb(void);
+int heat2d_device_count(int* n);
+
+int heat2d_make_layout(int64_t nrows, int64_t ncols, int64_t halo, int64_t row0,
+                       int64_t nrows_global, heat2d_layout* out);
+int heat2d_decompose(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nrows);
+int heat2d_plan_tb(int dtype, const heat2d_layout* L, int64_t rb, int64_t re, int k,
+                   int64_t tile_rows, heat2d_tb_plan* out);
+
+/* Raw ops on caller-owned memory (device pointers for the HIP ops; host for cpu_*).
+ * `stream` is a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). */
+int heat2d_tb(int dtype, const void* src, void* dst, const heat2d_layout* L, int64_t rb,
+              int64_t re, int k, double r, void* stream, int64_t tile_rows);
+int heat2d_init_field(int dtype, void* field, const heat2d_layout* L, const heat2d_ic* ic,
+                      const double* xcoord_dev, const double* ycoord_dev, void* stream);
+int heat2d_stats(int dtype, const void* field, const void* other, const heat2d_layout* L,
+                 double* work_dev, double* out_dev, void* stream);
+int64_t heat2d_stats_work_elems(void);
+int heat2d_pack_rows(int dtype, const void* field, const heat2d_layout* L, int64_t row,
+                     int64_t nrows, void* buf, void* stream);
+int heat2d_unpack_rows(int dtype, void* field, const heat2d_layout* L, int64_t row,
+                       int64_t nrows, const void* buf, void* stream);
+
+int heat2d_cpu_tb(int dtype, const void* src, void* dst, const heat2d_layout* L, int64_t rb,
+                  int64_t re, int k, double r);
+int heat2d_cpu_init_field(int dtype, void* field, const heat2d_layout* L, const heat2d_ic* ic,
+                          const double* xcoord, const double* ycoord);
+int heat2d_cpu_stats(int dtype, const void* field, const void* other, const heat2d_layout* L,
+                     double* out6);
+
+/* Transports (opaque handles). */
+int heat2d_rccl_unique_id(void* out128);
+int heat2d_transport_self(void** out);
+int heat2d_transport_rccl(const void* uid128, int rank, int size, int device, void** out);
+int heat2d_transport_callback(heat2d_exchange_fn ex, heat2d_allreduce_fn ar, heat2d_barrier_fn br,
+                              void* ctx, int rank, int size, void** out);
+int heat2d_transport_free(void* t);
+
+/* Solver. */
+int heat2d_solver_create(const heat2d_config* cfg, void* transport, void** out);
+int heat2d_solver_free(void* s);
+int heat2d_solver_init(void* s, const heat2d_ic* ic, const double* xg, const double* yg);
+int heat2d_solver_step(void* s, int64_t n);
+int heat2d_solver_sync(void* s);
+int heat2d_solver_stats(void* s, double* out6, int residual);
+int heat2d_solver_download(void* s, void* host, int64_t ld);
+int heat2d_solver_upload(void* s, const void* host, int64_t ld);
+int heat2d_solver_layout(void* s, heat2d_layout* out);
+int heat2d_solver_info(void* s, int32_t* tb, int64_t* band, int64_t* steps, void** field,
+                       void** stream);
+
+/* Loopback group: P slabs on one device (or host). */
+int heat2d_group_create(const heat2d_config* cfg, int nranks, void** out);
+int heat2d_group_free(void* g);
+int heat2d_group_init(void* g, const heat2d_ic* ic, const double* xg, const double* yg);
+int heat2d_group_step(void* g, int64_t n);
+int heat2d_group_download(void* g, void* host, int64_t ld);
+
+/* I/O (io.cpp). */
+int heat2d_write_xyz(const char* path, int dtype, const void* host, int64_t nrows, int64_t ncols,
+                     int64_t ld, const double* x, const double* y, int append);
+int heat2d_write_npy(const char* path, int dtype, const void* host, int64_t nrows, int64_t ncols,
+                     int64_t ld);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HEAT2D_CAPI_H */

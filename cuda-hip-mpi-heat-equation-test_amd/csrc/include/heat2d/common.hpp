@@ -1,0 +1,104 @@
+// heat2d — MI355X-native 2-D heat-equation framework.
+// Common types, error handling and the slab memory layout shared by kernels,
+// the runtime and the C ABI.
+//
+// Layout (replaces the x-fastest, 1-ghost, 32-bit-indexed layout of
+// reference fortran/hip/heat_kernel.cpp:26 `idx(i,j)`):
+//   * row-major T[i][j]; i = x index (slow, decomposed across ranks exactly as
+//     the reference splits x, fortran/hip/heat.F90:147), j = y index (fast);
+//   * `halo` ghost rows above and below the owned rows (>= temporal-block depth),
+//     so a halo exchange is a contiguous block of rows (zero-copy for RCCL);
+//   * `cpad` padding columns on the left (column -1 is the Dirichlet column),
+//     pitch rounded so every row starts 256-B aligned;
+//   * all offsets int64 (a 288 GB HBM field holds ~3.6e10 fp64 points).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+namespace heat2d {
+
+enum class DType : int32_t { F32 = 0, F64 = 1 };
+
+inline size_t dtype_size(DType d) { return d == DType::F32 ? 4 : 8; }
+inline const char* dtype_name(DType d) { return d == DType::F32 ? "fp32" : "fp64"; }
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+[[noreturn]] inline void fail(const char* file, int line, const std::string& msg) {
+  throw Error(std::string(file) + ":" + std::to_string(line) + ": " + msg);
+}
+
+#define HEAT2D_REQUIRE(cond, msg)                                              \
+  do {                                                                         \
+    if (!(cond)) ::heat2d::fail(__FILE__, __LINE__, std::string("requirement failed: ") + #cond + " — " + (msg)); \
+  } while (0)
+
+// Column padding on the left of every row (elements). Must be >= the largest
+// temporal-block depth (rounded to the vector width) and keep rows aligned.
+constexpr int64_t kColPad = 32;
+// Largest supported temporal-block depth (time steps fused per HBM pass).
+constexpr int kMaxTB = 16;
+// Default halo depth (ghost rows per side). Must be >= temporal depth used.
+constexpr int64_t kDefaultHalo = kMaxTB;
+
+// Memory layout of one rank's slab. POD so it can cross the C ABI.
+struct SlabLayout {
+  int64_t nrows;         // owned rows on this slab (local nx)
+  int64_t ncols;         // owned columns (ny)
+  int64_t halo;          // ghost rows above and below
+  int64_t cpad;          // padding columns left of column 0
+  int64_t pitch;         // elements per row
+  int64_t row0;          // global row index of local row 0
+  int64_t nrows_global;  // global owned rows (n)
+
+  __host__ __device__ int64_t rows_alloc() const { return nrows + 2 * halo; }
+  __host__ __device__ int64_t elems() const { return rows_alloc() * pitch; }
+  // offset of element (i, j), i in [-halo, nrows+halo), j in [-cpad, pitch-cpad)
+  __host__ __device__ int64_t offset(int64_t i, int64_t j) const { return (i + halo) * pitch + (j + cpad); }
+  __host__ __device__ int64_t origin() const { return offset(0, 0); }
+  __host__ __device__ int64_t col_hi() const { return pitch - cpad; }  // exclusive upper column bound
+};
+
+// Pitch rule: left pad + owned + >=1 Dirichlet column, rounded up to 64
+// elements (256 B fp32 / 512 B fp64 row alignment).
+inline int64_t make_pitch(int64_t ncols, int64_t cpad) {
+  int64_t need = cpad + ncols + kColPad;  // right pad: room for the widest strip overrun
+  return (need + 63) / 64 * 64;
+}
+
+inline SlabLayout make_layout(int64_t nrows, int64_t ncols, int64_t halo, int64_t row0,
+                              int64_t nrows_global) {
+  SlabLayout L{};
+  L.nrows = nrows;
+  L.ncols = ncols;
+  L.halo = halo;
+  L.cpad = kColPad;
+  L.pitch = make_pitch(ncols, L.cpad);
+  L.row0 = row0;
+  L.nrows_global = nrows_global;
+  return L;
+}
+
+// 1-D slab decomposition of `n` global rows over `nranks` ranks, remainder
+// spread over the first ranks (the reference silently drops n mod P,
+// fortran/hip/heat.F90:147 `nx = n/nblocks(1)`).
+struct SlabRange {
+  int64_t row0;
+  int64_t nrows;
+};
+inline SlabRange decompose(int64_t n, int nranks, int rank) {
+  HEAT2D_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+  int64_t base = n / nranks, rem = n % nranks;
+  int64_t nrows = base + (rank < rem ? 1 : 0);
+  int64_t row0 = rank * base + (rank < rem ? rank : rem);
+  return {row0, nrows};
+}
+
+}  // namespace heat2d

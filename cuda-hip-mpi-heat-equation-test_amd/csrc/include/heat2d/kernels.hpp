@@ -1,0 +1,80 @@
+// heat2d device-kernel launchers (gfx950). Every launcher is capture-safe:
+// no allocation, no synchronisation, only kernel launches on `stream`.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "heat2d/common.hpp"
+
+namespace heat2d {
+namespace kern {
+
+// Tiling of one temporal-block launch. Filled by plan_tb(); exposed so tests
+// and the autotuner can inspect / override it.
+struct TbPlan {
+  int32_t k;          // time steps fused in this launch (1..kMaxTB)
+  int32_t vec;        // elements per lane (16 B: 4 fp32 / 2 fp64)
+  int32_t strip_w;    // columns loaded per wave (64 * vec)
+  int32_t useful_w;   // columns produced per wave (strip_w - 2*ceil(k, vec))
+  int64_t tile_rows;  // output rows per wave tile
+  int64_t nstrips;
+  int64_t ntiles;
+  int64_t nwaves;
+  int64_t nblocks;    // 256-thread workgroups (4 independent waves each)
+};
+
+// Plan a launch that advances rows [row_begin, row_end) of the slab by k steps.
+// tile_rows <= 0 selects the occupancy-driven default.
+TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k,
+               int64_t tile_rows = 0);
+
+// dst(rows [row_begin,row_end)) = k FTCS steps of src. `src`/`dst` are
+// allocation bases laid out per `L`. Requires k <= L.halo and the k ghost rows
+// on both sides of the range to hold valid data at time t (Dirichlet rows are
+// recognised from L.row0 / L.nrows_global and kept fixed).
+void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin,
+               int64_t row_end, int k, double r, hipStream_t stream, int64_t tile_rows = 0);
+
+// Initial / boundary condition kinds (covers every IC of the reference
+// variants, see models/presets.py for the mapping).
+enum class IcKind : int32_t {
+  Uniform = 0,   // interior = a, Dirichlet frame = b   (fortran/hip/heat.F90:274-282)
+  Box = 1,       // a inside [x0,x1]x[y0,y1] (frame included), else b (fortran/serial/heat.f90:40-48)
+  IndexBox = 2,  // a for global frame-index ranges [i0,i1) x [j0,j1), else b (python/serial/heat.py:25)
+  Sine = 3,      // a * sin(kx*pi*(x-x0)/(x1-x0)) * sin(ky*pi*(y-y0)/(y1-y0)), frame = 0 (analytic oracle)
+  Const = 4,     // a everywhere
+};
+
+struct IcParams {
+  int32_t kind;
+  double a, b;
+  double x0, x1, y0, y1;     // box / sine extents
+  int64_t i0, i1, j0, j1;    // index box (frame-inclusive global indices: frame row = 0)
+  double kx, ky;             // sine mode numbers
+  double pad;                // value for allocation padding outside the frame
+};
+
+// Fill the whole allocation (owned points, Dirichlet frame, ghost/pad rows)
+// from the IC. `xcoord` has nrows_global+2 entries (frame-inclusive, entry 0
+// is global row -1), `ycoord` has ncols+2 entries — both device arrays.
+void launch_init(DType dt, void* field, const SlabLayout& L, const IcParams& ic,
+                 const double* xcoord, const double* ycoord, hipStream_t stream);
+
+// Statistics over the owned region: [sum, sum_sq, min, max, sum_sq_diff, max_abs_diff]
+// (diff terms vs `other`, zero if other == nullptr). Deterministic two-pass
+// reduction; `work` must hold stats_work_elems() doubles; result (6 doubles)
+// written to `out` (device).
+int64_t stats_work_elems();
+void launch_stats(DType dt, const void* field, const void* other, const SlabLayout& L,
+                  double* work, double* out, hipStream_t stream);
+
+// Pack/unpack `nrows` rows starting at local row `row` into / from a
+// contiguous buffer of nrows*ncols elements (the owned columns only). Used for
+// generic transports and host staging; the RCCL path sends rows in place.
+void launch_pack_rows(DType dt, const void* field, const SlabLayout& L, int64_t row,
+                      int64_t nrows, void* buf, hipStream_t stream);
+void launch_unpack_rows(DType dt, void* field, const SlabLayout& L, int64_t row, int64_t nrows,
+                        const void* buf, hipStream_t stream);
+
+}  // namespace kern
+}  // namespace heat2d

@@ -1,0 +1,187 @@
+// heat2d native runtime: slab solver, transports, CPU twin kernels.
+//
+// Replaces the reference's host drivers (fortran/hip/heat.F90 setup/swap/
+// heat_eqn, fortran/mpi+cuda/heat.F90) with one engine that
+//   * keeps two pitched fields (ping-pong, no per-step D2D copy),
+//   * advances K steps per HBM pass (temporal blocking, kernels.hpp),
+//   * splits each cycle into boundary bands + interior so the halo exchange of
+//     the bands (RCCL send/recv on a comm stream, zero-copy rows) overlaps the
+//     interior kernel, ordered only by hipEvents,
+//   * runs the same schedule on a CPU backend (for CPU-only CI with gloo) and
+//     on a loopback group (P slabs on one GPU, bitwise == P=1).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "heat2d/common.hpp"
+#include "heat2d/kernels.hpp"
+
+namespace heat2d {
+
+enum class Backend : int32_t { Hip = 0, Cpu = 1 };
+
+// POD config (crosses the C ABI).
+struct SolverConfig {
+  int64_t n_rows;      // global owned rows (x points)
+  int64_t n_cols;      // owned columns (y points)
+  int32_t dtype;       // DType
+  int32_t backend;     // Backend
+  double r;            // FTCS coefficient nu*dt/delta^2
+  int32_t tb;          // temporal-block depth K (steps per HBM pass)
+  int32_t overlap;     // 1: boundary/interior split + comm stream (P>1)
+  int32_t copy_swap;   // 1: reference-parity mode, full D2D copy each step (K forced to 1)
+  int32_t managed;     // 1: hipMallocManaged fields (parity with fortran/cuda_kernel/heat_managed.F90)
+  int32_t device;      // HIP device ordinal (-1: current)
+  int32_t use_graph;   // 1: replay cycles from a captured hipGraph
+  int64_t tile_rows;   // 0: auto
+  int64_t halo;        // 0: auto (= kMaxTB)
+};
+
+// ---------------------------------------------------------------- transports
+
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  // Halo exchange of k rows of `field` (allocation base, layout L): rows
+  // [0,k) -> rank-1, rows [nrows-k,nrows) -> rank+1; receive into [-k,0) from
+  // rank-1 and [nrows,nrows+k) from rank+1. on_device: `field` is device
+  // memory and the exchange is enqueued on `stream`; otherwise host memory,
+  // synchronous.
+  virtual void exchange(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
+                        bool on_device) = 0;
+  // Blocking all-reduce of host doubles (op 0 = sum, 1 = max, 2 = min).
+  virtual void allreduce(double* vals, int n, int op) = 0;
+  virtual void barrier() = 0;
+  virtual std::string name() const = 0;
+  virtual bool capturable() const { return false; }  // safe inside hipGraph capture
+};
+
+std::shared_ptr<Transport> make_self_transport();
+// RCCL over xGMI. `uid` = 128-byte ncclUniqueId produced by rccl_unique_id()
+// on rank 0 and broadcast out of band (torch.distributed store, file, or a
+// shared variable for thread-per-GPU).
+std::shared_ptr<Transport> make_rccl_transport(const void* uid, int rank, int size, int device);
+void rccl_unique_id(void* out128);
+// Host callbacks (Python / gloo, tests). Buffers passed are host pointers to
+// packed rows (k*ncols elements): send_lo/send_hi may be null at domain ends.
+struct CallbackOps {
+  void* ctx;
+  int (*exchange)(void* ctx, void* send_lo, void* send_hi, void* recv_lo, void* recv_hi,
+                  int64_t count, int32_t dtype);
+  int (*allreduce)(void* ctx, double* vals, int32_t n, int32_t op);
+  int (*barrier)(void* ctx);
+};
+std::shared_ptr<Transport> make_callback_transport(const CallbackOps& ops, int rank, int size);
+
+// ---------------------------------------------------------------- CPU twins
+
+namespace cpu {
+void tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin,
+        int64_t row_end, int k, double r);
+void init(DType dt, void* field, const SlabLayout& L, const kern::IcParams& ic,
+          const double* xcoord, const double* ycoord);
+void stats(DType dt, const void* field, const void* other, const SlabLayout& L, double out[6]);
+void pack_rows(DType dt, const void* field, const SlabLayout& L, int64_t row, int64_t nrows, void* buf);
+void unpack_rows(DType dt, void* field, const SlabLayout& L, int64_t row, int64_t nrows, const void* buf);
+int num_threads();
+}  // namespace cpu
+
+// ---------------------------------------------------------------- solver
+
+class Solver {
+ public:
+  Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream_t external_stream = nullptr);
+  ~Solver();
+  Solver(const Solver&) = delete;
+  Solver& operator=(const Solver&) = delete;
+
+  // IC on the device. xg: n_rows+2 frame-inclusive global x coordinates,
+  // yg: n_cols+2 y coordinates. Ghost rows come from the global IC (no exchange).
+  void init(const kern::IcParams& ic, const double* xg, const double* yg);
+  // Advance n time steps (asynchronous on the HIP backend).
+  void step(int64_t n);
+  void synchronize();
+  // Global statistics over all ranks: sum, sum_sq, min, max, and residual
+  // terms vs the previous buffer (valid right after a step()).
+  void stats(double out[6], bool residual);
+  // Owned region <-> host (rows x n_cols, leading dimension ld elements).
+  void download(void* host, int64_t ld);
+  void upload(const void* host, int64_t ld);  // followed by a halo exchange
+  // Any rectangle of the current buffer (local rows [r0,r1), cols [c0,c1),
+  // ghost/frame included) -> host.
+  void download_region(int64_t r0, int64_t r1, int64_t c0, int64_t c1, void* host, int64_t ld);
+
+  // Phase API (used by the loopback group; step() drives these itself).
+  void cycle_compute(int k);   // whole-slab compute cur -> nxt (no exchange)
+  void cycle_swap();
+  void exchange_now();         // exchange halos of the current buffer on the compute stream
+
+  const SlabLayout& layout() const { return L_; }
+  const SolverConfig& config() const { return cfg_; }
+  DType dtype() const { return (DType)cfg_.dtype; }
+  void* field() const { return buf_[cur_]; }
+  void* other_field() const { return buf_[cur_ ^ 1]; }
+  int64_t steps_done() const { return steps_; }
+  int rank() const { return tr_->rank(); }
+  int size() const { return tr_->size(); }
+  hipStream_t stream() const { return s_compute_; }
+  Transport& transport() { return *tr_; }
+  int64_t band() const { return band_; }
+  // Kernel time accumulated from events (ms) when timing is enabled.
+  void set_timing(bool on) { timing_ = on; }
+
+ private:
+  void cycle_overlap(int k);
+  void cycle_serial(int k);
+  void cycle_copy_swap();
+  void launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k);
+  void exchange_on(void* field, hipStream_t s);
+  void run_graph_cycles(int64_t npairs);
+
+  SolverConfig cfg_;
+  std::shared_ptr<Transport> tr_;
+  SlabLayout L_{};
+  bool hip_ = true;
+  void* buf_[2] = {nullptr, nullptr};
+  int cur_ = 0;
+  int64_t steps_ = 0;
+  int64_t band_ = 0;     // boundary band rows (= halo exchange depth = K)
+  hipStream_t s_compute_ = nullptr, s_comm_ = nullptr;
+  bool own_streams_ = false;
+  hipEvent_t ev_bnd_ = nullptr, ev_comm_ = nullptr;
+  double* d_work_ = nullptr;   // stats workspace + 6 results
+  bool timing_ = false;
+  hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K
+  int graph_k_ = 0;
+  std::vector<char> host_stage_;  // CPU-backend / callback staging
+};
+
+// P slabs of one domain on ONE device (or host), halos moved by device
+// copies: proves the decomposition, band split and exchange schedule without
+// a cluster (must be bitwise identical to P = 1).
+class LoopbackGroup {
+ public:
+  LoopbackGroup(const SolverConfig& cfg, int nranks);
+  ~LoopbackGroup();
+  void init(const kern::IcParams& ic, const double* xg, const double* yg);
+  void step(int64_t n);
+  void synchronize();
+  void download(void* host, int64_t ld);  // whole global owned region
+  int nranks() const { return (int)members_.size(); }
+  Solver& member(int i) { return *members_[i]; }
+
+ private:
+  void exchange_all();
+  SolverConfig cfg_;
+  hipStream_t stream_ = nullptr;
+  std::vector<std::unique_ptr<Solver>> members_;
+};
+
+}  // namespace heat2d

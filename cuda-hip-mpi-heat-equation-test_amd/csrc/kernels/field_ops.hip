@@ -1,0 +1,227 @@
+// Field utility kernels for gfx950: initial/boundary conditions generated on
+// the device (the reference builds T on the host and copies the whole field,
+// fortran/hip/heat.F90:274-287 — infeasible for a 288 GB grid), deterministic
+// statistics (the reference's commented-out checksum, fortran/hip/heat.F90:297-306,
+// enabled and extended with a residual), and row pack/unpack (the generic
+// replacement for the strided K2-K4 gather/scatter, fortran/hip/heat_kernel.cpp:63-150).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "heat2d/kernels.hpp"
+
+namespace heat2d {
+namespace kern {
+namespace {
+
+constexpr int kStatsBlocks = 1024;
+constexpr int kStatsThreads = 256;
+constexpr int kNStat = 6;
+
+template <typename T>
+__global__ __launch_bounds__(256) void init_kernel(T* __restrict__ f, SlabLayout L, IcParams ic,
+                                                   const double* __restrict__ xc,
+                                                   const double* __restrict__ yc) {
+  // grid-stride over the whole allocation, one element per thread per step
+  const int64_t total = L.elems();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
+    const int64_t ia = idx / L.pitch;
+    const int64_t ja = idx - ia * L.pitch;
+    const int64_t i = ia - L.halo;        // local row
+    const int64_t j = ja - L.cpad;        // local column
+    const int64_t g = L.row0 + i;         // global row
+    const bool in_frame_rows = g >= -1 && g <= L.nrows_global;
+    const bool in_frame_cols = j >= -1 && j <= L.ncols;
+    double v;
+    if (!(in_frame_rows && in_frame_cols)) {
+      v = ic.pad;
+    } else {
+      const bool frame = g < 0 || g >= L.nrows_global || j < 0 || j >= L.ncols;
+      const double x = xc[g + 1];
+      const double y = yc[j + 1];
+      switch (ic.kind) {
+        case (int)IcKind::Uniform:
+          v = frame ? ic.b : ic.a;
+          break;
+        case (int)IcKind::Box:
+          v = (x <= ic.x1 && x >= ic.x0 && y <= ic.y1 && y >= ic.y0) ? ic.a : ic.b;
+          break;
+        case (int)IcKind::IndexBox: {
+          const int64_t gi = g + 1, gj = j + 1;  // frame-inclusive indices
+          v = (gi >= ic.i0 && gi < ic.i1 && gj >= ic.j0 && gj < ic.j1) ? ic.a : ic.b;
+          break;
+        }
+        case (int)IcKind::Sine:
+          v = frame ? 0.0
+                    : ic.a * sin(ic.kx * M_PI * (x - ic.x0) / (ic.x1 - ic.x0)) *
+                          sin(ic.ky * M_PI * (y - ic.y0) / (ic.y1 - ic.y0));
+          break;
+        default:
+          v = ic.a;
+      }
+    }
+    f[idx] = (T)v;
+  }
+}
+
+// Pass 1: each block reduces a set of owned rows; partials written per block
+// in a fixed order (no atomics) so the result is bitwise reproducible.
+template <typename T>
+__global__ __launch_bounds__(kStatsThreads) void stats_pass1(const T* __restrict__ f,
+                                                             const T* __restrict__ o, SlabLayout L,
+                                                             double* __restrict__ work) {
+  double s = 0.0, ss = 0.0, mn = DBL_MAX, mx = -DBL_MAX, dd = 0.0, md = 0.0;
+  const int64_t origin = L.origin();
+  for (int64_t i = blockIdx.x; i < L.nrows; i += gridDim.x) {
+    const T* row = f + origin + i * L.pitch;
+    const T* orow = o ? o + origin + i * L.pitch : nullptr;
+    for (int64_t j = threadIdx.x; j < L.ncols; j += blockDim.x) {
+      const double v = (double)row[j];
+      s += v;
+      ss += v * v;
+      mn = fmin(mn, v);
+      mx = fmax(mx, v);
+      if (orow) {
+        const double d = v - (double)orow[j];
+        dd += d * d;
+        md = fmax(md, fabs(d));
+      }
+    }
+  }
+  __shared__ double red[kNStat][kStatsThreads];
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = ss;
+  red[2][threadIdx.x] = mn;
+  red[3][threadIdx.x] = mx;
+  red[4][threadIdx.x] = dd;
+  red[5][threadIdx.x] = md;
+  __syncthreads();
+  for (int w = kStatsThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+      red[2][threadIdx.x] = fmin(red[2][threadIdx.x], red[2][threadIdx.x + w]);
+      red[3][threadIdx.x] = fmax(red[3][threadIdx.x], red[3][threadIdx.x + w]);
+      red[4][threadIdx.x] += red[4][threadIdx.x + w];
+      red[5][threadIdx.x] = fmax(red[5][threadIdx.x], red[5][threadIdx.x + w]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < kNStat) work[threadIdx.x * kStatsBlocks + blockIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(kStatsThreads) void stats_pass2(const double* __restrict__ work,
+                                                             double* __restrict__ out) {
+  __shared__ double red[kNStat][kStatsThreads];
+  double acc[kNStat] = {0.0, 0.0, DBL_MAX, -DBL_MAX, 0.0, 0.0};
+  for (int b = threadIdx.x; b < kStatsBlocks; b += blockDim.x) {
+    acc[0] += work[0 * kStatsBlocks + b];
+    acc[1] += work[1 * kStatsBlocks + b];
+    acc[2] = fmin(acc[2], work[2 * kStatsBlocks + b]);
+    acc[3] = fmax(acc[3], work[3 * kStatsBlocks + b]);
+    acc[4] += work[4 * kStatsBlocks + b];
+    acc[5] = fmax(acc[5], work[5 * kStatsBlocks + b]);
+  }
+  for (int k = 0; k < kNStat; ++k) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  for (int w = kStatsThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+      red[2][threadIdx.x] = fmin(red[2][threadIdx.x], red[2][threadIdx.x + w]);
+      red[3][threadIdx.x] = fmax(red[3][threadIdx.x], red[3][threadIdx.x + w]);
+      red[4][threadIdx.x] += red[4][threadIdx.x + w];
+      red[5][threadIdx.x] = fmax(red[5][threadIdx.x], red[5][threadIdx.x + w]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < kNStat) out[threadIdx.x] = red[threadIdx.x][0];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ f, SlabLayout L,
+                                                        int64_t row, int64_t nrows,
+                                                        T* __restrict__ buf) {
+  const int64_t total = nrows * L.ncols;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t i = t / L.ncols, j = t - i * L.ncols;
+    buf[t] = f[L.offset(row + i, j)];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void unpack_rows_kernel(T* __restrict__ f, SlabLayout L,
+                                                          int64_t row, int64_t nrows,
+                                                          const T* __restrict__ buf) {
+  const int64_t total = nrows * L.ncols;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t i = t / L.ncols, j = t - i * L.ncols;
+    f[L.offset(row + i, j)] = buf[t];
+  }
+}
+
+inline unsigned grid_for(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;  // grid-stride beyond 8 blocks per CU
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+inline void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fail(__FILE__, __LINE__, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+void launch_init(DType dt, void* field, const SlabLayout& L, const IcParams& ic,
+                 const double* xcoord, const double* ycoord, hipStream_t stream) {
+  const unsigned g = grid_for(L.elems());
+  if (dt == DType::F32)
+    hipLaunchKernelGGL(init_kernel<float>, dim3(g), dim3(256), 0, stream, static_cast<float*>(field), L, ic, xcoord, ycoord);
+  else
+    hipLaunchKernelGGL(init_kernel<double>, dim3(g), dim3(256), 0, stream, static_cast<double*>(field), L, ic, xcoord, ycoord);
+  check_launch("init_kernel");
+}
+
+int64_t stats_work_elems() { return (int64_t)kNStat * kStatsBlocks; }
+
+void launch_stats(DType dt, const void* field, const void* other, const SlabLayout& L, double* work,
+                  double* out, hipStream_t stream) {
+  if (dt == DType::F32)
+    hipLaunchKernelGGL(stats_pass1<float>, dim3(kStatsBlocks), dim3(kStatsThreads), 0, stream,
+                       static_cast<const float*>(field), static_cast<const float*>(other), L, work);
+  else
+    hipLaunchKernelGGL(stats_pass1<double>, dim3(kStatsBlocks), dim3(kStatsThreads), 0, stream,
+                       static_cast<const double*>(field), static_cast<const double*>(other), L, work);
+  check_launch("stats_pass1");
+  hipLaunchKernelGGL(stats_pass2, dim3(1), dim3(kStatsThreads), 0, stream, work, out);
+  check_launch("stats_pass2");
+}
+
+void launch_pack_rows(DType dt, const void* field, const SlabLayout& L, int64_t row, int64_t nrows,
+                      void* buf, hipStream_t stream) {
+  const unsigned g = grid_for(nrows * L.ncols);
+  if (dt == DType::F32)
+    hipLaunchKernelGGL(pack_rows_kernel<float>, dim3(g), dim3(256), 0, stream, static_cast<const float*>(field), L, row, nrows, static_cast<float*>(buf));
+  else
+    hipLaunchKernelGGL(pack_rows_kernel<double>, dim3(g), dim3(256), 0, stream, static_cast<const double*>(field), L, row, nrows, static_cast<double*>(buf));
+  check_launch("pack_rows");
+}
+
+void launch_unpack_rows(DType dt, void* field, const SlabLayout& L, int64_t row, int64_t nrows,
+                        const void* buf, hipStream_t stream) {
+  const unsigned g = grid_for(nrows * L.ncols);
+  if (dt == DType::F32)
+    hipLaunchKernelGGL(unpack_rows_kernel<float>, dim3(g), dim3(256), 0, stream, static_cast<float*>(field), L, row, nrows, static_cast<const float*>(buf));
+  else
+    hipLaunchKernelGGL(unpack_rows_kernel<double>, dim3(g), dim3(256), 0, stream, static_cast<double*>(field), L, row, nrows, static_cast<const double*>(buf));
+  check_launch("unpack_rows");
+}
+
+}  // namespace kern
+}  // namespace heat2d

@@ -1,0 +1,396 @@
+// Slab solver: the time loop of fortran/hip/heat.F90:232-254 (heat_eqn) and
+// fortran/mpi+cuda/heat.F90:197-223, re-designed for MI355X.
+//
+// Reference, per step: full-field D2D copy; stencil kernel; device sync;
+// pack; sync; 2 D2H; 2 blocking MPI_Sendrecv; 2 H2D; unpack (+sync) — all
+// serialised on the null stream.
+//
+// Here, per cycle of k <= K steps (one HBM pass):
+//   compute stream:  wait(ev_comm) -> tb(bands [0,B) and [n-B,n)) -> record(ev_bnd)
+//                    -> tb(interior [B, n-B))                      (runs concurrently)
+//   comm stream:     wait(ev_bnd) -> RCCL grouped send/recv of B rows -> record(ev_comm)
+// with ping-pong buffers (no copy). Ordering is carried entirely by events;
+// the host never synchronises inside the loop.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "heat2d/runtime.hpp"
+
+namespace heat2d {
+
+#define H2D_HIP(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) fail(__FILE__, __LINE__, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+void* host_alloc(size_t bytes) {
+  const size_t a = 256;
+  void* p = std::aligned_alloc(a, (bytes + a - 1) / a * a);
+  HEAT2D_REQUIRE(p != nullptr, "host allocation failed");
+  return p;
+}
+}  // namespace
+
+Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream_t external_stream)
+    : cfg_(cfg), tr_(std::move(tr)) {
+  HEAT2D_REQUIRE(tr_ != nullptr, "transport required");
+  HEAT2D_REQUIRE(cfg_.n_rows >= 1 && cfg_.n_cols >= 1, "empty grid");
+  HEAT2D_REQUIRE(cfg_.dtype == 0 || cfg_.dtype == 1, "dtype must be 0 (fp32) or 1 (fp64)");
+  hip_ = cfg_.backend == (int32_t)Backend::Hip;
+  const int P = tr_->size(), rank = tr_->rank();
+  HEAT2D_REQUIRE(cfg_.n_rows >= P, "fewer rows than ranks");
+
+  int K = std::max(1, std::min<int>(cfg_.tb <= 0 ? 1 : cfg_.tb, kMaxTB));
+  if (cfg_.copy_swap) K = 1;
+  // every rank must own >= K rows so a neighbour's K ghost rows come from one rank
+  K = (int)std::min<int64_t>(K, cfg_.n_rows / P);
+  cfg_.tb = K;
+  band_ = K;
+  const int64_t halo = cfg_.halo > 0 ? cfg_.halo : kDefaultHalo;
+  HEAT2D_REQUIRE(halo >= K, "halo must be >= temporal depth");
+  const SlabRange sr = decompose(cfg_.n_rows, P, rank);
+  L_ = make_layout(sr.nrows, cfg_.n_cols, halo, sr.row0, cfg_.n_rows);
+
+  const size_t bytes = (size_t)L_.elems() * dtype_size(dtype());
+  if (hip_) {
+    if (cfg_.device >= 0) H2D_HIP(hipSetDevice(cfg_.device));
+    else H2D_HIP(hipGetDevice(&cfg_.device));
+    for (int b = 0; b < 2; ++b) {
+      if (cfg_.managed) H2D_HIP(hipMallocManaged(&buf_[b], bytes));
+      else H2D_HIP(hipMalloc(&buf_[b], bytes));
+    }
+    H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_work_), (size_t)(kern::stats_work_elems() + 8) * sizeof(double)));
+    if (external_stream) {
+      s_compute_ = s_comm_ = external_stream;
+      cfg_.overlap = 0;
+    } else {
+      H2D_HIP(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
+      H2D_HIP(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+      own_streams_ = true;
+    }
+    H2D_HIP(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
+    H2D_HIP(hipEventCreateWithFlags(&ev_comm_, hipEventDisableTiming));
+    H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
+  } else {
+    for (int b = 0; b < 2; ++b) buf_[b] = host_alloc(bytes);
+    cfg_.overlap = 0;
+    cfg_.use_graph = 0;
+  }
+}
+
+Solver::~Solver() {
+  if (hip_) {
+    (void)hipSetDevice(cfg_.device);
+    if (s_compute_) (void)hipStreamSynchronize(s_compute_);
+    if (s_comm_ && s_comm_ != s_compute_) (void)hipStreamSynchronize(s_comm_);
+    if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
+    for (auto& b : buf_)
+      if (b) (void)hipFree(b);
+    if (d_work_) (void)hipFree(d_work_);
+    if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
+    if (ev_comm_) (void)hipEventDestroy(ev_comm_);
+    if (own_streams_) {
+      (void)hipStreamDestroy(s_compute_);
+      (void)hipStreamDestroy(s_comm_);
+    }
+  } else {
+    for (auto& b : buf_) std::free(b);
+  }
+}
+
+void Solver::init(const kern::IcParams& ic, const double* xg, const double* yg) {
+  const size_t nx = (size_t)(cfg_.n_rows + 2), ny = (size_t)(cfg_.n_cols + 2);
+  if (hip_) {
+    H2D_HIP(hipSetDevice(cfg_.device));
+    double* d = nullptr;
+    H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d), (nx + ny) * sizeof(double)));
+    H2D_HIP(hipMemcpyAsync(d, xg, nx * sizeof(double), hipMemcpyHostToDevice, s_compute_));
+    H2D_HIP(hipMemcpyAsync(d + nx, yg, ny * sizeof(double), hipMemcpyHostToDevice, s_compute_));
+    for (int b = 0; b < 2; ++b) kern::launch_init(dtype(), buf_[b], L_, ic, d, d + nx, s_compute_);
+    H2D_HIP(hipStreamSynchronize(s_compute_));
+    H2D_HIP(hipFree(d));
+  } else {
+    for (int b = 0; b < 2; ++b) cpu::init(dtype(), buf_[b], L_, ic, xg, yg);
+  }
+  // ghost rows are filled from the global IC directly: no exchange needed
+  cur_ = 0;
+  steps_ = 0;
+}
+
+void Solver::launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k) {
+  if (re <= rb) return;
+  if (hip_)
+    kern::launch_tb(dtype(), src, dst, L_, rb, re, k, cfg_.r, s_compute_, cfg_.tile_rows);
+  else
+    cpu::tb(dtype(), src, dst, L_, rb, re, k, cfg_.r);
+}
+
+void Solver::exchange_on(void* field, hipStream_t s) {
+  if (tr_->size() == 1) return;
+  tr_->exchange(field, L_, dtype(), band_, s, hip_);
+}
+
+void Solver::cycle_compute(int k) { launch_tb(buf_[cur_], buf_[cur_ ^ 1], 0, L_.nrows, k); }
+
+void Solver::cycle_swap() {
+  cur_ ^= 1;
+}
+
+void Solver::exchange_now() { exchange_on(buf_[cur_], s_compute_); }
+
+void Solver::cycle_serial(int k) {
+  cycle_compute(k);
+  exchange_on(buf_[cur_ ^ 1], s_compute_);
+  cycle_swap();
+}
+
+void Solver::cycle_overlap(int k) {
+  void* src = buf_[cur_];
+  void* dst = buf_[cur_ ^ 1];
+  const int64_t n = L_.nrows, B = band_;
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
+  if (n <= 2 * B) {
+    launch_tb(src, dst, 0, n, k);
+    H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_bnd_, 0));
+    exchange_on(dst, s_comm_);
+    H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
+  } else {
+    launch_tb(src, dst, 0, B, k);
+    launch_tb(src, dst, n - B, n, k);
+    H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_bnd_, 0));
+    exchange_on(dst, s_comm_);
+    H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
+    launch_tb(src, dst, B, n - B, k);
+  }
+  cycle_swap();
+}
+
+void Solver::cycle_copy_swap() {
+  // Reference-parity schedule (fortran/hip/heat.F90:243-249): T_old <- T (full
+  // D2D copy), T <- stencil(T_old), halo swap into T. No pointer swap.
+  void* cur = buf_[cur_];
+  void* old = buf_[cur_ ^ 1];
+  const size_t bytes = (size_t)L_.elems() * dtype_size(dtype());
+  if (hip_) H2D_HIP(hipMemcpyAsync(old, cur, bytes, hipMemcpyDeviceToDevice, s_compute_));
+  else std::memcpy(old, cur, bytes);
+  launch_tb(old, cur, 0, L_.nrows, 1);
+  exchange_on(cur, s_compute_);
+}
+
+void Solver::run_graph_cycles(int64_t npairs) {
+  const int K = cfg_.tb;
+  if (!graph_exec_ || graph_k_ != K) {
+    if (graph_exec_) H2D_HIP(hipGraphExecDestroy(graph_exec_));
+    hipGraph_t g = nullptr;
+    H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
+    const int saved = cur_;
+    cycle_serial(K);
+    cycle_serial(K);
+    cur_ = saved;
+    H2D_HIP(hipStreamEndCapture(s_compute_, &g));
+    H2D_HIP(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
+    H2D_HIP(hipGraphDestroy(g));
+    graph_k_ = K;
+  }
+  // the graph was captured for buffer parity 0 -> 1 -> 0
+  for (int64_t i = 0; i < npairs; ++i) H2D_HIP(hipGraphLaunch(graph_exec_, s_compute_));
+}
+
+void Solver::step(int64_t n) {
+  if (n <= 0) return;
+  if (hip_) H2D_HIP(hipSetDevice(cfg_.device));
+  if (cfg_.copy_swap) {
+    for (int64_t i = 0; i < n; ++i) cycle_copy_swap();
+    steps_ += n;
+    return;
+  }
+  const int K = cfg_.tb;
+  const bool multi = tr_->size() > 1;
+  int64_t left = n;
+  while (left > 0) {
+    if (cfg_.use_graph && hip_ && (!multi || tr_->capturable()) && !cfg_.overlap && left >= 2 * K &&
+        cur_ == 0) {
+      const int64_t pairs = left / (2 * K);
+      run_graph_cycles(pairs);
+      left -= pairs * 2 * K;
+      steps_ += pairs * 2 * K;
+      continue;
+    }
+    const int k = (int)std::min<int64_t>(K, left);
+    if (multi && cfg_.overlap && hip_) cycle_overlap(k);
+    else cycle_serial(k);
+    left -= k;
+    steps_ += k;
+  }
+}
+
+void Solver::synchronize() {
+  if (!hip_) return;
+  H2D_HIP(hipSetDevice(cfg_.device));
+  H2D_HIP(hipStreamSynchronize(s_compute_));
+  if (s_comm_ != s_compute_) H2D_HIP(hipStreamSynchronize(s_comm_));
+}
+
+void Solver::stats(double out[6], bool residual) {
+  double loc[6];
+  const void* other = residual ? buf_[cur_ ^ 1] : nullptr;
+  if (hip_) {
+    synchronize();
+    kern::launch_stats(dtype(), buf_[cur_], other, L_, d_work_, d_work_ + kern::stats_work_elems(), s_compute_);
+    H2D_HIP(hipMemcpyAsync(loc, d_work_ + kern::stats_work_elems(), sizeof(loc), hipMemcpyDeviceToHost, s_compute_));
+    H2D_HIP(hipStreamSynchronize(s_compute_));
+  } else {
+    cpu::stats(dtype(), buf_[cur_], other, L_, loc);
+  }
+  double sums[3] = {loc[0], loc[1], loc[4]};
+  double maxs[3] = {loc[3], loc[5], -loc[2]};
+  tr_->allreduce(sums, 3, 0);
+  tr_->allreduce(maxs, 3, 1);
+  out[0] = sums[0];
+  out[1] = sums[1];
+  out[2] = -maxs[2];
+  out[3] = maxs[0];
+  out[4] = sums[2];
+  out[5] = maxs[1];
+}
+
+void Solver::download(void* host, int64_t ld) { download_region(0, L_.nrows, 0, L_.ncols, host, ld); }
+
+void Solver::download_region(int64_t r0, int64_t r1, int64_t c0, int64_t c1, void* host, int64_t ld) {
+  HEAT2D_REQUIRE(r0 >= -L_.halo && r1 <= L_.nrows + L_.halo && r0 <= r1, "row range outside allocation");
+  HEAT2D_REQUIRE(c0 >= -L_.cpad && c1 <= L_.col_hi() && c0 <= c1, "column range outside allocation");
+  if (r1 == r0 || c1 == c0) return;
+  const size_t es = dtype_size(dtype());
+  const char* src = static_cast<const char*>(buf_[cur_]) + (size_t)L_.offset(r0, c0) * es;
+  const size_t w = (size_t)(c1 - c0) * es;
+  if (hip_) {
+    synchronize();
+    H2D_HIP(hipMemcpy2DAsync(host, (size_t)ld * es, src, (size_t)L_.pitch * es, w, (size_t)(r1 - r0),
+                             hipMemcpyDeviceToHost, s_compute_));
+    H2D_HIP(hipStreamSynchronize(s_compute_));
+  } else {
+    for (int64_t i = 0; i < r1 - r0; ++i)
+      std::memcpy(static_cast<char*>(host) + (size_t)(i * ld) * es, src + (size_t)(i * L_.pitch) * es, w);
+  }
+}
+
+void Solver::upload(const void* host, int64_t ld) {
+  const size_t es = dtype_size(dtype());
+  char* dst = static_cast<char*>(buf_[cur_]) + (size_t)L_.origin() * es;
+  if (hip_) {
+    synchronize();
+    H2D_HIP(hipMemcpy2DAsync(dst, (size_t)L_.pitch * es, host, (size_t)ld * es, (size_t)L_.ncols * es,
+                             (size_t)L_.nrows, hipMemcpyHostToDevice, s_compute_));
+  } else {
+    for (int64_t i = 0; i < L_.nrows; ++i)
+      std::memcpy(dst + (size_t)(i * L_.pitch) * es, static_cast<const char*>(host) + (size_t)(i * ld) * es,
+                  (size_t)L_.ncols * es);
+  }
+  exchange_now();
+  synchronize();
+}
+
+// ------------------------------------------------------------------ loopback
+
+namespace {
+// Member transport: reports its rank within the group; the group moves halos.
+class GroupMemberTransport final : public Transport {
+ public:
+  GroupMemberTransport(int r, int n) : r_(r), n_(n) {}
+  int rank() const override { return r_; }
+  int size() const override { return n_; }
+  void exchange(void*, const SlabLayout&, DType, int64_t, hipStream_t, bool) override {}
+  void allreduce(double*, int, int) override {}
+  void barrier() override {}
+  std::string name() const override { return "loopback"; }
+
+ private:
+  int r_, n_;
+};
+}  // namespace
+
+LoopbackGroup::LoopbackGroup(const SolverConfig& cfg, int nranks) : cfg_(cfg) {
+  HEAT2D_REQUIRE(nranks >= 1, "nranks >= 1");
+  const bool hip = cfg.backend == (int32_t)Backend::Hip;
+  if (hip) {
+    if (cfg.device >= 0) H2D_HIP(hipSetDevice(cfg.device));
+    H2D_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  }
+  for (int i = 0; i < nranks; ++i)
+    members_.emplace_back(new Solver(cfg, std::make_shared<GroupMemberTransport>(i, nranks), stream_));
+}
+
+LoopbackGroup::~LoopbackGroup() {
+  members_.clear();
+  if (stream_) {
+    (void)hipStreamSynchronize(stream_);
+    (void)hipStreamDestroy(stream_);
+  }
+}
+
+void LoopbackGroup::init(const kern::IcParams& ic, const double* xg, const double* yg) {
+  for (auto& m : members_) m->init(ic, xg, yg);
+}
+
+void LoopbackGroup::exchange_all() {
+  const int P = nranks();
+  if (P == 1) return;
+  const bool hip = cfg_.backend == (int32_t)Backend::Hip;
+  for (int i = 0; i < P; ++i) {
+    Solver& me = *members_[i];
+    const SlabLayout& L = me.layout();
+    const int64_t B = me.band();
+    const size_t es = dtype_size(me.dtype());
+    const size_t bytes = (size_t)(B * L.pitch) * es;
+    char* mine = static_cast<char*>(me.field());
+    auto rowp = [&](char* base, const SlabLayout& LL, int64_t r) { return base + (size_t)((r + LL.halo) * LL.pitch) * es; };
+    if (i > 0) {
+      Solver& lo = *members_[i - 1];
+      const SlabLayout& LL = lo.layout();
+      char* src = rowp(static_cast<char*>(lo.field()), LL, LL.nrows - B);
+      char* dst = rowp(mine, L, -B);
+      if (hip) H2D_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream_));
+      else std::memcpy(dst, src, bytes);
+    }
+    if (i < P - 1) {
+      Solver& hi = *members_[i + 1];
+      const SlabLayout& LH = hi.layout();
+      char* src = rowp(static_cast<char*>(hi.field()), LH, 0);
+      char* dst = rowp(mine, L, L.nrows);
+      if (hip) H2D_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream_));
+      else std::memcpy(dst, src, bytes);
+    }
+  }
+}
+
+void LoopbackGroup::step(int64_t n) {
+  const int K = members_[0]->config().tb;
+  while (n > 0) {
+    const int k = (int)std::min<int64_t>(K, n);
+    for (auto& m : members_) m->cycle_compute(k);
+    for (auto& m : members_) m->cycle_swap();
+    exchange_all();
+    n -= k;
+  }
+}
+
+void LoopbackGroup::synchronize() {
+  if (stream_) H2D_HIP(hipStreamSynchronize(stream_));
+}
+
+void LoopbackGroup::download(void* host, int64_t ld) {
+  const size_t es = dtype_size(members_[0]->dtype());
+  for (auto& m : members_) {
+    const SlabLayout& L = m->layout();
+    m->download(static_cast<char*>(host) + (size_t)(L.row0 * ld) * es, ld);
+  }
+}
+
+}  // namespace heat2d

@@ -1,0 +1,253 @@
+"""The heat-equation model: a distributed 2-D FTCS slab solver on the native engine.
+
+One :class:`HeatSolver` per rank (process or host thread). It owns a native
+``heat2d::Solver`` (csrc/runtime/solver.cpp) holding this rank's slab of the
+global grid in two pitched device (or host) fields, and a transport for the
+halo exchange. Everything in the time loop runs natively; Python only issues
+``step(n)``.
+
+Parity map (reference -> here):
+  * fortran/hip/heat.F90 setup()/heat_eqn()/swap()  -> HeatSolver(problem, backend="hip")
+  * fortran/mpi+cuda/heat.F90 (CUDA-aware / staged)  -> RCCL transport (device-direct)
+  * fortran/cuda_kernel/heat_managed.F90             -> managed=True
+  * fortran/serial/heat.f90                          -> backend="cpu"
+  * per-step D2D ``Td_old = Td`` (heat.F90:243)      -> copy_swap=True (parity mode)
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from ..ops import _native as N
+from ..parallel import transport as T
+from ..utils.config import Problem
+
+DTYPES = {"fp32": N.F32, "float32": N.F32, "fp64": N.F64, "float64": N.F64}
+NP_DTYPES = {N.F32: np.float32, N.F64: np.float64}
+
+
+def resolve_backend(backend: str) -> str:
+    if backend == "auto":
+        try:
+            import torch
+            return "hip" if torch.cuda.is_available() else "cpu"
+        except Exception:  # pragma: no cover
+            return "cpu"
+    if backend not in ("hip", "cpu"):
+        raise ValueError("backend must be hip|cpu|auto")
+    return backend
+
+
+class HeatSolver:
+    """Distributed FTCS solver for one rank.
+
+    Args:
+        problem: resolved :class:`~utils.config.Problem`.
+        dtype: "fp64" (reference precision) or "fp32".
+        backend: "hip", "cpu" or "auto".
+        tb: temporal-block depth K (time steps fused per HBM pass, 1..16).
+        overlap: boundary/interior split with the halo exchange on a comm stream.
+        copy_swap: reference-parity schedule (full field copy every step, K=1).
+        managed: allocate fields with hipMallocManaged.
+        graph: replay step pairs from a captured hipGraph (single-rank / serial schedule).
+        transport: a :class:`parallel.transport.Transport`; default picks self / RCCL / gloo.
+        device: HIP device ordinal (default: torch's current device).
+    """
+
+    def __init__(self, problem: Problem, *, dtype: str = "fp64", backend: str = "auto", tb: int = 8,
+                 overlap: bool = True, copy_swap: bool = False, managed: bool = False, graph: bool = False,
+                 tile_rows: int = 0, halo: int = 0, transport: Optional[T.Transport] = None,
+                 device: Optional[int] = None, init: bool = True):
+        self.problem = problem
+        self.backend = resolve_backend(backend)
+        self.dtype = DTYPES[dtype]
+        self.np_dtype = NP_DTYPES[self.dtype]
+        if self.backend == "hip" and device is None:
+            import torch
+            device = torch.cuda.current_device()
+        self.device = -1 if self.backend == "cpu" else int(device)
+        self.transport = transport or T.default_transport(self.backend, None if self.device < 0 else self.device)
+        cfg = N.Config()
+        cfg.n_rows = problem.n_owned
+        cfg.n_cols = problem.n_owned
+        cfg.dtype = self.dtype
+        cfg.backend = N.BACKEND_HIP if self.backend == "hip" else N.BACKEND_CPU
+        cfg.r = problem.r
+        cfg.tb = tb
+        cfg.overlap = int(overlap)
+        cfg.copy_swap = int(copy_swap)
+        cfg.managed = int(managed)
+        cfg.device = self.device
+        cfg.use_graph = int(graph)
+        cfg.tile_rows = tile_rows
+        cfg.halo = halo
+        self._cfg = cfg
+        h = C.c_void_p()
+        N.call("heat2d_solver_create", C.byref(cfg), self.transport.handle, C.byref(h))
+        self._h = h
+        self.layout = N.Layout()
+        N.call("heat2d_solver_layout", self._h, C.byref(self.layout))
+        if init:
+            self.init()
+
+    # ------------------------------------------------------------------ info
+    @property
+    def rank(self) -> int:
+        return self.transport.rank
+
+    @property
+    def size(self) -> int:
+        return self.transport.size
+
+    @property
+    def row0(self) -> int:
+        return int(self.layout.row0)
+
+    @property
+    def nrows(self) -> int:
+        return int(self.layout.nrows)
+
+    @property
+    def ncols(self) -> int:
+        return int(self.layout.ncols)
+
+    def info(self) -> dict:
+        tb, band, steps = C.c_int32(), C.c_int64(), C.c_int64()
+        field, stream = C.c_void_p(), C.c_void_p()
+        N.call("heat2d_solver_info", self._h, C.byref(tb), C.byref(band), C.byref(steps), C.byref(field),
+               C.byref(stream))
+        return {"tb": tb.value, "band": band.value, "steps": steps.value, "field": field.value,
+                "stream": stream.value, "backend": self.backend, "transport": self.transport.name,
+                "rank": self.rank, "size": self.size, "layout": self.layout.as_dict()}
+
+    @property
+    def tb(self) -> int:
+        return self.info()["tb"]
+
+    @property
+    def steps_done(self) -> int:
+        return self.info()["steps"]
+
+    # ------------------------------------------------------------------ ops
+    def init(self) -> None:
+        x = np.ascontiguousarray(self.problem.x, dtype=np.float64)
+        ic = self.problem.ic.to_native()
+        N.call("heat2d_solver_init", self._h, C.byref(ic), x.ctypes.data_as(C.c_void_p),
+               x.ctypes.data_as(C.c_void_p))
+
+    def step(self, n: int = 1) -> None:
+        """Advance n time steps (asynchronous on the GPU)."""
+        N.call("heat2d_solver_step", self._h, int(n))
+
+    def run(self, ntime: Optional[int] = None) -> None:
+        self.step(self.problem.ntime if ntime is None else ntime)
+
+    def synchronize(self) -> None:
+        N.call("heat2d_solver_sync", self._h)
+
+    def stats(self, residual: bool = False) -> dict:
+        """Global (all-rank) statistics of the current field."""
+        out = (C.c_double * 6)()
+        N.call("heat2d_solver_stats", self._h, out, int(residual))
+        s = list(out)
+        d = {"sum": s[0], "sum_sq": s[1], "min": s[2], "max": s[3]}
+        if residual:
+            d["residual_l2"] = float(np.sqrt(s[4]))
+            d["residual_max"] = s[5]
+        return d
+
+    def download(self) -> np.ndarray:
+        """This rank's owned rows (nrows x ncols) as a host array."""
+        out = np.empty((self.nrows, self.ncols), dtype=self.np_dtype)
+        N.call("heat2d_solver_download", self._h, out.ctypes.data_as(C.c_void_p), self.ncols)
+        return out
+
+    def upload(self, arr: np.ndarray) -> None:
+        """Set this rank's owned rows (collective: followed by a halo exchange)."""
+        a = np.ascontiguousarray(arr, dtype=self.np_dtype)
+        if a.shape != (self.nrows, self.ncols):
+            raise ValueError(f"expected {(self.nrows, self.ncols)}, got {a.shape}")
+        N.call("heat2d_solver_upload", self._h, a.ctypes.data_as(C.c_void_p), self.ncols)
+
+    def gather(self) -> Optional[np.ndarray]:
+        """Whole owned grid on rank 0 (None elsewhere). Uses torch.distributed when size > 1."""
+        local = self.download()
+        if self.size == 1:
+            return local
+        import torch
+        import torch.distributed as dist
+        parts = [None] * self.size if self.rank == 0 else None
+        dist.gather_object(local, parts, dst=0)
+        return np.concatenate(parts, axis=0) if self.rank == 0 else None
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            N.call("heat2d_solver_free", self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class LoopbackGroup:
+    """P slabs of one domain on a single device (or host), halos moved by copies.
+
+    The decomposition / band-split / exchange schedule of the distributed solver
+    proven without a cluster: results must be bitwise identical to P = 1.
+    """
+
+    def __init__(self, problem: Problem, nranks: int, *, dtype: str = "fp64", backend: str = "auto",
+                 tb: int = 8, tile_rows: int = 0, device: Optional[int] = None):
+        self.problem = problem
+        self.backend = resolve_backend(backend)
+        self.dtype = DTYPES[dtype]
+        if self.backend == "hip" and device is None:
+            import torch
+            device = torch.cuda.current_device()
+        cfg = N.Config()
+        cfg.n_rows = problem.n_owned
+        cfg.n_cols = problem.n_owned
+        cfg.dtype = self.dtype
+        cfg.backend = N.BACKEND_HIP if self.backend == "hip" else N.BACKEND_CPU
+        cfg.r = problem.r
+        cfg.tb = tb
+        cfg.device = -1 if device is None else int(device)
+        cfg.tile_rows = tile_rows
+        h = C.c_void_p()
+        N.call("heat2d_group_create", C.byref(cfg), nranks, C.byref(h))
+        self._h = h
+        x = np.ascontiguousarray(problem.x, dtype=np.float64)
+        ic = problem.ic.to_native()
+        N.call("heat2d_group_init", self._h, C.byref(ic), x.ctypes.data_as(C.c_void_p),
+               x.ctypes.data_as(C.c_void_p))
+
+    def step(self, n: int) -> None:
+        N.call("heat2d_group_step", self._h, int(n))
+
+    def download(self) -> np.ndarray:
+        m = self.problem.n_owned
+        out = np.empty((m, m), dtype=NP_DTYPES[self.dtype])
+        N.call("heat2d_group_download", self._h, out.ctypes.data_as(C.c_void_p), m)
+        return out
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            N.call("heat2d_group_free", self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass

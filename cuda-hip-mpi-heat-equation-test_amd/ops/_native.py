@@ -1,0 +1,218 @@
+"""ctypes binding of the native engine ``_native/libheat2d.so`` (C ABI:
+``csrc/include/heat2d/capi.h``).
+
+The library carries the gfx950 HIP kernels, the CPU twin kernels, the slab
+solver runtime and the RCCL / callback transports. It is built in-tree
+(``make -C csrc``, or :func:`build`) so that it travels with the repository
+snapshot to the GPU box. Loading it is mandatory for every compute path: there
+is no silent Python fallback — :func:`lib` raises if the library is missing.
+
+``import torch`` happens before the library is loaded so that the HIP runtime
+and RCCL already mapped by PyTorch (same SONAMEs: libamdhip64.so.7,
+librccl.so.1) are the ones the engine binds to.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import threading
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE_DIR = os.path.join(_PKG_DIR, "_native")
+CSRC_DIR = os.path.join(_PKG_DIR, "csrc")
+LIB_PATH = os.path.join(NATIVE_DIR, "libheat2d.so")
+CLI_PATH = os.path.join(NATIVE_DIR, "heat2d")
+
+F32, F64 = 0, 1
+BACKEND_HIP, BACKEND_CPU = 0, 1
+
+
+class Layout(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("nrows", "ncols", "halo", "cpad", "pitch", "row0", "nrows_global")]
+
+    def rows_alloc(self) -> int:
+        return self.nrows + 2 * self.halo
+
+    def elems(self) -> int:
+        return self.rows_alloc() * self.pitch
+
+    def offset(self, i: int, j: int) -> int:
+        return (i + self.halo) * self.pitch + (j + self.cpad)
+
+    def as_dict(self) -> dict:
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class IcParams(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("a", C.c_double), ("b", C.c_double),
+        ("x0", C.c_double), ("x1", C.c_double), ("y0", C.c_double), ("y1", C.c_double),
+        ("i0", C.c_int64), ("i1", C.c_int64), ("j0", C.c_int64), ("j1", C.c_int64),
+        ("kx", C.c_double), ("ky", C.c_double),
+        ("pad", C.c_double),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("n_rows", C.c_int64), ("n_cols", C.c_int64),
+        ("dtype", C.c_int32), ("backend", C.c_int32),
+        ("r", C.c_double),
+        ("tb", C.c_int32), ("overlap", C.c_int32), ("copy_swap", C.c_int32), ("managed", C.c_int32),
+        ("device", C.c_int32), ("use_graph", C.c_int32),
+        ("tile_rows", C.c_int64), ("halo", C.c_int64),
+    ]
+
+
+class TbPlan(C.Structure):
+    _fields_ = [
+        ("k", C.c_int32), ("vec", C.c_int32), ("strip_w", C.c_int32), ("useful_w", C.c_int32),
+        ("tile_rows", C.c_int64), ("nstrips", C.c_int64), ("ntiles", C.c_int64),
+        ("nwaves", C.c_int64), ("nblocks", C.c_int64),
+    ]
+
+
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                          C.c_int64, C.c_int32)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int32, C.c_int32)
+BARRIER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p)
+
+_P = C.c_void_p
+_I64 = C.c_int64
+_LP = C.POINTER(Layout)
+_SIGS = {
+    "heat2d_last_error": (C.c_char_p, []),
+    "heat2d_version": (C.c_int, []),
+    "heat2d_max_tb": (C.c_int, []),
+    "heat2d_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "heat2d_make_layout": (C.c_int, [_I64, _I64, _I64, _I64, _I64, _LP]),
+    "heat2d_decompose": (C.c_int, [_I64, C.c_int, C.c_int, C.POINTER(_I64), C.POINTER(_I64)]),
+    "heat2d_plan_tb": (C.c_int, [C.c_int, _LP, _I64, _I64, C.c_int, _I64, C.POINTER(TbPlan)]),
+    "heat2d_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double, _P, _I64]),
+    "heat2d_init_field": (C.c_int, [C.c_int, _P, _LP, C.POINTER(IcParams), _P, _P, _P]),
+    "heat2d_stats": (C.c_int, [C.c_int, _P, _P, _LP, _P, _P, _P]),
+    "heat2d_stats_work_elems": (_I64, []),
+    "heat2d_pack_rows": (C.c_int, [C.c_int, _P, _LP, _I64, _I64, _P, _P]),
+    "heat2d_unpack_rows": (C.c_int, [C.c_int, _P, _LP, _I64, _I64, _P, _P]),
+    "heat2d_cpu_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double]),
+    "heat2d_cpu_init_field": (C.c_int, [C.c_int, _P, _LP, C.POINTER(IcParams), _P, _P]),
+    "heat2d_cpu_stats": (C.c_int, [C.c_int, _P, _P, _LP, _P]),
+    "heat2d_rccl_unique_id": (C.c_int, [_P]),
+    "heat2d_transport_self": (C.c_int, [C.POINTER(_P)]),
+    "heat2d_transport_rccl": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
+    "heat2d_transport_callback": (C.c_int, [EXCHANGE_FN, ALLREDUCE_FN, BARRIER_FN, _P, C.c_int, C.c_int,
+                                            C.POINTER(_P)]),
+    "heat2d_transport_free": (C.c_int, [_P]),
+    "heat2d_solver_create": (C.c_int, [C.POINTER(Config), _P, C.POINTER(_P)]),
+    "heat2d_solver_free": (C.c_int, [_P]),
+    "heat2d_solver_init": (C.c_int, [_P, C.POINTER(IcParams), _P, _P]),
+    "heat2d_solver_step": (C.c_int, [_P, _I64]),
+    "heat2d_solver_sync": (C.c_int, [_P]),
+    "heat2d_solver_stats": (C.c_int, [_P, _P, C.c_int]),
+    "heat2d_solver_download": (C.c_int, [_P, _P, _I64]),
+    "heat2d_solver_upload": (C.c_int, [_P, _P, _I64]),
+    "heat2d_solver_layout": (C.c_int, [_P, _LP]),
+    "heat2d_solver_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(_I64), C.POINTER(_I64),
+                                     C.POINTER(_P), C.POINTER(_P)]),
+    "heat2d_group_create": (C.c_int, [C.POINTER(Config), C.c_int, C.POINTER(_P)]),
+    "heat2d_group_free": (C.c_int, [_P]),
+    "heat2d_group_init": (C.c_int, [_P, C.POINTER(IcParams), _P, _P]),
+    "heat2d_group_step": (C.c_int, [_P, _I64]),
+    "heat2d_group_download": (C.c_int, [_P, _P, _I64]),
+    "heat2d_write_xyz": (C.c_int, [C.c_char_p, C.c_int, _P, _I64, _I64, _I64, _P, _P, C.c_int]),
+    "heat2d_write_npy": (C.c_int, [C.c_char_p, C.c_int, _P, _I64, _I64, _I64]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    """An error reported by the native engine."""
+
+
+def build(jobs: int = 8, quiet: bool = True) -> None:
+    """Compile the engine in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+    cmd = ["make", "-C", CSRC_DIR, f"-j{jobs}"]
+    out = subprocess.run(cmd, capture_output=True, text=True)
+    if out.returncode != 0:
+        raise NativeError(f"native build failed:\n{out.stdout[-4000:]}\n{out.stderr[-4000:]}")
+    if not quiet:
+        print(out.stdout)
+
+
+def available() -> bool:
+    return os.path.exists(LIB_PATH)
+
+
+def lib():
+    """Load (once) and return the native library. Raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  (map torch's HIP runtime / RCCL first: shared SONAMEs)
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"native engine not built: {LIB_PATH} missing. Run `make -C {CSRC_DIR}` "
+                "or `python -c 'import __graft_entry__ as g; g.build()'`.")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+        return _lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise NativeError(lib().heat2d_last_error().decode(errors="replace"))
+
+
+def call(name: str, *args):
+    """Call a native function returning an int status; raise NativeError on failure."""
+    check(getattr(lib(), name)(*args))
+
+
+def make_layout(nrows: int, ncols: int, halo: int, row0: int = 0, nrows_global: int | None = None) -> Layout:
+    out = Layout()
+    call("heat2d_make_layout", nrows, ncols, halo, row0, nrows if nrows_global is None else nrows_global,
+         C.byref(out))
+    return out
+
+
+def decompose(n: int, nranks: int, rank: int) -> tuple[int, int]:
+    r0, nr = C.c_int64(), C.c_int64()
+    call("heat2d_decompose", n, nranks, rank, C.byref(r0), C.byref(nr))
+    return r0.value, nr.value
+
+
+def plan_tb(dtype: int, layout: Layout, rb: int, re: int, k: int, tile_rows: int = 0) -> TbPlan:
+    out = TbPlan()
+    call("heat2d_plan_tb", dtype, C.byref(layout), rb, re, k, tile_rows, C.byref(out))
+    return out
+
+
+def max_tb() -> int:
+    return int(lib().heat2d_max_tb())
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    call("heat2d_device_count", C.byref(n))
+    return n.value
+
+
+def rccl_unique_id() -> bytes:
+    buf = (C.c_ubyte * 128)()
+    call("heat2d_rccl_unique_id", buf)
+    return bytes(buf)
+
+
+def loaded_path() -> str:
+    return LIB_PATH

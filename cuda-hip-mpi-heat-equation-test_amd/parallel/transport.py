@@ -1,0 +1,194 @@
+"""Halo-exchange transports for the native slab solver.
+
+Reference: two blocking ``MPI_Sendrecv`` per step over host-staged (or
+CUDA-aware) buffers (fortran/hip/heat.F90:196-230, fortran/mpi+cuda/heat.F90:143-195).
+Here a transport is a native object the solver calls once per cycle:
+
+* :class:`SelfTransport`  — one rank, no exchange.
+* :class:`RcclTransport`  — RCCL over xGMI, zero-copy rows, grouped send/recv on the
+  solver's comm stream (device-direct; the production path, one process or one
+  host thread per GPU). The 128-byte ``ncclUniqueId`` is created by rank 0 and
+  broadcast through ``torch.distributed`` (any backend) or passed explicitly.
+* :class:`TorchDistTransport` — host callbacks over ``torch.distributed`` point-to-point
+  (gloo on CPU): runs the *same native schedule* in CPU-only multi-process CI.
+* :class:`CallbackTransport` — any Python callables (tests, custom fabrics).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import traceback
+from typing import Callable, Optional
+
+import numpy as np
+
+from ..ops import _native as N
+
+
+class Transport:
+    """Owns a native transport handle."""
+
+    def __init__(self, handle, rank: int, size: int, name: str):
+        self._h = handle
+        self.rank = rank
+        self.size = size
+        self.name = name
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self) -> None:
+        if self._h:
+            N.call("heat2d_transport_free", self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SelfTransport(Transport):
+    def __init__(self):
+        h = C.c_void_p()
+        N.call("heat2d_transport_self", C.byref(h))
+        super().__init__(h, 0, 1, "self")
+
+
+class RcclTransport(Transport):
+    """RCCL communicator created from an ncclUniqueId (collective over all ranks)."""
+
+    def __init__(self, rank: int, size: int, device: int, uid: Optional[bytes] = None, group=None):
+        if uid is None:
+            uid = broadcast_unique_id(rank, group)
+        buf = (C.c_ubyte * 128).from_buffer_copy(uid)
+        h = C.c_void_p()
+        N.call("heat2d_transport_rccl", buf, rank, size, device, C.byref(h))
+        super().__init__(h, rank, size, "rccl")
+
+
+def broadcast_unique_id(rank: int, group=None) -> bytes:
+    """Rank 0 creates the RCCL unique id; everyone receives it via torch.distributed."""
+    import torch
+    import torch.distributed as dist
+    t = torch.zeros(128, dtype=torch.uint8)
+    if rank == 0:
+        t.copy_(torch.frombuffer(bytearray(N.rccl_unique_id()), dtype=torch.uint8))
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+        td = t.to(dev)
+        dist.broadcast(td, src=0, group=group)
+        t = td.cpu()
+    else:
+        dist.broadcast(t, src=0, group=group)
+    return bytes(t.numpy().tobytes())
+
+
+_NP_DTYPES = {N.F32: np.float32, N.F64: np.float64}
+
+
+class CallbackTransport(Transport):
+    """Transport driven by Python callables on host buffers.
+
+    exchange(send_lo, send_hi, recv_lo, recv_hi) receives numpy arrays (or None at the
+    domain ends) of ``k*ncols`` elements; allreduce(vals, op) gets a float64 numpy array
+    to reduce in place (op 0 sum, 1 max, 2 min); barrier() blocks.
+    """
+
+    def __init__(self, rank: int, size: int, exchange: Callable, allreduce: Callable, barrier: Callable,
+                 name: str = "callback"):
+        self._py = (exchange, allreduce, barrier)
+
+        def _arr(ptr, count, dtype):
+            if not ptr:
+                return None
+            ct = C.c_float if dtype == N.F32 else C.c_double
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(count,))
+
+        def ex(ctx, s_lo, s_hi, r_lo, r_hi, count, dtype):
+            try:
+                exchange(_arr(s_lo, count, dtype), _arr(s_hi, count, dtype), _arr(r_lo, count, dtype),
+                         _arr(r_hi, count, dtype))
+                return 0
+            except Exception:
+                traceback.print_exc()
+                return 1
+
+        def ar(ctx, vals, n, op):
+            try:
+                allreduce(np.ctypeslib.as_array(vals, shape=(n,)), int(op))
+                return 0
+            except Exception:
+                traceback.print_exc()
+                return 1
+
+        def br(ctx):
+            try:
+                barrier()
+                return 0
+            except Exception:
+                traceback.print_exc()
+                return 1
+
+        # keep the CFUNCTYPE objects alive as long as the native transport exists
+        self._cbs = (N.EXCHANGE_FN(ex), N.ALLREDUCE_FN(ar), N.BARRIER_FN(br))
+        h = C.c_void_p()
+        N.call("heat2d_transport_callback", self._cbs[0], self._cbs[1], self._cbs[2], None, rank, size,
+               C.byref(h))
+        super().__init__(h, rank, size, name)
+
+
+class TorchDistTransport(CallbackTransport):
+    """Host-side halo exchange over torch.distributed point-to-point (gloo)."""
+
+    TAG_DOWN, TAG_UP = 11, 12
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        rank, size = dist.get_rank(group), dist.get_world_size(group)
+        self._group = group
+
+        def exchange(s_lo, s_hi, r_lo, r_hi):
+            ops = []
+            if s_lo is not None:  # my first rows -> rank-1 (its high ghost rows)
+                ops.append(dist.P2POp(dist.isend, torch.from_numpy(s_lo), rank - 1, group, self.TAG_DOWN))
+            if r_hi is not None:
+                ops.append(dist.P2POp(dist.irecv, torch.from_numpy(r_hi), rank + 1, group, self.TAG_DOWN))
+            if s_hi is not None:  # my last rows -> rank+1 (its low ghost rows)
+                ops.append(dist.P2POp(dist.isend, torch.from_numpy(s_hi), rank + 1, group, self.TAG_UP))
+            if r_lo is not None:
+                ops.append(dist.P2POp(dist.irecv, torch.from_numpy(r_lo), rank - 1, group, self.TAG_UP))
+            if ops:
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+
+        def allreduce(vals, op):
+            t = torch.from_numpy(vals)
+            rop = {0: dist.ReduceOp.SUM, 1: dist.ReduceOp.MAX, 2: dist.ReduceOp.MIN}[op]
+            dist.all_reduce(t, op=rop, group=group)
+
+        def barrier():
+            dist.barrier(group=group)
+
+        super().__init__(rank, size, exchange, allreduce, barrier, name="torch-dist")
+
+
+def default_transport(backend: str, device: Optional[int] = None) -> Transport:
+    """Pick the transport for the current process: self if not distributed, RCCL for
+    device fields, torch.distributed host callbacks for CPU fields."""
+    try:
+        import torch.distributed as dist
+        distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    except Exception:  # pragma: no cover
+        distributed = False
+    if not distributed:
+        return SelfTransport()
+    import torch.distributed as dist
+    rank, size = dist.get_rank(), dist.get_world_size()
+    if backend == "hip":
+        import torch
+        dev = torch.cuda.current_device() if device is None else device
+        return RcclTransport(rank, size, dev)
+    return TorchDistTransport()

@@ -1,0 +1,110 @@
+"""GPU numerics: the native HIP engine against the NumPy golden (fp64 reference
+order, bitwise) on a real MI355X. Every test runs the HIP kernels through
+_native/libheat2d.so — there is no fallback path."""
+import numpy as np
+import pytest
+
+import heat2d
+from heat2d.models import reference as R
+from heat2d.models.heat2d import HeatSolver, LoopbackGroup
+
+pytestmark = pytest.mark.gpu
+
+
+def prob(n, steps, conv="ghost", ic="uniform", dom=1.0):
+    return heat2d.make_problem(heat2d.InputDat(n=n, sigma=0.25, nu=0.05, dom_len=dom, ntime=steps), conv, ic)
+
+
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("tb", [1, 2, 3, 5, 8, 13, 16])
+def test_hip_matches_golden_bitwise(gpu, native, dtype, tb):
+    p = prob(203, 37, "inclusive", "hat", dom=2.0)  # odd size: partial strips / lanes
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0)
+    s.step(p.ntime)
+    got = s.download()
+    ref = R.owned(R.ftcs(p, dtype=npdt))
+    assert got.dtype == npdt
+    assert np.array_equal(got, ref), np.abs(got.astype(np.float64) - ref).max()
+    s.close()
+
+
+@pytest.mark.parametrize("n", [3, 17, 64, 130, 257, 1000])
+def test_hip_sizes(gpu, native, n):
+    p = prob(n, 21, "ghost", "uniform")
+    s = HeatSolver(p, dtype="fp64", backend="hip", tb=8, device=0)
+    s.step(p.ntime)
+    assert np.array_equal(s.download(), R.owned(R.ftcs(p)))
+    s.close()
+
+
+@pytest.mark.parametrize("tile_rows", [1, 7, 64, 512])
+def test_hip_tile_rows(gpu, native, tile_rows):
+    p = prob(300, 19, "inclusive", "hat-cuda", dom=2.0)
+    s = HeatSolver(p, dtype="fp64", backend="hip", tb=6, tile_rows=tile_rows, device=0)
+    s.step(p.ntime)
+    assert np.array_equal(s.download(), R.owned(R.ftcs(p)))
+    s.close()
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("tb", [1, 4, 8])
+def test_loopback_group_bitwise(gpu, native, P, tb):
+    """P slabs on one GPU with device-copy halo exchange == the single-slab run."""
+    p = prob(161, 29, "ghost", "uniform")
+    g = LoopbackGroup(p, P, dtype="fp64", backend="hip", tb=tb, device=0)
+    g.step(p.ntime)
+    got = g.download()
+    assert np.array_equal(got, R.owned(R.ftcs(p)))
+    g.close()
+
+
+def test_copy_swap_and_managed(gpu, native):
+    p = prob(150, 11, "inclusive", "hat", dom=2.0)
+    ref = R.owned(R.ftcs(p))
+    for kw in (dict(copy_swap=True), dict(managed=True), dict(graph=True, tb=4)):
+        s = HeatSolver(p, dtype="fp64", backend="hip", device=0, **kw)
+        s.step(p.ntime)
+        assert np.array_equal(s.download(), ref), kw
+        s.close()
+
+
+def test_graph_replay_many(gpu, native):
+    p = prob(512, 200, "ghost", "uniform")
+    s = HeatSolver(p, dtype="fp64", backend="hip", tb=8, graph=True, device=0)
+    s.step(123)
+    s.step(77)
+    assert np.array_equal(s.download(), R.owned(R.ftcs(p)))
+    s.close()
+
+
+def test_stats_and_residual(gpu, native):
+    p = prob(300, 10, "ghost", "uniform")
+    s = HeatSolver(p, dtype="fp64", backend="hip", tb=1, device=0)
+    s.step(10)
+    st = s.stats(residual=True)
+    T = R.ftcs(p)
+    T9 = R.ftcs(p, 9)
+    assert np.isclose(st["sum"], R.owned(T).sum(), rtol=1e-13)
+    assert st["min"] == R.owned(T).min() and st["max"] == R.owned(T).max()
+    d = R.owned(T) - R.owned(T9)
+    assert np.isclose(st["residual_l2"], np.sqrt((d * d).sum()), rtol=1e-10)
+    s.close()
+
+
+def test_eigenmode_gpu(gpu, native):
+    p = prob(129, 200, "inclusive", "sine")
+    s = HeatSolver(p, dtype="fp64", backend="hip", tb=8, device=0)
+    s.step(p.ntime)
+    exact = R.owned(R.eigenmode(p, p.ntime))
+    assert np.abs(s.download() - exact).max() < 1e-12
+    s.close()
+
+
+def test_upload_roundtrip(gpu, native):
+    p = prob(100, 5, "ghost", "uniform")
+    s = HeatSolver(p, dtype="fp64", backend="hip", tb=4, device=0)
+    a = np.random.default_rng(0).random((100, 100))
+    s.upload(a)
+    assert np.array_equal(s.download(), a)
+    s.close()
