@@ -112,6 +112,14 @@ int heat2d_stats(int dtype, const void* field, const void* other, const heat2d_l
 
 int64_t heat2d_stats_work_elems(void) { return kern::stats_work_elems(); }
 
+int heat2d_copy(void* dst, const void* src, int64_t bytes, void* stream, int blocks) {
+  return guarded([&] { kern::launch_copy(dst, src, bytes, as_stream(stream), blocks); });
+}
+
+int heat2d_read(const void* src, int64_t bytes, void* sink, void* stream, int blocks) {
+  return guarded([&] { kern::launch_read(src, bytes, static_cast<unsigned*>(sink), as_stream(stream), blocks); });
+}
+
 int heat2d_pack_rows(int dtype, const void* field, const heat2d_layout* L, int64_t row, int64_t nrows,
                      void* buf, void* stream) {
   return guarded([&] { kern::launch_pack_rows((DType)dtype, field, to_layout(L), row, nrows, buf, as_stream(stream)); });

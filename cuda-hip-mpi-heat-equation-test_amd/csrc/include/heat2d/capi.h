@@ -36,6 +36,7 @@ typedef struct heat2d_config {
 typedef struct heat2d_tb_plan {
   int32_t k, vec, strip_w, useful_w;
   int64_t tile_rows, nstrips, ntiles, nwaves, nblocks;
+  int32_t skew, blocks_per_cu;
 } heat2d_tb_plan;
 
 typedef int (*heat2d_exchange_fn)(void* ctx, void* send_lo, void* send_hi, void* recv_lo,
@@ -63,6 +64,8 @@ int heat2d_init_field(int dtype, void* field, const heat2d_layout* L, const heat
 int heat2d_stats(int dtype, const void* field, const void* other, const heat2d_layout* L,
                  double* work_dev, double* out_dev, void* stream);
 int64_t heat2d_stats_work_elems(void);
+int heat2d_copy(void* dst, const void* src, int64_t bytes, void* stream, int blocks);
+int heat2d_read(const void* src, int64_t bytes, void* sink, void* stream, int blocks);
 int heat2d_pack_rows(int dtype, const void* field, const heat2d_layout* L, int64_t row,
                      int64_t nrows, void* buf, void* stream);
 int heat2d_unpack_rows(int dtype, void* field, const heat2d_layout* L, int64_t row,

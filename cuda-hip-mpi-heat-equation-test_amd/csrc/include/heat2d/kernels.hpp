@@ -21,6 +21,8 @@ struct TbPlan {
   int64_t ntiles;
   int64_t nwaves;
   int64_t nblocks;    // 256-thread workgroups (4 independent waves each)
+  int32_t skew;       // level pipeline skew (1 or 2)
+  int32_t blocks_per_cu;  // resident workgroups per CU (occupancy API)
 };
 
 // Plan a launch that advances rows [row_begin, row_end) of the slab by k steps.
@@ -67,6 +69,10 @@ void launch_init(DType dt, void* field, const SlabLayout& L, const IcParams& ic,
 int64_t stats_work_elems();
 void launch_stats(DType dt, const void* field, const void* other, const SlabLayout& L,
                   double* work, double* out, hipStream_t stream);
+
+// Vectorised streaming copy / read (bandwidth roof probes; copy-swap mode).
+void launch_copy(void* dst, const void* src, int64_t bytes, hipStream_t stream, int blocks = 0);
+void launch_read(const void* src, int64_t bytes, unsigned* sink, hipStream_t stream, int blocks = 0);
 
 // Pack/unpack `nrows` rows starting at local row `row` into / from a
 // contiguous buffer of nrows*ncols elements (the owned columns only). Used for

@@ -164,6 +164,34 @@ __global__ __launch_bounds__(256) void unpack_rows_kernel(T* __restrict__ f, Sla
   }
 }
 
+// Streaming copy, 16 B per lane per access, 4 accesses in flight per lane,
+// grid-stride. Used by the copy-swap parity mode (the reference's per-step
+// `Td_old = Td`) and as the measured bandwidth roof (bench/bw_probe.py).
+__global__ __launch_bounds__(256) void copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                     int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void read16_kernel(const uint4* __restrict__ src, int64_t n16,
+                                                     unsigned* __restrict__ sink) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+    const uint4 a = src[i];
+    acc ^= a.x ^ a.y ^ a.z ^ a.w;
+  }
+  if (acc == 0x9e3779b9u) sink[0] = acc;  // keep the loads alive
+}
+
 inline unsigned grid_for(int64_t n) {
   int64_t b = (n + 255) / 256;
   if (b > 8192) b = 8192;  // grid-stride beyond 8 blocks per CU
@@ -201,6 +229,22 @@ void launch_stats(DType dt, const void* field, const void* other, const SlabLayo
   check_launch("stats_pass1");
   hipLaunchKernelGGL(stats_pass2, dim3(1), dim3(kStatsThreads), 0, stream, work, out);
   check_launch("stats_pass2");
+}
+
+void launch_copy(void* dst, const void* src, int64_t bytes, hipStream_t stream, int blocks) {
+  HEAT2D_REQUIRE(bytes % 16 == 0, "copy size must be a multiple of 16 bytes");
+  const int64_t n16 = bytes / 16;
+  unsigned g = blocks > 0 ? (unsigned)blocks : 256u * 8u;
+  hipLaunchKernelGGL(copy16_kernel, dim3(g), dim3(256), 0, stream, static_cast<const uint4*>(src),
+                     static_cast<uint4*>(dst), n16);
+  check_launch("copy16_kernel");
+}
+
+void launch_read(const void* src, int64_t bytes, unsigned* sink, hipStream_t stream, int blocks) {
+  const int64_t n16 = bytes / 16;
+  unsigned g = blocks > 0 ? (unsigned)blocks : 256u * 8u;
+  hipLaunchKernelGGL(read16_kernel, dim3(g), dim3(256), 0, stream, static_cast<const uint4*>(src), n16, sink);
+  check_launch("read16_kernel");
 }
 
 void launch_pack_rows(DType dt, const void* field, const SlabLayout& L, int64_t row, int64_t nrows,

@@ -178,7 +178,7 @@ void Solver::cycle_copy_swap() {
   void* cur = buf_[cur_];
   void* old = buf_[cur_ ^ 1];
   const size_t bytes = (size_t)L_.elems() * dtype_size(dtype());
-  if (hip_) H2D_HIP(hipMemcpyAsync(old, cur, bytes, hipMemcpyDeviceToDevice, s_compute_));
+  if (hip_) kern::launch_copy(old, cur, (int64_t)bytes, s_compute_);
   else std::memcpy(old, cur, bytes);
   launch_tb(old, cur, 0, L_.nrows, 1);
   exchange_on(cur, s_compute_);

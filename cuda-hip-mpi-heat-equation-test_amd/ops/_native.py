@@ -71,6 +71,7 @@ class TbPlan(C.Structure):
         ("k", C.c_int32), ("vec", C.c_int32), ("strip_w", C.c_int32), ("useful_w", C.c_int32),
         ("tile_rows", C.c_int64), ("nstrips", C.c_int64), ("ntiles", C.c_int64),
         ("nwaves", C.c_int64), ("nblocks", C.c_int64),
+        ("skew", C.c_int32), ("blocks_per_cu", C.c_int32),
     ]
 
 
@@ -94,6 +95,8 @@ _SIGS = {
     "heat2d_init_field": (C.c_int, [C.c_int, _P, _LP, C.POINTER(IcParams), _P, _P, _P]),
     "heat2d_stats": (C.c_int, [C.c_int, _P, _P, _LP, _P, _P, _P]),
     "heat2d_stats_work_elems": (_I64, []),
+    "heat2d_copy": (C.c_int, [_P, _P, _I64, _P, C.c_int]),
+    "heat2d_read": (C.c_int, [_P, _I64, _P, _P, C.c_int]),
     "heat2d_pack_rows": (C.c_int, [C.c_int, _P, _LP, _I64, _I64, _P, _P]),
     "heat2d_unpack_rows": (C.c_int, [C.c_int, _P, _LP, _I64, _I64, _P, _P]),
     "heat2d_cpu_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double]),
