@@ -31,6 +31,7 @@ typedef struct heat2d_config {
   double r;
   int32_t tb, overlap, copy_swap, managed, device, use_graph;
   int64_t tile_rows, halo;
+  int32_t comm_cus, reserved_;
 } heat2d_config;
 
 typedef struct heat2d_tb_plan {

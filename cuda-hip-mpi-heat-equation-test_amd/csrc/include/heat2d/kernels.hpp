@@ -26,16 +26,17 @@ struct TbPlan {
 };
 
 // Plan a launch that advances rows [row_begin, row_end) of the slab by k steps.
-// tile_rows <= 0 selects the occupancy-driven default.
+// tile_rows <= 0 selects the occupancy-driven default; cus > 0 plans for a
+// stream restricted to that many CUs (comm-reserving CU mask).
 TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k,
-               int64_t tile_rows = 0);
+               int64_t tile_rows = 0, int cus = 0);
 
 // dst(rows [row_begin,row_end)) = k FTCS steps of src. `src`/`dst` are
 // allocation bases laid out per `L`. Requires k <= L.halo and the k ghost rows
 // on both sides of the range to hold valid data at time t (Dirichlet rows are
 // recognised from L.row0 / L.nrows_global and kept fixed).
 void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin,
-               int64_t row_end, int k, double r, hipStream_t stream, int64_t tile_rows = 0);
+               int64_t row_end, int k, double r, hipStream_t stream, int64_t tile_rows = 0, int cus = 0);
 
 // Initial / boundary condition kinds (covers every IC of the reference
 // variants, see models/presets.py for the mapping).

@@ -40,6 +40,8 @@ struct SolverConfig {
   int32_t use_graph;   // 1: replay cycles from a captured hipGraph
   int64_t tile_rows;   // 0: auto
   int64_t halo;        // 0: auto (= kMaxTB)
+  int32_t comm_cus;    // P>1 overlap: CUs kept free of the compute stream for RCCL (0: default 8, -1: none)
+  int32_t reserved_;
 };
 
 // ---------------------------------------------------------------- transports
@@ -158,6 +160,7 @@ class Solver {
   hipEvent_t ev_bnd_ = nullptr, ev_comm_ = nullptr;
   double* d_work_ = nullptr;   // stats workspace + 6 results
   bool timing_ = false;
+  int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all
   hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K
   int graph_k_ = 0;
   std::vector<char> host_stage_;  // CPU-backend / callback staging

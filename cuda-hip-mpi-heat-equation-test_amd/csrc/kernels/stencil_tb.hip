@@ -65,8 +65,11 @@ int useful_width(int k) {
 int default_nv(DType dt, int k) {
   const char* env = std::getenv("HEAT2D_TB_NV");  // read per plan: tunable at run time
   (void)dt;
-  if (env && std::atoi(env) == 2 && k <= 8) return 2;
-  return 1;
+  if (env) return (std::atoi(env) == 2 && k <= 8) ? 2 : 1;
+  // measured on MI355X (bench/sweep.py, 32768^2): 32 B/lane wins for fp64 while
+  // the kernel is still bandwidth-bound (k <= 6); beyond that the register
+  // state costs more occupancy than the halved halo redundancy returns
+  return (dt == DType::F64 && k <= 6) ? 2 : 1;
 }
 
 // Level pipeline skew (1: levels chained within a row iteration; 2: levels
@@ -74,8 +77,9 @@ int default_nv(DType dt, int k) {
 int default_skew(DType dt, int k) {
   const char* env = std::getenv("HEAT2D_TB_SKEW");
   (void)dt;
+  (void)k;
   if (env) return std::atoi(env) == 2 ? 2 : 1;
-  return k >= 2 ? 2 : 1;
+  return 1;  // skew-2's extra row of state per level costs more occupancy than its ILP returns (measured)
 }
 
 template <typename T>
@@ -98,7 +102,8 @@ void dispatch_variant(int nv, int sk, int k, unsigned nblocks, const T* s, T* d,
 
 }  // namespace
 
-TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k, int64_t tile_rows) {
+TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k, int64_t tile_rows,
+               int cus) {
   HEAT2D_REQUIRE(k >= 1 && k <= kMaxTB, "k must be in [1, kMaxTB]");
   HEAT2D_REQUIRE(row_begin >= 0 && row_end <= L.nrows && row_begin < row_end, "bad row range");
   TbPlan p{};
@@ -116,7 +121,7 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
   const int64_t rows = row_end - row_begin;
   const int bpc = dt == DType::F32 ? occupancy<float>(nv, p.skew, k) : occupancy<double>(nv, p.skew, k);
   p.blocks_per_cu = bpc;
-  const int64_t slots = (int64_t)cu_count() * bpc * 4;  // resident waves
+  const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;  // resident waves
   int64_t nbands;
   if (tile_rows > 0) {
     nbands = (rows + tile_rows - 1) / tile_rows;
@@ -137,11 +142,11 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
 }
 
 void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k,
-               double r, hipStream_t stream, int64_t tile_rows) {
+               double r, hipStream_t stream, int64_t tile_rows, int cus) {
   HEAT2D_REQUIRE(k <= L.halo, "temporal depth exceeds the halo depth");
   HEAT2D_REQUIRE(L.cpad >= 16, "column padding too small for the strip halo");
   if (row_end <= row_begin) return;
-  const TbPlan p = plan_tb(dt, L, row_begin, row_end, k, tile_rows);
+  const TbPlan p = plan_tb(dt, L, row_begin, row_end, k, tile_rows, cus);
   TbArgs a{};
   a.pitch = L.pitch;
   a.ncols = L.ncols;

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "heat2d/runtime.hpp"
 
@@ -69,7 +70,26 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
       s_compute_ = s_comm_ = external_stream;
       cfg_.overlap = 0;
     } else {
-      H2D_HIP(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
+      int ncu = 0;
+      H2D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg_.device));
+      const int reserve = cfg_.comm_cus < 0 ? 0 : (cfg_.comm_cus == 0 ? 8 : cfg_.comm_cus);
+      if (P > 1 && cfg_.overlap && reserve > 0 && reserve < ncu) {
+        // The persistent stencil kernel fills every resident wave slot; RCCL's
+        // send/recv kernels would then only start after it (no overlap) or
+        // delay some of its waves (a tail). Keep `reserve` CUs, spread over the
+        // XCDs, out of the compute stream's CU mask so the halo exchange always
+        // finds room, and plan the stencil grid for the remaining CUs.
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+        for (int j = 0; j < reserve; ++j) {
+          const int i = (int)((int64_t)j * ncu / reserve);
+          mask[(size_t)i / 32] &= ~(1u << (i % 32));
+        }
+        H2D_HIP(hipExtStreamCreateWithCUMask(&s_compute_, (uint32_t)mask.size(), mask.data()));
+        compute_cus_ = ncu - reserve;
+      } else {
+        H2D_HIP(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
+      }
       H2D_HIP(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
       own_streams_ = true;
     }
@@ -125,7 +145,7 @@ void Solver::init(const kern::IcParams& ic, const double* xg, const double* yg) 
 void Solver::launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k) {
   if (re <= rb) return;
   if (hip_)
-    kern::launch_tb(dtype(), src, dst, L_, rb, re, k, cfg_.r, s_compute_, cfg_.tile_rows);
+    kern::launch_tb(dtype(), src, dst, L_, rb, re, k, cfg_.r, s_compute_, cfg_.tile_rows, compute_cus_);
   else
     cpu::tb(dtype(), src, dst, L_, rb, re, k, cfg_.r);
 }

@@ -63,6 +63,7 @@ class Config(C.Structure):
         ("tb", C.c_int32), ("overlap", C.c_int32), ("copy_swap", C.c_int32), ("managed", C.c_int32),
         ("device", C.c_int32), ("use_graph", C.c_int32),
         ("tile_rows", C.c_int64), ("halo", C.c_int64),
+        ("comm_cus", C.c_int32), ("reserved_", C.c_int32),
     ]
 
 

@@ -1,0 +1,51 @@
+"""Worker for multi-process tests: one rank of a distributed heat2d run over
+torch.distributed (gloo) with the native solver + TorchDistTransport.
+
+Launched as `python tests/dist_worker.py RANK WORLD PORT OUTDIR JSON_ARGS`.
+Rank 0 gathers the field and writes OUTDIR/result.npy.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    rank, world, port, outdir = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    args = json.loads(sys.argv[5])
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import heat2d
+    from heat2d.models.heat2d import HeatSolver
+    from heat2d.parallel.transport import TorchDistTransport
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    inp = heat2d.InputDat(n=args["n"], sigma=0.25, nu=0.05, dom_len=args.get("dom", 1.0), ntime=args["steps"])
+    prob = heat2d.make_problem(inp, args.get("conv", "ghost"), args.get("ic", "uniform"))
+    backend = args.get("backend", "cpu")
+    if backend == "hip":
+        torch.cuda.set_device(0)
+    tr = TorchDistTransport()
+    s = HeatSolver(prob, dtype=args.get("dtype", "fp64"), backend=backend, tb=args.get("tb", 8),
+                   overlap=args.get("overlap", True), transport=tr, device=0 if backend == "hip" else None)
+    # split the stepping to exercise restarts of the cycle schedule
+    first = args["steps"] // 3
+    s.step(first)
+    s.step(args["steps"] - first)
+    st = s.stats(residual=True)
+    full = s.gather()
+    if rank == 0:
+        np.save(os.path.join(outdir, "result.npy"), full)
+        with open(os.path.join(outdir, "stats.json"), "w") as f:
+            json.dump({"stats": st, "info": {k: v for k, v in s.info().items() if k != "layout"}}, f)
+    s.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

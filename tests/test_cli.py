@@ -1,0 +1,97 @@
+"""The native `heat2d` executable: reference run behaviour (input.dat in the
+working directory, stdout lines, int.dat / soln.dat / soln%05d.dat outputs)
+for the serial, cuda and mpi variants; values round-trip exactly (17
+significant digits) and match the NumPy golden bitwise."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import heat2d
+from heat2d.models import reference as R
+from heat2d.ops import _native as N
+
+
+def run_cli(cwd, *args, timeout=300):
+    out = subprocess.run([N.CLI_PATH, *args], cwd=cwd, capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stdout + out.stderr
+    return out.stdout
+
+
+def read_xyz(path):
+    a = np.loadtxt(path)
+    assert a.ndim == 2 and a.shape[1] == 3
+    return a
+
+
+@pytest.fixture(scope="module")
+def cli(native):
+    if not os.path.exists(N.CLI_PATH):
+        N.build()
+    return N.CLI_PATH
+
+
+@pytest.mark.parametrize("variant,ic", [("serial", "hat"), ("cuda", "hat-cuda")])
+def test_cli_serial_variants_cpu(cli, tmp_path, variant, ic):
+    (tmp_path / "input.dat").write_text("40 0.25 0.05 2.0 25\n")
+    out = run_cli(tmp_path, "--cpu", "--variant", variant)
+    assert "simulation completed!!!!" in out and "total time:" in out
+    inp = heat2d.read_input(str(tmp_path / "input.dat"))
+    prob = heat2d.make_problem(inp, "inclusive", ic)
+    T0 = R.initial_field(prob)
+    T = R.ftcs(prob)
+    a0 = read_xyz(tmp_path / "int.dat")
+    a = read_xyz(tmp_path / "soln.dat")
+    assert a.shape == (40 * 40, 3)
+    assert np.array_equal(a0[:, 2], T0.ravel())
+    assert np.array_equal(a[:, 2], T.ravel())
+    # coordinates: x outer, y inner (fortran/serial/heat.f90:77-83)
+    assert np.array_equal(a[:, 0].reshape(40, 40)[:, 0], prob.x)
+    assert np.array_equal(a[:, 1].reshape(40, 40)[0, :], prob.x)
+
+
+def test_cli_mpi_variant_cpu(cli, tmp_path):
+    (tmp_path / "input.dat").write_text("64 0.25 0.05 1.0 17 1\n")
+    out = run_cli(tmp_path, "--cpu")
+    assert "Automatic MPI decomposition:" in out and "Average time:" in out
+    a = read_xyz(tmp_path / "soln00000.dat")
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(a[:, 2], R.owned(R.ftcs(prob)).ravel())
+    assert np.array_equal(np.unique(a[:, 0]), prob.x[1:-1])
+
+
+def test_cli_flags_and_json(cli, tmp_path):
+    (tmp_path / "input.dat").write_text("32768 0.25 0.05 1.0 25000 0\n")  # the reference benchmark file
+    out = run_cli(tmp_path, "--cpu", "--n", "48", "--ntime", "9", "--tb", "4", "--dtype", "fp32", "--json", "r.json",
+                  "--check-every", "3", "--print-every", "3")
+    assert "time_it:" in out and "residual_l2" in out
+    import json
+    r = json.loads((tmp_path / "r.json").read_text())
+    assert r["n"] == 48 and r["steps"] == 9 and r["dtype"] == "fp32" and r["backend"] == "cpu"
+
+
+def test_cli_bad_input(cli, tmp_path):
+    (tmp_path / "input.dat").write_text("10 0.25\n")
+    out = subprocess.run([N.CLI_PATH, "--cpu"], cwd=tmp_path, capture_output=True, text=True)
+    assert out.returncode != 0 and "at least 5 fields" in out.stderr
+
+
+@pytest.mark.gpu
+def test_cli_gpu_mpi_variant(cli, gpu, tmp_path):
+    (tmp_path / "input.dat").write_text("300 0.25 0.05 1.0 40 1\n")
+    out = run_cli(tmp_path, "--gpus", "1", "--tb", "8")
+    assert "MPI rank" in out and "using GPU" in out
+    a = read_xyz(tmp_path / "soln00000.dat")
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(a[:, 2], R.owned(R.ftcs(prob)).ravel())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--copy-swap"], ["--managed"], ["--graph"]])
+def test_cli_gpu_serial_variant(cli, gpu, tmp_path, extra):
+    (tmp_path / "input.dat").write_text("100 0.25 0.05 2.0 60\n")
+    run_cli(tmp_path, "--variant", "serial", *extra)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "inclusive", "hat")
+    a = read_xyz(tmp_path / "soln.dat")
+    assert np.array_equal(a[:, 2], R.ftcs(prob).ravel())
