@@ -7,6 +7,7 @@
 #include <memory>
 #include <string>
 
+#include "heat2d/config.hpp"
 #include "heat2d/runtime.hpp"
 
 extern "C" int heat2d_io_write_xyz_impl(const char*, int, const void*, int64_t, int64_t, int64_t,
@@ -83,6 +84,19 @@ int heat2d_decompose(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nr
     SlabRange r = decompose(n, nranks, rank);
     *row0 = r.row0;
     *nrows = r.nrows;
+  });
+}
+
+int heat2d_parse_input(const char* text, double* out7) {
+  return guarded([&] {
+    InputDat in = parse_input_text(text);
+    out7[0] = (double)in.n;
+    out7[1] = in.sigma;
+    out7[2] = in.nu;
+    out7[3] = in.dom_len;
+    out7[4] = (double)in.ntime;
+    out7[5] = (double)in.soln;
+    out7[6] = (double)in.nfields;
   });
 }
 

@@ -56,6 +56,9 @@ int heat2d_decompose(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nr
 int heat2d_plan_tb(int dtype, const heat2d_layout* L, int64_t rb, int64_t re, int k,
                    int64_t tile_rows, heat2d_tb_plan* out);
 
+/* input.dat parsing (C++ twin of utils/config.py): out = {n, sigma, nu, dom_len, ntime, soln, nfields} */
+int heat2d_parse_input(const char* text, double* out7);
+
 /* Raw ops on caller-owned memory (device pointers for the HIP ops; host for cpu_*).
  * `stream` is a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). */
 int heat2d_tb(int dtype, const void* src, void* dst, const heat2d_layout* L, int64_t rb,

@@ -90,6 +90,7 @@ _SIGS = {
     "heat2d_max_tb": (C.c_int, []),
     "heat2d_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "heat2d_make_layout": (C.c_int, [_I64, _I64, _I64, _I64, _I64, _LP]),
+    "heat2d_parse_input": (C.c_int, [C.c_char_p, C.POINTER(C.c_double)]),
     "heat2d_decompose": (C.c_int, [_I64, C.c_int, C.c_int, C.POINTER(_I64), C.POINTER(_I64)]),
     "heat2d_plan_tb": (C.c_int, [C.c_int, _LP, _I64, _I64, C.c_int, _I64, C.POINTER(TbPlan)]),
     "heat2d_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double, _P, _I64]),
@@ -194,6 +195,15 @@ def decompose(n: int, nranks: int, rank: int) -> tuple[int, int]:
     r0, nr = C.c_int64(), C.c_int64()
     call("heat2d_decompose", n, nranks, rank, C.byref(r0), C.byref(nr))
     return r0.value, nr.value
+
+
+def parse_input_native(text: str) -> dict:
+    """Parse input.dat text with the C++ parser (csrc/runtime/config.cpp)."""
+    out = (C.c_double * 7)()
+    call("heat2d_parse_input", text.encode(), out)
+    v = list(out)
+    return {"n": int(v[0]), "sigma": v[1], "nu": v[2], "dom_len": v[3], "ntime": int(v[4]), "soln": int(v[5]),
+            "nfields": int(v[6])}
 
 
 def plan_tb(dtype: int, layout: Layout, rb: int, re: int, k: int, tile_rows: int = 0) -> TbPlan:

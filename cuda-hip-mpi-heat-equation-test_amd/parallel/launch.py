@@ -1,0 +1,217 @@
+"""Python driver: `python -m heat2d [input.dat] [flags]`, torchrun-aware.
+
+Behaves like the reference programs (reads ./input.dat, prints
+"MPI rank r using GPU d", "Automatic MPI decomposition: P x 1", "nx:", "ny:",
+optional per-step "time_it:", "simulation completed!!!!", and "Average time:"
+or "total time:"; writes int.dat / soln.dat / soln%05d.dat per variant) on the
+native engine. One process per GPU:
+
+    python -m heat2d input.dat                                   # 1 GPU (or CPU)
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m heat2d input.dat   # 8 GPUs, RCCL
+    torchrun --nproc-per-node 4 -m heat2d input.dat --backend cpu              # 4 CPU ranks, gloo
+
+Extras: --tb K, --dtype, --check-every N (global sum / residual, NaN abort),
+--checkpoint DIR --checkpoint-every N, --restart DIR, --json FILE, --output npy.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def build_parser():
+    ap = argparse.ArgumentParser(prog="python -m heat2d", description=__doc__.split("\n")[0])
+    ap.add_argument("input", nargs="?", default="input.dat")
+    ap.add_argument("--variant", default=None, help="mpi | serial | cuda | managed | python | pycuda")
+    ap.add_argument("--backend", default="auto", choices=["auto", "hip", "cpu"])
+    ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+    ap.add_argument("--ic", default=None)
+    ap.add_argument("--tb", type=int, default=8)
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--copy-swap", action="store_true")
+    ap.add_argument("--managed", action="store_true")
+    ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--ntime", type=int, default=None)
+    ap.add_argument("--print-every", type=int, default=0)
+    ap.add_argument("--check-every", type=int, default=0)
+    ap.add_argument("--output", default="ascii", choices=["ascii", "npy", "none"])
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--checkpoint", default=None)
+    ap.add_argument("--checkpoint-every", type=int, default=0)
+    ap.add_argument("--restart", default=None)
+    ap.add_argument("--quiet", action="store_true")
+    return ap
+
+
+def _dist_setup(backend: str):
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "hip":
+        torch.cuda.set_device(local)
+    if world > 1 and not dist.is_initialized():
+        if backend == "hip":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    return rank, world, local
+
+
+def run(argv=None) -> int:
+    a = build_parser().parse_args(argv)
+    import heat2d
+    from heat2d.models import presets
+    from heat2d.models.heat2d import HeatSolver, resolve_backend
+    from heat2d.parallel import transport as T
+    from heat2d.utils import checkpoint, io, metrics
+    from heat2d.utils.config import make_problem, read_input
+
+    backend = resolve_backend(a.backend)
+    rank, world, local = _dist_setup(backend)
+    root = rank == 0
+    inp = read_input(a.input)
+    if a.n:
+        inp.n = a.n
+    if a.ntime is not None:
+        inp.ntime = a.ntime
+    var = presets.get(a.variant or presets.default_variant(inp))
+    prob = make_problem(inp, var.convention, a.ic or var.ic)
+    nsteps = inp.ntime + (1 if var.extra_step else 0)
+    if prob.r > 0.25 + 1e-12 and root:
+        print(f"warning: r = {prob.r:.6g} > 0.25: FTCS is unstable in 2-D", file=sys.stderr)
+
+    if backend == "hip" and not a.quiet:
+        print(f" MPI rank {rank:12d} using GPU {local:12d}", flush=True)
+    if world > 1:
+        tr = T.RcclTransport(rank, world, local) if backend == "hip" else T.TorchDistTransport()
+    else:
+        tr = T.SelfTransport()
+    s = HeatSolver(prob, dtype=a.dtype, backend=backend, tb=a.tb, overlap=not a.no_overlap, copy_swap=a.copy_swap,
+                   managed=a.managed or var.managed, graph=a.graph, transport=tr,
+                   device=local if backend == "hip" else None)
+    if root and not a.quiet:
+        if world > 1 or var.outputs == "mpi":
+            print(f" Automatic MPI decomposition: {world:12d}  x 1")
+        print(f" nx: {s.nrows:12d}")
+        print(f" ny: {s.ncols:12d}", flush=True)
+
+    start_step = 0
+    if a.restart:
+        meta = checkpoint.load(s, a.restart)
+        start_step = int(meta["step"])
+        if root and not a.quiet:
+            print(f" restarted from {a.restart} at step {start_step}")
+
+    x = prob.x
+    if var.outputs == "serial" and a.output == "ascii" and start_step == 0:
+        _write_inclusive(s, prob, "int.dat", world)
+
+    _barrier(world)
+    s.synchronize()
+    t0 = time.perf_counter()
+    done = start_step
+    chunk_rules = [v for v in (a.print_every, a.check_every, a.checkpoint_every) if v > 0]
+    while done < nsteps:
+        chunk = nsteps - done
+        for v in chunk_rules:
+            chunk = min(chunk, v - done % v)
+        s.step(chunk)
+        done += chunk
+        if root and a.print_every and done % a.print_every == 0:
+            print(f" time_it: {done:12d}")
+        if a.check_every and done % a.check_every == 0:
+            st = s.stats(residual=True)
+            if root:
+                print(f" step {done}: sum={st['sum']:.17g} min={st['min']:.6g} max={st['max']:.6g} "
+                      f"residual_l2={st['residual_l2']:.6e}", flush=True)
+            if not np.isfinite(st["sum"]):
+                raise FloatingPointError(f"non-finite temperature at step {done}")
+        if a.checkpoint and a.checkpoint_every and done % a.checkpoint_every == 0 and done < nsteps:
+            checkpoint.save(s, a.checkpoint, step=done)
+    s.synchronize()
+    _barrier(world)
+    elapsed = time.perf_counter() - t0
+    elapsed = _max_over_ranks(elapsed, world, backend)
+    ran = nsteps - start_step
+
+    if a.checkpoint:
+        checkpoint.save(s, a.checkpoint, step=done)
+    if a.output != "none":
+        if var.outputs == "serial":
+            if a.output == "ascii":
+                _write_inclusive(s, prob, "soln.dat", world)
+            else:
+                full = s.gather()
+                if root:
+                    io.write_npy("soln.npy", full)
+        elif inp.soln == 1 or a.output == "npy":
+            local_T = s.download()
+            if a.output == "npy":
+                io.write_npy(f"soln{rank:05d}.npy", local_T)
+            else:
+                io.write_xyz(f"soln{rank:05d}.dat", local_T, x[1 + s.row0:1 + s.row0 + s.nrows], x[1:-1])
+    st = s.stats()
+    if root:
+        print(" simulation completed!!!!")
+        if var.timing_line == "Average time:":
+            print(f" Average time: {elapsed / max(ran, 1):24.16g}")
+        else:
+            print(f" total time: {elapsed:24.16g}")
+        rec = metrics.record(prob.n_owned, ran, elapsed, world, a.dtype, s.tb, backend, a.copy_swap,
+                             {"variant": var.name, "sum": st["sum"], "min": st["min"], "max": st["max"]})
+        if not a.quiet:
+            print(f" heat2d: n={prob.n_owned} P={world} {a.dtype} K={s.tb} steps={ran} wall={elapsed:.6f} s  "
+                  f"{rec['gpts_per_s']:.3f} Gpts/s  {rec['model_hbm_gb_per_s']:.1f} GB/s(model)  "
+                  f"sum(T)={st['sum']:.17g}", flush=True)
+        if a.json:
+            metrics.write_json(a.json, rec)
+    s.close()
+    tr.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0
+
+
+def _write_inclusive(s, prob, path, world):
+    """Frame-inclusive n x n dump (fortran/serial/heat.f90:50-55): rank 0 gathers."""
+    from heat2d.utils import io
+    full = s.gather()
+    if s.rank != 0:
+        return
+    m = prob.n_owned
+    T = np.empty((m + 2, m + 2), dtype=full.dtype)
+    T[1:-1, 1:-1] = full
+    # frame values: the IC on the frame (kept fixed by the solver)
+    from heat2d.models.reference import initial_field
+    frame = initial_field(prob, full.dtype)
+    T[0, :], T[-1, :], T[:, 0], T[:, -1] = frame[0, :], frame[-1, :], frame[:, 0], frame[:, -1]
+    io.write_xyz(path, T, prob.x, prob.x)
+
+
+def _barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def _max_over_ranks(v, world, backend):
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if backend == "hip" else "cpu"
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+if __name__ == "__main__":
+    sys.exit(run())

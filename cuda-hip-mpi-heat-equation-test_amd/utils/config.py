@@ -132,11 +132,19 @@ def make_ic(name: str, dom_len: float = 2.0, coords: Optional[np.ndarray] = None
     if name == "hotspot":  # synthetic benchmark data: zero field + unit hot spot
         L = dom_len
         return IcSpec(kind=IC_BOX, a=1.0, b=0.0, x0=0.4 * L, x1=0.6 * L, y0=0.4 * L, y1=0.6 * L, pad=0.0)
+    if name in ("python-hat", "pycuda-hat", "const-1"):
+        # python/serial/heat.py:25 : u[int(.5/dy):int(1/dy+1), int(.5/dx):int(1/dx+1)] = 2 (frame-inclusive
+        # indices); python/cuda/cuda.py:53 slices [int(1.5/dy):int(1/dy+1)], an EMPTY range -> all ones.
+        n = len(coords) if coords is not None else 31
+        d = dom_len / (n - 1)
+        lo = int((1.5 if name != "python-hat" else 0.5) / d)
+        hi = int(1 / d + 1)
+        return IcSpec(kind=IC_INDEX_BOX, a=2.0, b=1.0, i0=lo, i1=hi, j0=lo, j1=hi)
     if name == "sine":  # analytic FTCS eigenmode (zero Dirichlet)
         lo = float(coords[0]) if coords is not None else 0.0
         hi = float(coords[-1]) if coords is not None else dom_len
         return IcSpec(kind=IC_SINE, a=1.0, x0=lo, x1=hi, y0=lo, y1=hi, kx=1.0, ky=1.0, pad=0.0)
-    raise ValueError(f"unknown IC '{name}' (uniform|hat|hat-cuda|hotspot|sine)")
+    raise ValueError(f"unknown IC '{name}' (uniform|hat|hat-cuda|hotspot|sine|python-hat|pycuda-hat)")
 
 
 GHOST, INCLUSIVE = "ghost", "inclusive"

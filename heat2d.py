@@ -15,3 +15,8 @@ _spec = importlib.util.spec_from_file_location("heat2d", os.path.join(_PKG_DIR, 
 _mod = importlib.util.module_from_spec(_spec)
 sys.modules["heat2d"] = _mod
 _spec.loader.exec_module(_mod)
+
+if __name__ == "__main__":  # `python -m heat2d [input.dat] [flags]` (torchrun -m heat2d ...)
+    from heat2d.parallel.launch import run
+
+    sys.exit(run())

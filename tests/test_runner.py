@@ -1,0 +1,107 @@
+"""Python driver (`python -m heat2d`), torchrun multi-rank (gloo, CPU), I/O
+helpers, plotting and checkpoint/restart across different rank counts."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import heat2d
+from heat2d.models import reference as R
+from heat2d.utils import io
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def py(cwd, *args, nproc=1, timeout=300):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", HEAT2D_CPU_THREADS="2")
+    if nproc == 1:
+        cmd = [sys.executable, "-m", "heat2d", *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(nproc), "--master-addr",
+               "127.0.0.1", "--master-port", str(port()), "-m", "heat2d", *args]
+    out = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    return out.stdout
+
+
+def test_python_driver_serial(native, tmp_path):
+    (tmp_path / "input.dat").write_text("36 0.25 0.05 2.0 21\n")
+    out = py(tmp_path, "--backend", "cpu", "--json", "m.json")
+    assert "simulation completed!!!!" in out and "total time:" in out
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "inclusive", "hat")
+    x, y, T = io.read_xyz(str(tmp_path / "soln.dat"))
+    assert np.array_equal(T, R.ftcs(prob))
+    assert np.array_equal(x, prob.x) and np.array_equal(y, prob.x)
+    _, _, T0 = io.read_xyz(str(tmp_path / "int.dat"))
+    assert np.array_equal(T0, R.initial_field(prob))
+    m = json.loads((tmp_path / "m.json").read_text())
+    assert m["steps"] == 21 and m["variant"] == "serial"
+
+
+def test_python_variant_demo(native, tmp_path):
+    """python/serial/heat.py: 31x31, diffuse(10) = 11 steps, index-slice hat."""
+    (tmp_path / "input.dat").write_text("31 0.25 0.05 2.0 10\n")
+    py(tmp_path, "--backend", "cpu", "--variant", "python")
+    _, _, T = io.read_xyz(str(tmp_path / "soln.dat"))
+    demo = R.python_serial_demo()
+    assert np.abs(T - demo.T).max() < 1e-13
+
+
+def test_torchrun_gloo_mpi_variant_and_merge(native, tmp_path):
+    (tmp_path / "input.dat").write_text("48 0.25 0.05 1.0 19 1\n")
+    out = py(tmp_path, "--backend", "cpu", "--tb", "4", nproc=3)
+    assert "Automatic MPI decomposition:            3  x 1" in out and "Average time:" in out
+    merged = io.merge_rank_files(str(tmp_path))
+    x, y, T = io.read_xyz(merged)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
+    assert np.array_equal(x, prob.x[1:-1])
+
+
+@pytest.mark.parametrize("p_write,p_read", [(2, 1), (1, 3), (3, 2)])
+def test_checkpoint_restart_changes_rank_count(native, tmp_path, p_write, p_read):
+    (tmp_path / "input.dat").write_text("50 0.25 0.05 1.0 30 1\n")
+    # run 12 steps with a checkpoint, then resume to 30 steps on a different rank count
+    py(tmp_path, "--backend", "cpu", "--ntime", "12", "--checkpoint", "ck", "--output", "none", nproc=p_write)
+    meta = json.loads((tmp_path / "ck" / "meta.json").read_text())
+    assert meta["step"] == 12 and meta["nranks"] == p_write
+    for f in tmp_path.glob("soln*.dat"):
+        f.unlink()
+    py(tmp_path, "--backend", "cpu", "--restart", "ck", nproc=p_read)
+    T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
+
+
+def test_plot_out(native, tmp_path):
+    pytest.importorskip("matplotlib")
+    (tmp_path / "input.dat").write_text("30 0.25 0.05 2.0 5\n")
+    py(tmp_path, "--backend", "cpu")
+    from heat2d.utils import plot
+    fig = plot.plot(str(tmp_path / "soln.dat"), save=str(tmp_path / "sol.png"))
+    assert (tmp_path / "sol.png").stat().st_size > 1000
+    plot.plot(str(tmp_path / "int.dat"), save=str(tmp_path / "int.png"), heatmap=True)
+    assert (tmp_path / "int.png").exists()
+    del fig
+
+
+def test_io_roundtrip_and_npy(native, tmp_path):
+    rng = np.random.default_rng(3)
+    T = rng.random((7, 5))
+    x = np.linspace(0, 1, 7)
+    y = np.linspace(-1e-3, 2e5, 5)
+    io.write_xyz(str(tmp_path / "a.dat"), T, x, y)
+    x2, y2, T2 = io.read_xyz(str(tmp_path / "a.dat"))
+    assert np.array_equal(T, T2) and np.array_equal(x, x2) and np.array_equal(y, y2)
+    io.write_npy(str(tmp_path / "a.npy"), T.astype(np.float32))
+    assert np.array_equal(np.load(tmp_path / "a.npy", allow_pickle=False), T.astype(np.float32))
