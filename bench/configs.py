@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""The BASELINE.json configuration list, measured on one MI355X (plus the CPU
+serial case). Prints one JSON line per configuration.
+
+    python bench/configs.py [--only NAME ...] [--max-gb 240]
+
+  cpu-256-fp64      256x256 fp64, native CPU path (python/serial + fortran/serial scale)
+  gpu-4096-fp32     4096x4096 fp32, 1000 steps (fields live in the 256 MiB Infinity Cache)
+  gpu-16384-fp64    16384x16384 fp64 (HBM-bound regime)
+  gpu-32768-fp64    32768x32768 fp64 — the reference's benchmark input (fortran/hip/input.dat)
+  gpu-32768-fp32    32768x32768 fp32 (the 8-GPU config of BASELINE.json, here on 1 GPU)
+  gpu-max-fp32      the largest fp32 grid two fields fit in --max-gb of HBM (weak-scaling unit)
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(name, n, dtype, steps, warmup, backend, tb, graph=False):
+    import heat2d
+    from heat2d.models.heat2d import HeatSolver
+    inp = heat2d.InputDat(n=n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=steps, nfields=6)
+    prob = heat2d.make_problem(inp, "ghost", "uniform")
+    t_init = time.perf_counter()
+    s = HeatSolver(prob, dtype=dtype, backend=backend, tb=tb, graph=graph, device=0 if backend == "hip" else None)
+    s.synchronize()
+    t_init = time.perf_counter() - t_init
+    s.step(warmup)
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.step(steps)
+    s.synchronize()
+    dt = time.perf_counter() - t0
+    st = s.stats()
+    es = 8 if dtype == "fp64" else 4
+    k = s.tb
+    gpts = float(n) * n * steps / dt / 1e9
+    rec = {"config": name, "n": n, "dtype": dtype, "backend": backend, "tb": k, "graph": graph, "steps": steps,
+           "s": round(dt, 6), "ms_per_step": round(dt / steps * 1e3, 5), "gpts": round(gpts, 2),
+           "model_gbps": round(gpts * 2 * es / k, 1), "field_gb": round(s.layout.elems() * es / 1e9, 2),
+           "init_s": round(t_init, 3), "finite": bool(math.isfinite(st["sum"]))}
+    s.close()
+    return rec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--max-gb", type=float, default=240.0)
+    a = ap.parse_args()
+    import torch
+    have_gpu = torch.cuda.is_available()
+    if have_gpu:
+        torch.cuda.set_device(0)
+    es32 = 4
+    nmax = int(math.sqrt(a.max_gb * 1e9 / (2 * es32)))
+    nmax = nmax // 1024 * 1024
+    plan = [
+        ("cpu-256-fp64", 256, "fp64", 200, 8, "cpu", 8, False),
+        ("gpu-4096-fp32", 4096, "fp32", 1000, 64, "hip", 8, False),
+        ("gpu-4096-fp32-graph", 4096, "fp32", 1000, 64, "hip", 8, True),
+        ("gpu-16384-fp64", 16384, "fp64", 400, 32, "hip", 8, False),
+        ("gpu-32768-fp64", 32768, "fp64", 400, 48, "hip", 8, False),
+        ("gpu-32768-fp32", 32768, "fp32", 400, 48, "hip", 8, False),
+        ("gpu-max-fp32", nmax, "fp32", 64, 8, "hip", 8, False),
+    ]
+    for name, n, dt, steps, warm, be, tb, graph in plan:
+        if a.only and not any(name.startswith(o) for o in a.only):
+            continue
+        if be == "hip" and not have_gpu:
+            continue
+        print(json.dumps(run(name, n, dt, steps, warm, be, tb, graph)), flush=True)
+        if have_gpu:
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
