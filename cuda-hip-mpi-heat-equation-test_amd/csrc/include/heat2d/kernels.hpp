@@ -23,6 +23,8 @@ struct TbPlan {
   int64_t nblocks;    // 256-thread workgroups (4 independent waves each)
   int32_t skew;       // level pipeline skew (1 or 2)
   int32_t blocks_per_cu;  // resident workgroups per CU (occupancy API)
+  int32_t prefetch;   // rows in flight per wave (3 or 6)
+  int32_t reserved_;
 };
 
 // Plan a launch that advances rows [row_begin, row_end) of the slab by k steps.

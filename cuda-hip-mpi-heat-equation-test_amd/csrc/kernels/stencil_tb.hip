@@ -82,21 +82,35 @@ int default_skew(DType dt, int k) {
   return 1;  // skew-2's extra row of state per level costs more occupancy than its ILP returns (measured)
 }
 
-template <typename T>
-int occupancy(int nv, int sk, int k) {
-  if (nv == 1) return sk == 2 ? occupancy_blocks<T, 1, 2>(k) : occupancy_blocks<T, 1, 1>(k);
-  return sk == 2 ? occupancy_blocks<T, 2, 2>(k) : occupancy_blocks<T, 2, 1>(k);
+// Prefetch depth (units of 3 rows). 6 rows in flight hides the HBM latency
+// of the compute-heavier deep pipelines; instantiated for 16 B/lane, skew 1.
+// Override: HEAT2D_TB_PF=1|2.
+int default_pf(DType dt, int k, int nv, int sk) {
+  if (nv != 1 || sk != 1) return 1;
+  const char* env = std::getenv("HEAT2D_TB_PF");
+  if (env) return std::atoi(env) == 2 ? 2 : 1;
+  return (dt == DType::F64 ? k >= 7 : k >= 9) ? 2 : 1;  // measured (bench/sweep.py, A/B in one box)
 }
 
 template <typename T>
-void dispatch_variant(int nv, int sk, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
+int occupancy(int nv, int sk, int pf, int k) {
+  if (nv == 1) {
+    if (sk == 2) return occupancy_blocks<T, 1, 2, 1>(k);
+    return pf == 2 ? occupancy_blocks<T, 1, 1, 2>(k) : occupancy_blocks<T, 1, 1, 1>(k);
+  }
+  return sk == 2 ? occupancy_blocks<T, 2, 2, 1>(k) : occupancy_blocks<T, 2, 1, 1>(k);
+}
+
+template <typename T>
+void dispatch_variant(int nv, int sk, int pf, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
                       hipStream_t st) {
   if (nv == 1) {
-    if (sk == 2) dispatch<T, 1, 2>(k, nblocks, s, d, a, r, st);
-    else dispatch<T, 1, 1>(k, nblocks, s, d, a, r, st);
+    if (sk == 2) dispatch<T, 1, 2, 1>(k, nblocks, s, d, a, r, st);
+    else if (pf == 2) dispatch<T, 1, 1, 2>(k, nblocks, s, d, a, r, st);
+    else dispatch<T, 1, 1, 1>(k, nblocks, s, d, a, r, st);
   } else {
-    if (sk == 2) dispatch<T, 2, 2>(k, nblocks, s, d, a, r, st);
-    else dispatch<T, 2, 1>(k, nblocks, s, d, a, r, st);
+    if (sk == 2) dispatch<T, 2, 2, 1>(k, nblocks, s, d, a, r, st);
+    else dispatch<T, 2, 1, 1>(k, nblocks, s, d, a, r, st);
   }
 }
 
@@ -119,7 +133,9 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
     p.useful_w = nv == 1 ? useful_width<double, 1>(k) : useful_width<double, 2>(k);
   p.nstrips = (L.ncols + p.useful_w - 1) / p.useful_w;
   const int64_t rows = row_end - row_begin;
-  const int bpc = dt == DType::F32 ? occupancy<float>(nv, p.skew, k) : occupancy<double>(nv, p.skew, k);
+  p.prefetch = 3 * default_pf(dt, k, nv, p.skew);
+  const int pf = p.prefetch / 3;
+  const int bpc = dt == DType::F32 ? occupancy<float>(nv, p.skew, pf, k) : occupancy<double>(nv, p.skew, pf, k);
   p.blocks_per_cu = bpc;
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;  // resident waves
   int64_t nbands;
@@ -164,11 +180,11 @@ void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_
   if (dt == DType::F32) {
     const float* s = static_cast<const float*>(src) + o;
     float* d = static_cast<float*>(dst) + o;
-    dispatch_variant<float>(nv, p.skew, p.k, (unsigned)p.nblocks, s, d, a, (float)r, stream);
+    dispatch_variant<float>(nv, p.skew, p.prefetch / 3, p.k, (unsigned)p.nblocks, s, d, a, (float)r, stream);
   } else {
     const double* s = static_cast<const double*>(src) + o;
     double* d = static_cast<double*>(dst) + o;
-    dispatch_variant<double>(nv, p.skew, p.k, (unsigned)p.nblocks, s, d, a, r, stream);
+    dispatch_variant<double>(nv, p.skew, p.prefetch / 3, p.k, (unsigned)p.nblocks, s, d, a, r, stream);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("tb_kernel launch: ") + hipGetErrorString(e));

@@ -86,6 +86,7 @@ struct TbShape {
 // ring precisely (vmcnt(N>0)) instead of draining it every row.
 constexpr int32_t kOob = (int32_t)0x80000000u;
 
+
 template <typename T>
 struct Bits;
 template <>
@@ -101,7 +102,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uin
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
-template <typename T, int NV, int K, bool EDGE>
+// PF: prefetch depth in units of 3 rows (PF = 2 -> 6 rows in flight per wave).
+template <typename T, int NV, int K, bool EDGE, int PF>
 struct March {
   using S = TbShape<T, NV, K>;
   static constexpr int V = S::V;
@@ -123,7 +125,24 @@ struct March {
   unsigned fixmask;  // EDGE: per-element Dirichlet column bits
 
   T X[3][K][V];      // level state: 3-phase rotating window (SSA after unroll)
-  VT Lb[3][NV];      // level-0 prefetch ring (3 rows ahead)
+  // level-0 prefetch ring: 3*PFJ rows in flight; row m sits in Lb[m%3][0]
+  // when consumed, the slot's older entries shift down, row m+3*PFJ lands last
+  VT Lb[3][PF][NV];
+
+  template <int PH>
+  __device__ __forceinline__ void prefetch_advance(int64_t m) {
+#pragma unroll
+    for (int j = 0; j + 1 < PF; ++j)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) Lb[PH][j][v] = Lb[PH][j + 1][v];
+    const int64_t nxt = m + 3 * PF;
+    load_row(nxt < me ? nxt : me - 1, Lb[PH][PF - 1]);
+  }
+
+  __device__ __forceinline__ void prefetch_prime(int64_t mb) {
+#pragma unroll
+    for (int q = 0; q < 3 * PF; ++q) load_row(mb + q < me ? mb + q : me - 1, Lb[q % 3][q / 3]);
+  }
 
   __device__ __forceinline__ void load_row(int64_t m, VT (&out)[NV]) const {
     const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + m * pitch_b, nrec);
@@ -163,8 +182,8 @@ struct March {
 #pragma unroll
     for (int v = 0; v < NV; ++v)
 #pragma unroll
-      for (int e = 0; e < VM; ++e) X[PN][0][v * VM + e] = Lb[PH][v][e];
-    load_row(m + 3 < me ? m + 3 : me - 1, Lb[PH]);
+      for (int e = 0; e < VM; ++e) X[PN][0][v * VM + e] = Lb[PH][0][v][e];
+    prefetch_advance<PH>(m);
 #pragma unroll
     for (int s = 1; s <= K; ++s) {
       const T* o = X[PO][s - 1];  // row m-s-1 (north, x-1)
@@ -204,8 +223,7 @@ struct March {
   __device__ __forceinline__ void run() {
     const int64_t mb = t0 - K;
     me = t1 + K;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) load_row(mb + q < me ? mb + q : me - 1, Lb[q]);
+    prefetch_prime(mb);
     int64_t m = mb;
 #pragma unroll 1
     for (int i = 0; i < (2 * K) / 3; ++i) {
@@ -235,9 +253,9 @@ struct March {
 // south neighbour, a 6-deep fp dependency per level). Levels are evaluated
 // from K down to 1 so each level reads its 3 input rows before the level below
 // overwrites the oldest of them: 3 rows per level, ring index (row mod 3).
-template <typename T, int NV, int K, bool EDGE>
-struct March2 : March<T, NV, K, EDGE> {
-  using B = March<T, NV, K, EDGE>;
+template <typename T, int NV, int K, bool EDGE, int PF>
+struct March2 : March<T, NV, K, EDGE, PF> {
+  using B = March<T, NV, K, EDGE, PF>;
   using B::r;
   using B::X;
   using B::Lb;
@@ -290,8 +308,8 @@ struct March2 : March<T, NV, K, EDGE> {
 #pragma unroll
     for (int v = 0; v < NV; ++v)
 #pragma unroll
-      for (int e = 0; e < VM; ++e) X[PH][0][v * VM + e] = Lb[PH][v][e];
-    B::load_row(m + 3 < me ? m + 3 : me - 1, Lb[PH]);
+      for (int e = 0; e < VM; ++e) X[PH][0][v * VM + e] = Lb[PH][0][v][e];
+    B::template prefetch_advance<PH>(m);
   }
 
   // level-0 rows [t0-K, t1+K); march rows [t0-K, t1+2K); output row m-2K for
@@ -300,8 +318,7 @@ struct March2 : March<T, NV, K, EDGE> {
     const int64_t mb = t0 - K;
     me = t1 + K;
     mend = t1 + 2 * K;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) B::load_row(mb + q < me ? mb + q : me - 1, Lb[q]);
+    B::prefetch_prime(mb);
     int64_t m = mb;
     // phase PH = (m - mb) mod 3 (mb plays the role of row 0 for the rings)
 #pragma unroll 1
@@ -321,7 +338,7 @@ struct March2 : March<T, NV, K, EDGE> {
   }
 };
 
-template <typename T, int NV, int K, bool EDGE, int SK>
+template <typename T, int NV, int K, bool EDGE, int SK, int PF>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
                                       int64_t t1, int lane) {
   using S = TbShape<T, NV, K>;
@@ -331,7 +348,7 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   const int64_t c0 = u0 - S::KA;
   const int64_t mycol = c0 + (int64_t)lane * V;
   const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
-  using M = typename std::conditional<SK == 2, March2<T, NV, K, EDGE>, March<T, NV, K, EDGE>>::type;
+  using M = typename std::conditional<SK == 2, March2<T, NV, K, EDGE, PF>, March<T, NV, K, EDGE, PF>>::type;
   M w;
   // row base = column col_lo (= -cpad) of row 0; offsets are relative to it
   w.srow = reinterpret_cast<const char*>(src + a.col_lo);
@@ -361,7 +378,7 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   w.run();
 }
 
-template <typename T, int NV, int K, int SK>
+template <typename T, int NV, int K, int SK, int PF>
 __global__ __launch_bounds__(256) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a,
                                                  T r) {
   using S = TbShape<T, NV, K>;
@@ -387,20 +404,20 @@ __global__ __launch_bounds__(256) void tb_kernel(const T* __restrict__ src, T* _
     const int64_t t0 = a.row_begin + r0, t1 = a.row_begin + r1;
     const bool edge = (c0 < 0) || (c0 + S::W > a.ncols) || (t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi);
     if (edge)
-      march<T, NV, K, true, SK>(src, dst, a, r, strip, t0, t1, lane);
+      march<T, NV, K, true, SK, PF>(src, dst, a, r, strip, t0, t1, lane);
     else
-      march<T, NV, K, false, SK>(src, dst, a, r, strip, t0, t1, lane);
+      march<T, NV, K, false, SK, PF>(src, dst, a, r, strip, t0, t1, lane);
   }
 }
 
-template <typename T, int NV, int K, int SK>
+template <typename T, int NV, int K, int SK, int PF>
 constexpr auto kernel_ptr() {
-  return &tb_kernel<T, NV, K, SK>;
+  return &tb_kernel<T, NV, K, SK, PF>;
 }
 
 // Resident 256-thread workgroups per CU for one kernel instance (occupancy
 // API; these kernels use ~44 SGPRs, inside the range where the API is exact).
-template <typename T, int NV, int K, int SK>
+template <typename T, int NV, int K, int SK, int PF>
 int blocks_per_cu() {
   static std::mutex mu;
   static std::map<int, int> cache;  // device -> blocks/CU
@@ -410,7 +427,7 @@ int blocks_per_cu() {
   auto it = cache.find(dev);
   if (it != cache.end()) return it->second;
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, SK>()), 256, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, SK, PF>()), 256, 0) !=
           hipSuccess ||
       nb <= 0)
     nb = 1;
@@ -420,18 +437,18 @@ int blocks_per_cu() {
 
 // Per-(T, NV) entry points, explicitly instantiated in tb_<dtype>_nv<NV>.hip
 // (one translation unit each, compiled in parallel).
-template <typename T, int NV, int SK>
+template <typename T, int NV, int SK, int PF>
 void dispatch(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
-template <typename T, int NV, int SK>
+template <typename T, int NV, int SK, int PF>
 int occupancy_blocks(int k);
 
-#define H2D_TB_CASE(T, NV, SK, KK)                                                              \
-  case KK:                                                                                      \
-    hipLaunchKernelGGL((tb_kernel<T, NV, KK, SK>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
+#define H2D_TB_CASE(T, NV, SK, PF, KK)                                                              \
+  case KK:                                                                                          \
+    hipLaunchKernelGGL((tb_kernel<T, NV, KK, SK, PF>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
     return;
-#define H2D_OCC_CASE(T, NV, SK, KK) \
-  case KK:                          \
-    return blocks_per_cu<T, NV, KK, SK>();
+#define H2D_OCC_CASE(T, NV, SK, PF, KK) \
+  case KK:                              \
+    return blocks_per_cu<T, NV, KK, SK, PF>();
 
 }  // namespace tbimpl
 }  // namespace kern

@@ -21,7 +21,8 @@ import threading
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NATIVE_DIR = os.path.join(_PKG_DIR, "_native")
 CSRC_DIR = os.path.join(_PKG_DIR, "csrc")
-LIB_PATH = os.path.join(NATIVE_DIR, "libheat2d.so")
+# HEAT2D_LIB: load an alternative build (kernel A/B experiments, bench/ab.py)
+LIB_PATH = os.environ.get("HEAT2D_LIB") or os.path.join(NATIVE_DIR, "libheat2d.so")
 CLI_PATH = os.path.join(NATIVE_DIR, "heat2d")
 
 F32, F64 = 0, 1
@@ -72,7 +73,7 @@ class TbPlan(C.Structure):
         ("k", C.c_int32), ("vec", C.c_int32), ("strip_w", C.c_int32), ("useful_w", C.c_int32),
         ("tile_rows", C.c_int64), ("nstrips", C.c_int64), ("ntiles", C.c_int64),
         ("nwaves", C.c_int64), ("nblocks", C.c_int64),
-        ("skew", C.c_int32), ("blocks_per_cu", C.c_int32),
+        ("skew", C.c_int32), ("blocks_per_cu", C.c_int32), ("prefetch", C.c_int32), ("reserved_", C.c_int32),
     ]
 
 
