@@ -64,10 +64,10 @@ def main():
         ("cpu-256-fp64", 256, "fp64", 200, 8, "cpu", 8, False),
         ("gpu-4096-fp32", 4096, "fp32", 1000, 64, "hip", 8, False),
         ("gpu-4096-fp32-graph", 4096, "fp32", 1000, 64, "hip", 8, True),
-        ("gpu-16384-fp64", 16384, "fp64", 400, 32, "hip", 8, False),
-        ("gpu-32768-fp64", 32768, "fp64", 400, 48, "hip", 8, False),
-        ("gpu-32768-fp32", 32768, "fp32", 400, 48, "hip", 8, False),
-        ("gpu-max-fp32", nmax, "fp32", 64, 8, "hip", 8, False),
+        ("gpu-16384-fp64", 16384, "fp64", 400, 40, "hip", 10, False),
+        ("gpu-32768-fp64", 32768, "fp64", 400, 40, "hip", 10, False),
+        ("gpu-32768-fp32", 32768, "fp32", 405, 45, "hip", 9, False),
+        ("gpu-max-fp32", nmax, "fp32", 63, 9, "hip", 9, False),
     ]
     for name, n, dt, steps, warm, be, tb, graph in plan:
         if a.only and not any(name.startswith(o) for o in a.only):

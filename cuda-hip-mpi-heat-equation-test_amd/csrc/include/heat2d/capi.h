@@ -37,7 +37,7 @@ typedef struct heat2d_config {
 typedef struct heat2d_tb_plan {
   int32_t k, vec, strip_w, useful_w;
   int64_t tile_rows, nstrips, ntiles, nwaves, nblocks;
-  int32_t skew, blocks_per_cu, prefetch, reserved_;
+  int32_t skew, blocks_per_cu, prefetch, tight;
 } heat2d_tb_plan;
 
 typedef int (*heat2d_exchange_fn)(void* ctx, void* send_lo, void* send_hi, void* recv_lo,

@@ -21,10 +21,10 @@ struct TbPlan {
   int64_t ntiles;
   int64_t nwaves;
   int64_t nblocks;    // 256-thread workgroups (4 independent waves each)
-  int32_t skew;       // level pipeline skew (1 or 2)
+  int32_t skew;       // level pipeline skew (always 1: upward march, see tb_impl.hpp)
   int32_t blocks_per_cu;  // resident workgroups per CU (occupancy API)
-  int32_t prefetch;   // rows in flight per wave (3 or 6)
-  int32_t reserved_;
+  int32_t prefetch;   // level-0 row ring per wave (RING; RING-2 rows in flight)
+  int32_t tight;      // 1: occupancy-targeted register budget (tight_waves)
 };
 
 // Plan a launch that advances rows [row_begin, row_end) of the slab by k steps.

@@ -7,29 +7,29 @@
 //
 // Design (wave64, no LDS, no barriers):
 //   * one WAVE owns a column strip of 64*V columns (V = NV * 16 B / sizeof(T))
-//     and marches down a run of rows, loading each input row exactly once with
+//     and marches UP a run of rows, loading each input row exactly once with
 //     NV 16-B loads per lane (1 KiB per wave instruction);
 //   * K time levels are pipelined in registers: at march row m the wave loads
-//     row m of level 0 and computes row m-s of level s for s = 1..K, so K time
+//     row m of level 0 and computes row m+s of level s for s = 1..K, so K time
 //     steps cost ONE HBM read + ONE HBM write per point (the single-step
 //     roofline is 16 B/pt fp64; at K = 8 the kernel needs 2 B/pt);
+//   * marching upward puts the OLDEST row first in the reference's summation
+//     order, so each level needs only 2 rows of register state (parity ring)
+//     and a 5-op dependency chain from the freshly computed row;
 //   * east/west neighbours come from the adjacent lane through DPP
 //     wave_shr:1 / wave_shl:1 (VALU modifiers, no LDS traffic); the strip's
 //     outer K columns are redundant halo work (shrinking valid region);
-//   * the 3-row window per level rotates through a 3-phase unrolled loop, so no
-//     register moves are needed for the rotation;
 //   * loads/stores are raw buffer ops on per-row descriptors with out-of-range
-//     voffsets for masked lanes: no memory op under control flow, so the
-//     prefetch ring (3 rows ahead) is waited for with counted vmcnt(N);
-//   * persistent, balanced schedule: exactly as many waves as the chip holds
-//     resident (occupancy API x CUs); wave w owns the contiguous row-units
-//     [w*R/S, (w+1)*R/S) of the strip-major list of R = strips x rows, so all
-//     waves finish together (no partial last round) and every march is long
-//     (the 2K-row start-up of a march is amortised);
+//     voffsets for masked lanes (and num_records = 0 for priming rows): no
+//     memory op under control flow, so the RING-row prefetch is waited for
+//     with counted vmcnt(N);
+//   * persistent schedule: as many waves as the chip holds resident
+//     (occupancy API x CUs), work items = (row band, strip), band-major;
 //   * the arithmetic order is exactly the reference's
-//     c + r*((((E + N) + W) + S) - 4c) (fortran/hip/heat_kernel.cpp:43) and the
-//     file is built with -ffp-contract=off: results are bitwise identical to the
-//     CPU reference and to an unblocked K=1 run.
+//     c + r*((((S + E) + N) + W) - 4c) (fortran/hip/heat_kernel.cpp:43, with
+//     S = T(x+1,y), E = T(x,y+1), N = T(x-1,y), W = T(x,y-1)) and the file is
+//     built with -ffp-contract=off: results are bitwise identical to the CPU
+//     reference and to an unblocked K=1 run, in fp64 and in fp32.
 #include "tb_impl.hpp"
 
 namespace heat2d {
@@ -60,57 +60,56 @@ int useful_width(int k) {
 
 
 // Vector width (16-B vectors per lane). 2 halves the strip-halo redundancy
-// but doubles the register state; instantiated for K <= 8 only.
-// Override: HEAT2D_TB_NV=1|2.
+// (and the DPP moves per point) but doubles the register state.
+// Override: HEAT2D_TB_NV=1|2 (read per plan: tunable at run time).
 int default_nv(DType dt, int k) {
-  const char* env = std::getenv("HEAT2D_TB_NV");  // read per plan: tunable at run time
-  (void)dt;
-  if (env) return (std::atoi(env) == 2 && k <= 8) ? 2 : 1;
-  // measured on MI355X (bench/sweep.py, 32768^2): 32 B/lane wins for fp64 while
-  // the kernel is still bandwidth-bound (k <= 6); beyond that the register
-  // state costs more occupancy than the halved halo redundancy returns
-  return (dt == DType::F64 && k <= 6) ? 2 : 1;
-}
-
-// Level pipeline skew (1: levels chained within a row iteration; 2: levels
-// independent, more ILP, +1 row of state per level). Override: HEAT2D_TB_SKEW.
-int default_skew(DType dt, int k) {
-  const char* env = std::getenv("HEAT2D_TB_SKEW");
+  if (const char* env = std::getenv("HEAT2D_TB_NV")) return std::atoi(env) == 2 ? 2 : 1;
   (void)dt;
   (void)k;
-  if (env) return std::atoi(env) == 2 ? 2 : 1;
-  return 1;  // skew-2's extra row of state per level costs more occupancy than its ILP returns (measured)
+  return 1;
 }
 
-// Prefetch depth (units of 3 rows). 6 rows in flight hides the HBM latency
-// of the compute-heavier deep pipelines; instantiated for 16 B/lane, skew 1.
-// Override: HEAT2D_TB_PF=1|2.
-int default_pf(DType dt, int k, int nv, int sk) {
-  if (nv != 1 || sk != 1) return 1;
-  const char* env = std::getenv("HEAT2D_TB_PF");
-  if (env) return std::atoi(env) == 2 ? 2 : 1;
-  return (dt == DType::F64 ? k >= 7 : k >= 9) ? 2 : 1;  // measured (bench/sweep.py, A/B in one box)
-}
-
-template <typename T>
-int occupancy(int nv, int sk, int pf, int k) {
-  if (nv == 1) {
-    if (sk == 2) return occupancy_blocks<T, 1, 2, 1>(k);
-    return pf == 2 ? occupancy_blocks<T, 1, 1, 2>(k) : occupancy_blocks<T, 1, 1, 1>(k);
+// Level-0 row ring per wave (RING - 2 rows in flight; the march loop is
+// unrolled RING times). Override: HEAT2D_TB_RING=4|6|8 (8 only for 16 B/lane).
+int default_ring(DType dt, int k, int nv) {
+  if (const char* env = std::getenv("HEAT2D_TB_RING")) {
+    const int r = std::atoi(env);
+    if (r == 4 || r == 6 || (r == 8 && nv == 1)) return r;
   }
-  return sk == 2 ? occupancy_blocks<T, 2, 2, 1>(k) : occupancy_blocks<T, 2, 1, 1>(k);
+  // measured on MI355X (bench/sweep.py, 32768^2, profiles/sweep_ring_tight_32768.txt)
+  if (dt == DType::F64) return k <= 10 ? 6 : 4;
+  return k <= 9 ? 4 : 6;
+}
+
+// Register budget: tight (occupancy target tight_waves()) or the compiler's
+// own. Override: HEAT2D_TB_TIGHT=0|1.
+bool default_tight(DType dt, int k, int nv, int ring) {
+  if (const char* env = std::getenv("HEAT2D_TB_TIGHT")) return std::atoi(env) != 0;
+  (void)dt;
+  (void)k;
+  (void)nv;
+  (void)ring;
+  return true;
 }
 
 template <typename T>
-void dispatch_variant(int nv, int sk, int pf, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
-                      hipStream_t st) {
-  if (nv == 1) {
-    if (sk == 2) dispatch<T, 1, 2, 1>(k, nblocks, s, d, a, r, st);
-    else if (pf == 2) dispatch<T, 1, 1, 2>(k, nblocks, s, d, a, r, st);
-    else dispatch<T, 1, 1, 1>(k, nblocks, s, d, a, r, st);
+int occupancy(int nv, int ring, int k, bool tight) {
+  if (nv == 2) return ring == 4 ? occupancy_blocks<T, 2, 4>(k, tight) : occupancy_blocks<T, 2, 6>(k, tight);
+  return ring == 4   ? occupancy_blocks<T, 1, 4>(k, tight)
+         : ring == 6 ? occupancy_blocks<T, 1, 6>(k, tight)
+                     : occupancy_blocks<T, 1, 8>(k, tight);
+}
+
+template <typename T>
+void dispatch_variant(int nv, int ring, bool tight, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a,
+                      T r, hipStream_t st) {
+  if (nv == 2) {
+    if (ring == 4) dispatch<T, 2, 4>(k, tight, nblocks, s, d, a, r, st);
+    else dispatch<T, 2, 6>(k, tight, nblocks, s, d, a, r, st);
   } else {
-    if (sk == 2) dispatch<T, 2, 2, 1>(k, nblocks, s, d, a, r, st);
-    else dispatch<T, 2, 1, 1>(k, nblocks, s, d, a, r, st);
+    if (ring == 4) dispatch<T, 1, 4>(k, tight, nblocks, s, d, a, r, st);
+    else if (ring == 6) dispatch<T, 1, 6>(k, tight, nblocks, s, d, a, r, st);
+    else dispatch<T, 1, 8>(k, tight, nblocks, s, d, a, r, st);
   }
 }
 
@@ -123,7 +122,7 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
   TbPlan p{};
   p.k = k;
   const int nv = default_nv(dt, k);
-  p.skew = default_skew(dt, k);
+  p.skew = 1;
   const int vm = dt == DType::F32 ? 4 : 2;
   p.vec = nv * vm;
   p.strip_w = 64 * p.vec;
@@ -133,9 +132,10 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
     p.useful_w = nv == 1 ? useful_width<double, 1>(k) : useful_width<double, 2>(k);
   p.nstrips = (L.ncols + p.useful_w - 1) / p.useful_w;
   const int64_t rows = row_end - row_begin;
-  p.prefetch = 3 * default_pf(dt, k, nv, p.skew);
-  const int pf = p.prefetch / 3;
-  const int bpc = dt == DType::F32 ? occupancy<float>(nv, p.skew, pf, k) : occupancy<double>(nv, p.skew, pf, k);
+  p.prefetch = default_ring(dt, k, nv);
+  p.tight = default_tight(dt, k, nv, p.prefetch) ? 1 : 0;
+  const int bpc = dt == DType::F32 ? occupancy<float>(nv, p.prefetch, k, p.tight)
+                                   : occupancy<double>(nv, p.prefetch, k, p.tight);
   p.blocks_per_cu = bpc;
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;  // resident waves
   int64_t nbands;
@@ -161,6 +161,9 @@ void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_
                double r, hipStream_t stream, int64_t tile_rows, int cus) {
   HEAT2D_REQUIRE(k <= L.halo, "temporal depth exceeds the halo depth");
   HEAT2D_REQUIRE(L.cpad >= 16, "column padding too small for the strip halo");
+  // the march keeps row indices in 32 bits (scalar compares)
+  HEAT2D_REQUIRE(L.nrows_global + 2 * L.halo < (int64_t(1) << 31) && L.row0 < (int64_t(1) << 31),
+                 "row count exceeds the 32-bit row index of the stencil kernel");
   if (row_end <= row_begin) return;
   const TbPlan p = plan_tb(dt, L, row_begin, row_end, k, tile_rows, cus);
   TbArgs a{};
@@ -180,11 +183,11 @@ void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_
   if (dt == DType::F32) {
     const float* s = static_cast<const float*>(src) + o;
     float* d = static_cast<float*>(dst) + o;
-    dispatch_variant<float>(nv, p.skew, p.prefetch / 3, p.k, (unsigned)p.nblocks, s, d, a, (float)r, stream);
+    dispatch_variant<float>(nv, p.prefetch, p.tight != 0, p.k, (unsigned)p.nblocks, s, d, a, (float)r, stream);
   } else {
     const double* s = static_cast<const double*>(src) + o;
     double* d = static_cast<double*>(dst) + o;
-    dispatch_variant<double>(nv, p.skew, p.prefetch / 3, p.k, (unsigned)p.nblocks, s, d, a, r, stream);
+    dispatch_variant<double>(nv, p.prefetch, p.tight != 0, p.k, (unsigned)p.nblocks, s, d, a, r, stream);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("tb_kernel launch: ") + hipGetErrorString(e));

@@ -1,14 +1,14 @@
 // Device implementation of the temporal-blocked stencil (see stencil_tb.hip
-// for the design notes). Included by the per-(dtype, vector width)
-// instantiation units tb_*.hip so they compile in parallel.
+// for the design notes). Included by the per-(dtype, vector width, prefetch
+// ring) instantiation units tb_*.hip so they compile in parallel.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <type_traits>
 #include <cstdlib>
-#include <mutex>
 #include <map>
+#include <mutex>
+#include <type_traits>
 
 #include "heat2d/kernels.hpp"
 
@@ -28,6 +28,12 @@ struct Vec16<double> {
   using type = double __attribute__((ext_vector_type(2)));
   static constexpr int n = 2;
 };
+
+// Precision-preserving fma: __builtin_fma is the DOUBLE builtin — on floats it
+// silently promotes the whole update to fp64 (v_cvt_f64_f32 + fp64 VALU at half
+// rate, and a different rounding than the fp32 reference).
+__device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
 // DPP wave shifts (GFX9 family). wave_shr:1 -> lane i reads lane i-1;
 // wave_shl:1 -> lane i reads lane i+1. Lanes without a source get 0 (garbage
@@ -80,72 +86,65 @@ struct TbShape {
 
 // Branch-free memory access: every row load / store goes through a raw buffer
 // descriptor whose base is the (wave-uniform) row address; lanes that must not
-// touch memory carry an out-of-range voffset, so the hardware range check
-// returns 0 / drops the store instead of an exec-masked branch. With no
-// memory op under control flow, hipcc's waitcnt pass can count the prefetch
-// ring precisely (vmcnt(N>0)) instead of draining it every row.
+// touch memory carry an out-of-range voffset, and a store whose row is not an
+// output row gets a descriptor with num_records = 0, so the hardware range
+// check returns 0 / drops the access instead of an exec-masked branch. With no
+// memory op under control flow, the waitcnt pass counts the prefetch ring
+// precisely (vmcnt(N>0)) instead of draining it every row.
 constexpr int32_t kOob = (int32_t)0x80000000u;
-
-
-template <typename T>
-struct Bits;
-template <>
-struct Bits<float> {
-  using U = unsigned int;
-};
-template <>
-struct Bits<double> {
-  using U = unsigned long long;
-};
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
-// PF: prefetch depth in units of 3 rows (PF = 2 -> 6 rows in flight per wave).
-template <typename T, int NV, int K, bool EDGE, int PF>
+// One wave marching UP a column strip (decreasing row index) with K time
+// levels pipelined in registers.
+//
+// At march row m the wave loads level-0 row m and computes row m+s of level s
+// (s = 1..K) from level s-1 rows m+s+1 (south, x+1: the OLDEST, produced two
+// iterations ago), m+s (centre) and m+s-1 (north, x-1: produced earlier in
+// THIS iteration). The reference sums T(x+1,y) + T(x,y+1) + T(x-1,y) + T(x,y-1)
+// (fortran/hip/heat_kernel.cpp:43) — south first — so marching upward lets the
+// partial (S + E) be formed from the oldest row BEFORE that row's register is
+// overwritten by the level's new row. Each level therefore keeps 2 rows of
+// state (ring indexed by iteration parity) instead of 3, and the dependency
+// chain from the fresh row is 5 ops instead of 6 — both with the reference's
+// exact operation order (bitwise identical results).
+//
+// Level 0 lives directly in the RING-slot load ring (row m in slot
+// phase(m) = (mtop - m) mod RING): a slot is refilled as soon as its row has
+// been used as a south neighbour, so RING - 2 rows are in flight and no
+// register ever receives a copy of a value with a pending load (which would
+// force a vmcnt drain). The loop is unrolled RING times so every slot is a
+// fixed register set. Row indices are 32-bit so every row test is a scalar
+// compare (gfx9 has no 64-bit scalar less-than).
+template <typename T, int NV, int K, bool EDGE, int RING>
 struct March {
   using S = TbShape<T, NV, K>;
   static constexpr int V = S::V;
   static constexpr int VM = S::VM;
+  static constexpr int KX = K > 1 ? K - 1 : 1;  // levels 1..K-1 kept in X
   using VT = typename Vec16<T>::type;
   using U4 = unsigned int __attribute__((ext_vector_type(4)));
+  static_assert(RING % 2 == 0 && RING >= 4, "ring must be even (parity-indexed level rings) and >= 4");
 
   const char* srow;  // byte address of (row 0, column -cpad) in src   [wave-uniform]
   char* drow;        // same in dst                                      [wave-uniform]
   int64_t pitch_b;   // bytes per row                                    [wave-uniform]
   uint32_t nrec;     // descriptor size (= pitch_b)
   T r;
-  int64_t t0, t1;    // output rows
-  int64_t fixed_lo, fixed_hi;
-  int64_t me;        // end of level-0 rows
+  int32_t t0, t1;    // output rows [t0, t1)
+  int32_t fixed_lo, fixed_hi;
+  int32_t mlo;       // lowest level-0 row (t0 - K)
   int32_t ld_off;    // per-lane load byte offset (kOob outside the allocation)
-  int32_t st_off;    // per-lane vector store offset (kOob unless all V columns are owned output)
-  int32_t st_e[EDGE ? V : 1];  // EDGE: per-element store offsets
-  unsigned fixmask;  // EDGE: per-element Dirichlet column bits
+  int32_t st_off;    // per-lane vector store offset (kOob unless the lane holds output columns)
+  bool fixed[EDGE ? V : 1];  // EDGE: element is a Dirichlet / pad column (kept at its value)
 
-  T X[3][K][V];      // level state: 3-phase rotating window (SSA after unroll)
-  // level-0 prefetch ring: 3*PFJ rows in flight; row m sits in Lb[m%3][0]
-  // when consumed, the slot's older entries shift down, row m+3*PFJ lands last
-  VT Lb[3][PF][NV];
+  T X[2][KX][V];     // levels 1..K-1: X[parity][level-1][elem]
+  VT Lb[RING][NV];   // level 0: load ring
 
-  template <int PH>
-  __device__ __forceinline__ void prefetch_advance(int64_t m) {
-#pragma unroll
-    for (int j = 0; j + 1 < PF; ++j)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) Lb[PH][j][v] = Lb[PH][j + 1][v];
-    const int64_t nxt = m + 3 * PF;
-    load_row(nxt < me ? nxt : me - 1, Lb[PH][PF - 1]);
-  }
-
-  __device__ __forceinline__ void prefetch_prime(int64_t mb) {
-#pragma unroll
-    for (int q = 0; q < 3 * PF; ++q) load_row(mb + q < me ? mb + q : me - 1, Lb[q % 3][q / 3]);
-  }
-
-  __device__ __forceinline__ void load_row(int64_t m, VT (&out)[NV]) const {
-    const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + m * pitch_b, nrec);
+  __device__ __forceinline__ void load_row(int32_t m, VT (&out)[NV]) const {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + (int64_t)m * pitch_b, nrec);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       U4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off + v * 16, 0, 0);
@@ -153,192 +152,142 @@ struct March {
     }
   }
 
-  __device__ __forceinline__ void store_row(int64_t row, const T (&out)[V]) const {
-    const __amdgpu_buffer_rsrc_t rs = row_rsrc(drow + row * pitch_b, nrec);
-    if (!EDGE) {
+  // live == false (priming rows): num_records 0 drops the whole store.
+  __device__ __forceinline__ void store_row(int32_t row, bool live, const T (&out)[V]) const {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(drow + (int64_t)row * pitch_b, live ? nrec : 0u);
 #pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        VT w;
+    for (int v = 0; v < NV; ++v) {
+      VT w;
 #pragma unroll
-        for (int e = 0; e < VM; ++e) w[e] = out[v * VM + e];
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off + v * 16, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < V; ++e) {
-        if constexpr (sizeof(T) == 4)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, out[e]), rs, st_e[e], 0, 0);
-        else
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(unsigned int __attribute__((ext_vector_type(2))), out[e]), rs, st_e[e], 0, 0);
-      }
+      for (int e = 0; e < VM; ++e) w[e] = out[v * VM + e];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off + v * 16, 0, 0);
     }
   }
 
-  template <int PH, bool STORE>
-  __device__ __forceinline__ void step(int64_t m) {
-    constexpr int PO = PH, PQ = (PH + 1) % 3, PN = (PH + 2) % 3;
-    // level 0: consume the prefetched row m, refill the slot with row m+3
-    // (clamped to the last row: a harmless re-read keeps the loop branch-free)
+  __device__ __forceinline__ void unpack(const VT (&x)[NV], T (&out)[V]) const {
 #pragma unroll
     for (int v = 0; v < NV; ++v)
 #pragma unroll
-      for (int e = 0; e < VM; ++e) X[PN][0][v * VM + e] = Lb[PH][0][v][e];
-    prefetch_advance<PH>(m);
+      for (int e = 0; e < VM; ++e) out[v * VM + e] = x[v][e];
+  }
+
+  // part = S + E(C): the first partial sum of the reference order, from the
+  // level's oldest row S and the east neighbours of its centre row C.
+  __device__ __forceinline__ void partial(const T (&Sx)[V], const T (&C)[V], T (&part)[V]) const {
+    const T eastL = from_upper(C[0]);
+#pragma unroll
+    for (int e = 0; e < V; ++e) part[e] = Sx[e] + (e < V - 1 ? C[e + 1] : eastL);
+  }
+
+  // ((part + N) + W) then C + r*(sum - 4C), pinned columns / rows kept.
+  __device__ __forceinline__ void update(const T (&part)[V], const T (&C)[V], const T (&N)[V], int32_t row,
+                                         T (&out)[V]) const {
+    const T west0 = from_lower(C[V - 1]);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const T west = e > 0 ? C[e - 1] : west0;
+      // reference order: ((S + E) + N) + W - 4C; sum - 4C as fma(-4, C, sum)
+      // is bitwise identical (4C is exact) and saves one op; C + r*(...)
+      // stays unfused, as in the reference.
+      const T sum = (part[e] + N[e]) + west;
+      T val = C[e] + r * fma_t(T(-4), C[e], sum);
+      if constexpr (EDGE) val = fixed[e] ? C[e] : val;
+      out[e] = val;
+    }
+    if (EDGE && (row < fixed_lo || row >= fixed_hi)) {  // Dirichlet row (global frame): keep
+#pragma unroll
+      for (int e = 0; e < V; ++e) out[e] = C[e];
+    }
+  }
+
+  template <int PH>
+  __device__ __forceinline__ void step(int32_t m) {
+    constexpr int P = PH & 1, Q = P ^ 1;  // level rings: P = oldest row (-> new row), Q = centre
+    constexpr int sN = PH, sC = (PH + RING - 1) % RING, sS = (PH + RING - 2) % RING;  // level-0 slots
+    T part[V];
+    T C0[V], N0[V];
+    {
+      T S0[V];
+      unpack(Lb[sS], S0);
+      unpack(Lb[sC], C0);
+      partial(S0, C0, part);  // level 1's S+E
+    }
+    {  // row m+2 is dead: refill its slot with row m+2-RING (clamped: a harmless re-read).
+      // The scheduling fence keeps the load below the slot's last use: hoisted
+      // above it, the load would need a fresh register and a copy at the loop
+      // latch (which waits for the load and serialises the ring).
+      const int32_t nxt = m + 2 - RING;
+      __builtin_amdgcn_sched_barrier(0);
+      load_row(nxt >= mlo ? nxt : mlo, Lb[sS]);
+    }
+    unpack(Lb[sN], N0);
 #pragma unroll
     for (int s = 1; s <= K; ++s) {
-      const T* o = X[PO][s - 1];  // row m-s-1 (north, x-1)
-      const T* q = X[PQ][s - 1];  // row m-s   (centre)
-      const T* n = X[PN][s - 1];  // row m-s+1 (south, x+1)
-      const T west0 = from_lower(q[V - 1]);
-      const T eastL = from_upper(q[0]);
-      T out[V];
+      T C[V], N[V], out[V], nxtpart[V];
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        const T west = e > 0 ? q[e - 1] : west0;
-        const T east = e < V - 1 ? q[e + 1] : eastL;
-        // reference order: T(x+1,y) + T(x,y+1) + T(x-1,y) + T(x,y-1) - 4*T(x,y).
-        // sum - 4c as fma(-4, c, sum) is bitwise identical (4c is exact) and
-        // saves one fp op; c + r*(...) stays unfused, as in the reference.
-        const T sum = ((n[e] + east) + o[e]) + west;
-        T val = q[e] + r * __builtin_fma(T(-4), q[e], sum);
-        if (EDGE && ((fixmask >> e) & 1u)) val = q[e];
-        out[e] = val;
+        C[e] = s == 1 ? C0[e] : X[Q][s > 1 ? s - 2 : 0][e];  // row m+s   (centre)
+        N[e] = s == 1 ? N0[e] : X[P][s > 1 ? s - 2 : 0][e];  // row m+s-1 (north, x-1; fresh)
       }
-      const int64_t row = m - s;
-      if (EDGE && (row < fixed_lo || row >= fixed_hi)) {  // Dirichlet row (global frame): keep
-#pragma unroll
-        for (int e = 0; e < V; ++e) out[e] = q[e];
-      }
+      if (s < K) partial(X[P][s - 1], X[Q][s - 1], nxtpart);  // level s+1's S+E, before level s's new row lands
+      update(part, C, N, m + s, out);
       if (s < K) {
 #pragma unroll
-        for (int e = 0; e < V; ++e) X[PN][s][e] = out[e];
-      } else if (STORE) {
-        store_row(row, out);
+        for (int e = 0; e < V; ++e) X[P][s - 1][e] = out[e];
+#pragma unroll
+        for (int e = 0; e < V; ++e) part[e] = nxtpart[e];
+      } else {
+        store_row(m + s, m + s < t1 && m + s >= t0, out);
       }
     }
   }
 
-  // Levels are primed for 2K rows (no output yet), then every row m in
-  // [t0+K, t1+K) emits output row m-K.
+  // March rows m = t1+K-1 down to t0-K (level-0 rows [t0-K, t1+K)). Level K
+  // row m+K is an output row once m+K < t1: the first 2K iterations only prime
+  // the levels (their stores are dropped by the descriptor). The trip count is
+  // rounded up to whole RING-phase bodies (the extra rows re-read row t0-K and
+  // their stores are dropped too): a loop body with a single exit, so no
+  // load can be sunk past a mid-body exit (which would serialise the ring).
   __device__ __forceinline__ void run() {
-    const int64_t mb = t0 - K;
-    me = t1 + K;
-    prefetch_prime(mb);
-    int64_t m = mb;
+    mlo = t0 - K;
+    const int32_t mtop = t1 + K - 1;
+    // slots 0..RING-3: rows mtop, mtop-1, ...; slots RING-2 / RING-1 stand for
+    // rows mtop+2 / mtop+1 (priming only: their results are never stored)
+#pragma unroll
+    for (int q = 0; q < RING - 2; ++q) load_row(mtop - q >= mlo ? mtop - q : mlo, Lb[q]);
+#pragma unroll
+    for (int q = RING - 2; q < RING; ++q)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) Lb[q][v] = VT{};
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int s = 0; s < KX; ++s)
+#pragma unroll
+        for (int e = 0; e < V; ++e) X[p][s][e] = T(0);
+    const int32_t iters = mtop - mlo + 1;
+    const int32_t bodies = (iters + RING - 1) / RING;
+    int32_t m = mtop;
 #pragma unroll 1
-    for (int i = 0; i < (2 * K) / 3; ++i) {
-      step<0, false>(m++);
-      step<1, false>(m++);
-      step<2, false>(m++);
-    }
-    constexpr int P0 = (2 * K) % 3;
-    if constexpr (P0 >= 1) step<0, false>(m++);
-    if constexpr (P0 >= 2) step<1, false>(m++);
-    // main loop: m in [t0+K, me), at least one row (t1 > t0)
-    for (;;) {
-      step<P0, true>(m);
-      if (++m >= me) break;
-      step<(P0 + 1) % 3, true>(m);
-      if (++m >= me) break;
-      step<(P0 + 2) % 3, true>(m);
-      if (++m >= me) break;
+    for (int32_t b = 0; b < bodies; ++b) {
+      step<0>(m);
+      step<1>(m - 1);
+      step<2>(m - 2);
+      step<3>(m - 3);
+      if constexpr (RING >= 6) {
+        step<4 % RING>(m - 4);
+        step<5 % RING>(m - 5);
+      }
+      if constexpr (RING >= 8) {
+        step<6 % RING>(m - 6);
+        step<7 % RING>(m - 7);
+      }
+      m -= RING;
     }
   }
 };
 
-// Skew-2 pipeline. Level s computes row m-2s at march row m (instead of m-s),
-// so within one row iteration the K levels read only rows produced in EARLIER
-// iterations: the K level updates are mutually independent (ILP = K*V instead
-// of V; the skew-1 pipeline chains all K levels through the freshly computed
-// south neighbour, a 6-deep fp dependency per level). Levels are evaluated
-// from K down to 1 so each level reads its 3 input rows before the level below
-// overwrites the oldest of them: 3 rows per level, ring index (row mod 3).
-template <typename T, int NV, int K, bool EDGE, int PF>
-struct March2 : March<T, NV, K, EDGE, PF> {
-  using B = March<T, NV, K, EDGE, PF>;
-  using B::r;
-  using B::X;
-  using B::Lb;
-  using B::me;
-  using B::t0;
-  using B::t1;
-  static constexpr int V = B::V;
-  static constexpr int VM = B::VM;
-  int64_t mend;  // end of march rows (t1 + 2K)
-
-  template <int PH, bool STORE>
-  __device__ __forceinline__ void step2(int64_t m) {
-#pragma unroll
-    for (int s = K; s >= 1; --s) {
-      // level s-1 rows m-2s-1 (north), m-2s (centre), m-2s+1 (south); slot = row mod 3
-      constexpr int dummy = 0;
-      (void)dummy;
-      const int so = ((PH - 2 * s - 1) % 3 + 3) % 3;
-      const int sq = ((PH - 2 * s) % 3 + 3) % 3;
-      const int sn = ((PH - 2 * s + 1) % 3 + 3) % 3;
-      const T* o = X[so][s - 1];
-      const T* q = X[sq][s - 1];
-      const T* n = X[sn][s - 1];
-      const T west0 = from_lower(q[V - 1]);
-      const T eastL = from_upper(q[0]);
-      T out[V];
-#pragma unroll
-      for (int e = 0; e < V; ++e) {
-        const T west = e > 0 ? q[e - 1] : west0;
-        const T east = e < V - 1 ? q[e + 1] : eastL;
-        const T sum = ((n[e] + east) + o[e]) + west;
-        T val = q[e] + r * __builtin_fma(T(-4), q[e], sum);
-        if (EDGE && ((B::fixmask >> e) & 1u)) val = q[e];
-        out[e] = val;
-      }
-      const int64_t row = m - 2 * s;
-      if (EDGE && (row < B::fixed_lo || row >= B::fixed_hi)) {
-#pragma unroll
-        for (int e = 0; e < V; ++e) out[e] = q[e];
-      }
-      if (s < K) {
-        const int sw = ((PH - 2 * s) % 3 + 3) % 3;  // slot of row m-2s
-#pragma unroll
-        for (int e = 0; e < V; ++e) X[sw][s][e] = out[e];
-      } else if (STORE) {
-        B::store_row(row, out);
-      }
-    }
-    // level 0: row m lands in slot (m mod 3) = PH (level 1 has consumed row m-3)
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-#pragma unroll
-      for (int e = 0; e < VM; ++e) X[PH][0][v * VM + e] = Lb[PH][0][v][e];
-    B::template prefetch_advance<PH>(m);
-  }
-
-  // level-0 rows [t0-K, t1+K); march rows [t0-K, t1+2K); output row m-2K for
-  // m >= t0+2K (the first 3K rows only prime the levels)
-  __device__ __forceinline__ void run() {
-    const int64_t mb = t0 - K;
-    me = t1 + K;
-    mend = t1 + 2 * K;
-    B::prefetch_prime(mb);
-    int64_t m = mb;
-    // phase PH = (m - mb) mod 3 (mb plays the role of row 0 for the rings)
-#pragma unroll 1
-    for (int i = 0; i < K; ++i) {  // 3K priming rows
-      step2<0, false>(m++);
-      step2<1, false>(m++);
-      step2<2, false>(m++);
-    }
-    for (;;) {
-      step2<0, true>(m);
-      if (++m >= mend) break;
-      step2<1, true>(m);
-      if (++m >= mend) break;
-      step2<2, true>(m);
-      if (++m >= mend) break;
-    }
-  }
-};
-
-template <typename T, int NV, int K, bool EDGE, int SK, int PF>
+template <typename T, int NV, int K, bool EDGE, int RING>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
                                       int64_t t1, int lane) {
   using S = TbShape<T, NV, K>;
@@ -348,39 +297,54 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   const int64_t c0 = u0 - S::KA;
   const int64_t mycol = c0 + (int64_t)lane * V;
   const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
-  using M = typename std::conditional<SK == 2, March2<T, NV, K, EDGE, PF>, March<T, NV, K, EDGE, PF>>::type;
-  M w;
+  March<T, NV, K, EDGE, RING> w;
   // row base = column col_lo (= -cpad) of row 0; offsets are relative to it
   w.srow = reinterpret_cast<const char*>(src + a.col_lo);
   w.drow = reinterpret_cast<char*>(dst + a.col_lo);
   w.pitch_b = a.pitch * ES;
   w.nrec = (uint32_t)(a.pitch * ES);
   w.r = r;
-  w.t0 = t0;
-  w.t1 = t1;
-  w.fixed_lo = a.fixed_lo;
-  w.fixed_hi = a.fixed_hi;
+  w.t0 = (int32_t)t0;
+  w.t1 = (int32_t)t1;
+  w.fixed_lo = (int32_t)a.fixed_lo;
+  w.fixed_hi = (int32_t)a.fixed_hi;
   const int32_t off = (int32_t)((mycol - a.col_lo) * ES);
   const bool in_alloc = (mycol >= a.col_lo) && (mycol + V <= a.col_hi);
   w.ld_off = in_alloc ? off : kOob;
-  const bool full = (mycol >= u0) && (mycol + V <= ustop);
-  w.st_off = full ? off : kOob;
-  unsigned fm = 0;
+  // Strip boundaries u0 are multiples of V, so a lane holds either only halo
+  // columns or only useful ones — except the lane straddling ncols, whose
+  // vector also covers the Dirichlet column / right pad. Those elements are
+  // pinned (fixed[]) to their src value at every level, so storing the whole
+  // vector writes them back unchanged: one 16-B store per lane, no per-element
+  // stores. (dst's frame equals src's frame by construction.)
+  const bool useful = (mycol >= u0) && (mycol < ustop);
+  w.st_off = useful && in_alloc ? off : kOob;
   if constexpr (EDGE) {
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       const int64_t c = mycol + e;
-      if (c < 0 || c >= a.ncols) fm |= 1u << e;
-      w.st_e[e] = (c >= u0 && c < ustop) ? off + e * ES : kOob;
+      w.fixed[e] = (c < 0 || c >= a.ncols);
     }
   }
-  w.fixmask = fm;
   w.run();
 }
 
-template <typename T, int NV, int K, int SK, int PF>
-__global__ __launch_bounds__(256) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a,
-                                                 T r) {
+// Occupancy target for the "tight" instantiation. Left alone, the scheduler
+// spends registers on ILP (e.g. fp64, 16 B/lane, K = 10: 169 VGPRs -> 2
+// waves/SIMD); told to fit 3 waves it needs 161 and spills nothing. The
+// estimate is the level state (2 rows x K-1 levels), the load ring and a
+// measured overhead (address/DPP/transient registers); waves = 512 / VGPRs.
+template <typename T, int NV, int K, int RING>
+constexpr int tight_waves() {
+  const int need = 8 * NV * (K - 1) + 4 * NV * RING + (sizeof(T) == 8 ? 48 : 72) + 16 * NV + 4 * (RING - 4);
+  const int alloc = (need + 7) / 8 * 8;
+  const int w = 512 / alloc;
+  return w > 8 ? 8 : (w < 3 ? 1 : w);  // <= 2 waves: no constraint (the compiler has 256 VGPRs)
+}
+
+template <typename T, int NV, int K, int RING, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void tb_kernel(
+    const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
   using S = TbShape<T, NV, K>;
   const int lane = threadIdx.x & 63;
   // readfirstlane: make the wave id (and everything derived from it: strip, rows,
@@ -404,20 +368,20 @@ __global__ __launch_bounds__(256) void tb_kernel(const T* __restrict__ src, T* _
     const int64_t t0 = a.row_begin + r0, t1 = a.row_begin + r1;
     const bool edge = (c0 < 0) || (c0 + S::W > a.ncols) || (t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi);
     if (edge)
-      march<T, NV, K, true, SK, PF>(src, dst, a, r, strip, t0, t1, lane);
+      march<T, NV, K, true, RING>(src, dst, a, r, strip, t0, t1, lane);
     else
-      march<T, NV, K, false, SK, PF>(src, dst, a, r, strip, t0, t1, lane);
+      march<T, NV, K, false, RING>(src, dst, a, r, strip, t0, t1, lane);
   }
 }
 
-template <typename T, int NV, int K, int SK, int PF>
+template <typename T, int NV, int K, int RING, int WPE>
 constexpr auto kernel_ptr() {
-  return &tb_kernel<T, NV, K, SK, PF>;
+  return &tb_kernel<T, NV, K, RING, WPE>;
 }
 
 // Resident 256-thread workgroups per CU for one kernel instance (occupancy
 // API; these kernels use ~44 SGPRs, inside the range where the API is exact).
-template <typename T, int NV, int K, int SK, int PF>
+template <typename T, int NV, int K, int RING, int WPE>
 int blocks_per_cu() {
   static std::mutex mu;
   static std::map<int, int> cache;  // device -> blocks/CU
@@ -427,28 +391,65 @@ int blocks_per_cu() {
   auto it = cache.find(dev);
   if (it != cache.end()) return it->second;
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, SK, PF>()), 256, 0) !=
-          hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, RING, WPE>()),
+                                                   256, 0) != hipSuccess ||
       nb <= 0)
     nb = 1;
   cache[dev] = nb;
   return nb;
 }
 
-// Per-(T, NV) entry points, explicitly instantiated in tb_<dtype>_nv<NV>.hip
-// (one translation unit each, compiled in parallel).
-template <typename T, int NV, int SK, int PF>
-void dispatch(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
-template <typename T, int NV, int SK, int PF>
-int occupancy_blocks(int k);
+// Per-(T, NV, RING) entry points, explicitly instantiated in tb_<dtype>_nv<NV>_r<RING>.hip
+// (one translation unit each, compiled in parallel). tight: use the
+// tight_waves() occupancy target (else the compiler's own register budget).
+template <typename T, int NV, int RING>
+void dispatch(int k, bool tight, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
+template <typename T, int NV, int RING>
+int occupancy_blocks(int k, bool tight);
 
-#define H2D_TB_CASE(T, NV, SK, PF, KK)                                                              \
-  case KK:                                                                                          \
-    hipLaunchKernelGGL((tb_kernel<T, NV, KK, SK, PF>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
+#define H2D_TB_CASE(T, NV, RING, KK)                                                                       \
+  case KK:                                                                                                 \
+    if (tight)                                                                                             \
+      hipLaunchKernelGGL((tb_kernel<T, NV, KK, RING, tight_waves<T, NV, KK, RING>()>), dim3(nblocks),      \
+                         dim3(256), 0, s, src, dst, a, r);                                                 \
+    else                                                                                                   \
+      hipLaunchKernelGGL((tb_kernel<T, NV, KK, RING, 1>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
     return;
-#define H2D_OCC_CASE(T, NV, SK, PF, KK) \
-  case KK:                              \
-    return blocks_per_cu<T, NV, KK, SK, PF>();
+#define H2D_OCC_CASE(T, NV, RING, KK) \
+  case KK:                            \
+    return tight ? blocks_per_cu<T, NV, KK, RING, tight_waves<T, NV, KK, RING>()>() : blocks_per_cu<T, NV, KK, RING, 1>();
+
+// Instantiate dispatch/occupancy for K = 1..16 of one (T, NV, RING).
+#define H2D_TB_UNIT(T, NV, RING)                                                                      \
+  template <>                                                                                         \
+  void dispatch<T, NV, RING>(int k, bool tight, unsigned nblocks, const T* src, T* dst, const TbArgs& a, \
+                             T r, hipStream_t s) {                                                    \
+    switch (k) {                                                                                      \
+      H2D_TB_CASE(T, NV, RING, 1) H2D_TB_CASE(T, NV, RING, 2) H2D_TB_CASE(T, NV, RING, 3)             \
+      H2D_TB_CASE(T, NV, RING, 4) H2D_TB_CASE(T, NV, RING, 5) H2D_TB_CASE(T, NV, RING, 6)             \
+      H2D_TB_CASE(T, NV, RING, 7) H2D_TB_CASE(T, NV, RING, 8) H2D_TB_CASE(T, NV, RING, 9)             \
+      H2D_TB_CASE(T, NV, RING, 10) H2D_TB_CASE(T, NV, RING, 11) H2D_TB_CASE(T, NV, RING, 12)          \
+      H2D_TB_CASE(T, NV, RING, 13) H2D_TB_CASE(T, NV, RING, 14) H2D_TB_CASE(T, NV, RING, 15)          \
+      H2D_TB_CASE(T, NV, RING, 16)                                                                    \
+      default:                                                                                        \
+        break;                                                                                        \
+    }                                                                                                 \
+    HEAT2D_REQUIRE(false, "temporal depth not instantiated for this variant");                        \
+  }                                                                                                   \
+  template <>                                                                                         \
+  int occupancy_blocks<T, NV, RING>(int k, bool tight) {                                              \
+    switch (k) {                                                                                      \
+      H2D_OCC_CASE(T, NV, RING, 1) H2D_OCC_CASE(T, NV, RING, 2) H2D_OCC_CASE(T, NV, RING, 3)          \
+      H2D_OCC_CASE(T, NV, RING, 4) H2D_OCC_CASE(T, NV, RING, 5) H2D_OCC_CASE(T, NV, RING, 6)          \
+      H2D_OCC_CASE(T, NV, RING, 7) H2D_OCC_CASE(T, NV, RING, 8) H2D_OCC_CASE(T, NV, RING, 9)          \
+      H2D_OCC_CASE(T, NV, RING, 10) H2D_OCC_CASE(T, NV, RING, 11) H2D_OCC_CASE(T, NV, RING, 12)       \
+      H2D_OCC_CASE(T, NV, RING, 13) H2D_OCC_CASE(T, NV, RING, 14) H2D_OCC_CASE(T, NV, RING, 15)       \
+      H2D_OCC_CASE(T, NV, RING, 16)                                                                   \
+      default:                                                                                        \
+        break;                                                                                        \
+    }                                                                                                 \
+    return 1;                                                                                         \
+  }
 
 }  // namespace tbimpl
 }  // namespace kern

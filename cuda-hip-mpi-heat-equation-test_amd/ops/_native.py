@@ -73,7 +73,7 @@ class TbPlan(C.Structure):
         ("k", C.c_int32), ("vec", C.c_int32), ("strip_w", C.c_int32), ("useful_w", C.c_int32),
         ("tile_rows", C.c_int64), ("nstrips", C.c_int64), ("ntiles", C.c_int64),
         ("nwaves", C.c_int64), ("nblocks", C.c_int64),
-        ("skew", C.c_int32), ("blocks_per_cu", C.c_int32), ("prefetch", C.c_int32), ("reserved_", C.c_int32),
+        ("skew", C.c_int32), ("blocks_per_cu", C.c_int32), ("prefetch", C.c_int32), ("tight", C.c_int32),
     ]
 
 

@@ -29,6 +29,24 @@ def test_hip_matches_golden_bitwise(gpu, native, dtype, tb):
     s.close()
 
 
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("tb", [1, 4, 7, 10, 16])
+def test_hip_sine_bitwise(gpu, native, dtype, tb):
+    """Non-dyadic data (the sine eigenmode): every rounding step of the update
+    is exercised, so an fp32 kernel that silently computes in fp64 (or any
+    reassociation) fails here."""
+    p = prob(301, 29, "ghost", "sine")
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0)
+    # host IC (device sin() and NumPy's may differ in the last ulp; the frame is exactly 0)
+    s.upload(R.owned(R.initial_field(p, npdt)))
+    s.step(p.ntime)
+    got = s.download()
+    ref = R.owned(R.ftcs(p, dtype=npdt))
+    assert np.array_equal(got, ref), np.abs(got.astype(np.float64) - ref).max()
+    s.close()
+
+
 @pytest.mark.parametrize("n", [3, 17, 64, 130, 257, 1000])
 def test_hip_sizes(gpu, native, n):
     p = prob(n, 21, "ghost", "uniform")

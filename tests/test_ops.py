@@ -38,8 +38,16 @@ def run_guard(device, dtype, n, k, rows, row0=0, nrows=None, tile_rows=0):
     rb, re = rows
     assert np.array_equal(got[rb:re], ref[rb:re])
     v = K.view2d(dst, L).cpu().numpy().copy()
+    sv = K.view2d(src, L).cpu().numpy()
     v[L.halo + rb:L.halo + re, L.cpad:L.cpad + L.ncols] = np.nan
-    assert np.isnan(v).all(), "kernel wrote outside its output rectangle"
+    # The only writes allowed outside the output rectangle: the HIP kernel's
+    # last 16-B vector of a row may cover the right Dirichlet column / pad of
+    # the SAME output rows, written back with src's (pinned) values.
+    rr, cc = np.nonzero(~np.isnan(v))
+    assert ((rr >= L.halo + rb) & (rr < L.halo + re)).all(), "kernel wrote outside its output rows"
+    assert (cc >= L.cpad + L.ncols).all(), "kernel wrote left of / inside the owned columns"
+    assert (cc < L.cpad + L.ncols + 8).all(), "kernel wrote beyond one vector of right pad"
+    assert np.array_equal(v[rr, cc], sv[rr, cc]), "frame / pad write changed a value"
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
