@@ -40,7 +40,13 @@ def main():
     ap.add_argument("--tb", type=int, default=10, help="time steps fused per HBM pass (measured best fp64: 10)")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--comm-cus", type=int, default=0, help="CUs reserved for bands + RCCL (0: default, -1: none)")
     ap.add_argument("--check", action="store_true", help="print field statistics after the run")
+    ap.add_argument("--rows", type=int, default=0,
+                    help="with --rehearse-comm: rows of the slab (e.g. 4096 = one of 8 ranks of 32768)")
+    ap.add_argument("--rehearse-comm", action="store_true",
+                    help="1 GPU only: run the multi-GPU schedule (bands + RCCL self-exchange beside a CU-masked "
+                         "interior) to measure its per-rank cost; not the headline (periodic halo)")
     args = ap.parse_args()
 
     import torch
@@ -57,13 +63,20 @@ def main():
 
     import heat2d
     from heat2d.models.heat2d import HeatSolver
-    from heat2d.parallel.transport import RcclTransport, SelfTransport
+    from heat2d.parallel.transport import RcclLoopTransport, RcclTransport, SelfTransport
 
     inp = heat2d.InputDat(n=args.n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
-    tr = RcclTransport(rank, world, local) if world > 1 else SelfTransport()
+    if world > 1:
+        tr = RcclTransport(rank, world, local)
+    elif args.rehearse_comm:
+        tr = RcclLoopTransport(local)
+    else:
+        tr = SelfTransport()
+    rows = args.rows if (args.rows and world == 1) else None
     s = HeatSolver(prob, dtype=args.dtype, backend="hip", tb=args.tb, overlap=not args.no_overlap,
-                   tile_rows=args.tile_rows, transport=tr, device=local)
+                   tile_rows=args.tile_rows, transport=tr, device=local, rows=rows,
+                   comm_cus=args.comm_cus)
 
     def barrier():
         if world > 1:
@@ -86,7 +99,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    pts = float(prob.n_owned) ** 2
+    pts = float(prob.n_owned) * float(rows or prob.n_owned)
     gpts = pts * args.steps / elapsed / 1e9
     es = 8 if args.dtype == "fp64" else 4
     info = s.info()
@@ -110,10 +123,10 @@ def main():
             "data": "synthetic (reference benchmark IC: T=2 interior, Dirichlet T=1 frame)",
             "config": {
                 "model": "heat2d FTCS 5-point, fortran/hip/input.dat (32768 0.25 0.05 1.0 25000 0)",
-                "grid": [prob.n_owned, prob.n_owned],
+                "grid": [rows or prob.n_owned, prob.n_owned],
                 "global_batch": 1,
                 "seq_len": prob.n_owned,
-                "parallelism": f"slab{world}",
+                "parallelism": f"slab{world}" + ("-rehearsal" if args.rehearse_comm and world == 1 else ""),
                 "temporal_block": tb,
                 "overlap": not args.no_overlap,
             },

@@ -170,6 +170,10 @@ int heat2d_transport_rccl(const void* uid128, int rank, int size, int device, vo
   return guarded([&] { *out = new TransportHandle{make_rccl_transport(uid128, rank, size, device)}; });
 }
 
+int heat2d_transport_rccl_loop(int device, void** out) {
+  return guarded([&] { *out = new TransportHandle{make_rccl_loop_transport(device)}; });
+}
+
 int heat2d_transport_callback(heat2d_exchange_fn ex, heat2d_allreduce_fn ar, heat2d_barrier_fn br, void* ctx,
                               int rank, int size, void** out) {
   return guarded([&] {

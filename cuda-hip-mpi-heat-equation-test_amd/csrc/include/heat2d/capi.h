@@ -86,6 +86,8 @@ int heat2d_cpu_stats(int dtype, const void* field, const void* other, const heat
 int heat2d_rccl_unique_id(void* out128);
 int heat2d_transport_self(void** out);
 int heat2d_transport_rccl(const void* uid128, int rank, int size, int device, void** out);
+/* 1-rank periodic self-exchange over RCCL: perf rehearsal of the multi-GPU schedule on one GPU */
+int heat2d_transport_rccl_loop(int device, void** out);
 int heat2d_transport_callback(heat2d_exchange_fn ex, heat2d_allreduce_fn ar, heat2d_barrier_fn br,
                               void* ctx, int rank, int size, void** out);
 int heat2d_transport_free(void* t);

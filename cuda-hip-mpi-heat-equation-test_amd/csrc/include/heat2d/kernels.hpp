@@ -39,6 +39,10 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
 // recognised from L.row0 / L.nrows_global and kept fixed).
 void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin,
                int64_t row_end, int k, double r, hipStream_t stream, int64_t tile_rows = 0, int cus = 0);
+// Same for TWO disjoint row ranges [rb0, re0) and [rb1, re1) in one launch
+// (the slab's two boundary bands in the overlapped schedule).
+void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t rb0, int64_t re0, int64_t rb1,
+                int64_t re1, int k, double r, hipStream_t stream, int64_t tile_rows = 0, int cus = 0);
 
 // Initial / boundary condition kinds (covers every IC of the reference
 // variants, see models/presets.py for the mapping).

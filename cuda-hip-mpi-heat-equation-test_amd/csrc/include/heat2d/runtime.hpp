@@ -4,9 +4,9 @@
 // heat_eqn, fortran/mpi+cuda/heat.F90) with one engine that
 //   * keeps two pitched fields (ping-pong, no per-step D2D copy),
 //   * advances K steps per HBM pass (temporal blocking, kernels.hpp),
-//   * splits each cycle into boundary bands + interior so the halo exchange of
-//     the bands (RCCL send/recv on a comm stream, zero-copy rows) overlaps the
-//     interior kernel, ordered only by hipEvents,
+//   * splits each cycle into boundary bands + interior: the bands and their
+//     halo exchange (RCCL send/recv, zero-copy rows) run on a comm stream
+//     beside the interior kernel, ordered only by hipEvents (solver.cpp),
 //   * runs the same schedule on a CPU backend (for CPU-only CI with gloo) and
 //     on a loopback group (P slabs on one GPU, bitwise == P=1).
 #pragma once
@@ -40,7 +40,7 @@ struct SolverConfig {
   int32_t use_graph;   // 1: replay cycles from a captured hipGraph
   int64_t tile_rows;   // 0: auto
   int64_t halo;        // 0: auto (= kMaxTB)
-  int32_t comm_cus;    // P>1 overlap: CUs kept free of the compute stream for RCCL (0: default 8, -1: none)
+  int32_t comm_cus;    // P>1 overlap: >0 CUs masked off the compute stream; 0 soft (interior planned for ncu-2); -1 none
   int32_t reserved_;
 };
 
@@ -63,6 +63,8 @@ class Transport {
   virtual void barrier() = 0;
   virtual std::string name() const = 0;
   virtual bool capturable() const { return false; }  // safe inside hipGraph capture
+  // true if exchange() moves data (size > 1, or a 1-rank periodic rehearsal)
+  virtual bool exchanges() const { return size() > 1; }
 };
 
 std::shared_ptr<Transport> make_self_transport();
@@ -71,6 +73,11 @@ std::shared_ptr<Transport> make_self_transport();
 // shared variable for thread-per-GPU).
 std::shared_ptr<Transport> make_rccl_transport(const void* uid, int rank, int size, int device);
 void rccl_unique_id(void* out128);
+// 1-rank RCCL communicator whose exchange sends the slab's boundary rows to
+// ITSELF (periodic wrap) — a performance rehearsal of the multi-GPU schedule
+// (bands + RCCL kernels + CU-masked interior) on one GPU. Not for physics:
+// it overwrites the Dirichlet frame rows.
+std::shared_ptr<Transport> make_rccl_loop_transport(int device);
 // Host callbacks (Python / gloo, tests). Buffers passed are host pointers to
 // packed rows (k*ncols elements): send_lo/send_hi may be null at domain ends.
 struct CallbackOps {
@@ -157,7 +164,7 @@ class Solver {
   int64_t band_ = 0;     // boundary band rows (= halo exchange depth = K)
   hipStream_t s_compute_ = nullptr, s_comm_ = nullptr;
   bool own_streams_ = false;
-  hipEvent_t ev_bnd_ = nullptr, ev_comm_ = nullptr;
+  hipEvent_t ev_bnd_ = nullptr, ev_comm_ = nullptr, ev_int_ = nullptr;
   double* d_work_ = nullptr;   // stats workspace + 6 results
   bool timing_ = false;
   int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all

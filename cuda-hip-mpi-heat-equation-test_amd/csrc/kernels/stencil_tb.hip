@@ -119,6 +119,7 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
                int cus) {
   HEAT2D_REQUIRE(k >= 1 && k <= kMaxTB, "k must be in [1, kMaxTB]");
   HEAT2D_REQUIRE(row_begin >= 0 && row_end <= L.nrows && row_begin < row_end, "bad row range");
+  HEAT2D_REQUIRE(L.cpad >= 16, "column padding too small for the strip halo");
   TbPlan p{};
   p.k = k;
   const int nv = default_nv(dt, k);
@@ -159,22 +160,47 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
 
 void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k,
                double r, hipStream_t stream, int64_t tile_rows, int cus) {
+  launch_tb2(dt, src, dst, L, row_begin, row_end, 0, 0, k, r, stream, tile_rows, cus);
+}
+
+void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t rb0, int64_t re0, int64_t rb1,
+                int64_t re1, int k, double r, hipStream_t stream, int64_t tile_rows, int cus) {
   HEAT2D_REQUIRE(k <= L.halo, "temporal depth exceeds the halo depth");
   HEAT2D_REQUIRE(L.cpad >= 16, "column padding too small for the strip halo");
   // the march keeps row indices in 32 bits (scalar compares)
   HEAT2D_REQUIRE(L.nrows_global + 2 * L.halo < (int64_t(1) << 31) && L.row0 < (int64_t(1) << 31),
                  "row count exceeds the 32-bit row index of the stencil kernel");
-  if (row_end <= row_begin) return;
-  const TbPlan p = plan_tb(dt, L, row_begin, row_end, k, tile_rows, cus);
+  if (re0 <= rb0) {  // range 1 only
+    rb0 = rb1;
+    re0 = re1;
+    rb1 = re1 = 0;
+  }
+  if (re0 <= rb0) return;
+  const int64_t n0 = re0 - rb0, n1 = re1 > rb1 ? re1 - rb1 : 0;
+  HEAT2D_REQUIRE(n1 == 0 || rb1 >= 0 && re1 <= L.nrows, "bad second row range");
+  // plan over the concatenated rows, then give each range its share of bands
+  TbPlan p = plan_tb(dt, L, 0, n0 + n1, k, tile_rows, cus);
+  int64_t nb0 = p.ntiles;
+  if (n1 > 0) {
+    const int64_t nb = std::max<int64_t>(p.ntiles, 2);
+    nb0 = std::min<int64_t>(nb - 1, std::max<int64_t>(1, (nb * n0 + (n0 + n1) / 2) / (n0 + n1)));
+    const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * p.blocks_per_cu * 4;
+    p.ntiles = nb;
+    p.nwaves = std::max<int64_t>(1, std::min<int64_t>(nb * p.nstrips, slots));
+    p.nblocks = (p.nwaves + 3) / 4;
+  }
   TbArgs a{};
   a.pitch = L.pitch;
   a.ncols = L.ncols;
   a.col_lo = -L.cpad;
   a.col_hi = L.col_hi();
-  a.row_begin = row_begin;
-  a.row_end = row_end;
+  a.row_begin = rb0;
+  a.row_end = re0;
+  a.row_begin1 = rb1;
+  a.row_end1 = n1 > 0 ? re1 : rb1;
   a.nstrips = p.nstrips;
   a.nbands = p.ntiles;
+  a.nbands0 = nb0;
   a.nwaves = p.nwaves;
   a.fixed_lo = -L.row0;
   a.fixed_hi = L.nrows_global - L.row0;

@@ -67,9 +67,11 @@ struct TbArgs {
   int64_t ncols;
   int64_t col_lo;  // allocation column bounds [col_lo, col_hi)
   int64_t col_hi;
-  int64_t row_begin, row_end;
+  int64_t row_begin, row_end;    // row range 0
+  int64_t row_begin1, row_end1;  // row range 1 (may be empty): both boundary bands in ONE launch
   int64_t nstrips;
-  int64_t nbands;  // row bands (work item = band x strip)
+  int64_t nbands;   // row bands (work item = band x strip)
+  int64_t nbands0;  // bands [0, nbands0) split range 0, the rest split range 1
   int64_t nwaves;  // launched waves (grid-stride over items)
   int64_t fixed_lo, fixed_hi;  // local rows outside [fixed_lo, fixed_hi) are Dirichlet
 };
@@ -354,18 +356,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
   // Work items = (row band, strip), band-major: consecutive waves take adjacent
   // strips of the same band, so the waves in flight stream whole contiguous
   // rows (HBM page locality) and all march in step.
-  const int64_t rows = a.row_end - a.row_begin;
   const int64_t items = a.nbands * a.nstrips;
   for (int64_t it = wid; it < items; it += a.nwaves) {
     const int64_t band = it / a.nstrips;
     const int64_t strip = it - band * a.nstrips;
-    const int64_t r0 = band * rows / a.nbands;
-    const int64_t r1 = (band + 1) * rows / a.nbands;
+    const bool second = band >= a.nbands0;
+    const int64_t rb = second ? a.row_begin1 : a.row_begin;
+    const int64_t rows = second ? a.row_end1 - a.row_begin1 : a.row_end - a.row_begin;
+    const int64_t bl = second ? band - a.nbands0 : band;
+    const int64_t nb = second ? a.nbands - a.nbands0 : a.nbands0;
+    const int64_t r0 = bl * rows / nb;
+    const int64_t r1 = (bl + 1) * rows / nb;
     if (r1 <= r0) continue;
     // safe path: the strip reaches a Dirichlet/pad column, or the march's
     // rows [t0-K, t1+K) reach a Dirichlet row; everything else runs mask-free
     const int64_t c0 = strip * S::U - S::KA;
-    const int64_t t0 = a.row_begin + r0, t1 = a.row_begin + r1;
+    const int64_t t0 = rb + r0, t1 = rb + r1;
     const bool edge = (c0 < 0) || (c0 + S::W > a.ncols) || (t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi);
     if (edge)
       march<T, NV, K, true, RING>(src, dst, a, r, strip, t0, t1, lane);

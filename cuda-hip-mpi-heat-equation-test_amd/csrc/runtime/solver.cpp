@@ -5,12 +5,24 @@
 // pack; sync; 2 D2H; 2 blocking MPI_Sendrecv; 2 H2D; unpack (+sync) — all
 // serialised on the null stream.
 //
-// Here, per cycle of k <= K steps (one HBM pass):
-//   compute stream:  wait(ev_comm) -> tb(bands [0,B) and [n-B,n)) -> record(ev_bnd)
-//                    -> tb(interior [B, n-B))                      (runs concurrently)
-//   comm stream:     wait(ev_bnd) -> RCCL grouped send/recv of B rows -> record(ev_comm)
-// with ping-pong buffers (no copy). Ordering is carried entirely by events;
-// the host never synchronises inside the loop.
+// Here, per cycle of k <= K steps (one HBM pass), src -> dst (ping-pong, no
+// copy), with B = K boundary rows per side:
+//   compute stream: wait(ev_bnd: previous bands) -> tb(interior [B, n-B))
+//                   -> record(ev_int)
+//   comm stream:    wait(ev_int: previous interior) -> tb(bands [0,B) and
+//                   [n-B,n), ONE launch) -> record(ev_bnd) -> RCCL grouped
+//                   send/recv of the B band rows -> record(ev_comm)
+// The interior never reads ghost rows (it reads owned rows [0, n)), so it
+// does not wait for any exchange: interiors run back to back on the compute
+// stream (CU-masked, leaving a few CUs to the comm stream) while the bands and
+// the halo exchange of the same cycle proceed beside them. Ordering is carried
+// entirely by events; the host never synchronises inside the loop. Hazards
+// covered (cycle c, src_c = dst_{c-1}):
+//   * interior c reads src_c band rows written by bands c-1, and overwrites
+//     dst_c rows that bands c-1 read                         -> wait ev_bnd
+//   * bands c read src_c rows next to the bands written by interior c-1, and
+//     overwrite dst_c band rows that interior c-1 read       -> wait ev_int
+//   * bands c read ghost rows received by exchange c-1       -> comm-stream order
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -72,30 +84,41 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     } else {
       int ncu = 0;
       H2D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg_.device));
-      const int reserve = cfg_.comm_cus < 0 ? 0 : (cfg_.comm_cus == 0 ? 8 : cfg_.comm_cus);
-      if (P > 1 && cfg_.overlap && reserve > 0 && reserve < ncu) {
-        // The persistent stencil kernel fills every resident wave slot; RCCL's
-        // send/recv kernels would then only start after it (no overlap) or
-        // delay some of its waves (a tail). Keep `reserve` CUs, spread over the
-        // XCDs, out of the compute stream's CU mask so the halo exchange always
-        // finds room, and plan the stencil grid for the remaining CUs.
+      int want = cfg_.comm_cus;
+      if (want == 0) {
+        if (const char* env = std::getenv("HEAT2D_COMM_CUS")) want = std::atoi(env);
+      }
+      const bool ovl = tr_->exchanges() && cfg_.overlap;
+      if (ovl && want > 0 && want < ncu) {
+        // Hard reservation: `want` CUs, spread over the XCDs, out of the
+        // compute stream's CU mask. Measured on MI355X (rehearsal, 4096 x 32768
+        // fp64 slab, profiles/overlap_rehearsal.md): 8 masked CUs cost the
+        // interior ~20 %, far more than 8/256 — kept as an option only.
         std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
         for (int i = 0; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
-        for (int j = 0; j < reserve; ++j) {
-          const int i = (int)((int64_t)j * ncu / reserve);
+        for (int j = 0; j < want; ++j) {
+          const int i = (int)((int64_t)j * ncu / want);
           mask[(size_t)i / 32] &= ~(1u << (i % 32));
         }
         H2D_HIP(hipExtStreamCreateWithCUMask(&s_compute_, (uint32_t)mask.size(), mask.data()));
-        compute_cus_ = ncu - reserve;
+        compute_cus_ = ncu - want;
       } else {
+        // Soft reservation (default): no mask; the persistent interior grid is
+        // planned for ncu - 2 CUs, so the bands' and RCCL's workgroups always
+        // find free wave slots beside it (measured: 2387 vs 2408 Gpts/s for
+        // the same slab without any exchange).
         H2D_HIP(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
+        if (ovl && want == 0 && ncu > 16) compute_cus_ = ncu - 2;
       }
       H2D_HIP(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
       own_streams_ = true;
     }
     H2D_HIP(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_comm_, hipEventDisableTiming));
+    H2D_HIP(hipEventCreateWithFlags(&ev_int_, hipEventDisableTiming));
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
   } else {
     for (int b = 0; b < 2; ++b) buf_[b] = host_alloc(bytes);
     cfg_.overlap = 0;
@@ -114,6 +137,7 @@ Solver::~Solver() {
     if (d_work_) (void)hipFree(d_work_);
     if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
+    if (ev_int_) (void)hipEventDestroy(ev_int_);
     if (own_streams_) {
       (void)hipStreamDestroy(s_compute_);
       (void)hipStreamDestroy(s_comm_);
@@ -151,7 +175,7 @@ void Solver::launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k
 }
 
 void Solver::exchange_on(void* field, hipStream_t s) {
-  if (tr_->size() == 1) return;
+  if (!tr_->exchanges()) return;
   tr_->exchange(field, L_, dtype(), band_, s, hip_);
 }
 
@@ -173,22 +197,18 @@ void Solver::cycle_overlap(int k) {
   void* src = buf_[cur_];
   void* dst = buf_[cur_ ^ 1];
   const int64_t n = L_.nrows, B = band_;
-  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
-  if (n <= 2 * B) {
-    launch_tb(src, dst, 0, n, k);
-    H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
-    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_bnd_, 0));
-    exchange_on(dst, s_comm_);
-    H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
-  } else {
-    launch_tb(src, dst, 0, B, k);
-    launch_tb(src, dst, n - B, n, k);
-    H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
-    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_bnd_, 0));
-    exchange_on(dst, s_comm_);
-    H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
-    launch_tb(src, dst, B, n - B, k);
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));  // bands c-1 (record not yet replaced)
+  H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));     // interior c-1
+  if (n > 2 * B) {
+    kern::launch_tb(dtype(), src, dst, L_, B, n - B, k, cfg_.r, s_compute_, cfg_.tile_rows, compute_cus_);
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    kern::launch_tb2(dtype(), src, dst, L_, 0, B, n - B, n, k, cfg_.r, s_comm_, 0, 0);
+  } else {  // slab no thicker than its two bands: all of it beside the exchange
+    kern::launch_tb(dtype(), src, dst, L_, 0, n, k, cfg_.r, s_comm_, 0, 0);
   }
+  H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+  exchange_on(dst, s_comm_);
+  H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
   cycle_swap();
 }
 
@@ -232,7 +252,7 @@ void Solver::step(int64_t n) {
     return;
   }
   const int K = cfg_.tb;
-  const bool multi = tr_->size() > 1;
+  const bool multi = tr_->exchanges();
   int64_t left = n;
   while (left > 0) {
     if (cfg_.use_graph && hip_ && (!multi || tr_->capturable()) && !cfg_.overlap && left >= 2 * K &&

@@ -47,7 +47,8 @@ class SelfTransport final : public Transport {
 // ------------------------------------------------------------------ RCCL
 class RcclTransport final : public Transport {
  public:
-  RcclTransport(const void* uid, int rank, int size, int device) : rank_(rank), size_(size) {
+  RcclTransport(const void* uid, int rank, int size, int device, bool loop = false)
+      : rank_(rank), size_(size), loop_(loop && size == 1) {
     if (device >= 0) H2D_HIP(hipSetDevice(device));
     H2D_HIP(hipGetDevice(&device_));
     ncclUniqueId id;
@@ -63,18 +64,28 @@ class RcclTransport final : public Transport {
   }
   int rank() const override { return rank_; }
   int size() const override { return size_; }
-  std::string name() const override { return "rccl"; }
+  std::string name() const override { return loop_ ? "rccl-loop" : "rccl"; }
   bool capturable() const override { return true; }
+  bool exchanges() const override { return size_ > 1 || loop_; }
 
   void exchange(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
                 bool on_device) override {
     HEAT2D_REQUIRE(on_device, "RCCL transport needs device-resident fields");
-    if (size_ == 1 || k <= 0) return;
+    if ((size_ == 1 && !loop_) || k <= 0) return;
     const size_t es = dtype_size(dt);
     char* base = static_cast<char*>(field);
     auto row_ptr = [&](int64_t i) { return base + (size_t)((i + L.halo) * L.pitch) * es; };
     const size_t count = (size_t)(k * L.pitch);  // whole padded rows: contiguous, zero-copy
     const ncclDataType_t t = dt == DType::F32 ? ncclFloat32 : ncclFloat64;
+    if (loop_) {  // periodic self-exchange (rehearsal): same message sizes and kernels as 2 peers
+      H2D_NCCL(ncclGroupStart());
+      H2D_NCCL(ncclSend(row_ptr(0), count, t, 0, comm_, stream));
+      H2D_NCCL(ncclRecv(row_ptr(L.nrows), count, t, 0, comm_, stream));
+      H2D_NCCL(ncclSend(row_ptr(L.nrows - k), count, t, 0, comm_, stream));
+      H2D_NCCL(ncclRecv(row_ptr(-k), count, t, 0, comm_, stream));
+      H2D_NCCL(ncclGroupEnd());
+      return;
+    }
     H2D_NCCL(ncclGroupStart());
     if (rank_ > 0) {
       H2D_NCCL(ncclSend(row_ptr(0), count, t, rank_ - 1, comm_, stream));
@@ -103,6 +114,7 @@ class RcclTransport final : public Transport {
 
  private:
   int rank_, size_;
+  bool loop_ = false;
   int device_ = 0;
   ncclComm_t comm_ = nullptr;
   hipStream_t aux_ = nullptr;
@@ -179,6 +191,12 @@ std::shared_ptr<Transport> make_self_transport() { return std::make_shared<SelfT
 
 std::shared_ptr<Transport> make_rccl_transport(const void* uid, int rank, int size, int device) {
   return std::make_shared<RcclTransport>(uid, rank, size, device);
+}
+
+std::shared_ptr<Transport> make_rccl_loop_transport(int device) {
+  ncclUniqueId id;
+  H2D_NCCL(ncclGetUniqueId(&id));
+  return std::make_shared<RcclTransport>(&id, 0, 1, device, true);
 }
 
 void rccl_unique_id(void* out128) {

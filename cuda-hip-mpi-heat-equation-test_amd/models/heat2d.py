@@ -54,12 +54,18 @@ class HeatSolver:
         graph: replay step pairs from a captured hipGraph (single-rank / serial schedule).
         transport: a :class:`parallel.transport.Transport`; default picks self / RCCL / gloo.
         device: HIP device ordinal (default: torch's current device).
+        comm_cus: room for the bands + RCCL beside the interior kernel when
+            overlapping: >0 CUs masked off the compute stream; 0 (default, or
+            $HEAT2D_COMM_CUS) interior planned for all CUs but 2, no mask; -1 none.
+        rows: solve only the first ``rows`` x-rows of the grid (a rectangular
+            rows x n domain, e.g. one rank's slab shape for a 1-GPU rehearsal).
     """
 
     def __init__(self, problem: Problem, *, dtype: str = "fp64", backend: str = "auto", tb: int = 8,
                  overlap: bool = True, copy_swap: bool = False, managed: bool = False, graph: bool = False,
                  tile_rows: int = 0, halo: int = 0, transport: Optional[T.Transport] = None,
-                 device: Optional[int] = None, init: bool = True):
+                 device: Optional[int] = None, init: bool = True, rows: Optional[int] = None,
+                 comm_cus: int = 0):
         self.problem = problem
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]
@@ -70,7 +76,9 @@ class HeatSolver:
         self.device = -1 if self.backend == "cpu" else int(device)
         self.transport = transport or T.default_transport(self.backend, None if self.device < 0 else self.device)
         cfg = N.Config()
-        cfg.n_rows = problem.n_owned
+        if rows is not None and not 1 <= rows <= problem.n_owned:
+            raise ValueError(f"rows must be in [1, {problem.n_owned}]")
+        cfg.n_rows = problem.n_owned if rows is None else int(rows)  # rows < n: the first rows x n of the grid
         cfg.n_cols = problem.n_owned
         cfg.dtype = self.dtype
         cfg.backend = N.BACKEND_HIP if self.backend == "hip" else N.BACKEND_CPU
@@ -83,6 +91,7 @@ class HeatSolver:
         cfg.use_graph = int(graph)
         cfg.tile_rows = tile_rows
         cfg.halo = halo
+        cfg.comm_cus = comm_cus
         self._cfg = cfg
         h = C.c_void_p()
         N.call("heat2d_solver_create", C.byref(cfg), self.transport.handle, C.byref(h))

@@ -108,6 +108,7 @@ _SIGS = {
     "heat2d_rccl_unique_id": (C.c_int, [_P]),
     "heat2d_transport_self": (C.c_int, [C.POINTER(_P)]),
     "heat2d_transport_rccl": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
+    "heat2d_transport_rccl_loop": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "heat2d_transport_callback": (C.c_int, [EXCHANGE_FN, ALLREDUCE_FN, BARRIER_FN, _P, C.c_int, C.c_int,
                                             C.POINTER(_P)]),
     "heat2d_transport_free": (C.c_int, [_P]),

@@ -9,6 +9,8 @@ Here a transport is a native object the solver calls once per cycle:
   solver's comm stream (device-direct; the production path, one process or one
   host thread per GPU). The 128-byte ``ncclUniqueId`` is created by rank 0 and
   broadcast through ``torch.distributed`` (any backend) or passed explicitly.
+* :class:`RcclLoopTransport` — 1-rank periodic self-exchange: perf rehearsal of the
+  multi-GPU schedule on one GPU.
 * :class:`TorchDistTransport` — host callbacks over ``torch.distributed`` point-to-point
   (gloo on CPU): runs the *same native schedule* in CPU-only multi-process CI.
 * :class:`CallbackTransport` — any Python callables (tests, custom fabrics).
@@ -66,6 +68,19 @@ class RcclTransport(Transport):
         h = C.c_void_p()
         N.call("heat2d_transport_rccl", buf, rank, size, device, C.byref(h))
         super().__init__(h, rank, size, "rccl")
+
+
+class RcclLoopTransport(Transport):
+    """1-rank RCCL communicator exchanging the slab's boundary rows with ITSELF
+    (periodic wrap): rehearses the multi-GPU schedule — boundary bands and RCCL
+    send/recv kernels on the comm stream beside a CU-masked interior — on one
+    GPU, with the same message sizes. Performance only: it overwrites the
+    Dirichlet frame rows, so the physics is not the problem's."""
+
+    def __init__(self, device: int):
+        h = C.c_void_p()
+        N.call("heat2d_transport_rccl_loop", device, C.byref(h))
+        super().__init__(h, 0, 1, "rccl-loop")
 
 
 def broadcast_unique_id(rank: int, group=None) -> bytes:

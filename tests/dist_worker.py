@@ -12,6 +12,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def random_field(prob, dtype):
+    """Frame-inclusive field: the problem's frame, seeded uniform noise inside."""
+    import numpy as np
+    from heat2d.models import reference as R
+    dt = np.float64 if dtype == "fp64" else np.float32
+    T0 = R.initial_field(prob, dt)
+    T0[1:-1, 1:-1] = np.random.default_rng(1234).random(T0[1:-1, 1:-1].shape).astype(dt)
+    return T0
+
+
 def main():
     rank, world, port, outdir = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     args = json.loads(sys.argv[5])
@@ -32,6 +42,11 @@ def main():
     tr = TorchDistTransport()
     s = HeatSolver(prob, dtype=args.get("dtype", "fp64"), backend=backend, tb=args.get("tb", 8),
                    overlap=args.get("overlap", True), transport=tr, device=0 if backend == "hip" else None)
+    if args.get("random"):  # non-trivial data everywhere: a stale halo cannot hide
+        from heat2d.models import reference as R
+        T0 = random_field(prob, args.get("dtype", "fp64"))
+        lay = s.layout
+        s.upload(R.owned(T0)[lay.row0:lay.row0 + lay.nrows])
     # split the stepping to exercise restarts of the cycle schedule
     first = args["steps"] // 3
     s.step(first)

@@ -54,12 +54,16 @@ def golden(args):
     inp = heat2d.InputDat(n=args["n"], sigma=0.25, nu=0.05, dom_len=args.get("dom", 1.0), ntime=args["steps"])
     prob = heat2d.make_problem(inp, args.get("conv", "ghost"), args.get("ic", "uniform"))
     dt = np.float64 if args.get("dtype", "fp64") == "fp64" else np.float32
+    if args.get("random"):
+        sys.path.insert(0, HERE)
+        from dist_worker import random_field
+        return R.owned(R.ftcs(prob, dtype=dt, T0=random_field(prob, args.get("dtype", "fp64"))))
     return R.owned(R.ftcs(prob, dtype=dt))
 
 
 @pytest.mark.parametrize("world,tb", [(2, 1), (2, 8), (3, 3), (4, 5)])
 def test_gloo_cpu_bitwise(native, tmp_path, world, tb):
-    args = {"n": 67, "steps": 23, "tb": tb, "backend": "cpu"}
+    args = {"n": 67, "steps": 23, "tb": tb, "backend": "cpu", "random": True}
     got, meta = run_world(tmp_path, world, args)
     assert np.array_equal(got, golden(args))
     assert meta["info"]["size"] == world
@@ -73,8 +77,12 @@ def test_gloo_cpu_inclusive_fp32(native, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,tb,overlap", [(2, 8, True), (3, 4, True), (2, 6, False), (4, 8, True)])
-def test_gloo_hip_ranks_share_gpu(native, gpu, tmp_path, world, tb, overlap):
-    args = {"n": 301, "steps": 37, "tb": tb, "backend": "hip", "overlap": overlap}
+@pytest.mark.parametrize("world,tb,overlap,n", [(2, 8, True, 301), (3, 4, True, 301), (2, 6, False, 301),
+                                                (4, 8, True, 301), (4, 8, True, 60), (2, 10, True, 1500)])
+def test_gloo_hip_ranks_share_gpu(native, gpu, tmp_path, world, tb, overlap, n):
+    """Overlapped schedule (interior on the compute stream, bands + exchange on
+    the comm stream) on random data; n=60 at 4 ranks makes every slab thinner
+    than its two bands (the all-on-comm-stream branch)."""
+    args = {"n": n, "steps": 37, "tb": tb, "backend": "hip", "overlap": overlap, "random": True}
     got, meta = run_world(tmp_path, world, args)
     assert np.array_equal(got, golden(args))
