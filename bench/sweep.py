@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--repeats", type=int, default=3)
     ap.add_argument("--copy-swap", action="store_true", help="also time the reference-parity copy schedule")
     ap.add_argument("--variants", nargs="+", default=["default"],
-                    help="kernel variants nv<1|2>r<4|6|8>[t<0|1>] (HEAT2D_TB_NV / _RING / _TIGHT), or default")
+                    help="kernel variants r<4|6>[s] (HEAT2D_TB_RING; s = serial schedule: one general launch per "
+                         "cycle instead of the MAIN + EDGE split), or default")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
 
@@ -44,14 +45,12 @@ def main():
     if args.copy_swap:
         configs += [(dt, 1, 0, True, "default") for dt in args.dtype]
     for dt, tb, tr, cs, var in configs:
-        for e in ("HEAT2D_TB_NV", "HEAT2D_TB_RING", "HEAT2D_TB_TIGHT"):
-            os.environ.pop(e, None)
-        if var != "default":  # nv<1|2>r<4|6|8>[t<0|1>]
-            os.environ["HEAT2D_TB_NV"] = var[2]
-            os.environ["HEAT2D_TB_RING"] = var[4]
-            if len(var) > 6:
-                os.environ["HEAT2D_TB_TIGHT"] = var[6]
-        s = HeatSolver(prob, dtype=dt, backend="hip", tb=tb, tile_rows=tr, copy_swap=cs, device=0)
+        os.environ.pop("HEAT2D_TB_RING", None)
+        serial = var.endswith("s")
+        if var.startswith("r"):  # r<4|6>[s]
+            os.environ["HEAT2D_TB_RING"] = var[1]
+        s = HeatSolver(prob, dtype=dt, backend="hip", tb=tb, tile_rows=tr, copy_swap=cs, device=0,
+                       overlap=not serial)
         s.step(2 * tb)
         s.synchronize()
         times = []
@@ -65,7 +64,7 @@ def main():
         k = s.tb
         from heat2d.ops import _native as N
         plan = N.plan_tb(s.dtype, s.layout, 0, s.nrows, k)
-        rec = {"variant": var, "vec": plan.vec, "ring": plan.prefetch, "tight": plan.tight, "bpc": plan.blocks_per_cu,
+        rec = {"variant": var, "vec": plan.vec, "ring": plan.prefetch, "bpc": plan.blocks_per_cu,
                "nwaves": plan.nwaves, "dtype": dt, "tb": k, "tile_rows": tr, "copy_swap": cs, "n": args.n, "steps": args.steps,
                "gpts": pts * args.steps / med / 1e9, "gpts_best": pts * args.steps / min(times) / 1e9}
         rec["model_gbps"] = rec["gpts"] * ((4.0 * es) if cs else (2.0 * es / k))

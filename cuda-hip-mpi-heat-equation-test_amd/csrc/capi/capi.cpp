@@ -109,6 +109,14 @@ int heat2d_plan_tb(int dtype, const heat2d_layout* L, int64_t rb, int64_t re, in
   });
 }
 
+int heat2d_plan_split(int dtype, const heat2d_layout* L, int k, int64_t band, heat2d_split_plan* out) {
+  return guarded([&] {
+    kern::SplitPlan p = kern::plan_split((DType)dtype, to_layout(L), k, band);
+    static_assert(sizeof(heat2d_split_plan) == sizeof(kern::SplitPlan), "split plan ABI");
+    std::memcpy(out, &p, sizeof(p));
+  });
+}
+
 int heat2d_tb(int dtype, const void* src, void* dst, const heat2d_layout* L, int64_t rb, int64_t re, int k,
               double r, void* stream, int64_t tile_rows) {
   return guarded([&] { kern::launch_tb((DType)dtype, src, dst, to_layout(L), rb, re, k, r, as_stream(stream), tile_rows); });

@@ -37,8 +37,19 @@ typedef struct heat2d_config {
 typedef struct heat2d_tb_plan {
   int32_t k, vec, strip_w, useful_w;
   int64_t tile_rows, nstrips, ntiles, nwaves, nblocks;
-  int32_t skew, blocks_per_cu, prefetch, tight;
+  int32_t skew, blocks_per_cu, prefetch, main;
 } heat2d_tb_plan;
+
+typedef struct heat2d_rect {
+  int64_t r0, r1, s0, s1, nb;
+} heat2d_rect;
+
+typedef struct heat2d_split_plan {
+  int32_t k, ring, valid, nedge;
+  heat2d_rect main;
+  heat2d_rect edge[4];
+  int64_t main_waves, edge_waves, main_items, edge_items;
+} heat2d_split_plan;
 
 typedef int (*heat2d_exchange_fn)(void* ctx, void* send_lo, void* send_hi, void* recv_lo,
                                   void* recv_hi, int64_t count, int32_t dtype);
@@ -53,6 +64,8 @@ int heat2d_device_count(int* n);
 int heat2d_make_layout(int64_t nrows, int64_t ncols, int64_t halo, int64_t row0,
                        int64_t nrows_global, heat2d_layout* out);
 int heat2d_decompose(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nrows);
+/* MAIN + EDGE split of one cycle (the overlapped schedule's two launches) */
+int heat2d_plan_split(int dtype, const heat2d_layout* L, int k, int64_t band, heat2d_split_plan* out);
 int heat2d_plan_tb(int dtype, const heat2d_layout* L, int64_t rb, int64_t re, int k,
                    int64_t tile_rows, heat2d_tb_plan* out);
 

@@ -24,7 +24,7 @@ struct TbPlan {
   int32_t skew;       // level pipeline skew (always 1: upward march, see tb_impl.hpp)
   int32_t blocks_per_cu;  // resident workgroups per CU (occupancy API)
   int32_t prefetch;   // level-0 row ring per wave (RING; RING-2 rows in flight)
-  int32_t tight;      // 1: occupancy-targeted register budget (tight_waves)
+  int32_t main;       // 1: interior-only (MAIN) kernel instance
 };
 
 // Plan a launch that advances rows [row_begin, row_end) of the slab by k steps.
@@ -39,10 +39,29 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
 // recognised from L.row0 / L.nrows_global and kept fixed).
 void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin,
                int64_t row_end, int k, double r, hipStream_t stream, int64_t tile_rows = 0, int cus = 0);
-// Same for TWO disjoint row ranges [rb0, re0) and [rb1, re1) in one launch
-// (the slab's two boundary bands in the overlapped schedule).
+// Same for TWO disjoint row ranges [rb0, re0) and [rb1, re1) in one launch.
 void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t rb0, int64_t re0, int64_t rb1,
                 int64_t re1, int k, double r, hipStream_t stream, int64_t tile_rows = 0, int cus = 0);
+
+// Split schedule of one cycle (k steps over the whole slab) into two launches
+// on two streams:
+//   MAIN: rows [band, n-band), all strips — the interior kernel (no frame-row
+//         code: fewer registers), a persistent grid on all wave slots;
+//   EDGE: the two boundary bands (all strips), general kernel.
+// The caller orders them with events (solver.cpp). valid = 0: slab too thin
+// or narrow for the split (use launch_tb on the whole slab).
+struct TbRect {
+  int64_t r0, r1, s0, s1, nb;
+};
+struct SplitPlan {
+  int32_t k, ring, valid, nedge;
+  TbRect main;
+  TbRect edge[4];
+  int64_t main_waves, edge_waves, main_items, edge_items;
+};
+SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus = 0, int spare_waves = 0);
+void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
+                  double r, hipStream_t stream);
 
 // Initial / boundary condition kinds (covers every IC of the reference
 // variants, see models/presets.py for the mapping).

@@ -148,6 +148,7 @@ class Solver {
 
  private:
   void cycle_overlap(int k);
+  const kern::SplitPlan& split_plan(int k);
   void cycle_serial(int k);
   void cycle_copy_swap();
   void launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k);
@@ -168,6 +169,7 @@ class Solver {
   double* d_work_ = nullptr;   // stats workspace + 6 results
   bool timing_ = false;
   int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all
+  kern::SplitPlan split_[kMaxTB + 1] = {};  // per temporal depth (k == 0: not planned yet)
   hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K
   int graph_k_ = 0;
   std::vector<char> host_stage_;  // CPU-backend / callback staging

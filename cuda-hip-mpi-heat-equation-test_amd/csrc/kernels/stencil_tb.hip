@@ -30,6 +30,8 @@
 //     S = T(x+1,y), E = T(x,y+1), N = T(x-1,y), W = T(x,y-1)) and the file is
 //     built with -ffp-contract=off: results are bitwise identical to the CPU
 //     reference and to an unblocked K=1 run, in fp64 and in fp32.
+#include <cmath>
+
 #include "tb_impl.hpp"
 
 namespace heat2d {
@@ -51,92 +53,110 @@ int cu_count() {
   return n;
 }
 
-template <typename T, int NV>
-int useful_width(int k) {
-  constexpr int V = NV * Vec16<T>::n;
-  const int ka = (k + V - 1) / V * V;  // must match TbShape::KA
-  return 64 * V - 2 * ka;
+int vec_elems(DType dt) { return dt == DType::F32 ? 4 : 2; }
+// halo columns per strip side (whole lanes) and useful strip width; must match TbShape
+int halo_cols(DType dt, int k) {
+  const int v = vec_elems(dt);
+  return (k + v - 1) / v * v;
 }
-
-
-// Vector width (16-B vectors per lane). 2 halves the strip-halo redundancy
-// (and the DPP moves per point) but doubles the register state.
-// Override: HEAT2D_TB_NV=1|2 (read per plan: tunable at run time).
-int default_nv(DType dt, int k) {
-  if (const char* env = std::getenv("HEAT2D_TB_NV")) return std::atoi(env) == 2 ? 2 : 1;
-  (void)dt;
-  (void)k;
-  return 1;
-}
+int useful_width(DType dt, int k) { return 64 * vec_elems(dt) - 2 * halo_cols(dt, k); }
 
 // Level-0 row ring per wave (RING - 2 rows in flight; the march loop is
-// unrolled RING times). Override: HEAT2D_TB_RING=4|6|8 (8 only for 16 B/lane).
-int default_ring(DType dt, int k, int nv) {
+// unrolled RING times). Override: HEAT2D_TB_RING=4|6.
+int default_ring(DType dt, int k) {
   if (const char* env = std::getenv("HEAT2D_TB_RING")) {
     const int r = std::atoi(env);
-    if (r == 4 || r == 6 || (r == 8 && nv == 1)) return r;
+    if (r == 4 || r == 6) return r;
   }
-  // measured on MI355X (bench/sweep.py, 32768^2, profiles/sweep_ring_tight_32768.txt)
+  // measured on MI355X (bench/sweep.py, 32768^2, profiles/sweep_split_32768.txt)
   if (dt == DType::F64) return k <= 10 ? 6 : 4;
-  return k <= 9 ? 4 : 6;
+  return (k == 10 || k == 11) ? 6 : 4;
 }
 
-// Register budget: tight (occupancy target tight_waves()) or the compiler's
-// own. Override: HEAT2D_TB_TIGHT=0|1.
-bool default_tight(DType dt, int k, int nv, int ring) {
-  if (const char* env = std::getenv("HEAT2D_TB_TIGHT")) return std::atoi(env) != 0;
-  (void)dt;
-  (void)k;
-  (void)nv;
-  (void)ring;
-  return true;
-}
-
-template <typename T>
-int occupancy(int nv, int ring, int k, bool tight) {
-  if (nv == 2) return ring == 4 ? occupancy_blocks<T, 2, 4>(k, tight) : occupancy_blocks<T, 2, 6>(k, tight);
-  return ring == 4   ? occupancy_blocks<T, 1, 4>(k, tight)
-         : ring == 6 ? occupancy_blocks<T, 1, 6>(k, tight)
-                     : occupancy_blocks<T, 1, 8>(k, tight);
-}
-
-template <typename T>
-void dispatch_variant(int nv, int ring, bool tight, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a,
-                      T r, hipStream_t st) {
-  if (nv == 2) {
-    if (ring == 4) dispatch<T, 2, 4>(k, tight, nblocks, s, d, a, r, st);
-    else dispatch<T, 2, 6>(k, tight, nblocks, s, d, a, r, st);
-  } else {
-    if (ring == 4) dispatch<T, 1, 4>(k, tight, nblocks, s, d, a, r, st);
-    else if (ring == 6) dispatch<T, 1, 6>(k, tight, nblocks, s, d, a, r, st);
-    else dispatch<T, 1, 8>(k, tight, nblocks, s, d, a, r, st);
+int occupancy(DType dt, int ring, bool main, int k) {
+  if (dt == DType::F32) {
+    if (ring == 4) return main ? occupancy_blocks<float, 4, true>(k) : occupancy_blocks<float, 4, false>(k);
+    return main ? occupancy_blocks<float, 6, true>(k) : occupancy_blocks<float, 6, false>(k);
   }
+  if (ring == 4) return main ? occupancy_blocks<double, 4, true>(k) : occupancy_blocks<double, 4, false>(k);
+  return main ? occupancy_blocks<double, 6, true>(k) : occupancy_blocks<double, 6, false>(k);
+}
+
+template <typename T>
+void dispatch_t(int ring, bool main, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
+                hipStream_t st) {
+  if (ring == 4) {
+    if (main) dispatch<T, 4, true>(k, nblocks, s, d, a, r, st);
+    else dispatch<T, 4, false>(k, nblocks, s, d, a, r, st);
+  } else {
+    if (main) dispatch<T, 6, true>(k, nblocks, s, d, a, r, st);
+    else dispatch<T, 6, false>(k, nblocks, s, d, a, r, st);
+  }
+}
+
+void check_layout(const SlabLayout& L, int k) {
+  HEAT2D_REQUIRE(k >= 1 && k <= kMaxTB, "k must be in [1, kMaxTB]");
+  HEAT2D_REQUIRE(k <= L.halo, "temporal depth exceeds the halo depth");
+  HEAT2D_REQUIRE(L.cpad >= 16, "column padding too small for the strip halo");
+  // the march keeps row indices in 32 bits (scalar compares)
+  HEAT2D_REQUIRE(L.nrows_global + 2 * L.halo < (int64_t(1) << 31) && L.row0 < (int64_t(1) << 31),
+                 "row count exceeds the 32-bit row index of the stencil kernel");
+}
+
+// Launch `rects` (item counts from their nb and strip ranges) on `nwaves` waves.
+void launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
+                  const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream) {
+  HEAT2D_REQUIRE(nrect >= 1 && nrect <= kMaxRects, "bad rect count");
+  TbArgs a{};
+  a.pitch = L.pitch;
+  a.ncols = L.ncols;
+  a.col_lo = -L.cpad;
+  a.col_hi = L.col_hi();
+  a.fixed_lo = -L.row0;
+  a.fixed_hi = L.nrows_global - L.row0;
+  int64_t items = 0;
+  int q = 0;
+  for (int i = 0; i < nrect; ++i) {
+    const TbRect& R = rects[i];
+    if (R.r1 <= R.r0 || R.s1 <= R.s0 || R.nb <= 0) continue;
+    HEAT2D_REQUIRE(R.r0 >= 0 && R.r1 <= L.nrows, "rect rows outside the slab");
+    a.rect[q] = TbRectArg{R.r0, R.r1, R.s0, R.s1, R.nb, items};
+    items += R.nb * (R.s1 - R.s0);
+    ++q;
+  }
+  if (q == 0) return;
+  a.nrect = q;
+  a.nitems = items;
+  a.nwaves = std::max<int64_t>(1, std::min<int64_t>(nwaves, items));
+  const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
+  const int64_t o = L.origin();
+  if (dt == DType::F32)
+    dispatch_t<float>(ring, main, k, nblocks, static_cast<const float*>(src) + o, static_cast<float*>(dst) + o, a,
+                      (float)r, stream);
+  else
+    dispatch_t<double>(ring, main, k, nblocks, static_cast<const double*>(src) + o, static_cast<double*>(dst) + o,
+                       a, r, stream);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("tb_kernel launch: ") + hipGetErrorString(e));
 }
 
 }  // namespace
 
 TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k, int64_t tile_rows,
                int cus) {
-  HEAT2D_REQUIRE(k >= 1 && k <= kMaxTB, "k must be in [1, kMaxTB]");
+  check_layout(L, k);
   HEAT2D_REQUIRE(row_begin >= 0 && row_end <= L.nrows && row_begin < row_end, "bad row range");
-  HEAT2D_REQUIRE(L.cpad >= 16, "column padding too small for the strip halo");
   TbPlan p{};
   p.k = k;
-  const int nv = default_nv(dt, k);
   p.skew = 1;
-  const int vm = dt == DType::F32 ? 4 : 2;
-  p.vec = nv * vm;
+  p.vec = vec_elems(dt);
   p.strip_w = 64 * p.vec;
-  if (dt == DType::F32)
-    p.useful_w = nv == 1 ? useful_width<float, 1>(k) : useful_width<float, 2>(k);
-  else
-    p.useful_w = nv == 1 ? useful_width<double, 1>(k) : useful_width<double, 2>(k);
+  p.useful_w = useful_width(dt, k);
   p.nstrips = (L.ncols + p.useful_w - 1) / p.useful_w;
   const int64_t rows = row_end - row_begin;
-  p.prefetch = default_ring(dt, k, nv);
-  p.tight = default_tight(dt, k, nv, p.prefetch) ? 1 : 0;
-  const int bpc = dt == DType::F32 ? occupancy<float>(nv, p.prefetch, k, p.tight)
-                                   : occupancy<double>(nv, p.prefetch, k, p.tight);
+  p.prefetch = default_ring(dt, k);
+  p.main = 0;
+  const int bpc = occupancy(dt, p.prefetch, false, k);
   p.blocks_per_cu = bpc;
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;  // resident waves
   int64_t nbands;
@@ -150,11 +170,10 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
   }
   nbands = std::max<int64_t>(1, std::min<int64_t>(nbands, rows));
   const int64_t items = nbands * p.nstrips;
-  const int64_t nwaves = std::min<int64_t>(items, std::max<int64_t>(slots, 1));
   p.ntiles = nbands;
-  p.nwaves = nwaves;
+  p.nwaves = std::min<int64_t>(items, std::max<int64_t>(slots, 1));
   p.tile_rows = (rows + nbands - 1) / nbands;
-  p.nblocks = (nwaves + 3) / 4;
+  p.nblocks = (p.nwaves + 3) / 4;
   return p;
 }
 
@@ -165,58 +184,62 @@ void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_
 
 void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t rb0, int64_t re0, int64_t rb1,
                 int64_t re1, int k, double r, hipStream_t stream, int64_t tile_rows, int cus) {
-  HEAT2D_REQUIRE(k <= L.halo, "temporal depth exceeds the halo depth");
-  HEAT2D_REQUIRE(L.cpad >= 16, "column padding too small for the strip halo");
-  // the march keeps row indices in 32 bits (scalar compares)
-  HEAT2D_REQUIRE(L.nrows_global + 2 * L.halo < (int64_t(1) << 31) && L.row0 < (int64_t(1) << 31),
-                 "row count exceeds the 32-bit row index of the stencil kernel");
-  if (re0 <= rb0) {  // range 1 only
-    rb0 = rb1;
-    re0 = re1;
-    rb1 = re1 = 0;
-  }
-  if (re0 <= rb0) return;
-  const int64_t n0 = re0 - rb0, n1 = re1 > rb1 ? re1 - rb1 : 0;
-  HEAT2D_REQUIRE(n1 == 0 || rb1 >= 0 && re1 <= L.nrows, "bad second row range");
+  check_layout(L, k);
+  const int64_t n0 = std::max<int64_t>(0, re0 - rb0), n1 = std::max<int64_t>(0, re1 - rb1);
+  if (n0 + n1 == 0) return;
   // plan over the concatenated rows, then give each range its share of bands
-  TbPlan p = plan_tb(dt, L, 0, n0 + n1, k, tile_rows, cus);
-  int64_t nb0 = p.ntiles;
-  if (n1 > 0) {
-    const int64_t nb = std::max<int64_t>(p.ntiles, 2);
-    nb0 = std::min<int64_t>(nb - 1, std::max<int64_t>(1, (nb * n0 + (n0 + n1) / 2) / (n0 + n1)));
-    const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * p.blocks_per_cu * 4;
-    p.ntiles = nb;
-    p.nwaves = std::max<int64_t>(1, std::min<int64_t>(nb * p.nstrips, slots));
-    p.nblocks = (p.nwaves + 3) / 4;
-  }
-  TbArgs a{};
-  a.pitch = L.pitch;
-  a.ncols = L.ncols;
-  a.col_lo = -L.cpad;
-  a.col_hi = L.col_hi();
-  a.row_begin = rb0;
-  a.row_end = re0;
-  a.row_begin1 = rb1;
-  a.row_end1 = n1 > 0 ? re1 : rb1;
-  a.nstrips = p.nstrips;
-  a.nbands = p.ntiles;
-  a.nbands0 = nb0;
-  a.nwaves = p.nwaves;
-  a.fixed_lo = -L.row0;
-  a.fixed_hi = L.nrows_global - L.row0;
-  const int64_t o = L.origin();
-  const int nv = p.vec / (dt == DType::F32 ? 4 : 2);
-  if (dt == DType::F32) {
-    const float* s = static_cast<const float*>(src) + o;
-    float* d = static_cast<float*>(dst) + o;
-    dispatch_variant<float>(nv, p.prefetch, p.tight != 0, p.k, (unsigned)p.nblocks, s, d, a, (float)r, stream);
-  } else {
-    const double* s = static_cast<const double*>(src) + o;
-    double* d = static_cast<double*>(dst) + o;
-    dispatch_variant<double>(nv, p.prefetch, p.tight != 0, p.k, (unsigned)p.nblocks, s, d, a, r, stream);
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("tb_kernel launch: ") + hipGetErrorString(e));
+  const TbPlan p = plan_tb(dt, L, 0, std::min<int64_t>(n0 + n1, L.nrows), k, tile_rows, cus);
+  TbRect rects[2];
+  int nr = 0;
+  const int64_t nb = std::max<int64_t>(p.ntiles, (n0 > 0) + (n1 > 0));
+  const int64_t nb0 = n1 == 0 ? nb : (n0 == 0 ? 0 : std::min<int64_t>(nb - 1, std::max<int64_t>(1, (nb * n0 + (n0 + n1) / 2) / (n0 + n1))));
+  if (n0 > 0) rects[nr++] = TbRect{rb0, re0, 0, p.nstrips, std::min<int64_t>(nb0, n0)};
+  if (n1 > 0) rects[nr++] = TbRect{rb1, re1, 0, p.nstrips, std::min<int64_t>(nb - nb0, n1)};
+  const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * p.blocks_per_cu * 4;
+  launch_rects(dt, src, dst, L, k, p.prefetch, false, rects, nr, slots, r, stream);
+}
+
+SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus, int spare_waves) {
+  check_layout(L, k);
+  SplitPlan p{};
+  p.k = k;
+  p.ring = default_ring(dt, k);
+  const int64_t n = L.nrows, B = std::max<int64_t>(band, k);
+  const int64_t U = useful_width(dt, k);
+  const int64_t ns = (L.ncols + U - 1) / U;
+  const int64_t rows_m = n - 2 * B;
+  if (rows_m < 4 * k) return p;  // valid = 0: too thin to split
+  // MAIN: the interior rows, all strips, persistent (one item per resident wave)
+  const int bpc = occupancy(dt, p.ring, true, k);
+  const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
+  const int64_t mw = std::max<int64_t>(4, slots - std::max(0, spare_waves));
+  const int64_t min_rows = std::max<int64_t>(4 * (int64_t)k, 16);
+  int64_t nb_m = std::max<int64_t>(1, mw / ns);
+  nb_m = std::min<int64_t>(nb_m, std::max<int64_t>(1, rows_m / min_rows));
+  p.main = TbRect{B, n - B, 0, ns, nb_m};
+  p.main_items = nb_m * ns;
+  p.main_waves = std::min<int64_t>(p.main_items, mw);
+  // EDGE: the two boundary bands (one band each), general kernel. Short
+  // (B + 2k march rows per item): beside MAIN where wave slots allow, else
+  // right after it — either way the halo exchange that follows overlaps the
+  // NEXT cycle's MAIN, which does not wait for it.
+  p.edge[0] = TbRect{0, B, 0, ns, 1};
+  p.edge[1] = TbRect{n - B, n, 0, ns, 1};
+  p.nedge = 2;
+  p.edge_items = 2 * ns;
+  const int bpc_e = occupancy(dt, p.ring, false, k);
+  p.edge_waves = std::min<int64_t>(p.edge_items, (int64_t)cu_count() * bpc_e * 4);
+  p.valid = 1;
+  return p;
+}
+
+void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
+                  double r, hipStream_t stream) {
+  HEAT2D_REQUIRE(p.valid, "invalid split plan");
+  if (main_part)
+    launch_rects(dt, src, dst, L, p.k, p.ring, true, &p.main, 1, p.main_waves, r, stream);
+  else
+    launch_rects(dt, src, dst, L, p.k, p.ring, false, p.edge, p.nedge, p.edge_waves, r, stream);
 }
 
 }  // namespace kern

@@ -62,18 +62,26 @@ __device__ __forceinline__ double from_upper(double x) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Kernel arguments: the work is up to kMaxRects rectangles (output rows x
+// strips), each cut into `nb` row bands; a work item is one (band, strip) of
+// one rectangle. item0 = index of the rectangle's first item.
+constexpr int kMaxRects = 4;
+struct TbRectArg {
+  int64_t r0, r1;  // output rows [r0, r1)
+  int64_t s0, s1;  // strips [s0, s1)
+  int64_t nb;      // row bands
+  int64_t item0;
+};
 struct TbArgs {
   int64_t pitch;
   int64_t ncols;
   int64_t col_lo;  // allocation column bounds [col_lo, col_hi)
   int64_t col_hi;
-  int64_t row_begin, row_end;    // row range 0
-  int64_t row_begin1, row_end1;  // row range 1 (may be empty): both boundary bands in ONE launch
-  int64_t nstrips;
-  int64_t nbands;   // row bands (work item = band x strip)
-  int64_t nbands0;  // bands [0, nbands0) split range 0, the rest split range 1
+  int64_t nitems;  // total items over all rects
   int64_t nwaves;  // launched waves (grid-stride over items)
   int64_t fixed_lo, fixed_hi;  // local rows outside [fixed_lo, fixed_hi) are Dirichlet
+  int32_t nrect, pad_;
+  TbRectArg rect[kMaxRects];
 };
 
 template <typename T, int NV, int K>
@@ -120,7 +128,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uin
 // force a vmcnt drain). The loop is unrolled RING times so every slot is a
 // fixed register set. Row indices are 32-bit so every row test is a scalar
 // compare (gfx9 has no 64-bit scalar less-than).
-template <typename T, int NV, int K, bool EDGE, int RING>
+// Frame handling by edge kind EK (bit 0: the march reaches a Dirichlet ROW of
+// the global frame, bit 1: the strip reaches a Dirichlet / pad COLUMN). A
+// pinned point must keep its value at every level: the update C + r*x is done
+// with r = 0 there, so pinning costs no instruction in kinds 1 and 2 —
+// kind 1 zeroes the wave-uniform scalar r for frame rows (SALU select), kind 2
+// multiplies by a per-lane r vector with zeros in frame columns. Only kind 3
+// (corner items, both) pays a select per element and level; the kernel runs
+// those items in two half-height pieces so they do not become the tail.
+// (0 * x is +-0 and C + +-0 == C for the finite values the march carries.)
+template <typename T, int NV, int K, int EK, int RING>
 struct March {
   using S = TbShape<T, NV, K>;
   static constexpr int V = S::V;
@@ -136,11 +153,11 @@ struct March {
   uint32_t nrec;     // descriptor size (= pitch_b)
   T r;
   int32_t t0, t1;    // output rows [t0, t1)
-  int32_t fixed_lo, fixed_hi;
+  int32_t fixed_lo, fixed_hi;  // EK & 1: rows outside [fixed_lo, fixed_hi) are frame rows
   int32_t mlo;       // lowest level-0 row (t0 - K)
   int32_t ld_off;    // per-lane load byte offset (kOob outside the allocation)
   int32_t st_off;    // per-lane vector store offset (kOob unless the lane holds output columns)
-  bool fixed[EDGE ? V : 1];  // EDGE: element is a Dirichlet / pad column (kept at its value)
+  T rl[(EK & 2) ? V : 1];  // EK & 2: r per element, 0 in Dirichlet / pad columns
 
   T X[2][KX][V];     // levels 1..K-1: X[parity][level-1][elem]
   VT Lb[RING][NV];   // level 0: load ring
@@ -185,6 +202,8 @@ struct March {
   __device__ __forceinline__ void update(const T (&part)[V], const T (&C)[V], const T (&N)[V], int32_t row,
                                          T (&out)[V]) const {
     const T west0 = from_lower(C[V - 1]);
+    const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
+    const T rs = frame_row ? T(0) : r;                                      // EK 1: scalar select
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       const T west = e > 0 ? C[e - 1] : west0;
@@ -192,13 +211,12 @@ struct March {
       // is bitwise identical (4C is exact) and saves one op; C + r*(...)
       // stays unfused, as in the reference.
       const T sum = (part[e] + N[e]) + west;
-      T val = C[e] + r * fma_t(T(-4), C[e], sum);
-      if constexpr (EDGE) val = fixed[e] ? C[e] : val;
-      out[e] = val;
-    }
-    if (EDGE && (row < fixed_lo || row >= fixed_hi)) {  // Dirichlet row (global frame): keep
-#pragma unroll
-      for (int e = 0; e < V; ++e) out[e] = C[e];
+      T re;
+      if constexpr (EK == 0) re = r;
+      else if constexpr (EK == 1) re = rs;
+      else if constexpr (EK == 2) re = rl[e];
+      else re = frame_row ? T(0) : rl[e];
+      out[e] = C[e] + re * fma_t(T(-4), C[e], sum);
     }
   }
 
@@ -289,7 +307,7 @@ struct March {
   }
 };
 
-template <typename T, int NV, int K, bool EDGE, int RING>
+template <typename T, int NV, int K, int EK, int RING>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
                                       int64_t t1, int lane) {
   using S = TbShape<T, NV, K>;
@@ -299,7 +317,7 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   const int64_t c0 = u0 - S::KA;
   const int64_t mycol = c0 + (int64_t)lane * V;
   const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
-  March<T, NV, K, EDGE, RING> w;
+  March<T, NV, K, EK, RING> w;
   // row base = column col_lo (= -cpad) of row 0; offsets are relative to it
   w.srow = reinterpret_cast<const char*>(src + a.col_lo);
   w.drow = reinterpret_cast<char*>(dst + a.col_lo);
@@ -316,78 +334,89 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   // Strip boundaries u0 are multiples of V, so a lane holds either only halo
   // columns or only useful ones — except the lane straddling ncols, whose
   // vector also covers the Dirichlet column / right pad. Those elements are
-  // pinned (fixed[]) to their src value at every level, so storing the whole
-  // vector writes them back unchanged: one 16-B store per lane, no per-element
-  // stores. (dst's frame equals src's frame by construction.)
+  // pinned (r = 0) at every level, so storing the whole vector writes them
+  // back unchanged: one 16-B store per lane, no per-element stores. (dst's
+  // frame equals src's frame by construction.)
   const bool useful = (mycol >= u0) && (mycol < ustop);
   w.st_off = useful && in_alloc ? off : kOob;
-  if constexpr (EDGE) {
+  if constexpr ((EK & 2) != 0) {
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       const int64_t c = mycol + e;
-      w.fixed[e] = (c < 0 || c >= a.ncols);
+      w.rl[e] = (c < 0 || c >= a.ncols) ? T(0) : r;
     }
   }
   w.run();
 }
 
-// Occupancy target for the "tight" instantiation. Left alone, the scheduler
-// spends registers on ILP (e.g. fp64, 16 B/lane, K = 10: 169 VGPRs -> 2
-// waves/SIMD); told to fit 3 waves it needs 161 and spills nothing. The
-// estimate is the level state (2 rows x K-1 levels), the load ring and a
-// measured overhead (address/DPP/transient registers); waves = 512 / VGPRs.
-template <typename T, int NV, int K, int RING>
-constexpr int tight_waves() {
-  const int need = 8 * NV * (K - 1) + 4 * NV * RING + (sizeof(T) == 8 ? 48 : 72) + 16 * NV + 4 * (RING - 4);
-  const int alloc = (need + 7) / 8 * 8;
-  const int w = 512 / alloc;
-  return w > 8 ? 8 : (w < 3 ? 1 : w);  // <= 2 waves: no constraint (the compiler has 256 VGPRs)
+// Decode work item `it` -> (strip, output rows [t0, t1)); false if empty.
+__device__ __forceinline__ bool tb_item(const TbArgs& a, int64_t it, int64_t& strip, int64_t& t0, int64_t& t1) {
+  // select the rect with constant indices only (a dynamic index into the
+  // by-value kernarg struct would be lowered to a private-memory copy)
+  TbRectArg R = a.rect[0];
+#pragma unroll
+  for (int i = 1; i < kMaxRects; ++i)
+    if (i < a.nrect && it >= a.rect[i].item0) R = a.rect[i];
+  const int64_t local = it - R.item0;
+  const int64_t ns = R.s1 - R.s0;
+  const int64_t band = local / ns;
+  strip = R.s0 + (local - band * ns);
+  const int64_t rows = R.r1 - R.r0;
+  t0 = R.r0 + band * rows / R.nb;
+  t1 = R.r0 + (band + 1) * rows / R.nb;
+  return t1 > t0;
 }
 
-template <typename T, int NV, int K, int RING, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void tb_kernel(
-    const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
+// MAIN = true: the caller guarantees no item reaches a frame ROW (the slab
+// interior of the split schedule): items are kind 0, or kind 2 on the
+// frame-column strips — two code paths, fewer registers than the general
+// kernel (no per-level row tests, no corner selects). MAIN = false: the general
+// kernel classifies each item (edge kinds 0..3, see March).
+template <typename T, int NV, int K, int RING, bool MAIN>
+__global__ __launch_bounds__(256) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
   using S = TbShape<T, NV, K>;
   const int lane = threadIdx.x & 63;
   // readfirstlane: make the wave id (and everything derived from it: strip, rows,
   // row addresses) provably wave-uniform -> SGPRs and scalar buffer descriptors
   const int64_t wid = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (wid >= a.nwaves) return;  // whole wave exits; no barriers in this kernel
-  // Work items = (row band, strip), band-major: consecutive waves take adjacent
-  // strips of the same band, so the waves in flight stream whole contiguous
-  // rows (HBM page locality) and all march in step.
-  const int64_t items = a.nbands * a.nstrips;
-  for (int64_t it = wid; it < items; it += a.nwaves) {
-    const int64_t band = it / a.nstrips;
-    const int64_t strip = it - band * a.nstrips;
-    const bool second = band >= a.nbands0;
-    const int64_t rb = second ? a.row_begin1 : a.row_begin;
-    const int64_t rows = second ? a.row_end1 - a.row_begin1 : a.row_end - a.row_begin;
-    const int64_t bl = second ? band - a.nbands0 : band;
-    const int64_t nb = second ? a.nbands - a.nbands0 : a.nbands0;
-    const int64_t r0 = bl * rows / nb;
-    const int64_t r1 = (bl + 1) * rows / nb;
-    if (r1 <= r0) continue;
-    // safe path: the strip reaches a Dirichlet/pad column, or the march's
-    // rows [t0-K, t1+K) reach a Dirichlet row; everything else runs mask-free
+  // Items are band-major within a rect: consecutive waves take adjacent strips
+  // of the same band, so the waves in flight stream whole contiguous rows (HBM
+  // page locality) and all march in step.
+  for (int64_t it = wid; it < a.nitems; it += a.nwaves) {
+    int64_t strip, t0, t1;
+    if (!tb_item(a, it, strip, t0, t1)) continue;
     const int64_t c0 = strip * S::U - S::KA;
-    const int64_t t0 = rb + r0, t1 = rb + r1;
-    const bool edge = (c0 < 0) || (c0 + S::W > a.ncols) || (t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi);
-    if (edge)
-      march<T, NV, K, true, RING>(src, dst, a, r, strip, t0, t1, lane);
-    else
-      march<T, NV, K, false, RING>(src, dst, a, r, strip, t0, t1, lane);
+    if constexpr (MAIN) {
+      if ((c0 < 0) || (c0 + S::W > a.ncols))
+        march<T, NV, K, 2, RING>(src, dst, a, r, strip, t0, t1, lane);
+      else
+        march<T, NV, K, 0, RING>(src, dst, a, r, strip, t0, t1, lane);
+    } else {
+#ifdef HEAT2D_AB_NO_EDGE  // timing experiments only (bench A/B builds): frame handling off, wrong numerics
+      const int ek = 0;
+      (void)c0;
+#else
+      const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
+                     (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
+#endif
+      switch (ek) {
+        case 0: march<T, NV, K, 0, RING>(src, dst, a, r, strip, t0, t1, lane); break;
+        case 1: march<T, NV, K, 1, RING>(src, dst, a, r, strip, t0, t1, lane); break;
+        case 2: march<T, NV, K, 2, RING>(src, dst, a, r, strip, t0, t1, lane); break;
+        default: march<T, NV, K, 3, RING>(src, dst, a, r, strip, t0, t1, lane); break;
+      }
+    }
   }
 }
 
-template <typename T, int NV, int K, int RING, int WPE>
+template <typename T, int NV, int K, int RING, bool MAIN>
 constexpr auto kernel_ptr() {
-  return &tb_kernel<T, NV, K, RING, WPE>;
+  return &tb_kernel<T, NV, K, RING, MAIN>;
 }
 
-// Resident 256-thread workgroups per CU for one kernel instance (occupancy
-// API; these kernels use ~44 SGPRs, inside the range where the API is exact).
-template <typename T, int NV, int K, int RING, int WPE>
+// Resident 256-thread workgroups per CU for one kernel instance (occupancy API).
+template <typename T, int NV, int K, int RING, bool MAIN>
 int blocks_per_cu() {
   static std::mutex mu;
   static std::map<int, int> cache;  // device -> blocks/CU
@@ -397,7 +426,7 @@ int blocks_per_cu() {
   auto it = cache.find(dev);
   if (it != cache.end()) return it->second;
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, RING, WPE>()),
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, RING, MAIN>()),
                                                    256, 0) != hipSuccess ||
       nb <= 0)
     nb = 1;
@@ -405,56 +434,51 @@ int blocks_per_cu() {
   return nb;
 }
 
-// Per-(T, NV, RING) entry points, explicitly instantiated in tb_<dtype>_nv<NV>_r<RING>.hip
-// (one translation unit each, compiled in parallel). tight: use the
-// tight_waves() occupancy target (else the compiler's own register budget).
-template <typename T, int NV, int RING>
-void dispatch(int k, bool tight, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
-template <typename T, int NV, int RING>
-int occupancy_blocks(int k, bool tight);
+// Per-(T, RING, MAIN) entry points (16 B per lane), explicitly instantiated in
+// tb_<dtype>_r<RING>_<main|gen>.hip (one translation unit each, compiled in parallel).
+template <typename T, int RING, bool MAIN>
+void dispatch(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
+template <typename T, int RING, bool MAIN>
+int occupancy_blocks(int k);
 
-#define H2D_TB_CASE(T, NV, RING, KK)                                                                       \
-  case KK:                                                                                                 \
-    if (tight)                                                                                             \
-      hipLaunchKernelGGL((tb_kernel<T, NV, KK, RING, tight_waves<T, NV, KK, RING>()>), dim3(nblocks),      \
-                         dim3(256), 0, s, src, dst, a, r);                                                 \
-    else                                                                                                   \
-      hipLaunchKernelGGL((tb_kernel<T, NV, KK, RING, 1>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
+#define H2D_TB_CASE(T, RING, MAIN, KK)                                                                    \
+  case KK:                                                                                                \
+    hipLaunchKernelGGL((tb_kernel<T, 1, KK, RING, MAIN>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
     return;
-#define H2D_OCC_CASE(T, NV, RING, KK) \
-  case KK:                            \
-    return tight ? blocks_per_cu<T, NV, KK, RING, tight_waves<T, NV, KK, RING>()>() : blocks_per_cu<T, NV, KK, RING, 1>();
+#define H2D_OCC_CASE(T, RING, MAIN, KK) \
+  case KK:                              \
+    return blocks_per_cu<T, 1, KK, RING, MAIN>();
 
-// Instantiate dispatch/occupancy for K = 1..16 of one (T, NV, RING).
-#define H2D_TB_UNIT(T, NV, RING)                                                                      \
-  template <>                                                                                         \
-  void dispatch<T, NV, RING>(int k, bool tight, unsigned nblocks, const T* src, T* dst, const TbArgs& a, \
-                             T r, hipStream_t s) {                                                    \
-    switch (k) {                                                                                      \
-      H2D_TB_CASE(T, NV, RING, 1) H2D_TB_CASE(T, NV, RING, 2) H2D_TB_CASE(T, NV, RING, 3)             \
-      H2D_TB_CASE(T, NV, RING, 4) H2D_TB_CASE(T, NV, RING, 5) H2D_TB_CASE(T, NV, RING, 6)             \
-      H2D_TB_CASE(T, NV, RING, 7) H2D_TB_CASE(T, NV, RING, 8) H2D_TB_CASE(T, NV, RING, 9)             \
-      H2D_TB_CASE(T, NV, RING, 10) H2D_TB_CASE(T, NV, RING, 11) H2D_TB_CASE(T, NV, RING, 12)          \
-      H2D_TB_CASE(T, NV, RING, 13) H2D_TB_CASE(T, NV, RING, 14) H2D_TB_CASE(T, NV, RING, 15)          \
-      H2D_TB_CASE(T, NV, RING, 16)                                                                    \
-      default:                                                                                        \
-        break;                                                                                        \
-    }                                                                                                 \
-    HEAT2D_REQUIRE(false, "temporal depth not instantiated for this variant");                        \
-  }                                                                                                   \
-  template <>                                                                                         \
-  int occupancy_blocks<T, NV, RING>(int k, bool tight) {                                              \
-    switch (k) {                                                                                      \
-      H2D_OCC_CASE(T, NV, RING, 1) H2D_OCC_CASE(T, NV, RING, 2) H2D_OCC_CASE(T, NV, RING, 3)          \
-      H2D_OCC_CASE(T, NV, RING, 4) H2D_OCC_CASE(T, NV, RING, 5) H2D_OCC_CASE(T, NV, RING, 6)          \
-      H2D_OCC_CASE(T, NV, RING, 7) H2D_OCC_CASE(T, NV, RING, 8) H2D_OCC_CASE(T, NV, RING, 9)          \
-      H2D_OCC_CASE(T, NV, RING, 10) H2D_OCC_CASE(T, NV, RING, 11) H2D_OCC_CASE(T, NV, RING, 12)       \
-      H2D_OCC_CASE(T, NV, RING, 13) H2D_OCC_CASE(T, NV, RING, 14) H2D_OCC_CASE(T, NV, RING, 15)       \
-      H2D_OCC_CASE(T, NV, RING, 16)                                                                   \
-      default:                                                                                        \
-        break;                                                                                        \
-    }                                                                                                 \
-    return 1;                                                                                         \
+// Instantiate dispatch/occupancy for K = 1..16 of one (T, RING, MAIN).
+#define H2D_TB_UNIT(T, RING, MAIN)                                                                          \
+  template <>                                                                                               \
+  void dispatch<T, RING, MAIN>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r,         \
+                               hipStream_t s) {                                                             \
+    switch (k) {                                                                                            \
+      H2D_TB_CASE(T, RING, MAIN, 1) H2D_TB_CASE(T, RING, MAIN, 2) H2D_TB_CASE(T, RING, MAIN, 3)             \
+      H2D_TB_CASE(T, RING, MAIN, 4) H2D_TB_CASE(T, RING, MAIN, 5) H2D_TB_CASE(T, RING, MAIN, 6)             \
+      H2D_TB_CASE(T, RING, MAIN, 7) H2D_TB_CASE(T, RING, MAIN, 8) H2D_TB_CASE(T, RING, MAIN, 9)             \
+      H2D_TB_CASE(T, RING, MAIN, 10) H2D_TB_CASE(T, RING, MAIN, 11) H2D_TB_CASE(T, RING, MAIN, 12)          \
+      H2D_TB_CASE(T, RING, MAIN, 13) H2D_TB_CASE(T, RING, MAIN, 14) H2D_TB_CASE(T, RING, MAIN, 15)          \
+      H2D_TB_CASE(T, RING, MAIN, 16)                                                                        \
+      default:                                                                                              \
+        break;                                                                                              \
+    }                                                                                                       \
+    HEAT2D_REQUIRE(false, "temporal depth not instantiated for this variant");                              \
+  }                                                                                                         \
+  template <>                                                                                               \
+  int occupancy_blocks<T, RING, MAIN>(int k) {                                                              \
+    switch (k) {                                                                                            \
+      H2D_OCC_CASE(T, RING, MAIN, 1) H2D_OCC_CASE(T, RING, MAIN, 2) H2D_OCC_CASE(T, RING, MAIN, 3)          \
+      H2D_OCC_CASE(T, RING, MAIN, 4) H2D_OCC_CASE(T, RING, MAIN, 5) H2D_OCC_CASE(T, RING, MAIN, 6)          \
+      H2D_OCC_CASE(T, RING, MAIN, 7) H2D_OCC_CASE(T, RING, MAIN, 8) H2D_OCC_CASE(T, RING, MAIN, 9)          \
+      H2D_OCC_CASE(T, RING, MAIN, 10) H2D_OCC_CASE(T, RING, MAIN, 11) H2D_OCC_CASE(T, RING, MAIN, 12)       \
+      H2D_OCC_CASE(T, RING, MAIN, 13) H2D_OCC_CASE(T, RING, MAIN, 14) H2D_OCC_CASE(T, RING, MAIN, 15)       \
+      H2D_OCC_CASE(T, RING, MAIN, 16)                                                                       \
+      default:                                                                                              \
+        break;                                                                                              \
+    }                                                                                                       \
+    return 1;                                                                                               \
   }
 
 }  // namespace tbimpl

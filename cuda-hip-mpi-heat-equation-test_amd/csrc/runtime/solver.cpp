@@ -6,23 +6,26 @@
 // serialised on the null stream.
 //
 // Here, per cycle of k <= K steps (one HBM pass), src -> dst (ping-pong, no
-// copy), with B = K boundary rows per side:
-//   compute stream: wait(ev_bnd: previous bands) -> tb(interior [B, n-B))
-//                   -> record(ev_int)
-//   comm stream:    wait(ev_int: previous interior) -> tb(bands [0,B) and
-//                   [n-B,n), ONE launch) -> record(ev_bnd) -> RCCL grouped
-//                   send/recv of the B band rows -> record(ev_comm)
-// The interior never reads ghost rows (it reads owned rows [0, n)), so it
-// does not wait for any exchange: interiors run back to back on the compute
-// stream (CU-masked, leaving a few CUs to the comm stream) while the bands and
-// the halo exchange of the same cycle proceed beside them. Ordering is carried
-// entirely by events; the host never synchronises inside the loop. Hazards
-// covered (cycle c, src_c = dst_{c-1}):
-//   * interior c reads src_c band rows written by bands c-1, and overwrites
-//     dst_c rows that bands c-1 read                         -> wait ev_bnd
-//   * bands c read src_c rows next to the bands written by interior c-1, and
-//     overwrite dst_c band rows that interior c-1 read       -> wait ev_int
-//   * bands c read ghost rows received by exchange c-1       -> comm-stream order
+// copy), split into two concurrent launches (kern::plan_split):
+//   MAIN (compute stream): rows [B, n-B) x the strips that reach no frame
+//        column — the lean interior-only kernel on most wave slots;
+//   EDGE (comm stream): the two B-row boundary bands and the frame-column
+//        strips, cut into short items, on the remaining slots; then (P > 1)
+//        the RCCL grouped send/recv of the B band rows.
+//   compute: wait(ev_bnd: EDGE c-1) -> MAIN c -> record(ev_int)
+//   comm:    wait(ev_int: MAIN c-1) -> EDGE c -> record(ev_bnd) -> exchange
+//            -> record(ev_comm)
+// MAIN never reads ghost rows (only owned rows [0, n)), so it never waits for
+// an exchange: MAIN launches run back to back while EDGE and the halo exchange
+// of the same cycle proceed beside them — also at P = 1, where the split keeps
+// the frame-handling code out of the main kernel (its registers and its tail).
+// Ordering is carried entirely by events; the host never synchronises inside
+// the loop. Hazards covered (cycle c, src_c = dst_{c-1}):
+//   * MAIN c reads src_c cells written by EDGE c-1, and overwrites dst_c cells
+//     that EDGE c-1 read                                     -> wait ev_bnd
+//   * EDGE c reads src_c cells written by MAIN c-1, and overwrites dst_c
+//     cells that MAIN c-1 read                               -> wait ev_int
+//   * EDGE c reads ghost rows received by exchange c-1       -> comm-stream order
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -103,12 +106,10 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
         H2D_HIP(hipExtStreamCreateWithCUMask(&s_compute_, (uint32_t)mask.size(), mask.data()));
         compute_cus_ = ncu - want;
       } else {
-        // Soft reservation (default): no mask; the persistent interior grid is
-        // planned for ncu - 2 CUs, so the bands' and RCCL's workgroups always
-        // find free wave slots beside it (measured: 2387 vs 2408 Gpts/s for
-        // the same slab without any exchange).
+        // Soft reservation (default): no mask; the split plan sizes the
+        // persistent interior grid to leave wave slots for the edge launch
+        // and RCCL's workgroups (kern::plan_split).
         H2D_HIP(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
-        if (ovl && want == 0 && ncu > 16) compute_cus_ = ncu - 2;
       }
       H2D_HIP(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
       own_streams_ = true;
@@ -193,18 +194,29 @@ void Solver::cycle_serial(int k) {
   cycle_swap();
 }
 
+const kern::SplitPlan& Solver::split_plan(int k) {
+  kern::SplitPlan& p = split_[k];
+  if (p.k != k) {
+    // room for RCCL's workgroups beside the two stencil launches when exchanging
+    const int spare = tr_->exchanges() ? 8 : 0;
+    p = kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare);
+    p.k = k;
+  }
+  return p;
+}
+
 void Solver::cycle_overlap(int k) {
   void* src = buf_[cur_];
   void* dst = buf_[cur_ ^ 1];
-  const int64_t n = L_.nrows, B = band_;
-  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));  // bands c-1 (record not yet replaced)
-  H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));     // interior c-1
-  if (n > 2 * B) {
-    kern::launch_tb(dtype(), src, dst, L_, B, n - B, k, cfg_.r, s_compute_, cfg_.tile_rows, compute_cus_);
+  const kern::SplitPlan& sp = split_plan(k);
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));  // edge part c-1 (record not yet replaced)
+  H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));     // main part c-1
+  if (sp.valid) {
+    kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_);
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-    kern::launch_tb2(dtype(), src, dst, L_, 0, B, n - B, n, k, cfg_.r, s_comm_, 0, 0);
-  } else {  // slab no thicker than its two bands: all of it beside the exchange
-    kern::launch_tb(dtype(), src, dst, L_, 0, n, k, cfg_.r, s_comm_, 0, 0);
+    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_);
+  } else {  // slab too thin / narrow to split: all of it beside the exchange
+    kern::launch_tb(dtype(), src, dst, L_, 0, L_.nrows, k, cfg_.r, s_comm_, 0, 0);
   }
   H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
   exchange_on(dst, s_comm_);
@@ -264,7 +276,7 @@ void Solver::step(int64_t n) {
       continue;
     }
     const int k = (int)std::min<int64_t>(K, left);
-    if (multi && cfg_.overlap && hip_) cycle_overlap(k);
+    if (cfg_.overlap && hip_) cycle_overlap(k);
     else cycle_serial(k);
     left -= k;
     steps_ += k;

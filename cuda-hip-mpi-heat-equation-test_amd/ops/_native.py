@@ -68,12 +68,24 @@ class Config(C.Structure):
     ]
 
 
+class Rect(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("r0", "r1", "s0", "s1", "nb")]
+
+
+class SplitPlan(C.Structure):
+    _fields_ = [
+        ("k", C.c_int32), ("ring", C.c_int32), ("valid", C.c_int32), ("nedge", C.c_int32),
+        ("main", Rect), ("edge", Rect * 4),
+        ("main_waves", C.c_int64), ("edge_waves", C.c_int64), ("main_items", C.c_int64), ("edge_items", C.c_int64),
+    ]
+
+
 class TbPlan(C.Structure):
     _fields_ = [
         ("k", C.c_int32), ("vec", C.c_int32), ("strip_w", C.c_int32), ("useful_w", C.c_int32),
         ("tile_rows", C.c_int64), ("nstrips", C.c_int64), ("ntiles", C.c_int64),
         ("nwaves", C.c_int64), ("nblocks", C.c_int64),
-        ("skew", C.c_int32), ("blocks_per_cu", C.c_int32), ("prefetch", C.c_int32), ("tight", C.c_int32),
+        ("skew", C.c_int32), ("blocks_per_cu", C.c_int32), ("prefetch", C.c_int32), ("main", C.c_int32),
     ]
 
 
@@ -94,6 +106,7 @@ _SIGS = {
     "heat2d_parse_input": (C.c_int, [C.c_char_p, C.POINTER(C.c_double)]),
     "heat2d_decompose": (C.c_int, [_I64, C.c_int, C.c_int, C.POINTER(_I64), C.POINTER(_I64)]),
     "heat2d_plan_tb": (C.c_int, [C.c_int, _LP, _I64, _I64, C.c_int, _I64, C.POINTER(TbPlan)]),
+    "heat2d_plan_split": (C.c_int, [C.c_int, _LP, C.c_int, _I64, C.POINTER(SplitPlan)]),
     "heat2d_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double, _P, _I64]),
     "heat2d_init_field": (C.c_int, [C.c_int, _P, _LP, C.POINTER(IcParams), _P, _P, _P]),
     "heat2d_stats": (C.c_int, [C.c_int, _P, _P, _LP, _P, _P, _P]),
@@ -211,6 +224,13 @@ def parse_input_native(text: str) -> dict:
 def plan_tb(dtype: int, layout: Layout, rb: int, re: int, k: int, tile_rows: int = 0) -> TbPlan:
     out = TbPlan()
     call("heat2d_plan_tb", dtype, C.byref(layout), rb, re, k, tile_rows, C.byref(out))
+    return out
+
+
+def plan_split(dtype: int, layout: Layout, k: int, band: int) -> SplitPlan:
+    """The MAIN + EDGE launch split of one overlapped cycle (csrc/kernels/stencil_tb.hip)."""
+    out = SplitPlan()
+    call("heat2d_plan_split", dtype, C.byref(layout), k, band, C.byref(out))
     return out
 
 

@@ -47,6 +47,31 @@ def test_hip_sine_bitwise(gpu, native, dtype, tb):
     s.close()
 
 
+@pytest.mark.parametrize("dtype,tb,n", [("fp64", 10, 1100), ("fp32", 9, 1100), ("fp64", 4, 777),
+                                         ("fp32", 16, 1500), ("fp64", 1, 700)])
+def test_hip_split_schedule_bitwise(gpu, native, dtype, tb, n):
+    """Grids large enough for the MAIN + EDGE split (interior-only kernel on the
+    compute stream, bands + frame strips on the comm stream), on non-dyadic
+    data, against the golden; and identical to the serial single-launch
+    schedule."""
+    from heat2d.ops import _native as N
+    p = prob(n, 23, "ghost", "sine")
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    T0 = R.owned(R.initial_field(p, npdt))
+    outs = []
+    for overlap in (True, False):
+        s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, overlap=overlap)
+        s.upload(T0)
+        s.step(p.ntime)
+        outs.append(s.download())
+        s.close()
+    ref = R.owned(R.ftcs(p, dtype=npdt))
+    assert np.array_equal(outs[0], ref), np.abs(outs[0].astype(np.float64) - ref).max()
+    assert np.array_equal(outs[1], ref)
+    sp = N.plan_split(N.F64 if dtype == "fp64" else N.F32, N.make_layout(n, n, halo=16), min(tb, 16), min(tb, 16))
+    assert sp.valid == 1 and sp.main_items > 0 and sp.edge_items > 0
+
+
 @pytest.mark.parametrize("n", [3, 17, 64, 130, 257, 1000])
 def test_hip_sizes(gpu, native, n):
     p = prob(n, 21, "ghost", "uniform")
