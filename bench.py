@@ -33,11 +33,12 @@ REF_GPTS_PER_RANK = 50.0  # BASELINE.md derived ceiling, 1 MI250X GCD, fp64
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--steps", type=int, default=480)
     ap.add_argument("--warmup", type=int, default=48)
     ap.add_argument("--n", type=int, default=32768)
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
-    ap.add_argument("--tb", type=int, default=10, help="time steps fused per HBM pass (measured best fp64: 10)")
+    ap.add_argument("--tb", type=int, default=0,
+                    help="time steps fused per HBM pass (0: measured best, fp64 12 / fp32 10; profiles/autotune.md)")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--comm-cus", type=int, default=0, help="CUs reserved for bands + RCCL (0: default, -1: none)")
@@ -48,6 +49,8 @@ def main():
                     help="1 GPU only: run the multi-GPU schedule (bands + RCCL self-exchange beside a CU-masked "
                          "interior) to measure its per-rank cost; not the headline (periodic halo)")
     args = ap.parse_args()
+    if args.tb <= 0:
+        args.tb = 12 if args.dtype == "fp64" else 10
 
     import torch
     import torch.distributed as dist
@@ -84,6 +87,7 @@ def main():
             dist.all_reduce(tr_vals)
         torch.cuda.synchronize()
 
+    s.prepare(args.steps)  # plan / autotune every depth the timed run uses (outside the timed region)
     s.step(args.warmup)
     s.synchronize()
     barrier()
@@ -129,6 +133,7 @@ def main():
                 "parallelism": f"slab{world}" + ("-rehearsal" if args.rehearse_comm and world == 1 else ""),
                 "temporal_block": tb,
                 "overlap": not args.no_overlap,
+                "launch_plan": s.plan() if not args.no_overlap else None,
             },
             "hbm_gb_per_s_model": round(model_gbps, 1),
             "baseline_basis": "BASELINE.md derived ceiling 50 Gpts/s per MI250X GCD x n_gpus",

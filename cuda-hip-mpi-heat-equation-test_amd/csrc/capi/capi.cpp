@@ -237,6 +237,20 @@ int heat2d_solver_layout(void* s, heat2d_layout* out) {
   });
 }
 
+int heat2d_solver_prepare(void* s, int64_t n) {
+  return guarded([&] { static_cast<Solver*>(s)->prepare(n); });
+}
+
+int heat2d_solver_plan(void* s, int k, heat2d_split_plan* out, float* tuned_ms) {
+  return guarded([&] {
+    Solver& sv = *static_cast<Solver*>(s);
+    HEAT2D_REQUIRE(k >= 1 && k <= kMaxTB, "k out of range");
+    const kern::SplitPlan& p = sv.plan_for(k);
+    std::memcpy(out, &p, sizeof(p));
+    if (tuned_ms) *tuned_ms = sv.tuned_ms(k);
+  });
+}
+
 int heat2d_solver_info(void* s, int32_t* tb, int64_t* band, int64_t* steps, void** field, void** stream) {
   return guarded([&] {
     Solver* so = static_cast<Solver*>(s);

@@ -151,6 +151,7 @@ void run_rank(Shared& sh, int rank) {
     cfg.managed = a.managed ? 1 : 0;
     cfg.device = a.cpu ? -1 : rank;
     cfg.use_graph = a.graph ? 1 : 0;
+    cfg.autotune = -1;  // split schedule on big slabs: pick the fastest launch plan on the first cycle
     Solver s(cfg, tr);
     s.init(sh.prob.ic, sh.prob.x.data(), sh.prob.x.data());
     const bool inclusive = sh.prob.conv == Convention::Inclusive;

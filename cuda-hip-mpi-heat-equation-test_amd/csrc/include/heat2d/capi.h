@@ -31,7 +31,7 @@ typedef struct heat2d_config {
   double r;
   int32_t tb, overlap, copy_swap, managed, device, use_graph;
   int64_t tile_rows, halo;
-  int32_t comm_cus, reserved_;
+  int32_t comm_cus, autotune;
 } heat2d_config;
 
 typedef struct heat2d_tb_plan {
@@ -115,6 +115,10 @@ int heat2d_solver_stats(void* s, double* out6, int residual);
 int heat2d_solver_download(void* s, void* host, int64_t ld);
 int heat2d_solver_upload(void* s, const void* host, int64_t ld);
 int heat2d_solver_layout(void* s, heat2d_layout* out);
+/* plan / autotune every cycle depth a step(n) will use (keep planning out of timed regions) */
+int heat2d_solver_prepare(void* s, int64_t n);
+/* split plan used for depth k (planned / autotuned on first use); tuned_ms = autotuned cycle time or 0 */
+int heat2d_solver_plan(void* s, int k, heat2d_split_plan* out, float* tuned_ms);
 int heat2d_solver_info(void* s, int32_t* tb, int64_t* band, int64_t* steps, void** field,
                        void** stream);
 

@@ -59,7 +59,9 @@ struct SplitPlan {
   TbRect edge[4];
   int64_t main_waves, edge_waves, main_items, edge_items;
 };
-SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus = 0, int spare_waves = 0);
+// ring_override: 4 | 6 (0: default); main_bands: MAIN row bands (0: persistent default)
+SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus = 0, int spare_waves = 0,
+                     int ring_override = 0, int64_t main_bands = 0);
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream);
 

@@ -41,7 +41,8 @@ struct SolverConfig {
   int64_t tile_rows;   // 0: auto
   int64_t halo;        // 0: auto (= kMaxTB)
   int32_t comm_cus;    // P>1 overlap: >0 CUs masked off the compute stream; 0 soft (interior planned for ncu-2); -1 none
-  int32_t reserved_;
+  int32_t autotune;    // split schedule: time candidate (ring, bands) plans once per depth and keep the fastest
+                       // (-1 auto: on for slabs >= 2^24 points, 0 off, 1 on)
 };
 
 // ---------------------------------------------------------------- transports
@@ -116,6 +117,9 @@ class Solver {
   void init(const kern::IcParams& ic, const double* xg, const double* yg);
   // Advance n time steps (asynchronous on the HIP backend).
   void step(int64_t n);
+  // Plan (and autotune, if enabled) every cycle depth a step(n) will use, so
+  // that no planning happens inside a timed step(n).
+  void prepare(int64_t n);
   void synchronize();
   // Global statistics over all ranks: sum, sum_sq, min, max, and residual
   // terms vs the previous buffer (valid right after a step()).
@@ -143,12 +147,16 @@ class Solver {
   hipStream_t stream() const { return s_compute_; }
   Transport& transport() { return *tr_; }
   int64_t band() const { return band_; }
+  // Split plan in use for depth k (planned / autotuned on first use).
+  const kern::SplitPlan& plan_for(int k) { return split_plan(k); }
+  float tuned_ms(int k) const { return k >= 0 && k <= kMaxTB ? tuned_ms_[k] : 0.f; }
   // Kernel time accumulated from events (ms) when timing is enabled.
   void set_timing(bool on) { timing_ = on; }
 
  private:
   void cycle_overlap(int k);
   const kern::SplitPlan& split_plan(int k);
+  void autotune_split(int k);
   void cycle_serial(int k);
   void cycle_copy_swap();
   void launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k);
@@ -170,6 +178,7 @@ class Solver {
   bool timing_ = false;
   int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all
   kern::SplitPlan split_[kMaxTB + 1] = {};  // per temporal depth (k == 0: not planned yet)
+  float tuned_ms_[kMaxTB + 1] = {};           // autotuned cycle time (ms), 0 if not tuned
   hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K
   int graph_k_ = 0;
   std::vector<char> host_stage_;  // CPU-backend / callback staging

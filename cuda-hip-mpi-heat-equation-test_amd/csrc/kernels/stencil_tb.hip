@@ -199,11 +199,12 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
   launch_rects(dt, src, dst, L, k, p.prefetch, false, rects, nr, slots, r, stream);
 }
 
-SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus, int spare_waves) {
+SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus, int spare_waves,
+                     int ring_override, int64_t main_bands) {
   check_layout(L, k);
   SplitPlan p{};
   p.k = k;
-  p.ring = default_ring(dt, k);
+  p.ring = (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k);
   const int64_t n = L.nrows, B = std::max<int64_t>(band, k);
   const int64_t U = useful_width(dt, k);
   const int64_t ns = (L.ncols + U - 1) / U;
@@ -216,9 +217,10 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   const int64_t min_rows = std::max<int64_t>(4 * (int64_t)k, 16);
   int64_t nb_m = std::max<int64_t>(1, mw / ns);
   nb_m = std::min<int64_t>(nb_m, std::max<int64_t>(1, rows_m / min_rows));
+  if (main_bands > 0) nb_m = std::min<int64_t>(main_bands, std::max<int64_t>(1, rows_m / (2 * (int64_t)k)));
   p.main = TbRect{B, n - B, 0, ns, nb_m};
   p.main_items = nb_m * ns;
-  p.main_waves = std::min<int64_t>(p.main_items, mw);
+  p.main_waves = std::min<int64_t>(p.main_items, mw);  // > one item per wave if main_bands asks for it
   // EDGE: the two boundary bands (one band each), general kernel. Short
   // (B + 2k march rows per item): beside MAIN where wave slots allow, else
   // right after it — either way the halo exchange that follows overlaps the

@@ -201,8 +201,98 @@ const kern::SplitPlan& Solver::split_plan(int k) {
     const int spare = tr_->exchanges() ? 8 : 0;
     p = kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare);
     p.k = k;
+    const bool big = L_.nrows * L_.ncols >= (int64_t(1) << 24);
+    if (p.valid && (cfg_.autotune > 0 || (cfg_.autotune < 0 && big))) autotune_split(k);
   }
   return p;
+}
+
+// Time candidate split plans (ring 4/6 x MAIN band counts) in the steady
+// state of the real loop — consecutive ping-pong cycles on the real buffers,
+// same stream/event protocol, no exchange — and keep the fastest. The
+// current field is backed up (one device copy) and restored afterwards, so
+// the solution is untouched; without room for the backup the default plan is
+// kept. Measured on MI355X the cycle time at 32768^2 swings by up to ~25%
+// between band counts of the same depth (DRAM page / channel locality of the
+// waves marching in lockstep, and the item-per-wave tail), which no static
+// rule captured; a single isolated cycle mispredicts the loop, hence the
+// steady-state measurement (profiles/autotune.md).
+void Solver::autotune_split(int k) {
+  const int spare = tr_->exchanges() ? 8 : 0;
+  const size_t bytes = (size_t)L_.elems() * dtype_size(dtype());
+  synchronize();
+  size_t free_b = 0, total_b = 0;
+  H2D_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (free_b < bytes + (size_t(1) << 30)) return;  // no room for the backup: keep the default plan
+  void* backup = nullptr;
+  if (hipMalloc(&backup, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  const int cur0 = cur_;
+  kern::launch_copy(backup, buf_[cur_], (int64_t)bytes, s_compute_);
+  hipEvent_t e0, e1;
+  H2D_HIP(hipEventCreate(&e0));
+  H2D_HIP(hipEventCreate(&e1));
+  auto run_cycle = [&](const kern::SplitPlan& c) {
+    void* src = buf_[cur_];
+    void* dst = buf_[cur_ ^ 1];
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
+    kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_);
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_);
+    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+    cur_ ^= 1;
+  };
+  auto time_plan = [&](const kern::SplitPlan& c) {
+    constexpr int kWarm = 1, kTimed = 3;
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+    for (int i = 0; i < kWarm; ++i) run_cycle(c);
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+    H2D_HIP(hipEventRecord(e0, s_compute_));
+    for (int i = 0; i < kTimed; ++i) run_cycle(c);
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+    H2D_HIP(hipEventRecord(e1, s_compute_));
+    H2D_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    H2D_HIP(hipEventElapsedTime(&ms, e0, e1));
+    return ms / kTimed;
+  };
+  kern::SplitPlan best = split_[k];
+  float best_ms = time_plan(best);
+  const int64_t nb0 = best.main.nb;
+  for (int ring : {4, 6}) {
+    for (double f : {1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 1.25, 1.5, 2.0}) {
+      const int64_t nb = std::max<int64_t>(1, (int64_t)(nb0 * f + 0.5));
+      if (ring == best.ring && nb == best.main.nb) continue;
+      kern::SplitPlan c = kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, nb);
+      if (!c.valid) continue;
+      // more items than waves only via explicit band counts above the default
+      c.main_waves = std::min<int64_t>(c.main_items, std::max<int64_t>(c.main_waves, best.main_waves));
+      const float ms = time_plan(c);
+      if (ms < best_ms) {
+        best_ms = ms;
+        best = c;
+      }
+    }
+  }
+  // restore the field into the buffer that was current
+  synchronize();
+  cur_ = cur0;
+  kern::launch_copy(buf_[cur_], backup, (int64_t)bytes, s_compute_);
+  H2D_HIP(hipStreamSynchronize(s_compute_));
+  H2D_HIP(hipFree(backup));
+  H2D_HIP(hipEventDestroy(e0));
+  H2D_HIP(hipEventDestroy(e1));
+  best.k = k;
+  split_[k] = best;
+  tuned_ms_[k] = best_ms;
+  // restore the event protocol: both streams idle, events recorded
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+  synchronize();
 }
 
 void Solver::cycle_overlap(int k) {
@@ -281,6 +371,13 @@ void Solver::step(int64_t n) {
     left -= k;
     steps_ += k;
   }
+}
+
+void Solver::prepare(int64_t n) {
+  if (!hip_ || !cfg_.overlap || cfg_.copy_swap || n <= 0) return;
+  const int K = cfg_.tb;
+  if (n >= K) (void)split_plan(K);
+  if (n % K) (void)split_plan((int)(n % K));
 }
 
 void Solver::synchronize() {

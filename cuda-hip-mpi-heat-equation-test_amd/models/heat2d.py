@@ -57,6 +57,9 @@ class HeatSolver:
         comm_cus: room for the bands + RCCL beside the interior kernel when
             overlapping: >0 CUs masked off the compute stream; 0 (default, or
             $HEAT2D_COMM_CUS) interior planned for all CUs but 2, no mask; -1 none.
+        autotune: overlapped (split) schedule: time candidate (ring, band count)
+            launch plans on the first cycle of each depth and keep the fastest
+            (-1: only for slabs of >= 2**24 points, 0: off, 1: on).
         rows: solve only the first ``rows`` x-rows of the grid (a rectangular
             rows x n domain, e.g. one rank's slab shape for a 1-GPU rehearsal).
     """
@@ -65,7 +68,7 @@ class HeatSolver:
                  overlap: bool = True, copy_swap: bool = False, managed: bool = False, graph: bool = False,
                  tile_rows: int = 0, halo: int = 0, transport: Optional[T.Transport] = None,
                  device: Optional[int] = None, init: bool = True, rows: Optional[int] = None,
-                 comm_cus: int = 0):
+                 comm_cus: int = 0, autotune: int = -1):
         self.problem = problem
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]
@@ -92,6 +95,7 @@ class HeatSolver:
         cfg.tile_rows = tile_rows
         cfg.halo = halo
         cfg.comm_cus = comm_cus
+        cfg.autotune = autotune
         self._cfg = cfg
         h = C.c_void_p()
         N.call("heat2d_solver_create", C.byref(cfg), self.transport.handle, C.byref(h))
@@ -130,6 +134,19 @@ class HeatSolver:
         return {"tb": tb.value, "band": band.value, "steps": steps.value, "field": field.value,
                 "stream": stream.value, "backend": self.backend, "transport": self.transport.name,
                 "rank": self.rank, "size": self.size, "layout": self.layout.as_dict()}
+
+    def prepare(self, n: int) -> None:
+        """Plan / autotune every cycle depth a ``step(n)`` will use (call before timing it)."""
+        N.call("heat2d_solver_prepare", self._h, int(n))
+
+    def plan(self, k: Optional[int] = None) -> dict:
+        """The split plan (MAIN / EDGE launches) used for depth k (default: tb)."""
+        k = self.tb if k is None else k
+        p, ms = N.SplitPlan(), C.c_float()
+        N.call("heat2d_solver_plan", self._h, k, C.byref(p), C.byref(ms))
+        return {"k": p.k, "ring": p.ring, "valid": p.valid, "main_bands": p.main.nb, "main_items": p.main_items,
+                "main_waves": p.main_waves, "edge_items": p.edge_items, "edge_waves": p.edge_waves,
+                "tuned_ms": ms.value}
 
     @property
     def tb(self) -> int:

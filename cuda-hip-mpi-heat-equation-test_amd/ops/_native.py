@@ -64,7 +64,7 @@ class Config(C.Structure):
         ("tb", C.c_int32), ("overlap", C.c_int32), ("copy_swap", C.c_int32), ("managed", C.c_int32),
         ("device", C.c_int32), ("use_graph", C.c_int32),
         ("tile_rows", C.c_int64), ("halo", C.c_int64),
-        ("comm_cus", C.c_int32), ("reserved_", C.c_int32),
+        ("comm_cus", C.c_int32), ("autotune", C.c_int32),
     ]
 
 
@@ -107,6 +107,8 @@ _SIGS = {
     "heat2d_decompose": (C.c_int, [_I64, C.c_int, C.c_int, C.POINTER(_I64), C.POINTER(_I64)]),
     "heat2d_plan_tb": (C.c_int, [C.c_int, _LP, _I64, _I64, C.c_int, _I64, C.POINTER(TbPlan)]),
     "heat2d_plan_split": (C.c_int, [C.c_int, _LP, C.c_int, _I64, C.POINTER(SplitPlan)]),
+    "heat2d_solver_prepare": (C.c_int, [_P, _I64]),
+    "heat2d_solver_plan": (C.c_int, [_P, C.c_int, C.POINTER(SplitPlan), C.POINTER(C.c_float)]),
     "heat2d_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double, _P, _I64]),
     "heat2d_init_field": (C.c_int, [C.c_int, _P, _LP, C.POINTER(IcParams), _P, _P, _P]),
     "heat2d_stats": (C.c_int, [C.c_int, _P, _P, _LP, _P, _P, _P]),

@@ -72,6 +72,25 @@ def test_hip_split_schedule_bitwise(gpu, native, dtype, tb, n):
     assert sp.valid == 1 and sp.main_items > 0 and sp.edge_items > 0
 
 
+@pytest.mark.parametrize("dtype,tb", [("fp64", 12), ("fp32", 10)])
+def test_hip_autotune_keeps_state_bitwise(gpu, native, dtype, tb):
+    """The split-plan autotuner runs trial cycles on the real buffers and
+    restores the field from a device backup: the solution must be untouched
+    (bitwise vs the golden), and the chosen plan valid."""
+    p = prob(1100, 29, "ghost", "sine")
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, autotune=1)
+    s.upload(R.owned(R.initial_field(p, npdt)))
+    s.prepare(p.ntime)
+    pl = s.plan()
+    assert pl["valid"] == 1 and pl["tuned_ms"] > 0.0 and pl["ring"] in (4, 6)
+    s.step(p.ntime)
+    ref = R.owned(R.ftcs(p, dtype=npdt))
+    got = s.download()
+    assert np.array_equal(got, ref), np.abs(got.astype(np.float64) - ref).max()
+    s.close()
+
+
 @pytest.mark.parametrize("n", [3, 17, 64, 130, 257, 1000])
 def test_hip_sizes(gpu, native, n):
     p = prob(n, 21, "ghost", "uniform")
