@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--comm-cus", type=int, default=0, help="CUs reserved for bands + RCCL (0: default, -1: none)")
     ap.add_argument("--check", action="store_true", help="print field statistics after the run")
+    ap.add_argument("--phase-timers", action="store_true",
+                    help="record hipEvent phase timers in the timed region and report them (adds event records)")
     ap.add_argument("--rows", type=int, default=0,
                     help="with --rehearse-comm: rows of the slab (e.g. 4096 = one of 8 ranks of 32768)")
     ap.add_argument("--rehearse-comm", action="store_true",
@@ -90,6 +92,8 @@ def main():
     s.prepare(args.steps)  # plan / autotune every depth the timed run uses (outside the timed region)
     s.step(args.warmup)
     s.synchronize()
+    if args.phase_timers:
+        s.set_timing(True)
     barrier()
     t0 = time.perf_counter()
     s.step(args.steps)
@@ -111,6 +115,7 @@ def main():
     # model HBM traffic: one read + one write of the field per HBM pass (tb steps)
     model_gbps = gpts * (2.0 * es / tb)
     stats = s.stats() if args.check else None
+    phases = s.phase_times() if args.phase_timers else None
     if rank == 0:
         out = {
             "metric": "stencil Gpoints/sec (whole node)",
@@ -140,6 +145,8 @@ def main():
         }
         if stats:
             out["field_stats"] = stats
+        if phases:
+            out["phase_ms"] = phases
         print(json.dumps(out), flush=True)
     s.close()
     tr.close()

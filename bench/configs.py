@@ -27,9 +27,11 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False):
     inp = heat2d.InputDat(n=n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=steps, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     t_init = time.perf_counter()
-    s = HeatSolver(prob, dtype=dtype, backend=backend, tb=tb, graph=graph, device=0 if backend == "hip" else None)
+    s = HeatSolver(prob, dtype=dtype, backend=backend, tb=tb, graph=graph, overlap=not graph,
+                   device=0 if backend == "hip" else None)
     s.synchronize()
     t_init = time.perf_counter() - t_init
+    s.prepare(steps)  # plan / autotune outside the timed region
     s.step(warmup)
     s.synchronize()
     t0 = time.perf_counter()
@@ -44,6 +46,8 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False):
            "s": round(dt, 6), "ms_per_step": round(dt / steps * 1e3, 5), "gpts": round(gpts, 2),
            "model_gbps": round(gpts * 2 * es / k, 1), "field_gb": round(s.layout.elems() * es / 1e9, 2),
            "init_s": round(t_init, 3), "finite": bool(math.isfinite(st["sum"]))}
+    if backend == "hip" and not graph:
+        rec["launch_plan"] = s.plan()
     s.close()
     return rec
 
@@ -64,10 +68,10 @@ def main():
         ("cpu-256-fp64", 256, "fp64", 200, 8, "cpu", 8, False),
         ("gpu-4096-fp32", 4096, "fp32", 1000, 64, "hip", 8, False),
         ("gpu-4096-fp32-graph", 4096, "fp32", 1000, 64, "hip", 8, True),
-        ("gpu-16384-fp64", 16384, "fp64", 400, 40, "hip", 10, False),
-        ("gpu-32768-fp64", 32768, "fp64", 400, 40, "hip", 10, False),
-        ("gpu-32768-fp32", 32768, "fp32", 405, 45, "hip", 9, False),
-        ("gpu-max-fp32", nmax, "fp32", 63, 9, "hip", 9, False),
+        ("gpu-16384-fp64", 16384, "fp64", 480, 48, "hip", 12, False),
+        ("gpu-32768-fp64", 32768, "fp64", 480, 48, "hip", 12, False),
+        ("gpu-32768-fp32", 32768, "fp32", 480, 40, "hip", 10, False),
+        ("gpu-max-fp32", nmax, "fp32", 60, 10, "hip", 10, False),
     ]
     for name, n, dt, steps, warm, be, tb, graph in plan:
         if a.only and not any(name.startswith(o) for o in a.only):

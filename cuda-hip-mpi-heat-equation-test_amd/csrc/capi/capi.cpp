@@ -237,6 +237,14 @@ int heat2d_solver_layout(void* s, heat2d_layout* out) {
   });
 }
 
+int heat2d_solver_timing(void* s, int on) {
+  return guarded([&] { static_cast<Solver*>(s)->set_timing(on != 0); });
+}
+
+int heat2d_solver_phase_times(void* s, double* out5) {
+  return guarded([&] { static_cast<Solver*>(s)->phase_times(out5); });
+}
+
 int heat2d_solver_prepare(void* s, int64_t n) {
   return guarded([&] { static_cast<Solver*>(s)->prepare(n); });
 }

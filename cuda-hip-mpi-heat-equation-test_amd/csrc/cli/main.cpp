@@ -51,6 +51,7 @@ struct Args {
   int64_t ntime = -1;  // override
   int64_t n = -1;      // override
   bool quiet = false;
+  bool timers = false;
 };
 
 void usage() {
@@ -58,7 +59,7 @@ void usage() {
       "usage: heat2d [input.dat] [--variant mpi|serial|cuda] [--gpus N | --cpu] [--dtype fp64|fp32]\n"
       "              [--tb K] [--no-overlap] [--copy-swap] [--managed] [--graph] [--ic NAME]\n"
       "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
-      "              [--n N] [--ntime N] [--quiet]\n");
+      "              [--n N] [--ntime N] [--quiet] [--timers]\n");
 }
 
 Args parse_args(int argc, char** argv) {
@@ -90,6 +91,7 @@ Args parse_args(int argc, char** argv) {
     else if (s == "--ntime") a.ntime = std::atoll(need("--ntime").c_str());
     else if (s == "--n") a.n = std::atoll(need("--n").c_str());
     else if (s == "--quiet") a.quiet = true;
+    else if (s == "--timers") a.timers = true;
     else if (!s.empty() && s[0] != '-') a.input = s;
     else { std::fprintf(stderr, "unknown flag %s\n", s.c_str()); usage(); std::exit(2); }
   }
@@ -169,6 +171,11 @@ void run_rank(Shared& sh, int rank) {
     }
 
     const int64_t ntime = sh.in.ntime;
+    // plan / autotune every cycle depth the loop will use before the clock starts
+    s.prepare(ntime);
+    for (int64_t every : {a.print_every, a.check_every})
+      if (every > 0) s.prepare(std::min(every, ntime));
+    if (a.timers) s.set_timing(true);
     tr->barrier();
     s.synchronize();
     const auto t0 = std::chrono::steady_clock::now();
@@ -195,6 +202,13 @@ void run_rank(Shared& sh, int rank) {
     tr->barrier();
     const auto t1 = std::chrono::steady_clock::now();
     sh.t_elapsed[(size_t)rank] = std::chrono::duration<double>(t1 - t0).count();
+    if (a.timers) {
+      double ph[5];
+      s.phase_times(ph);
+      std::printf(" heat2d: rank %d phases (GPU timeline, summed over %lld cycles): main %.3f ms, edge %.3f ms, "
+                  "exchange %.3f ms, cycle %.3f ms\n",
+                  rank, (long long)ph[4], ph[0], ph[1], ph[2], ph[3]);
+    }
 
     // outputs
     if (a.output != "none") {

@@ -115,6 +115,9 @@ int heat2d_solver_stats(void* s, double* out6, int residual);
 int heat2d_solver_download(void* s, void* host, int64_t ld);
 int heat2d_solver_upload(void* s, const void* host, int64_t ld);
 int heat2d_solver_layout(void* s, heat2d_layout* out);
+/* phase timers (hipEvents): on/off; read = [main ms, edge ms, exchange ms, cycle ms, cycles], then reset */
+int heat2d_solver_timing(void* s, int on);
+int heat2d_solver_phase_times(void* s, double* out5);
 /* plan / autotune every cycle depth a step(n) will use (keep planning out of timed regions) */
 int heat2d_solver_prepare(void* s, int64_t n);
 /* split plan used for depth k (planned / autotuned on first use); tuned_ms = autotuned cycle time or 0 */

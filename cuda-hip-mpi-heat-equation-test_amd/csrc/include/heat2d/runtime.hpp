@@ -66,6 +66,9 @@ class Transport {
   virtual bool capturable() const { return false; }  // safe inside hipGraph capture
   // true if exchange() moves data (size > 1, or a 1-rank periodic rehearsal)
   virtual bool exchanges() const { return size() > 1; }
+  // Failure detection: raise if the fabric reported an asynchronous error
+  // (RCCL: ncclCommGetAsyncError). Polled at every synchronisation point.
+  virtual void check() {}
 };
 
 std::shared_ptr<Transport> make_self_transport();
@@ -150,8 +153,11 @@ class Solver {
   // Split plan in use for depth k (planned / autotuned on first use).
   const kern::SplitPlan& plan_for(int k) { return split_plan(k); }
   float tuned_ms(int k) const { return k >= 0 && k <= kMaxTB ? tuned_ms_[k] : 0.f; }
-  // Kernel time accumulated from events (ms) when timing is enabled.
-  void set_timing(bool on) { timing_ = on; }
+  // Phase timers (hipEvents on the GPU timeline) for every cycle while
+  // enabled: [main ms, edge ms, exchange ms, whole-cycle ms (serial schedule),
+  // cycles]. phase_times() synchronises, sums the recorded cycles and resets.
+  void set_timing(bool on);
+  void phase_times(double out[5]);
 
  private:
   void cycle_overlap(int k);
@@ -176,6 +182,14 @@ class Solver {
   hipEvent_t ev_bnd_ = nullptr, ev_comm_ = nullptr, ev_int_ = nullptr;
   double* d_work_ = nullptr;   // stats workspace + 6 results
   bool timing_ = false;
+  struct PhaseEvents {
+    hipEvent_t ev[6];  // main begin/end, edge begin/end, exchange begin/end
+    int kind;          // 0: split cycle, 1: serial cycle (ev[0..1] only)
+  };
+  std::vector<PhaseEvents> phase_ev_;   // recorded, not yet summed
+  std::vector<PhaseEvents> phase_pool_;  // reusable
+  double phase_acc_[5] = {};
+  PhaseEvents* phase_begin(int kind);
   int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all
   kern::SplitPlan split_[kMaxTB + 1] = {};  // per temporal depth (k == 0: not planned yet)
   float tuned_ms_[kMaxTB + 1] = {};           // autotuned cycle time (ms), 0 if not tuned

@@ -103,6 +103,30 @@ void check_layout(const SlabLayout& L, int k) {
                  "row count exceeds the 32-bit row index of the stencil kernel");
 }
 
+// Row-band count for `rows` x `ns` strips on `slots` resident waves: minimise
+// (idle wave-slots of the last round) x (2k priming rows per band). One item
+// per wave when ns divides the slots well; several rounds when the strips
+// alone leave many slots idle (e.g. 734 strips on 2048 slots: 1 band idles
+// 28 % of the chip, 11 bands lose 1.4 %).
+int64_t choose_bands(int64_t rows, int64_t ns, int64_t slots, int k) {
+  const int64_t min_rows = std::max<int64_t>(4 * (int64_t)k, 16);
+  const int64_t nb_max = std::max<int64_t>(1, std::min<int64_t>(rows / min_rows, 64 * slots / std::max<int64_t>(ns, 1) + 1));
+  int64_t best = 1;
+  double best_cost = 1e300;
+  for (int64_t nb = 1; nb <= nb_max; ++nb) {
+    const int64_t items = nb * ns;
+    const int64_t rounds = (items + slots - 1) / slots;
+    const double idle = (double)(rounds * slots) / (double)items;
+    const double prime = 1.0 + 2.0 * k * (double)nb / (double)rows;
+    const double cost = idle * prime;
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = nb;
+    }
+  }
+  return best;
+}
+
 // Launch `rects` (item counts from their nb and strip ranges) on `nwaves` waves.
 void launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
                   const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream) {
@@ -163,10 +187,7 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
   if (tile_rows > 0) {
     nbands = (rows + tile_rows - 1) / tile_rows;
   } else {
-    // persistent: one (band, strip) item per resident wave, bands >= ~4k rows
-    const int64_t min_rows = std::max<int64_t>(4 * (int64_t)k, 16);
-    nbands = std::max<int64_t>(1, slots / p.nstrips);
-    nbands = std::min<int64_t>(nbands, std::max<int64_t>(1, rows / min_rows));
+    nbands = choose_bands(rows, p.nstrips, std::max<int64_t>(slots, 1), k);
   }
   nbands = std::max<int64_t>(1, std::min<int64_t>(nbands, rows));
   const int64_t items = nbands * p.nstrips;
@@ -214,9 +235,7 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   const int bpc = occupancy(dt, p.ring, true, k);
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
   const int64_t mw = std::max<int64_t>(4, slots - std::max(0, spare_waves));
-  const int64_t min_rows = std::max<int64_t>(4 * (int64_t)k, 16);
-  int64_t nb_m = std::max<int64_t>(1, mw / ns);
-  nb_m = std::min<int64_t>(nb_m, std::max<int64_t>(1, rows_m / min_rows));
+  int64_t nb_m = choose_bands(rows_m, ns, mw, k);
   if (main_bands > 0) nb_m = std::min<int64_t>(main_bands, std::max<int64_t>(1, rows_m / (2 * (int64_t)k)));
   p.main = TbRect{B, n - B, 0, ns, nb_m};
   p.main_items = nb_m * ns;

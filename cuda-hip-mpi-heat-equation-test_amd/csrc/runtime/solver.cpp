@@ -35,6 +35,8 @@
 
 #include "heat2d/runtime.hpp"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 namespace heat2d {
 
 #define H2D_HIP(expr)                                                                   \
@@ -139,6 +141,9 @@ Solver::~Solver() {
     if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
     if (ev_int_) (void)hipEventDestroy(ev_int_);
+    for (auto* v : {&phase_ev_, &phase_pool_})
+      for (auto& pe : *v)
+        for (auto& e : pe.ev) (void)hipEventDestroy(e);
     if (own_streams_) {
       (void)hipStreamDestroy(s_compute_);
       (void)hipStreamDestroy(s_comm_);
@@ -189,9 +194,60 @@ void Solver::cycle_swap() {
 void Solver::exchange_now() { exchange_on(buf_[cur_], s_compute_); }
 
 void Solver::cycle_serial(int k) {
+  roctxRangePushA("heat2d.cycle.serial");
+  PhaseEvents* pe = (timing_ && hip_) ? phase_begin(1) : nullptr;
+  if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
   cycle_compute(k);
+  if (pe) H2D_HIP(hipEventRecord(pe->ev[4], s_compute_));
   exchange_on(buf_[cur_ ^ 1], s_compute_);
+  if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
+  roctxRangePop();
   cycle_swap();
+}
+
+Solver::PhaseEvents* Solver::phase_begin(int kind) {
+  if (phase_pool_.empty()) {
+    PhaseEvents pe{};
+    for (auto& e : pe.ev) H2D_HIP(hipEventCreate(&e));
+    phase_pool_.push_back(pe);
+  }
+  phase_ev_.push_back(phase_pool_.back());
+  phase_pool_.pop_back();
+  phase_ev_.back().kind = kind;
+  return &phase_ev_.back();
+}
+
+void Solver::set_timing(bool on) {
+  if (!hip_) return;
+  timing_ = on;
+}
+
+void Solver::phase_times(double out[5]) {
+  if (hip_ && !phase_ev_.empty()) {
+    synchronize();
+    auto el = [](hipEvent_t a, hipEvent_t b) {
+      float ms = 0.f;
+      H2D_HIP(hipEventElapsedTime(&ms, a, b));
+      return (double)ms;
+    };
+    for (auto& pe : phase_ev_) {
+      if (pe.kind == 0) {
+        phase_acc_[0] += el(pe.ev[0], pe.ev[1]);  // main (compute stream)
+        phase_acc_[1] += el(pe.ev[2], pe.ev[3]);  // edge (comm stream, from its wait)
+        phase_acc_[2] += el(pe.ev[3], pe.ev[5]);  // halo exchange
+        phase_acc_[3] += std::max(el(pe.ev[0], pe.ev[1]), el(pe.ev[2], pe.ev[5]));
+      } else {
+        phase_acc_[0] += el(pe.ev[0], pe.ev[4]);  // compute
+        phase_acc_[2] += el(pe.ev[4], pe.ev[1]);  // exchange
+        phase_acc_[3] += el(pe.ev[0], pe.ev[1]);
+      }
+      phase_acc_[4] += 1.0;
+      phase_pool_.push_back(pe);
+    }
+    phase_ev_.clear();
+  }
+  for (int i = 0; i < 5; ++i) out[i] = phase_acc_[i];
+  for (double& v : phase_acc_) v = 0.0;
 }
 
 const kern::SplitPlan& Solver::split_plan(int k) {
@@ -299,18 +355,30 @@ void Solver::cycle_overlap(int k) {
   void* src = buf_[cur_];
   void* dst = buf_[cur_ ^ 1];
   const kern::SplitPlan& sp = split_plan(k);
+  roctxRangePushA("heat2d.cycle.split");
+  PhaseEvents* pe = timing_ ? phase_begin(0) : nullptr;
   H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));  // edge part c-1 (record not yet replaced)
   H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));     // main part c-1
+  if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
   if (sp.valid) {
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
     kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_);
   } else {  // slab too thin / narrow to split: all of it beside the exchange
+    if (pe) {
+      H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
+      H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
+    }
     kern::launch_tb(dtype(), src, dst, L_, 0, L_.nrows, k, cfg_.r, s_comm_, 0, 0);
   }
+  if (pe) H2D_HIP(hipEventRecord(pe->ev[3], s_comm_));
   H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
   exchange_on(dst, s_comm_);
+  if (pe) H2D_HIP(hipEventRecord(pe->ev[5], s_comm_));
   H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
+  roctxRangePop();
   cycle_swap();
 }
 
@@ -385,6 +453,7 @@ void Solver::synchronize() {
   H2D_HIP(hipSetDevice(cfg_.device));
   H2D_HIP(hipStreamSynchronize(s_compute_));
   if (s_comm_ != s_compute_) H2D_HIP(hipStreamSynchronize(s_comm_));
+  tr_->check();
 }
 
 void Solver::stats(double out[6], bool residual) {

@@ -67,6 +67,13 @@ class RcclTransport final : public Transport {
   std::string name() const override { return loop_ ? "rccl-loop" : "rccl"; }
   bool capturable() const override { return true; }
   bool exchanges() const override { return size_ > 1 || loop_; }
+  void check() override {
+    ncclResult_t st = ncclSuccess;
+    H2D_NCCL(ncclCommGetAsyncError(comm_, &st));
+    if (st != ncclSuccess && st != ncclInProgress)
+      fail(__FILE__, __LINE__, std::string("RCCL communicator failed asynchronously: ") + ncclGetErrorString(st) +
+                                   " (rank " + std::to_string(rank_) + " of " + std::to_string(size_) + ")");
+  }
 
   void exchange(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
                 bool on_device) override {

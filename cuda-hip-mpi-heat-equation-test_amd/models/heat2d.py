@@ -135,6 +135,18 @@ class HeatSolver:
                 "stream": stream.value, "backend": self.backend, "transport": self.transport.name,
                 "rank": self.rank, "size": self.size, "layout": self.layout.as_dict()}
 
+    def set_timing(self, on: bool = True) -> None:
+        """Record hipEvent phase timers for every cycle from now on (HIP backend)."""
+        N.call("heat2d_solver_timing", self._h, int(bool(on)))
+
+    def phase_times(self) -> dict:
+        """Sum of the phase timers since the last call (synchronises, then resets):
+        main / edge / exchange / cycle milliseconds and the number of cycles."""
+        out = (C.c_double * 5)()
+        N.call("heat2d_solver_phase_times", self._h, out)
+        return {"main_ms": out[0], "edge_ms": out[1], "exchange_ms": out[2], "cycle_ms": out[3],
+                "cycles": int(out[4])}
+
     def prepare(self, n: int) -> None:
         """Plan / autotune every cycle depth a ``step(n)`` will use (call before timing it)."""
         N.call("heat2d_solver_prepare", self._h, int(n))

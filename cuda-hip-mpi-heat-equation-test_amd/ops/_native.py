@@ -108,6 +108,8 @@ _SIGS = {
     "heat2d_plan_tb": (C.c_int, [C.c_int, _LP, _I64, _I64, C.c_int, _I64, C.POINTER(TbPlan)]),
     "heat2d_plan_split": (C.c_int, [C.c_int, _LP, C.c_int, _I64, C.POINTER(SplitPlan)]),
     "heat2d_solver_prepare": (C.c_int, [_P, _I64]),
+    "heat2d_solver_timing": (C.c_int, [_P, C.c_int]),
+    "heat2d_solver_phase_times": (C.c_int, [_P, C.POINTER(C.c_double)]),
     "heat2d_solver_plan": (C.c_int, [_P, C.c_int, C.POINTER(SplitPlan), C.POINTER(C.c_float)]),
     "heat2d_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double, _P, _I64]),
     "heat2d_init_field": (C.c_int, [C.c_int, _P, _LP, C.POINTER(IcParams), _P, _P, _P]),

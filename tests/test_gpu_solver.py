@@ -170,3 +170,22 @@ def test_upload_roundtrip(gpu, native):
     s.upload(a)
     assert np.array_equal(s.download(), a)
     s.close()
+
+
+def test_phase_timers(gpu, native):
+    """hipEvent phase timers: split cycles report main/edge time, serial cycles
+    compute/exchange; counts match the number of cycles; reading resets."""
+    p = prob(1100, 40, "ghost", "uniform")
+    s = HeatSolver(p, dtype="fp64", backend="hip", tb=8, device=0)
+    s.set_timing(True)
+    s.step(40)
+    ph = s.phase_times()
+    assert ph["cycles"] == 5 and ph["main_ms"] > 0 and ph["edge_ms"] > 0 and ph["cycle_ms"] >= ph["main_ms"]
+    assert s.phase_times()["cycles"] == 0
+    s.close()
+    s = HeatSolver(p, dtype="fp64", backend="hip", tb=8, device=0, overlap=False)
+    s.set_timing(True)
+    s.step(20)
+    ph = s.phase_times()
+    assert ph["cycles"] == 3 and ph["main_ms"] > 0 and ph["edge_ms"] == 0
+    s.close()
