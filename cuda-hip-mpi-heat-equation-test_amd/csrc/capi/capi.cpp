@@ -1,5 +1,6 @@
 // C ABI over the native runtime (see heat2d/capi.h).
 #include "heat2d/capi.h"
+#include "heat2d/jit.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -235,6 +236,34 @@ int heat2d_solver_layout(void* s, heat2d_layout* out) {
     const SlabLayout& L = static_cast<Solver*>(s)->layout();
     std::memcpy(out, &L, sizeof(L));
   });
+}
+
+int heat2d_jit_create(int dtype, const heat2d_layout* L, double r, int device, void** out) {
+  return guarded([&] { *out = new JitStencil((DType)dtype, to_layout(L), r, device); });
+}
+
+int heat2d_jit_free(void* j) {
+  return guarded([&] { delete static_cast<JitStencil*>(j); });
+}
+
+int heat2d_jit_step(void* j, const void* src, void* dst, void* stream) {
+  return guarded([&] { static_cast<JitStencil*>(j)->step(src, dst, as_stream(stream)); });
+}
+
+int heat2d_jit_render(int dtype, const heat2d_layout* L, double r, char* buf, int64_t cap, int64_t* len) {
+  return guarded([&] {
+    const std::string s = jit_render((DType)dtype, to_layout(L), r);
+    *len = (int64_t)s.size();
+    if (buf && cap > 0) {
+      const size_t n = std::min<size_t>((size_t)cap - 1, s.size());
+      std::memcpy(buf, s.data(), n);
+      buf[n] = 0;
+    }
+  });
+}
+
+int heat2d_jit_compile_check(const char* source, const char* arch, int64_t* code_bytes) {
+  return guarded([&] { *code_bytes = (int64_t)jit_compile(source, arch).size(); });
 }
 
 int heat2d_solver_timing(void* s, int on) {

@@ -10,6 +10,7 @@
 //   --variant cuda    fortran/cuda_cuf + fortran/cuda_kernel (hat on y in [0.5,1.0])
 //   --managed         fortran/cuda_kernel/heat_managed.F90 (hipMallocManaged fields)
 //   --cpu             native CPU path (replaces the gfortran serial build)
+//   --engine jit      run-time specialised hipRTC kernel (python/cuda/cuda.py's JIT)
 // Multi-GPU is one host thread per GPU (hipSetDevice(rank), the reference's
 // node-local rank -> device binding, fortran/hip/heat.F90:119-125) with RCCL
 // communicators; the halo exchange is RCCL send/recv over xGMI.
@@ -52,6 +53,7 @@ struct Args {
   int64_t n = -1;      // override
   bool quiet = false;
   bool timers = false;
+  std::string engine = "tb";
 };
 
 void usage() {
@@ -59,7 +61,7 @@ void usage() {
       "usage: heat2d [input.dat] [--variant mpi|serial|cuda] [--gpus N | --cpu] [--dtype fp64|fp32]\n"
       "              [--tb K] [--no-overlap] [--copy-swap] [--managed] [--graph] [--ic NAME]\n"
       "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
-      "              [--n N] [--ntime N] [--quiet] [--timers]\n");
+      "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit]\n");
 }
 
 Args parse_args(int argc, char** argv) {
@@ -86,6 +88,7 @@ Args parse_args(int argc, char** argv) {
     else if (s == "--copy-swap") a.copy_swap = true;
     else if (s == "--managed") a.managed = true;
     else if (s == "--graph") a.graph = true;
+    else if (s == "--engine") a.engine = need("--engine");
     else if (s == "--print-every") a.print_every = std::atoll(need("--print-every").c_str());
     else if (s == "--check-every") a.check_every = std::atoll(need("--check-every").c_str());
     else if (s == "--ntime") a.ntime = std::atoll(need("--ntime").c_str());
@@ -108,6 +111,7 @@ struct Shared {
   std::atomic<int> failed{0};
   std::string err;
   double final_stats[6] = {0};
+  int tb_used = 1;  // temporal depth the solver actually ran (jit / copy-swap force 1)
 };
 
 std::string rank_file(int rank) {
@@ -154,6 +158,8 @@ void run_rank(Shared& sh, int rank) {
     cfg.device = a.cpu ? -1 : rank;
     cfg.use_graph = a.graph ? 1 : 0;
     cfg.autotune = -1;  // split schedule on big slabs: pick the fastest launch plan on the first cycle
+    if (a.engine != "tb" && a.engine != "jit") fail(__FILE__, __LINE__, "--engine must be tb or jit");
+    cfg.engine = a.engine == "jit" ? 1 : 0;  // jit: hipRTC kernel rendered for this slab (python/cuda/cuda.py)
     Solver s(cfg, tr);
     s.init(sh.prob.ic, sh.prob.x.data(), sh.prob.x.data());
     const bool inclusive = sh.prob.conv == Convention::Inclusive;
@@ -238,7 +244,10 @@ void run_rank(Shared& sh, int rank) {
     }
     double st[6];
     s.stats(st, false);
-    if (root) std::memcpy(sh.final_stats, st, sizeof(st));
+    if (root) {
+      std::memcpy(sh.final_stats, st, sizeof(st));
+      sh.tb_used = s.config().tb;
+    }
   } catch (const std::exception& e) {
     sh.failed = 1;
     if (sh.err.empty()) sh.err = e.what();
@@ -290,7 +299,7 @@ int main(int argc, char** argv) {
   const double pts = (double)sh.prob.n_owned * (double)sh.prob.n_owned;
   const double gpts = ntime > 0 && tmax > 0 ? pts * (double)ntime / tmax / 1e9 : 0.0;
   const int es = a.dtype == "fp32" ? 4 : 8;
-  const int K = a.copy_swap ? 1 : std::max(1, std::min(a.tb, kMaxTB));
+  const int K = sh.tb_used;
   // model bytes/pt/step: one read + one write per HBM pass (K steps); copy mode adds the copy
   const double bpp = a.copy_swap ? 4.0 * es : 2.0 * es / K;
   std::printf(" simulation completed!!!!\n");

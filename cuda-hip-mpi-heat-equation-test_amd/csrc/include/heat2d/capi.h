@@ -32,6 +32,7 @@ typedef struct heat2d_config {
   int32_t tb, overlap, copy_swap, managed, device, use_graph;
   int64_t tile_rows, halo;
   int32_t comm_cus, autotune;
+  int32_t engine, reserved2_;
 } heat2d_config;
 
 typedef struct heat2d_tb_plan {
@@ -115,6 +116,12 @@ int heat2d_solver_stats(void* s, double* out6, int residual);
 int heat2d_solver_download(void* s, void* host, int64_t ld);
 int heat2d_solver_upload(void* s, const void* host, int64_t ld);
 int heat2d_solver_layout(void* s, heat2d_layout* out);
+/* run-time specialised FTCS step (hipRTC; python/cuda/cuda.py parity) */
+int heat2d_jit_create(int dtype, const heat2d_layout* L, double r, int device, void** out);
+int heat2d_jit_free(void* j);
+int heat2d_jit_step(void* j, const void* src, void* dst, void* stream);
+int heat2d_jit_render(int dtype, const heat2d_layout* L, double r, char* buf, int64_t cap, int64_t* len);
+int heat2d_jit_compile_check(const char* source, const char* arch, int64_t* code_bytes);
 /* phase timers (hipEvents): on/off; read = [main ms, edge ms, exchange ms, cycle ms, cycles], then reset */
 int heat2d_solver_timing(void* s, int on);
 int heat2d_solver_phase_times(void* s, double* out5);

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "heat2d/common.hpp"
+#include "heat2d/jit.hpp"
 #include "heat2d/kernels.hpp"
 
 namespace heat2d {
@@ -43,6 +44,8 @@ struct SolverConfig {
   int32_t comm_cus;    // P>1 overlap: >0 CUs masked off the compute stream; 0 soft (interior planned for ncu-2); -1 none
   int32_t autotune;    // split schedule: time candidate (ring, bands) plans once per depth and keep the fastest
                        // (-1 auto: on for slabs >= 2^24 points, 0 off, 1 on)
+  int32_t engine;      // 0: temporal-blocked kernels; 1: run-time specialised hipRTC kernel (K = 1, jit.hpp)
+  int32_t reserved2_;
 };
 
 // ---------------------------------------------------------------- transports
@@ -196,6 +199,7 @@ class Solver {
   hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K
   int graph_k_ = 0;
   std::vector<char> host_stage_;  // CPU-backend / callback staging
+  std::unique_ptr<JitStencil> jit_;  // engine 1
 };
 
 // P slabs of one domain on ONE device (or host), halos moved by device

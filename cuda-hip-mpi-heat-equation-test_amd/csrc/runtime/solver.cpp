@@ -65,6 +65,12 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
 
   int K = std::max(1, std::min<int>(cfg_.tb <= 0 ? 1 : cfg_.tb, kMaxTB));
   if (cfg_.copy_swap) K = 1;
+  HEAT2D_REQUIRE(cfg_.engine == 0 || cfg_.engine == 1, "engine must be 0 (temporal-blocked) or 1 (jit)");
+  if (cfg_.engine == 1) {
+    HEAT2D_REQUIRE(hip_, "the jit engine runs on the HIP backend");
+    HEAT2D_REQUIRE(!cfg_.copy_swap, "the jit engine has no copy-swap mode");
+    K = 1;  // one step per launch, like the reference's JIT program
+  }
   // every rank must own >= K rows so a neighbour's K ghost rows come from one rank
   K = (int)std::min<int64_t>(K, cfg_.n_rows / P);
   cfg_.tb = K;
@@ -122,6 +128,11 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    if (cfg_.engine == 1) {
+      jit_.reset(new JitStencil(dtype(), L_, cfg_.r, cfg_.device));
+      cfg_.overlap = 0;
+      cfg_.use_graph = 0;
+    }
   } else {
     for (int b = 0; b < 2; ++b) buf_[b] = host_alloc(bytes);
     cfg_.overlap = 0;
@@ -185,7 +196,13 @@ void Solver::exchange_on(void* field, hipStream_t s) {
   tr_->exchange(field, L_, dtype(), band_, s, hip_);
 }
 
-void Solver::cycle_compute(int k) { launch_tb(buf_[cur_], buf_[cur_ ^ 1], 0, L_.nrows, k); }
+void Solver::cycle_compute(int k) {
+  if (jit_) {
+    jit_->step(buf_[cur_], buf_[cur_ ^ 1], s_compute_);  // k == 1
+    return;
+  }
+  launch_tb(buf_[cur_], buf_[cur_ ^ 1], 0, L_.nrows, k);
+}
 
 void Solver::cycle_swap() {
   cur_ ^= 1;

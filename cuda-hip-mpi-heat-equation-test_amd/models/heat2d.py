@@ -57,6 +57,9 @@ class HeatSolver:
         comm_cus: room for the bands + RCCL beside the interior kernel when
             overlapping: >0 CUs masked off the compute stream; 0 (default, or
             $HEAT2D_COMM_CUS) interior planned for all CUs but 2, no mask; -1 none.
+        engine: "tb" — the temporal-blocked gfx950 kernels; "jit" — a kernel
+            rendered for this slab and r and compiled at run time with hipRTC
+            (one step per launch; the reference's PyCUDA program, ops/jit.py).
         autotune: overlapped (split) schedule: time candidate (ring, band count)
             launch plans on the first cycle of each depth and keep the fastest
             (-1: only for slabs of >= 2**24 points, 0: off, 1: on).
@@ -68,7 +71,7 @@ class HeatSolver:
                  overlap: bool = True, copy_swap: bool = False, managed: bool = False, graph: bool = False,
                  tile_rows: int = 0, halo: int = 0, transport: Optional[T.Transport] = None,
                  device: Optional[int] = None, init: bool = True, rows: Optional[int] = None,
-                 comm_cus: int = 0, autotune: int = -1):
+                 comm_cus: int = 0, autotune: int = -1, engine: str = "tb"):
         self.problem = problem
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]
@@ -96,6 +99,9 @@ class HeatSolver:
         cfg.halo = halo
         cfg.comm_cus = comm_cus
         cfg.autotune = autotune
+        if engine not in ("tb", "jit"):
+            raise ValueError("engine must be 'tb' (temporal-blocked kernels) or 'jit' (hipRTC, one step per launch)")
+        cfg.engine = 1 if engine == "jit" else 0
         self._cfg = cfg
         h = C.c_void_p()
         N.call("heat2d_solver_create", C.byref(cfg), self.transport.handle, C.byref(h))

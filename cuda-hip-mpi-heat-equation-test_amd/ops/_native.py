@@ -65,6 +65,7 @@ class Config(C.Structure):
         ("device", C.c_int32), ("use_graph", C.c_int32),
         ("tile_rows", C.c_int64), ("halo", C.c_int64),
         ("comm_cus", C.c_int32), ("autotune", C.c_int32),
+        ("engine", C.c_int32), ("reserved2_", C.c_int32),
     ]
 
 
@@ -109,6 +110,11 @@ _SIGS = {
     "heat2d_plan_split": (C.c_int, [C.c_int, _LP, C.c_int, _I64, C.POINTER(SplitPlan)]),
     "heat2d_solver_prepare": (C.c_int, [_P, _I64]),
     "heat2d_solver_timing": (C.c_int, [_P, C.c_int]),
+    "heat2d_jit_create": (C.c_int, [C.c_int, _LP, C.c_double, C.c_int, C.POINTER(_P)]),
+    "heat2d_jit_free": (C.c_int, [_P]),
+    "heat2d_jit_step": (C.c_int, [_P, _P, _P, _P]),
+    "heat2d_jit_render": (C.c_int, [C.c_int, _LP, C.c_double, C.c_char_p, _I64, C.POINTER(_I64)]),
+    "heat2d_jit_compile_check": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(_I64)]),
     "heat2d_solver_phase_times": (C.c_int, [_P, C.POINTER(C.c_double)]),
     "heat2d_solver_plan": (C.c_int, [_P, C.c_int, C.POINTER(SplitPlan), C.POINTER(C.c_float)]),
     "heat2d_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double, _P, _I64]),

@@ -35,6 +35,9 @@ def build_parser():
     ap.add_argument("--copy-swap", action="store_true")
     ap.add_argument("--managed", action="store_true")
     ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--engine", default=None, choices=["tb", "jit"],
+                    help="tb: temporal-blocked kernels; jit: hipRTC kernel rendered at run time "
+                         "(default: jit for --variant pycuda on a GPU, else tb)")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--ntime", type=int, default=None)
     ap.add_argument("--print-every", type=int, default=0)
@@ -93,9 +96,10 @@ def run(argv=None) -> int:
         tr = T.RcclTransport(rank, world, local) if backend == "hip" else T.TorchDistTransport()
     else:
         tr = T.SelfTransport()
+    engine = a.engine or ("jit" if var.name == "pycuda" and backend == "hip" else "tb")
     s = HeatSolver(prob, dtype=a.dtype, backend=backend, tb=a.tb, overlap=not a.no_overlap, copy_swap=a.copy_swap,
                    managed=a.managed or var.managed, graph=a.graph, transport=tr,
-                   device=local if backend == "hip" else None)
+                   device=local if backend == "hip" else None, engine=engine)
     if root and not a.quiet:
         if world > 1 or var.outputs == "mpi":
             print(f" Automatic MPI decomposition: {world:12d}  x 1")
@@ -113,6 +117,7 @@ def run(argv=None) -> int:
     if var.outputs == "serial" and a.output == "ascii" and start_step == 0:
         _write_inclusive(s, prob, "int.dat", world)
 
+    s.prepare(nsteps - start_step)  # plan / autotune outside the timed region
     _barrier(world)
     s.synchronize()
     t0 = time.perf_counter()
