@@ -95,3 +95,15 @@ def test_cli_gpu_serial_variant(cli, gpu, tmp_path, extra):
     prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "inclusive", "hat")
     a = read_xyz(tmp_path / "soln.dat")
     assert np.array_equal(a[:, 2], R.ftcs(prob).ravel())
+
+
+def test_cmake_configures(tmp_path):
+    """The CMake build (alternative to csrc/Makefile) configures for gfx950."""
+    import shutil
+    import subprocess
+    if shutil.which("cmake") is None:
+        pytest.skip("cmake not installed")
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cuda-hip-mpi-heat-equation-test_amd", "csrc")
+    r = subprocess.run(["cmake", "-S", src, "-B", str(tmp_path / "b")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "gfx950" in open(tmp_path / "b" / "CMakeCache.txt").read()
