@@ -27,8 +27,7 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False):
     inp = heat2d.InputDat(n=n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=steps, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     t_init = time.perf_counter()
-    s = HeatSolver(prob, dtype=dtype, backend=backend, tb=tb, graph=graph, overlap=not graph,
-                   device=0 if backend == "hip" else None)
+    s = HeatSolver(prob, dtype=dtype, backend=backend, tb=tb, graph=graph, device=0 if backend == "hip" else None)
     s.synchronize()
     t_init = time.perf_counter() - t_init
     s.prepare(steps)  # plan / autotune outside the timed region
@@ -46,7 +45,7 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False):
            "s": round(dt, 6), "ms_per_step": round(dt / steps * 1e3, 5), "gpts": round(gpts, 2),
            "model_gbps": round(gpts * 2 * es / k, 1), "field_gb": round(s.layout.elems() * es / 1e9, 2),
            "init_s": round(t_init, 3), "finite": bool(math.isfinite(st["sum"]))}
-    if backend == "hip" and not graph:
+    if backend == "hip":
         rec["launch_plan"] = s.plan()
     s.close()
     return rec

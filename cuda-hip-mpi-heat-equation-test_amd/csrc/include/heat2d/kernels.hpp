@@ -49,7 +49,8 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 //         code: fewer registers), a persistent grid on all wave slots;
 //   EDGE: the two boundary bands (all strips), general kernel.
 // The caller orders them with events (solver.cpp). valid = 0: slab too thin
-// or narrow for the split (use launch_tb on the whole slab).
+// or narrow for the split (use launch_tb on the whole slab); valid = 2: a
+// single-launch plan (plan_single).
 struct TbRect {
   int64_t r0, r1, s0, s1, nb;
 };
@@ -62,6 +63,10 @@ struct SplitPlan {
 // ring_override: 4 | 6 (0: default); main_bands: MAIN row bands (0: persistent default)
 SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus = 0, int spare_waves = 0,
                      int ring_override = 0, int64_t main_bands = 0);
+// The alternative the autotuner weighs against the split (valid = 2): ONE
+// general launch over the whole slab (no edge part), e.g. for small grids
+// where the second launch costs more than it saves.
+SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int ring_override = 0, int64_t bands = 0);
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream);
 

@@ -254,9 +254,32 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   return p;
 }
 
+SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_override, int64_t bands) {
+  check_layout(L, k);
+  SplitPlan p{};
+  p.k = k;
+  p.ring = (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k);
+  const int64_t U = useful_width(dt, k);
+  const int64_t ns = (L.ncols + U - 1) / U;
+  const int bpc = occupancy(dt, p.ring, false, k);
+  const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
+  int64_t nb = choose_bands(L.nrows, ns, slots, k);
+  if (bands > 0) nb = std::min<int64_t>(bands, std::max<int64_t>(1, L.nrows / (2 * (int64_t)k)));
+  p.main = TbRect{0, L.nrows, 0, ns, nb};
+  p.main_items = nb * ns;
+  p.main_waves = std::min<int64_t>(p.main_items, slots);
+  p.nedge = 0;
+  p.valid = 2;
+  return p;
+}
+
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream) {
   HEAT2D_REQUIRE(p.valid, "invalid split plan");
+  if (p.valid == 2) {  // single general launch over the whole slab (no edge part)
+    if (main_part) launch_rects(dt, src, dst, L, p.k, p.ring, false, &p.main, 1, p.main_waves, r, stream);
+    return;
+  }
   if (main_part)
     launch_rects(dt, src, dst, L, p.k, p.ring, true, &p.main, 1, p.main_waves, r, stream);
   else

@@ -336,18 +336,25 @@ void Solver::autotune_split(int k) {
   kern::SplitPlan best = split_[k];
   float best_ms = time_plan(best);
   const int64_t nb0 = best.main.nb;
-  for (int ring : {4, 6}) {
-    for (double f : {1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 1.25, 1.5, 2.0}) {
-      const int64_t nb = std::max<int64_t>(1, (int64_t)(nb0 * f + 0.5));
-      if (ring == best.ring && nb == best.main.nb) continue;
-      kern::SplitPlan c = kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, nb);
-      if (!c.valid) continue;
-      // more items than waves only via explicit band counts above the default
-      c.main_waves = std::min<int64_t>(c.main_items, std::max<int64_t>(c.main_waves, best.main_waves));
-      const float ms = time_plan(c);
-      if (ms < best_ms) {
-        best_ms = ms;
-        best = c;
+  // without an exchange to hide, a single general launch per cycle competes too
+  const bool single_ok = !tr_->exchanges();
+  const int64_t nb1 = single_ok ? kern::plan_single(dtype(), L_, k, compute_cus_).main.nb : 0;
+  for (int mode : {1, 2}) {
+    if (mode == 2 && !single_ok) continue;
+    for (int ring : {4, 6}) {
+      for (double f : {1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 1.25, 1.5, 2.0}) {
+        const int64_t nb = std::max<int64_t>(1, (int64_t)((mode == 1 ? nb0 : nb1) * f + 0.5));
+        if (mode == 1 && ring == best.ring && nb == best.main.nb) continue;
+        kern::SplitPlan c = mode == 1 ? kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, nb)
+                                      : kern::plan_single(dtype(), L_, k, compute_cus_, ring, nb);
+        if (!c.valid) continue;
+        if (mode == 1)  // more items than waves only via explicit band counts above the default
+          c.main_waves = std::min<int64_t>(c.main_items, std::max<int64_t>(c.main_waves, best.main_waves));
+        const float ms = time_plan(c);
+        if (ms < best_ms) {
+          best_ms = ms;
+          best = c;
+        }
       }
     }
   }
@@ -413,21 +420,59 @@ void Solver::cycle_copy_swap() {
 
 void Solver::run_graph_cycles(int64_t npairs) {
   const int K = cfg_.tb;
+  const bool ovl = cfg_.overlap != 0;
+  if (ovl) (void)split_plan(K);  // plan / autotune (synchronising) before any capture
   if (!graph_exec_ || graph_k_ != K) {
     if (graph_exec_) H2D_HIP(hipGraphExecDestroy(graph_exec_));
     hipGraph_t g = nullptr;
-    H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
     const int saved = cur_;
-    cycle_serial(K);
-    cycle_serial(K);
+    if (!ovl) {
+      H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
+      cycle_serial(K);
+      cycle_serial(K);
+    } else {
+      // Two-stream capture: fork the comm stream off the capture, record the
+      // two overlapped cycles (their event protocol becomes graph edges), join.
+      // Cross-cycle overlap inside the graph is kept; at graph boundaries the
+      // launches serialise (the next graph's first cycle needs this one's
+      // second anyway, except the exchange, which then is not hidden).
+      hipEvent_t fork = nullptr, join = nullptr;
+      H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+      H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+      H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
+      H2D_HIP(hipEventRecord(fork, s_compute_));
+      H2D_HIP(hipStreamWaitEvent(s_comm_, fork, 0));
+      H2D_HIP(hipEventRecord(ev_int_, s_compute_));  // in-capture records replace the external ones
+      H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+      const bool timing = timing_;
+      timing_ = false;  // no timing events inside graphs
+      cycle_overlap(K);
+      cycle_overlap(K);
+      timing_ = timing;
+      H2D_HIP(hipEventRecord(join, s_comm_));
+      H2D_HIP(hipStreamWaitEvent(s_compute_, join, 0));
+      H2D_HIP(hipStreamEndCapture(s_compute_, &g));
+      H2D_HIP(hipEventDestroy(fork));
+      H2D_HIP(hipEventDestroy(join));
+    }
     cur_ = saved;
-    H2D_HIP(hipStreamEndCapture(s_compute_, &g));
+    if (!g) H2D_HIP(hipStreamEndCapture(s_compute_, &g));
     H2D_HIP(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
     H2D_HIP(hipGraphDestroy(g));
     graph_k_ = K;
   }
+  if (ovl) {  // the graph starts only when the eager work on both streams is done
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
+  }
   // the graph was captured for buffer parity 0 -> 1 -> 0
   for (int64_t i = 0; i < npairs; ++i) H2D_HIP(hipGraphLaunch(graph_exec_, s_compute_));
+  if (ovl) {  // eager cycles after the graph order against its end
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+    H2D_HIP(hipEventRecord(ev_comm_, s_compute_));
+    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_comm_, 0));
+  }
 }
 
 void Solver::step(int64_t n) {
@@ -442,8 +487,7 @@ void Solver::step(int64_t n) {
   const bool multi = tr_->exchanges();
   int64_t left = n;
   while (left > 0) {
-    if (cfg_.use_graph && hip_ && (!multi || tr_->capturable()) && !cfg_.overlap && left >= 2 * K &&
-        cur_ == 0) {
+    if (cfg_.use_graph && hip_ && (!multi || tr_->capturable()) && left >= 2 * K && cur_ == 0) {
       const int64_t pairs = left / (2 * K);
       run_graph_cycles(pairs);
       left -= pairs * 2 * K;
