@@ -14,6 +14,13 @@ ranks. One "step" = one full time step of every grid point (temporal blocking
 fuses up to --tb steps per HBM pass; every point is still updated every step).
 Rank 0 prints one JSON line.
 
+Arithmetic (--arith, default fma): the update is the reference expression
+c + r*(sum - 4c) (fortran/hip/heat_kernel.cpp:43) in fp64, contracted to
+fma(r, sum - 4c, c) — what hipcc's default -ffp-contract=fast makes of that
+line. With this config's r = 0.25 (a power of two) every rounding is the same
+as the uncontracted form, so the field is bitwise identical to --arith exact
+(checked on the GPU: tests/test_gpu_solver.py::test_hip_fma_equals_exact_pow2).
+
 vs_baseline: the reference publishes no numbers. We divide by the
 derived reference ceiling of BASELINE.md — 50 Gpts/s per MI250X GCD for its
 kernel + per-step D2D copy (>= 32 B/pt/step at 1.6 TB/s) — times N ranks.
@@ -40,6 +47,8 @@ def main():
     ap.add_argument("--tb", type=int, default=0,
                     help="time steps fused per HBM pass (0: measured best, fp64 12 / fp32 10; profiles/autotune.md)")
     ap.add_argument("--tile-rows", type=int, default=0)
+    ap.add_argument("--arith", default="fma", choices=["exact", "fma"],
+                    help="fma: contracted update (one op fewer per point); exact: every op rounded")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--comm-cus", type=int, default=0, help="CUs reserved for bands + RCCL (0: default, -1: none)")
     ap.add_argument("--check", action="store_true", help="print field statistics after the run")
@@ -81,7 +90,7 @@ def main():
     rows = args.rows if (args.rows and world == 1) else None
     s = HeatSolver(prob, dtype=args.dtype, backend="hip", tb=args.tb, overlap=not args.no_overlap,
                    tile_rows=args.tile_rows, transport=tr, device=local, rows=rows,
-                   comm_cus=args.comm_cus)
+                   comm_cus=args.comm_cus, arith=args.arith)
 
     def barrier():
         if world > 1:
@@ -137,6 +146,7 @@ def main():
                 "seq_len": prob.n_owned,
                 "parallelism": f"slab{world}" + ("-rehearsal" if args.rehearse_comm and world == 1 else ""),
                 "temporal_block": tb,
+                "arith": args.arith,
                 "overlap": not args.no_overlap,
                 "launch_plan": s.plan() if not args.no_overlap else None,
             },

@@ -119,8 +119,10 @@ int heat2d_plan_split(int dtype, const heat2d_layout* L, int k, int64_t band, he
 }
 
 int heat2d_tb(int dtype, const void* src, void* dst, const heat2d_layout* L, int64_t rb, int64_t re, int k,
-              double r, void* stream, int64_t tile_rows) {
-  return guarded([&] { kern::launch_tb((DType)dtype, src, dst, to_layout(L), rb, re, k, r, as_stream(stream), tile_rows); });
+              double r, void* stream, int64_t tile_rows, int arith) {
+  return guarded([&] {
+    kern::launch_tb((DType)dtype, src, dst, to_layout(L), rb, re, k, r, as_stream(stream), tile_rows, 0, arith);
+  });
 }
 
 int heat2d_init_field(int dtype, void* field, const heat2d_layout* L, const heat2d_ic* ic,
@@ -154,8 +156,8 @@ int heat2d_unpack_rows(int dtype, void* field, const heat2d_layout* L, int64_t r
 }
 
 int heat2d_cpu_tb(int dtype, const void* src, void* dst, const heat2d_layout* L, int64_t rb, int64_t re, int k,
-                  double r) {
-  return guarded([&] { cpu::tb((DType)dtype, src, dst, to_layout(L), rb, re, k, r); });
+                  double r, int arith) {
+  return guarded([&] { cpu::tb((DType)dtype, src, dst, to_layout(L), rb, re, k, r, arith); });
 }
 
 int heat2d_cpu_init_field(int dtype, void* field, const heat2d_layout* L, const heat2d_ic* ic, const double* xc,
@@ -238,8 +240,8 @@ int heat2d_solver_layout(void* s, heat2d_layout* out) {
   });
 }
 
-int heat2d_jit_create(int dtype, const heat2d_layout* L, double r, int device, void** out) {
-  return guarded([&] { *out = new JitStencil((DType)dtype, to_layout(L), r, device); });
+int heat2d_jit_create(int dtype, const heat2d_layout* L, double r, int device, int arith, void** out) {
+  return guarded([&] { *out = new JitStencil((DType)dtype, to_layout(L), r, device, arith); });
 }
 
 int heat2d_jit_free(void* j) {
@@ -250,9 +252,9 @@ int heat2d_jit_step(void* j, const void* src, void* dst, void* stream) {
   return guarded([&] { static_cast<JitStencil*>(j)->step(src, dst, as_stream(stream)); });
 }
 
-int heat2d_jit_render(int dtype, const heat2d_layout* L, double r, char* buf, int64_t cap, int64_t* len) {
+int heat2d_jit_render(int dtype, const heat2d_layout* L, double r, int arith, char* buf, int64_t cap, int64_t* len) {
   return guarded([&] {
-    const std::string s = jit_render((DType)dtype, to_layout(L), r);
+    const std::string s = jit_render((DType)dtype, to_layout(L), r, arith);
     *len = (int64_t)s.size();
     if (buf && cap > 0) {
       const size_t n = std::min<size_t>((size_t)cap - 1, s.size());

@@ -54,6 +54,7 @@ struct Args {
   bool quiet = false;
   bool timers = false;
   std::string engine = "tb";
+  std::string arith = "exact";  // exact | fma (SolverConfig::arith)
 };
 
 void usage() {
@@ -61,7 +62,7 @@ void usage() {
       "usage: heat2d [input.dat] [--variant mpi|serial|cuda] [--gpus N | --cpu] [--dtype fp64|fp32]\n"
       "              [--tb K] [--no-overlap] [--copy-swap] [--managed] [--graph] [--ic NAME]\n"
       "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
-      "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit]\n");
+      "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith exact|fma]\n");
 }
 
 Args parse_args(int argc, char** argv) {
@@ -89,6 +90,7 @@ Args parse_args(int argc, char** argv) {
     else if (s == "--managed") a.managed = true;
     else if (s == "--graph") a.graph = true;
     else if (s == "--engine") a.engine = need("--engine");
+    else if (s == "--arith") a.arith = need("--arith");
     else if (s == "--print-every") a.print_every = std::atoll(need("--print-every").c_str());
     else if (s == "--check-every") a.check_every = std::atoll(need("--check-every").c_str());
     else if (s == "--ntime") a.ntime = std::atoll(need("--ntime").c_str());
@@ -160,6 +162,8 @@ void run_rank(Shared& sh, int rank) {
     cfg.autotune = -1;  // split schedule on big slabs: pick the fastest launch plan on the first cycle
     if (a.engine != "tb" && a.engine != "jit") fail(__FILE__, __LINE__, "--engine must be tb or jit");
     cfg.engine = a.engine == "jit" ? 1 : 0;  // jit: hipRTC kernel rendered for this slab (python/cuda/cuda.py)
+    if (a.arith != "exact" && a.arith != "fma") fail(__FILE__, __LINE__, "--arith must be exact or fma");
+    cfg.arith = a.arith == "fma" ? 1 : 0;
     Solver s(cfg, tr);
     s.init(sh.prob.ic, sh.prob.x.data(), sh.prob.x.data());
     const bool inclusive = sh.prob.conv == Convention::Inclusive;
@@ -317,9 +321,10 @@ int main(int argc, char** argv) {
       std::fprintf(f,
                    "{\"n\": %lld, \"nranks\": %d, \"dtype\": \"%s\", \"tb\": %d, \"steps\": %lld, \"wall_s\": %.9g, "
                    "\"gpts_per_s\": %.9g, \"model_gb_per_s\": %.9g, \"sum\": %.17g, \"min\": %.17g, \"max\": %.17g, "
-                   "\"backend\": \"%s\", \"variant\": \"%s\"}\n",
+                   "\"backend\": \"%s\", \"variant\": \"%s\", \"arith\": \"%s\"}\n",
                    (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, (long long)ntime, tmax, gpts, gpts * bpp,
-                   sh.final_stats[0], sh.final_stats[2], sh.final_stats[3], a.cpu ? "cpu" : "hip", a.variant.c_str());
+                   sh.final_stats[0], sh.final_stats[2], sh.final_stats[3], a.cpu ? "cpu" : "hip", a.variant.c_str(),
+                   a.arith.c_str());
       std::fclose(f);
     }
   }

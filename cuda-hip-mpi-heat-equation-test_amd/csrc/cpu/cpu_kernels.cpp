@@ -39,7 +39,7 @@ void parallel_rows(int64_t begin, int64_t end, F&& f) {
 }
 
 template <typename T>
-void tb_impl(const T* src, T* dst, const SlabLayout& L, int64_t rb, int64_t re, int k, T r) {
+void tb_impl(const T* src, T* dst, const SlabLayout& L, int64_t rb, int64_t re, int k, T r, int arith) {
   const int64_t R = re - rb + 2 * k;  // level-0 rows [rb-k, re+k)
   const int64_t P = L.pitch;
   std::vector<T> A((size_t)(R * P)), B((size_t)(R * P));
@@ -64,7 +64,8 @@ void tb_impl(const T* src, T* dst, const SlabLayout& L, int64_t rb, int64_t re, 
         for (int64_t j = 0; j < L.ncols; ++j) {
           // reference order: T(x+1,y) + T(x,y+1) + T(x-1,y) + T(x,y-1) - 4*T(x,y)
           const T sum = ((dn[j] + mid[j + 1]) + up[j]) + mid[j - 1];
-          out[j] = mid[j] + r * (sum - T(4) * mid[j]);
+          // arith 1: the contracted fma form of the device kernel (tb_impl.hpp)
+          out[j] = arith == 1 ? std::fma(r, sum - T(4) * mid[j], mid[j]) : mid[j] + r * (sum - T(4) * mid[j]);
         }
       }
     });
@@ -150,13 +151,14 @@ int num_threads() {
 }
 
 void tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin, int64_t row_end,
-        int k, double r) {
+        int k, double r, int arith) {
   HEAT2D_REQUIRE(k >= 1 && k <= L.halo, "k out of range");
+  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 or 1");
   if (row_end <= row_begin) return;
   if (dt == DType::F32)
-    tb_impl<float>(static_cast<const float*>(src), static_cast<float*>(dst), L, row_begin, row_end, k, (float)r);
+    tb_impl<float>(static_cast<const float*>(src), static_cast<float*>(dst), L, row_begin, row_end, k, (float)r, arith);
   else
-    tb_impl<double>(static_cast<const double*>(src), static_cast<double*>(dst), L, row_begin, row_end, k, r);
+    tb_impl<double>(static_cast<const double*>(src), static_cast<double*>(dst), L, row_begin, row_end, k, r, arith);
 }
 
 void init(DType dt, void* field, const SlabLayout& L, const kern::IcParams& ic, const double* xc,

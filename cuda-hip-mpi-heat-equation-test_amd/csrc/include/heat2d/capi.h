@@ -32,7 +32,7 @@ typedef struct heat2d_config {
   int32_t tb, overlap, copy_swap, managed, device, use_graph;
   int64_t tile_rows, halo;
   int32_t comm_cus, autotune;
-  int32_t engine, reserved2_;
+  int32_t engine, arith; /* arith: 0 reference rounding, 1 contracted fma */
 } heat2d_config;
 
 typedef struct heat2d_tb_plan {
@@ -76,7 +76,7 @@ int heat2d_parse_input(const char* text, double* out7);
 /* Raw ops on caller-owned memory (device pointers for the HIP ops; host for cpu_*).
  * `stream` is a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). */
 int heat2d_tb(int dtype, const void* src, void* dst, const heat2d_layout* L, int64_t rb,
-              int64_t re, int k, double r, void* stream, int64_t tile_rows);
+              int64_t re, int k, double r, void* stream, int64_t tile_rows, int arith);
 int heat2d_init_field(int dtype, void* field, const heat2d_layout* L, const heat2d_ic* ic,
                       const double* xcoord_dev, const double* ycoord_dev, void* stream);
 int heat2d_stats(int dtype, const void* field, const void* other, const heat2d_layout* L,
@@ -90,7 +90,7 @@ int heat2d_unpack_rows(int dtype, void* field, const heat2d_layout* L, int64_t r
                        int64_t nrows, const void* buf, void* stream);
 
 int heat2d_cpu_tb(int dtype, const void* src, void* dst, const heat2d_layout* L, int64_t rb,
-                  int64_t re, int k, double r);
+                  int64_t re, int k, double r, int arith);
 int heat2d_cpu_init_field(int dtype, void* field, const heat2d_layout* L, const heat2d_ic* ic,
                           const double* xcoord, const double* ycoord);
 int heat2d_cpu_stats(int dtype, const void* field, const void* other, const heat2d_layout* L,
@@ -117,10 +117,10 @@ int heat2d_solver_download(void* s, void* host, int64_t ld);
 int heat2d_solver_upload(void* s, const void* host, int64_t ld);
 int heat2d_solver_layout(void* s, heat2d_layout* out);
 /* run-time specialised FTCS step (hipRTC; python/cuda/cuda.py parity) */
-int heat2d_jit_create(int dtype, const heat2d_layout* L, double r, int device, void** out);
+int heat2d_jit_create(int dtype, const heat2d_layout* L, double r, int device, int arith, void** out);
 int heat2d_jit_free(void* j);
 int heat2d_jit_step(void* j, const void* src, void* dst, void* stream);
-int heat2d_jit_render(int dtype, const heat2d_layout* L, double r, char* buf, int64_t cap, int64_t* len);
+int heat2d_jit_render(int dtype, const heat2d_layout* L, double r, int arith, char* buf, int64_t cap, int64_t* len);
 int heat2d_jit_compile_check(const char* source, const char* arch, int64_t* code_bytes);
 /* phase timers (hipEvents): on/off; read = [main ms, edge ms, exchange ms, cycle ms, cycles], then reset */
 int heat2d_solver_timing(void* s, int on);

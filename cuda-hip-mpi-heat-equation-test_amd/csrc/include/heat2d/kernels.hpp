@@ -30,18 +30,22 @@ struct TbPlan {
 // Plan a launch that advances rows [row_begin, row_end) of the slab by k steps.
 // tile_rows <= 0 selects the occupancy-driven default; cus > 0 plans for a
 // stream restricted to that many CUs (comm-reserving CU mask).
+// arith: 0 = reference arithmetic (every op rounded), 1 = contracted fma form
+// (tb_impl.hpp, March); every launcher below takes it last.
 TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k,
-               int64_t tile_rows = 0, int cus = 0);
+               int64_t tile_rows = 0, int cus = 0, int arith = 0);
 
 // dst(rows [row_begin,row_end)) = k FTCS steps of src. `src`/`dst` are
 // allocation bases laid out per `L`. Requires k <= L.halo and the k ghost rows
 // on both sides of the range to hold valid data at time t (Dirichlet rows are
 // recognised from L.row0 / L.nrows_global and kept fixed).
 void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin,
-               int64_t row_end, int k, double r, hipStream_t stream, int64_t tile_rows = 0, int cus = 0);
+               int64_t row_end, int k, double r, hipStream_t stream, int64_t tile_rows = 0, int cus = 0,
+               int arith = 0);
 // Same for TWO disjoint row ranges [rb0, re0) and [rb1, re1) in one launch.
 void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t rb0, int64_t re0, int64_t rb1,
-                int64_t re1, int k, double r, hipStream_t stream, int64_t tile_rows = 0, int cus = 0);
+                int64_t re1, int k, double r, hipStream_t stream, int64_t tile_rows = 0, int cus = 0,
+                int arith = 0);
 
 // Split schedule of one cycle (k steps over the whole slab) into two launches
 // on two streams:
@@ -62,13 +66,14 @@ struct SplitPlan {
 };
 // ring_override: 4 | 6 (0: default); main_bands: MAIN row bands (0: persistent default)
 SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus = 0, int spare_waves = 0,
-                     int ring_override = 0, int64_t main_bands = 0);
+                     int ring_override = 0, int64_t main_bands = 0, int arith = 0);
 // The alternative the autotuner weighs against the split (valid = 2): ONE
 // general launch over the whole slab (no edge part), e.g. for small grids
 // where the second launch costs more than it saves.
-SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int ring_override = 0, int64_t bands = 0);
+SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int ring_override = 0, int64_t bands = 0,
+                      int arith = 0);
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
-                  double r, hipStream_t stream);
+                  double r, hipStream_t stream, int arith = 0);
 
 // Initial / boundary condition kinds (covers every IC of the reference
 // variants, see models/presets.py for the mapping).

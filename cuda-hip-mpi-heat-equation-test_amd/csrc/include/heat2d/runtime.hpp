@@ -45,7 +45,8 @@ struct SolverConfig {
   int32_t autotune;    // split schedule: time candidate (ring, bands) plans once per depth and keep the fastest
                        // (-1 auto: on for slabs >= 2^24 points, 0 off, 1 on)
   int32_t engine;      // 0: temporal-blocked kernels; 1: run-time specialised hipRTC kernel (K = 1, jit.hpp)
-  int32_t reserved2_;
+  int32_t arith;       // 0: reference arithmetic, every op rounded (bitwise == NumPy golden);
+                       // 1: contracted fma(r, sum - 4c, c) (one op fewer per point, kernels.hpp)
 };
 
 // ---------------------------------------------------------------- transports
@@ -100,7 +101,7 @@ std::shared_ptr<Transport> make_callback_transport(const CallbackOps& ops, int r
 
 namespace cpu {
 void tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin,
-        int64_t row_end, int k, double r);
+        int64_t row_end, int k, double r, int arith = 0);
 void init(DType dt, void* field, const SlabLayout& L, const kern::IcParams& ic,
           const double* xcoord, const double* ycoord);
 void stats(DType dt, const void* field, const void* other, const SlabLayout& L, double out[6]);

@@ -29,7 +29,9 @@
 //     c + r*((((S + E) + N) + W) - 4c) (fortran/hip/heat_kernel.cpp:43, with
 //     S = T(x+1,y), E = T(x,y+1), N = T(x-1,y), W = T(x,y-1)) and the file is
 //     built with -ffp-contract=off: results are bitwise identical to the CPU
-//     reference and to an unblocked K=1 run, in fp64 and in fp32.
+//     reference and to an unblocked K=1 run, in fp64 and in fp32. arith = 1
+//     selects the contracted form fma(r, sum - 4c, c) (one op fewer per point;
+//     bitwise equal to its CPU twin; equal to arith 0 when r is a power of two).
 #include <cmath>
 
 #include "tb_impl.hpp"
@@ -73,25 +75,36 @@ int default_ring(DType dt, int k) {
   return (k == 10 || k == 11) ? 6 : 4;
 }
 
-int occupancy(DType dt, int ring, bool main, int k) {
-  if (dt == DType::F32) {
-    if (ring == 4) return main ? occupancy_blocks<float, 4, true>(k) : occupancy_blocks<float, 4, false>(k);
-    return main ? occupancy_blocks<float, 6, true>(k) : occupancy_blocks<float, 6, false>(k);
+template <typename T, int AR>
+int occupancy_t(int ring, bool main, int k) {
+  if (ring == 4) return main ? occupancy_blocks<T, 4, true, AR>(k) : occupancy_blocks<T, 4, false, AR>(k);
+  return main ? occupancy_blocks<T, 6, true, AR>(k) : occupancy_blocks<T, 6, false, AR>(k);
+}
+
+int occupancy(DType dt, int ring, bool main, int k, int arith) {
+  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 (exact) or 1 (fma)");
+  if (dt == DType::F32) return arith ? occupancy_t<float, 1>(ring, main, k) : occupancy_t<float, 0>(ring, main, k);
+  return arith ? occupancy_t<double, 1>(ring, main, k) : occupancy_t<double, 0>(ring, main, k);
+}
+
+template <typename T, int AR>
+void dispatch_ar(int ring, bool main, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
+                 hipStream_t st) {
+  if (ring == 4) {
+    if (main) dispatch<T, 4, true, AR>(k, nblocks, s, d, a, r, st);
+    else dispatch<T, 4, false, AR>(k, nblocks, s, d, a, r, st);
+  } else {
+    if (main) dispatch<T, 6, true, AR>(k, nblocks, s, d, a, r, st);
+    else dispatch<T, 6, false, AR>(k, nblocks, s, d, a, r, st);
   }
-  if (ring == 4) return main ? occupancy_blocks<double, 4, true>(k) : occupancy_blocks<double, 4, false>(k);
-  return main ? occupancy_blocks<double, 6, true>(k) : occupancy_blocks<double, 6, false>(k);
 }
 
 template <typename T>
-void dispatch_t(int ring, bool main, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
+void dispatch_t(int ring, bool main, int arith, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
                 hipStream_t st) {
-  if (ring == 4) {
-    if (main) dispatch<T, 4, true>(k, nblocks, s, d, a, r, st);
-    else dispatch<T, 4, false>(k, nblocks, s, d, a, r, st);
-  } else {
-    if (main) dispatch<T, 6, true>(k, nblocks, s, d, a, r, st);
-    else dispatch<T, 6, false>(k, nblocks, s, d, a, r, st);
-  }
+  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 (exact) or 1 (fma)");
+  if (arith) dispatch_ar<T, 1>(ring, main, k, nblocks, s, d, a, r, st);
+  else dispatch_ar<T, 0>(ring, main, k, nblocks, s, d, a, r, st);
 }
 
 void check_layout(const SlabLayout& L, int k) {
@@ -129,7 +142,7 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t slots, int k) {
 
 // Launch `rects` (item counts from their nb and strip ranges) on `nwaves` waves.
 void launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
-                  const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream) {
+                  const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith) {
   HEAT2D_REQUIRE(nrect >= 1 && nrect <= kMaxRects, "bad rect count");
   TbArgs a{};
   a.pitch = L.pitch;
@@ -155,10 +168,10 @@ void launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int
   const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
   const int64_t o = L.origin();
   if (dt == DType::F32)
-    dispatch_t<float>(ring, main, k, nblocks, static_cast<const float*>(src) + o, static_cast<float*>(dst) + o, a,
+    dispatch_t<float>(ring, main, arith, k, nblocks, static_cast<const float*>(src) + o, static_cast<float*>(dst) + o, a,
                       (float)r, stream);
   else
-    dispatch_t<double>(ring, main, k, nblocks, static_cast<const double*>(src) + o, static_cast<double*>(dst) + o,
+    dispatch_t<double>(ring, main, arith, k, nblocks, static_cast<const double*>(src) + o, static_cast<double*>(dst) + o,
                        a, r, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("tb_kernel launch: ") + hipGetErrorString(e));
@@ -167,7 +180,7 @@ void launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int
 }  // namespace
 
 TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k, int64_t tile_rows,
-               int cus) {
+               int cus, int arith) {
   check_layout(L, k);
   HEAT2D_REQUIRE(row_begin >= 0 && row_end <= L.nrows && row_begin < row_end, "bad row range");
   TbPlan p{};
@@ -180,7 +193,7 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
   const int64_t rows = row_end - row_begin;
   p.prefetch = default_ring(dt, k);
   p.main = 0;
-  const int bpc = occupancy(dt, p.prefetch, false, k);
+  const int bpc = occupancy(dt, p.prefetch, false, k, arith);
   p.blocks_per_cu = bpc;
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;  // resident waves
   int64_t nbands;
@@ -199,17 +212,17 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
 }
 
 void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k,
-               double r, hipStream_t stream, int64_t tile_rows, int cus) {
-  launch_tb2(dt, src, dst, L, row_begin, row_end, 0, 0, k, r, stream, tile_rows, cus);
+               double r, hipStream_t stream, int64_t tile_rows, int cus, int arith) {
+  launch_tb2(dt, src, dst, L, row_begin, row_end, 0, 0, k, r, stream, tile_rows, cus, arith);
 }
 
 void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t rb0, int64_t re0, int64_t rb1,
-                int64_t re1, int k, double r, hipStream_t stream, int64_t tile_rows, int cus) {
+                int64_t re1, int k, double r, hipStream_t stream, int64_t tile_rows, int cus, int arith) {
   check_layout(L, k);
   const int64_t n0 = std::max<int64_t>(0, re0 - rb0), n1 = std::max<int64_t>(0, re1 - rb1);
   if (n0 + n1 == 0) return;
   // plan over the concatenated rows, then give each range its share of bands
-  const TbPlan p = plan_tb(dt, L, 0, std::min<int64_t>(n0 + n1, L.nrows), k, tile_rows, cus);
+  const TbPlan p = plan_tb(dt, L, 0, std::min<int64_t>(n0 + n1, L.nrows), k, tile_rows, cus, arith);
   TbRect rects[2];
   int nr = 0;
   const int64_t nb = std::max<int64_t>(p.ntiles, (n0 > 0) + (n1 > 0));
@@ -217,11 +230,11 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
   if (n0 > 0) rects[nr++] = TbRect{rb0, re0, 0, p.nstrips, std::min<int64_t>(nb0, n0)};
   if (n1 > 0) rects[nr++] = TbRect{rb1, re1, 0, p.nstrips, std::min<int64_t>(nb - nb0, n1)};
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * p.blocks_per_cu * 4;
-  launch_rects(dt, src, dst, L, k, p.prefetch, false, rects, nr, slots, r, stream);
+  launch_rects(dt, src, dst, L, k, p.prefetch, false, rects, nr, slots, r, stream, arith);
 }
 
 SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus, int spare_waves,
-                     int ring_override, int64_t main_bands) {
+                     int ring_override, int64_t main_bands, int arith) {
   check_layout(L, k);
   SplitPlan p{};
   p.k = k;
@@ -232,7 +245,7 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   const int64_t rows_m = n - 2 * B;
   if (rows_m < 4 * k) return p;  // valid = 0: too thin to split
   // MAIN: the interior rows, all strips, persistent (one item per resident wave)
-  const int bpc = occupancy(dt, p.ring, true, k);
+  const int bpc = occupancy(dt, p.ring, true, k, arith);
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
   const int64_t mw = std::max<int64_t>(4, slots - std::max(0, spare_waves));
   int64_t nb_m = choose_bands(rows_m, ns, mw, k);
@@ -248,20 +261,20 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   p.edge[1] = TbRect{n - B, n, 0, ns, 1};
   p.nedge = 2;
   p.edge_items = 2 * ns;
-  const int bpc_e = occupancy(dt, p.ring, false, k);
+  const int bpc_e = occupancy(dt, p.ring, false, k, arith);
   p.edge_waves = std::min<int64_t>(p.edge_items, (int64_t)cu_count() * bpc_e * 4);
   p.valid = 1;
   return p;
 }
 
-SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_override, int64_t bands) {
+SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_override, int64_t bands, int arith) {
   check_layout(L, k);
   SplitPlan p{};
   p.k = k;
   p.ring = (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k);
   const int64_t U = useful_width(dt, k);
   const int64_t ns = (L.ncols + U - 1) / U;
-  const int bpc = occupancy(dt, p.ring, false, k);
+  const int bpc = occupancy(dt, p.ring, false, k, arith);
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
   int64_t nb = choose_bands(L.nrows, ns, slots, k);
   if (bands > 0) nb = std::min<int64_t>(bands, std::max<int64_t>(1, L.nrows / (2 * (int64_t)k)));
@@ -274,16 +287,16 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
 }
 
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
-                  double r, hipStream_t stream) {
+                  double r, hipStream_t stream, int arith) {
   HEAT2D_REQUIRE(p.valid, "invalid split plan");
   if (p.valid == 2) {  // single general launch over the whole slab (no edge part)
-    if (main_part) launch_rects(dt, src, dst, L, p.k, p.ring, false, &p.main, 1, p.main_waves, r, stream);
+    if (main_part) launch_rects(dt, src, dst, L, p.k, p.ring, false, &p.main, 1, p.main_waves, r, stream, arith);
     return;
   }
   if (main_part)
-    launch_rects(dt, src, dst, L, p.k, p.ring, true, &p.main, 1, p.main_waves, r, stream);
+    launch_rects(dt, src, dst, L, p.k, p.ring, true, &p.main, 1, p.main_waves, r, stream, arith);
   else
-    launch_rects(dt, src, dst, L, p.k, p.ring, false, p.edge, p.nedge, p.edge_waves, r, stream);
+    launch_rects(dt, src, dst, L, p.k, p.ring, false, p.edge, p.nedge, p.edge_waves, r, stream, arith);
 }
 
 }  // namespace kern

@@ -5,7 +5,7 @@
 namespace heat2d {
 namespace kern {
 namespace tbimpl {
-H2D_TB_UNIT(float, 6, false)
+H2D_TB_UNIT(float, 6, false, 0)
 }  // namespace tbimpl
 }  // namespace kern
 }  // namespace heat2d

@@ -137,7 +137,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uin
 // (corner items, both) pays a select per element and level; the kernel runs
 // those items in two half-height pieces so they do not become the tail.
 // (0 * x is +-0 and C + +-0 == C for the finite values the march carries.)
-template <typename T, int NV, int K, int EK, int RING>
+//
+// Arithmetic AR (SolverConfig::arith): 0 = the reference expression with every
+// operation rounded, C + r*(sum - 4C) (-ffp-contract=off; bitwise equal to the
+// CPU twin and the NumPy golden); 1 = the same expression contracted to
+// fma(r, sum - 4C, C) — what hipcc's default -ffp-contract=fast makes of the
+// reference's own kernel line (fortran/hip/heat_kernel.cpp:43): one VALU op
+// fewer per point (5 fp64 ops + 2 DPP moves instead of 6 + 2) for a kernel that
+// is VALU-co-bound. When r is a power of two (sigma = 0.25 in every shipped
+// input) r*x is exact and both forms round identically (normal range).
+template <typename T, int NV, int K, int EK, int RING, int AR>
 struct March {
   using S = TbShape<T, NV, K>;
   static constexpr int V = S::V;
@@ -216,7 +225,8 @@ struct March {
       else if constexpr (EK == 1) re = rs;
       else if constexpr (EK == 2) re = rl[e];
       else re = frame_row ? T(0) : rl[e];
-      out[e] = C[e] + re * fma_t(T(-4), C[e], sum);
+      if constexpr (AR == 1) out[e] = fma_t(re, fma_t(T(-4), C[e], sum), C[e]);
+      else out[e] = C[e] + re * fma_t(T(-4), C[e], sum);
     }
   }
 
@@ -307,7 +317,7 @@ struct March {
   }
 };
 
-template <typename T, int NV, int K, int EK, int RING>
+template <typename T, int NV, int K, int EK, int RING, int AR>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
                                       int64_t t1, int lane) {
   using S = TbShape<T, NV, K>;
@@ -317,7 +327,7 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   const int64_t c0 = u0 - S::KA;
   const int64_t mycol = c0 + (int64_t)lane * V;
   const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
-  March<T, NV, K, EK, RING> w;
+  March<T, NV, K, EK, RING, AR> w;
   // row base = column col_lo (= -cpad) of row 0; offsets are relative to it
   w.srow = reinterpret_cast<const char*>(src + a.col_lo);
   w.drow = reinterpret_cast<char*>(dst + a.col_lo);
@@ -372,7 +382,7 @@ __device__ __forceinline__ bool tb_item(const TbArgs& a, int64_t it, int64_t& st
 // frame-column strips — two code paths, fewer registers than the general
 // kernel (no per-level row tests, no corner selects). MAIN = false: the general
 // kernel classifies each item (edge kinds 0..3, see March).
-template <typename T, int NV, int K, int RING, bool MAIN>
+template <typename T, int NV, int K, int RING, bool MAIN, int AR>
 __global__ __launch_bounds__(256) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
   using S = TbShape<T, NV, K>;
   const int lane = threadIdx.x & 63;
@@ -389,9 +399,9 @@ __global__ __launch_bounds__(256) void tb_kernel(const T* __restrict__ src, T* _
     const int64_t c0 = strip * S::U - S::KA;
     if constexpr (MAIN) {
       if ((c0 < 0) || (c0 + S::W > a.ncols))
-        march<T, NV, K, 2, RING>(src, dst, a, r, strip, t0, t1, lane);
+        march<T, NV, K, 2, RING, AR>(src, dst, a, r, strip, t0, t1, lane);
       else
-        march<T, NV, K, 0, RING>(src, dst, a, r, strip, t0, t1, lane);
+        march<T, NV, K, 0, RING, AR>(src, dst, a, r, strip, t0, t1, lane);
     } else {
 #ifdef HEAT2D_AB_NO_EDGE  // timing experiments only (bench A/B builds): frame handling off, wrong numerics
       const int ek = 0;
@@ -401,22 +411,22 @@ __global__ __launch_bounds__(256) void tb_kernel(const T* __restrict__ src, T* _
                      (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
 #endif
       switch (ek) {
-        case 0: march<T, NV, K, 0, RING>(src, dst, a, r, strip, t0, t1, lane); break;
-        case 1: march<T, NV, K, 1, RING>(src, dst, a, r, strip, t0, t1, lane); break;
-        case 2: march<T, NV, K, 2, RING>(src, dst, a, r, strip, t0, t1, lane); break;
-        default: march<T, NV, K, 3, RING>(src, dst, a, r, strip, t0, t1, lane); break;
+        case 0: march<T, NV, K, 0, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
+        case 1: march<T, NV, K, 1, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
+        case 2: march<T, NV, K, 2, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
+        default: march<T, NV, K, 3, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
       }
     }
   }
 }
 
-template <typename T, int NV, int K, int RING, bool MAIN>
+template <typename T, int NV, int K, int RING, bool MAIN, int AR>
 constexpr auto kernel_ptr() {
-  return &tb_kernel<T, NV, K, RING, MAIN>;
+  return &tb_kernel<T, NV, K, RING, MAIN, AR>;
 }
 
 // Resident 256-thread workgroups per CU for one kernel instance (occupancy API).
-template <typename T, int NV, int K, int RING, bool MAIN>
+template <typename T, int NV, int K, int RING, bool MAIN, int AR>
 int blocks_per_cu() {
   static std::mutex mu;
   static std::map<int, int> cache;  // device -> blocks/CU
@@ -426,7 +436,7 @@ int blocks_per_cu() {
   auto it = cache.find(dev);
   if (it != cache.end()) return it->second;
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, RING, MAIN>()),
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, RING, MAIN, AR>()),
                                                    256, 0) != hipSuccess ||
       nb <= 0)
     nb = 1;
@@ -434,51 +444,46 @@ int blocks_per_cu() {
   return nb;
 }
 
-// Per-(T, RING, MAIN) entry points (16 B per lane), explicitly instantiated in
-// tb_<dtype>_r<RING>_<main|gen>.hip (one translation unit each, compiled in parallel).
-template <typename T, int RING, bool MAIN>
+// Per-(T, RING, MAIN, AR) entry points (16 B per lane), explicitly instantiated in
+// tb_<dtype>_r<RING>_<main|gen>[_fma].hip (one translation unit each, compiled in parallel).
+template <typename T, int RING, bool MAIN, int AR>
 void dispatch(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
-template <typename T, int RING, bool MAIN>
+template <typename T, int RING, bool MAIN, int AR>
 int occupancy_blocks(int k);
 
-#define H2D_TB_CASE(T, RING, MAIN, KK)                                                                    \
-  case KK:                                                                                                \
-    hipLaunchKernelGGL((tb_kernel<T, 1, KK, RING, MAIN>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
+#define H2D_TB_CASE(T, RING, MAIN, AR, KK)                                                                    \
+  case KK:                                                                                                    \
+    hipLaunchKernelGGL((tb_kernel<T, 1, KK, RING, MAIN, AR>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
     return;
-#define H2D_OCC_CASE(T, RING, MAIN, KK) \
-  case KK:                              \
-    return blocks_per_cu<T, 1, KK, RING, MAIN>();
+#define H2D_OCC_CASE(T, RING, MAIN, AR, KK) \
+  case KK:                                  \
+    return blocks_per_cu<T, 1, KK, RING, MAIN, AR>();
 
-// Instantiate dispatch/occupancy for K = 1..16 of one (T, RING, MAIN).
-#define H2D_TB_UNIT(T, RING, MAIN)                                                                          \
-  template <>                                                                                               \
-  void dispatch<T, RING, MAIN>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r,         \
-                               hipStream_t s) {                                                             \
-    switch (k) {                                                                                            \
-      H2D_TB_CASE(T, RING, MAIN, 1) H2D_TB_CASE(T, RING, MAIN, 2) H2D_TB_CASE(T, RING, MAIN, 3)             \
-      H2D_TB_CASE(T, RING, MAIN, 4) H2D_TB_CASE(T, RING, MAIN, 5) H2D_TB_CASE(T, RING, MAIN, 6)             \
-      H2D_TB_CASE(T, RING, MAIN, 7) H2D_TB_CASE(T, RING, MAIN, 8) H2D_TB_CASE(T, RING, MAIN, 9)             \
-      H2D_TB_CASE(T, RING, MAIN, 10) H2D_TB_CASE(T, RING, MAIN, 11) H2D_TB_CASE(T, RING, MAIN, 12)          \
-      H2D_TB_CASE(T, RING, MAIN, 13) H2D_TB_CASE(T, RING, MAIN, 14) H2D_TB_CASE(T, RING, MAIN, 15)          \
-      H2D_TB_CASE(T, RING, MAIN, 16)                                                                        \
-      default:                                                                                              \
-        break;                                                                                              \
-    }                                                                                                       \
-    HEAT2D_REQUIRE(false, "temporal depth not instantiated for this variant");                              \
-  }                                                                                                         \
-  template <>                                                                                               \
-  int occupancy_blocks<T, RING, MAIN>(int k) {                                                              \
-    switch (k) {                                                                                            \
-      H2D_OCC_CASE(T, RING, MAIN, 1) H2D_OCC_CASE(T, RING, MAIN, 2) H2D_OCC_CASE(T, RING, MAIN, 3)          \
-      H2D_OCC_CASE(T, RING, MAIN, 4) H2D_OCC_CASE(T, RING, MAIN, 5) H2D_OCC_CASE(T, RING, MAIN, 6)          \
-      H2D_OCC_CASE(T, RING, MAIN, 7) H2D_OCC_CASE(T, RING, MAIN, 8) H2D_OCC_CASE(T, RING, MAIN, 9)          \
-      H2D_OCC_CASE(T, RING, MAIN, 10) H2D_OCC_CASE(T, RING, MAIN, 11) H2D_OCC_CASE(T, RING, MAIN, 12)       \
-      H2D_OCC_CASE(T, RING, MAIN, 13) H2D_OCC_CASE(T, RING, MAIN, 14) H2D_OCC_CASE(T, RING, MAIN, 15)       \
-      H2D_OCC_CASE(T, RING, MAIN, 16)                                                                       \
-      default:                                                                                              \
-        break;                                                                                              \
-    }                                                                                                       \
-    return 1;                                                                                               \
+// Instantiate dispatch/occupancy for K = 1..16 of one (T, RING, MAIN, AR).
+#define H2D_TB_CASES(M, T, RING, MAIN, AR)                                                             \
+  M(T, RING, MAIN, AR, 1) M(T, RING, MAIN, AR, 2) M(T, RING, MAIN, AR, 3) M(T, RING, MAIN, AR, 4)       \
+  M(T, RING, MAIN, AR, 5) M(T, RING, MAIN, AR, 6) M(T, RING, MAIN, AR, 7) M(T, RING, MAIN, AR, 8)       \
+  M(T, RING, MAIN, AR, 9) M(T, RING, MAIN, AR, 10) M(T, RING, MAIN, AR, 11) M(T, RING, MAIN, AR, 12)    \
+  M(T, RING, MAIN, AR, 13) M(T, RING, MAIN, AR, 14) M(T, RING, MAIN, AR, 15) M(T, RING, MAIN, AR, 16)
+#define H2D_TB_UNIT(T, RING, MAIN, AR)                                                                  \
+  template <>                                                                                           \
+  void dispatch<T, RING, MAIN, AR>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, \
+                                   hipStream_t s) {                                                     \
+    switch (k) {                                                                                        \
+      H2D_TB_CASES(H2D_TB_CASE, T, RING, MAIN, AR)                                                      \
+      default:                                                                                          \
+        break;                                                                                          \
+    }                                                                                                   \
+    HEAT2D_REQUIRE(false, "temporal depth not instantiated for this variant");                          \
+  }                                                                                                     \
+  template <>                                                                                           \
+  int occupancy_blocks<T, RING, MAIN, AR>(int k) {                                                      \
+    switch (k) {                                                                                        \
+      H2D_TB_CASES(H2D_OCC_CASE, T, RING, MAIN, AR)                                                     \
+      default:                                                                                          \
+        break;                                                                                          \
+    }                                                                                                   \
+    return 1;                                                                                           \
   }
 
 }  // namespace tbimpl

@@ -53,7 +53,7 @@ std::map<std::pair<int, std::string>, Compiled> g_cache;  // (device, source) ->
 
 }  // namespace
 
-std::string jit_render(DType dt, const SlabLayout& L, double r) {
+std::string jit_render(DType dt, const SlabLayout& L, double r, int arith) {
   const bool f32 = dt == DType::F32;
   const char* T = f32 ? "float" : "double";
   std::string s;
@@ -67,6 +67,10 @@ std::string jit_render(DType dt, const SlabLayout& L, double r) {
   s += line;
   s += "#define R (" + hex_literal(r, f32) + ")\n";
   s += "#define FOUR ((real)4)\n";
+  // arith 1: the contracted form hipcc's default -ffp-contract=fast gives the
+  // reference line; spelled out, since the module is compiled with contraction off
+  s += arith == 1 ? "#define UPDATE(c, sum) fma(R, (sum) - FOUR * (c), (c))\n"
+                  : "#define UPDATE(c, sum) ((c) + R * ((sum) - FOUR * (c)))\n";
   s += R"(
 extern "C" __global__ void __launch_bounds__(256) heat2d_jit_ftcs(const real* __restrict__ src,
                                                                   real* __restrict__ dst) {
@@ -79,18 +83,19 @@ extern "C" __global__ void __launch_bounds__(256) heat2d_jit_ftcs(const real* __
     // (fortran/hip/heat_kernel.cpp:43); frame / ghost rows and columns are
     // inside the allocation, so no bounds test is needed for neighbours
     const real sum = ((src[o + PITCH] + src[o + 1]) + src[o - PITCH]) + src[o - 1];
-    dst[o] = c + R * (sum - FOUR * c);
+    dst[o] = UPDATE(c, sum);
   }
 }
 )";
   return s;
 }
 
-JitStencil::JitStencil(DType dt, const SlabLayout& L, double r, int device) : L_(L) {
+JitStencil::JitStencil(DType dt, const SlabLayout& L, double r, int device, int arith) : L_(L) {
   HEAT2D_REQUIRE(L.nrows >= 1 && L.ncols >= 1 && L.halo >= 1 && L.cpad >= 1, "layout needs a ghost frame");
   if (device >= 0) H2D_HIP(hipSetDevice(device));
   H2D_HIP(hipGetDevice(&device_));
-  src_ = jit_render(dt, L, r);
+  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 or 1");
+  src_ = jit_render(dt, L, r, arith);
   std::lock_guard<std::mutex> g(g_mu);
   auto key = std::make_pair(device_, src_);
   auto it = g_cache.find(key);

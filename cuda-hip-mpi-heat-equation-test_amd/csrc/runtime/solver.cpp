@@ -66,6 +66,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
   int K = std::max(1, std::min<int>(cfg_.tb <= 0 ? 1 : cfg_.tb, kMaxTB));
   if (cfg_.copy_swap) K = 1;
   HEAT2D_REQUIRE(cfg_.engine == 0 || cfg_.engine == 1, "engine must be 0 (temporal-blocked) or 1 (jit)");
+  HEAT2D_REQUIRE(cfg_.arith == 0 || cfg_.arith == 1, "arith must be 0 (reference rounding) or 1 (fma)");
   if (cfg_.engine == 1) {
     HEAT2D_REQUIRE(hip_, "the jit engine runs on the HIP backend");
     HEAT2D_REQUIRE(!cfg_.copy_swap, "the jit engine has no copy-swap mode");
@@ -129,7 +130,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     if (cfg_.engine == 1) {
-      jit_.reset(new JitStencil(dtype(), L_, cfg_.r, cfg_.device));
+      jit_.reset(new JitStencil(dtype(), L_, cfg_.r, cfg_.device, cfg_.arith));
       cfg_.overlap = 0;
       cfg_.use_graph = 0;
     }
@@ -186,9 +187,9 @@ void Solver::init(const kern::IcParams& ic, const double* xg, const double* yg) 
 void Solver::launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k) {
   if (re <= rb) return;
   if (hip_)
-    kern::launch_tb(dtype(), src, dst, L_, rb, re, k, cfg_.r, s_compute_, cfg_.tile_rows, compute_cus_);
+    kern::launch_tb(dtype(), src, dst, L_, rb, re, k, cfg_.r, s_compute_, cfg_.tile_rows, compute_cus_, cfg_.arith);
   else
-    cpu::tb(dtype(), src, dst, L_, rb, re, k, cfg_.r);
+    cpu::tb(dtype(), src, dst, L_, rb, re, k, cfg_.r, cfg_.arith);
 }
 
 void Solver::exchange_on(void* field, hipStream_t s) {
@@ -272,7 +273,7 @@ const kern::SplitPlan& Solver::split_plan(int k) {
   if (p.k != k) {
     // room for RCCL's workgroups beside the two stencil launches when exchanging
     const int spare = tr_->exchanges() ? 8 : 0;
-    p = kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare);
+    p = kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, 0, 0, cfg_.arith);
     p.k = k;
     const bool big = L_.nrows * L_.ncols >= (int64_t(1) << 24);
     if (p.valid && (cfg_.autotune > 0 || (cfg_.autotune < 0 && big))) autotune_split(k);
@@ -312,9 +313,9 @@ void Solver::autotune_split(int k) {
     void* dst = buf_[cur_ ^ 1];
     H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
     H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
-    kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_);
+    kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith);
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-    kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_);
+    kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_, cfg_.arith);
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
     cur_ ^= 1;
   };
@@ -338,15 +339,15 @@ void Solver::autotune_split(int k) {
   const int64_t nb0 = best.main.nb;
   // without an exchange to hide, a single general launch per cycle competes too
   const bool single_ok = !tr_->exchanges();
-  const int64_t nb1 = single_ok ? kern::plan_single(dtype(), L_, k, compute_cus_).main.nb : 0;
+  const int64_t nb1 = single_ok ? kern::plan_single(dtype(), L_, k, compute_cus_, 0, 0, cfg_.arith).main.nb : 0;
   for (int mode : {1, 2}) {
     if (mode == 2 && !single_ok) continue;
     for (int ring : {4, 6}) {
       for (double f : {1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 1.25, 1.5, 2.0}) {
         const int64_t nb = std::max<int64_t>(1, (int64_t)((mode == 1 ? nb0 : nb1) * f + 0.5));
         if (mode == 1 && ring == best.ring && nb == best.main.nb) continue;
-        kern::SplitPlan c = mode == 1 ? kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, nb)
-                                      : kern::plan_single(dtype(), L_, k, compute_cus_, ring, nb);
+        kern::SplitPlan c = mode == 1 ? kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, nb, cfg_.arith)
+                                      : kern::plan_single(dtype(), L_, k, compute_cus_, ring, nb, cfg_.arith);
         if (!c.valid) continue;
         if (mode == 1)  // more items than waves only via explicit band counts above the default
           c.main_waves = std::min<int64_t>(c.main_items, std::max<int64_t>(c.main_waves, best.main_waves));
@@ -386,16 +387,16 @@ void Solver::cycle_overlap(int k) {
   if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
   if (sp.valid) {
     if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
-    kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_);
+    kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_);
+    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_, cfg_.arith);
   } else {  // slab too thin / narrow to split: all of it beside the exchange
     if (pe) {
       H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
       H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
     }
-    kern::launch_tb(dtype(), src, dst, L_, 0, L_.nrows, k, cfg_.r, s_comm_, 0, 0);
+    kern::launch_tb(dtype(), src, dst, L_, 0, L_.nrows, k, cfg_.r, s_comm_, 0, 0, cfg_.arith);
   }
   if (pe) H2D_HIP(hipEventRecord(pe->ev[3], s_comm_));
   H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));

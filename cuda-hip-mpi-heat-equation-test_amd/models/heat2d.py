@@ -65,13 +65,19 @@ class HeatSolver:
             (-1: only for slabs of >= 2**24 points, 0: off, 1: on).
         rows: solve only the first ``rows`` x-rows of the grid (a rectangular
             rows x n domain, e.g. one rank's slab shape for a 1-GPU rehearsal).
+        arith: "exact" — every operation of the reference update rounded as
+            written (-ffp-contract=off; bitwise equal to the NumPy golden);
+            "fma" — the update contracted to fma(r, sum - 4c, c), what hipcc's
+            default contraction makes of fortran/hip/heat_kernel.cpp:43: one op
+            fewer per point; identical to "exact" when r is a power of two
+            (sigma = 0.25), bitwise equal to the CPU twin for any r.
     """
 
     def __init__(self, problem: Problem, *, dtype: str = "fp64", backend: str = "auto", tb: int = 8,
                  overlap: bool = True, copy_swap: bool = False, managed: bool = False, graph: bool = False,
                  tile_rows: int = 0, halo: int = 0, transport: Optional[T.Transport] = None,
                  device: Optional[int] = None, init: bool = True, rows: Optional[int] = None,
-                 comm_cus: int = 0, autotune: int = -1, engine: str = "tb"):
+                 comm_cus: int = 0, autotune: int = -1, engine: str = "tb", arith: str = "exact"):
         self.problem = problem
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]
@@ -102,6 +108,10 @@ class HeatSolver:
         if engine not in ("tb", "jit"):
             raise ValueError("engine must be 'tb' (temporal-blocked kernels) or 'jit' (hipRTC, one step per launch)")
         cfg.engine = 1 if engine == "jit" else 0
+        if arith not in N.ARITH:
+            raise ValueError(f"arith must be one of {sorted(N.ARITH)}")
+        cfg.arith = N.ARITH[arith]
+        self.arith = arith
         self._cfg = cfg
         h = C.c_void_p()
         N.call("heat2d_solver_create", C.byref(cfg), self.transport.handle, C.byref(h))
@@ -252,7 +262,7 @@ class LoopbackGroup:
     """
 
     def __init__(self, problem: Problem, nranks: int, *, dtype: str = "fp64", backend: str = "auto",
-                 tb: int = 8, tile_rows: int = 0, device: Optional[int] = None):
+                 tb: int = 8, tile_rows: int = 0, device: Optional[int] = None, arith: str = "exact"):
         self.problem = problem
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]
@@ -268,6 +278,7 @@ class LoopbackGroup:
         cfg.tb = tb
         cfg.device = -1 if device is None else int(device)
         cfg.tile_rows = tile_rows
+        cfg.arith = N.ARITH[arith]
         h = C.c_void_p()
         N.call("heat2d_group_create", C.byref(cfg), nranks, C.byref(h))
         self._h = h

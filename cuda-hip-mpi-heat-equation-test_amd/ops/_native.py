@@ -26,6 +26,8 @@ LIB_PATH = os.environ.get("HEAT2D_LIB") or os.path.join(NATIVE_DIR, "libheat2d.s
 CLI_PATH = os.path.join(NATIVE_DIR, "heat2d")
 
 F32, F64 = 0, 1
+# SolverConfig::arith: reference rounding (bitwise == NumPy golden) | contracted fma(r, sum - 4c, c)
+ARITH = {"exact": 0, "fma": 1}
 BACKEND_HIP, BACKEND_CPU = 0, 1
 
 
@@ -65,7 +67,7 @@ class Config(C.Structure):
         ("device", C.c_int32), ("use_graph", C.c_int32),
         ("tile_rows", C.c_int64), ("halo", C.c_int64),
         ("comm_cus", C.c_int32), ("autotune", C.c_int32),
-        ("engine", C.c_int32), ("reserved2_", C.c_int32),
+        ("engine", C.c_int32), ("arith", C.c_int32),
     ]
 
 
@@ -110,14 +112,14 @@ _SIGS = {
     "heat2d_plan_split": (C.c_int, [C.c_int, _LP, C.c_int, _I64, C.POINTER(SplitPlan)]),
     "heat2d_solver_prepare": (C.c_int, [_P, _I64]),
     "heat2d_solver_timing": (C.c_int, [_P, C.c_int]),
-    "heat2d_jit_create": (C.c_int, [C.c_int, _LP, C.c_double, C.c_int, C.POINTER(_P)]),
+    "heat2d_jit_create": (C.c_int, [C.c_int, _LP, C.c_double, C.c_int, C.c_int, C.POINTER(_P)]),
     "heat2d_jit_free": (C.c_int, [_P]),
     "heat2d_jit_step": (C.c_int, [_P, _P, _P, _P]),
-    "heat2d_jit_render": (C.c_int, [C.c_int, _LP, C.c_double, C.c_char_p, _I64, C.POINTER(_I64)]),
+    "heat2d_jit_render": (C.c_int, [C.c_int, _LP, C.c_double, C.c_int, C.c_char_p, _I64, C.POINTER(_I64)]),
     "heat2d_jit_compile_check": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(_I64)]),
     "heat2d_solver_phase_times": (C.c_int, [_P, C.POINTER(C.c_double)]),
     "heat2d_solver_plan": (C.c_int, [_P, C.c_int, C.POINTER(SplitPlan), C.POINTER(C.c_float)]),
-    "heat2d_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double, _P, _I64]),
+    "heat2d_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double, _P, _I64, C.c_int]),
     "heat2d_init_field": (C.c_int, [C.c_int, _P, _LP, C.POINTER(IcParams), _P, _P, _P]),
     "heat2d_stats": (C.c_int, [C.c_int, _P, _P, _LP, _P, _P, _P]),
     "heat2d_stats_work_elems": (_I64, []),
@@ -125,7 +127,7 @@ _SIGS = {
     "heat2d_read": (C.c_int, [_P, _I64, _P, _P, C.c_int]),
     "heat2d_pack_rows": (C.c_int, [C.c_int, _P, _LP, _I64, _I64, _P, _P]),
     "heat2d_unpack_rows": (C.c_int, [C.c_int, _P, _LP, _I64, _I64, _P, _P]),
-    "heat2d_cpu_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double]),
+    "heat2d_cpu_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double, C.c_int]),
     "heat2d_cpu_init_field": (C.c_int, [C.c_int, _P, _LP, C.POINTER(IcParams), _P, _P]),
     "heat2d_cpu_stats": (C.c_int, [C.c_int, _P, _P, _LP, _P]),
     "heat2d_rccl_unique_id": (C.c_int, [_P]),

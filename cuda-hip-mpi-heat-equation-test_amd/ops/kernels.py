@@ -85,9 +85,10 @@ def init_field(field: torch.Tensor, layout: N.Layout, ic, xcoord: np.ndarray,
 
 
 def tb_step(src: torch.Tensor, dst: torch.Tensor, layout: N.Layout, k: int, r: float,
-            rows: Optional[tuple[int, int]] = None, tile_rows: int = 0) -> None:
+            rows: Optional[tuple[int, int]] = None, tile_rows: int = 0, arith: str = "exact") -> None:
     """dst[rows] = k FTCS steps of src (temporal-blocked kernel). The k ghost rows
-    around ``rows`` must be valid in ``src``; Dirichlet rows/cols are kept."""
+    around ``rows`` must be valid in ``src``; Dirichlet rows/cols are kept.
+    ``arith``: "exact" (reference rounding) or "fma" (contracted update)."""
     _check_field(src, layout)
     _check_field(dst, layout)
     if src.dtype != dst.dtype or src.device != dst.device:
@@ -95,12 +96,13 @@ def tb_step(src: torch.Tensor, dst: torch.Tensor, layout: N.Layout, k: int, r: f
     if src.data_ptr() == dst.data_ptr():
         raise ValueError("tb_step is out-of-place (ping-pong fields)")
     rb, re = (0, layout.nrows) if rows is None else rows
+    ar = N.ARITH[arith]
     if src.is_cuda:
         N.call("heat2d_tb", dtype_code(src), C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
-               C.byref(layout), rb, re, k, r, _stream(src), tile_rows)
+               C.byref(layout), rb, re, k, r, _stream(src), tile_rows, ar)
     else:
         N.call("heat2d_cpu_tb", dtype_code(src), C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
-               C.byref(layout), rb, re, k, r)
+               C.byref(layout), rb, re, k, r, ar)
 
 
 def stats(field: torch.Tensor, layout: N.Layout, other: Optional[torch.Tensor] = None) -> dict:

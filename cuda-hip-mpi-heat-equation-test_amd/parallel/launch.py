@@ -38,6 +38,8 @@ def build_parser():
     ap.add_argument("--engine", default=None, choices=["tb", "jit"],
                     help="tb: temporal-blocked kernels; jit: hipRTC kernel rendered at run time "
                          "(default: jit for --variant pycuda on a GPU, else tb)")
+    ap.add_argument("--arith", default="exact", choices=["exact", "fma"],
+                    help="exact: reference rounding (bitwise == NumPy golden); fma: contracted update, one op fewer")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--ntime", type=int, default=None)
     ap.add_argument("--print-every", type=int, default=0)
@@ -99,7 +101,7 @@ def run(argv=None) -> int:
     engine = a.engine or ("jit" if var.name == "pycuda" and backend == "hip" else "tb")
     s = HeatSolver(prob, dtype=a.dtype, backend=backend, tb=a.tb, overlap=not a.no_overlap, copy_swap=a.copy_swap,
                    managed=a.managed or var.managed, graph=a.graph, transport=tr,
-                   device=local if backend == "hip" else None, engine=engine)
+                   device=local if backend == "hip" else None, engine=engine, arith=a.arith)
     if root and not a.quiet:
         if world > 1 or var.outputs == "mpi":
             print(f" Automatic MPI decomposition: {world:12d}  x 1")
@@ -170,7 +172,7 @@ def run(argv=None) -> int:
         else:
             print(f" total time: {elapsed:24.16g}")
         rec = metrics.record(prob.n_owned, ran, elapsed, world, a.dtype, s.tb, backend, a.copy_swap,
-                             {"variant": var.name, "sum": st["sum"], "min": st["min"], "max": st["max"]})
+                             {"variant": var.name, "arith": a.arith, "sum": st["sum"], "min": st["min"], "max": st["max"]})
         if not a.quiet:
             print(f" heat2d: n={prob.n_owned} P={world} {a.dtype} K={s.tb} steps={ran} wall={elapsed:.6f} s  "
                   f"{rec['gpts_per_s']:.3f} Gpts/s  {rec['model_hbm_gb_per_s']:.1f} GB/s(model)  "
