@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--n", type=int, default=32768)
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--tb", type=int, default=0,
-                    help="time steps fused per HBM pass (0: measured best, fp64 12 / fp32 10; profiles/autotune.md)")
+                    help="time steps fused per HBM pass (0: measured best, fp64 12 / fp32 16; profiles/README.md)")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--arith", default="fma", choices=["exact", "fma"],
                     help="fma: contracted update (one op fewer per point); exact: every op rounded")
@@ -61,7 +61,7 @@ def main():
                          "interior) to measure its per-rank cost; not the headline (periodic halo)")
     args = ap.parse_args()
     if args.tb <= 0:
-        args.tb = 12 if args.dtype == "fp64" else 10
+        args.tb = 12 if args.dtype == "fp64" else 16
 
     import torch
     import torch.distributed as dist

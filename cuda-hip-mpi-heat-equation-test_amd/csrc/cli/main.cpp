@@ -42,7 +42,7 @@ struct Args {
   std::string json;
   int gpus = -1;  // -1: 1 if a GPU exists
   bool cpu = false;
-  int tb = 8;
+  int tb = 0;  // 0: measured best per dtype (solver.cpp)
   bool overlap = true;
   bool copy_swap = false;
   bool managed = false;

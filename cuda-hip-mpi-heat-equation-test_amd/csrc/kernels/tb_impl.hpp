@@ -317,6 +317,179 @@ struct March {
   }
 };
 
+// fp32 march on PACKED math (v_pk_add_f32 / v_pk_fma_f32 / v_pk_mul_f32: two
+// fp32 lanes per VALU op, the fp32 rate CDNA4 quotes). A lane's 16-B vector
+// (columns c0..c3) is kept as an even/odd pair of register pairs
+// a = (c0, c2), b = (c1, c3), so the in-lane east/west neighbours of a whole
+// pair are the other pair (east of a is b, west of b is a) and only the
+// across-lane ones need a DPP move plus one pair assembly:
+//   east of b = (c2, c0 of lane+1),   west of a = (c3 of lane-1, c1).
+// Per row and level: 10 packed ops + 2 DPP moves + 2 pair assemblies for 4
+// points. With the element-wise layout March<float> uses, the compiler had to
+// rebuild misaligned pairs for every packed op (~4.9 VALU ops per point and
+// ~2x the registers: 209 VGPRs at K = 10). Same operation order and rounding
+// per element as March (bitwise identical); the loads / stores / ring /
+// descriptors / edge kinds are March's.
+template <int K, int EK, int RING, int AR>
+struct MarchF32 {
+  using F2 = float __attribute__((ext_vector_type(2)));
+  using VT = float __attribute__((ext_vector_type(4)));
+  using U4 = unsigned int __attribute__((ext_vector_type(4)));
+  static constexpr int KX = K > 1 ? K - 1 : 1;
+  static_assert(RING % 2 == 0 && RING >= 4, "ring must be even and >= 4");
+  struct Row {
+    F2 a, b;  // a = (c0, c2), b = (c1, c3)
+  };
+
+  const char* srow;
+  char* drow;
+  int64_t pitch_b;
+  uint32_t nrec;
+  float r;
+  int32_t t0, t1;
+  int32_t fixed_lo, fixed_hi;
+  int32_t mlo;
+  int32_t ld_off;
+  int32_t st_off;
+  Row rl;  // EK & 2: r per element (0 in Dirichlet / pad columns)
+
+  Row X[2][KX];
+  // Level-0 ring. A slot holds a row in memory order (a = (c0, c1),
+  // b = (c2, c3)) from its load until its first use (as the north row), where
+  // it is rearranged IN PLACE to the even/odd form: one swap per row instead
+  // of a rebuild at each of its three uses.
+  Row Lb[RING];
+
+  __device__ __forceinline__ void load_row(int32_t m, Row& out) const {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + (int64_t)m * pitch_b, nrec);
+    const VT v = __builtin_bit_cast(VT, __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off, 0, 0));
+    out = Row{F2{v.x, v.y}, F2{v.z, v.w}};
+  }
+  __device__ __forceinline__ void store_row(int32_t row, bool live, const VT& w) const {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(drow + (int64_t)row * pitch_b, live ? nrec : 0u);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off, 0, 0);
+  }
+  static __device__ __forceinline__ Row split(const Row& v) { return Row{F2{v.a.x, v.b.x}, F2{v.a.y, v.b.y}}; }
+
+  // part = S + E(C) (first partial sum of the reference order)
+  static __device__ __forceinline__ Row partial(const Row& S, const Row& C) {
+    const F2 eb = {C.a.y, from_upper(C.a.x)};
+    return Row{S.a + C.b, S.b + eb};
+  }
+  // sum - 4C (in) and the per-element r (re) of the update C + r*(sum - 4C)
+  __device__ __forceinline__ void terms(const Row& part, const Row& C, const Row& N, int32_t row, Row& in,
+                                        Row& re) const {
+    const F2 wa = {from_lower(C.b.y), C.b.x};
+    const Row sum = {(part.a + N.a) + wa, (part.b + N.b) + C.a};
+    const F2 m4 = {-4.f, -4.f};
+    in = Row{__builtin_elementwise_fma(m4, C.a, sum.a), __builtin_elementwise_fma(m4, C.b, sum.b)};
+    const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
+    if constexpr (EK == 0) {
+      re = Row{F2{r, r}, F2{r, r}};
+    } else if constexpr (EK == 1) {
+      const float rs = frame_row ? 0.f : r;
+      re = Row{F2{rs, rs}, F2{rs, rs}};
+    } else if constexpr (EK == 2) {
+      re = rl;
+    } else {
+      const F2 z = {0.f, 0.f};
+      re = frame_row ? Row{z, z} : rl;
+    }
+  }
+  __device__ __forceinline__ Row update(const Row& part, const Row& C, const Row& N, int32_t row) const {
+    Row in, re;
+    terms(part, C, N, row, in, re);
+    if constexpr (AR == 1)
+      return Row{__builtin_elementwise_fma(re.a, in.a, C.a), __builtin_elementwise_fma(re.b, in.b, C.b)};
+    else
+      return Row{C.a + re.a * in.a, C.b + re.b * in.b};
+  }
+  static __device__ __forceinline__ float fin(float re, float in, float c) {
+    if constexpr (AR == 1) return __builtin_fmaf(re, in, c);
+    else return c + re * in;
+  }
+  // The stored (last) level: its 4 final ops as scalar fp32 ops writing the
+  // store vector in memory order (c0, c1, c2, c3) — a packed op would produce
+  // the even/odd pairs and need a transpose before the 16-B store.
+  __device__ __forceinline__ VT update_last(const Row& part, const Row& C, const Row& N, int32_t row) const {
+    Row in, re;
+    terms(part, C, N, row, in, re);
+    return VT{fin(re.a.x, in.a.x, C.a.x), fin(re.b.x, in.b.x, C.b.x), fin(re.a.y, in.a.y, C.a.y),
+              fin(re.b.y, in.b.y, C.b.y)};
+  }
+
+  template <int PH>
+  __device__ __forceinline__ void step(int32_t m) {
+    constexpr int P = PH & 1, Q = P ^ 1;
+    constexpr int sN = PH, sC = (PH + RING - 1) % RING, sS = (PH + RING - 2) % RING;
+    const Row C0 = Lb[sC];
+    Row part = partial(Lb[sS], C0);
+    {
+      const int32_t nxt = m + 2 - RING;
+      __builtin_amdgcn_sched_barrier(0);
+      load_row(nxt >= mlo ? nxt : mlo, Lb[sS]);
+    }
+    Lb[sN] = split(Lb[sN]);  // first use of this row: to even/odd form, in place
+    const Row N0 = Lb[sN];
+#pragma unroll
+    for (int s = 1; s <= K; ++s) {
+      const Row C = s == 1 ? C0 : X[Q][s > 1 ? s - 2 : 0];
+      const Row N = s == 1 ? N0 : X[P][s > 1 ? s - 2 : 0];
+      if (s < K) {
+        const int i = s < K ? s - 1 : 0;
+        const Row nxtpart = partial(X[P][i], X[Q][i]);
+        X[P][i] = update(part, C, N, m + s);
+        part = nxtpart;
+      } else {
+        store_row(m + s, m + s < t1 && m + s >= t0, update_last(part, C, N, m + s));
+      }
+    }
+  }
+
+  __device__ __forceinline__ void run() {
+    mlo = t0 - K;
+    const int32_t mtop = t1 + K - 1;
+#pragma unroll
+    for (int q = 0; q < RING - 2; ++q) load_row(mtop - q >= mlo ? mtop - q : mlo, Lb[q]);
+#pragma unroll
+    for (int q = RING - 2; q < RING; ++q) Lb[q] = Row{F2{0.f, 0.f}, F2{0.f, 0.f}};
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int s = 0; s < KX; ++s) X[p][s] = Row{F2{0.f, 0.f}, F2{0.f, 0.f}};
+    const int32_t iters = mtop - mlo + 1;
+    const int32_t bodies = (iters + RING - 1) / RING;
+    int32_t m = mtop;
+#pragma unroll 1
+    for (int32_t b = 0; b < bodies; ++b) {
+      step<0>(m);
+      step<1>(m - 1);
+      step<2>(m - 2);
+      step<3>(m - 3);
+      if constexpr (RING >= 6) {
+        step<4 % RING>(m - 4);
+        step<5 % RING>(m - 5);
+      }
+      if constexpr (RING >= 8) {
+        step<6 % RING>(m - 6);
+        step<7 % RING>(m - 7);
+      }
+      m -= RING;
+    }
+  }
+};
+
+// Packed fp32 march (MarchF32) for the 16-B-per-lane float kernels; set
+// HEAT2D_NO_PACKED_F32 at build time to compile the element-wise March instead
+// (A/B builds).
+#ifndef HEAT2D_NO_PACKED_F32
+template <typename T, int NV>
+constexpr bool kPackedF32 = std::is_same<T, float>::value && NV == 1;
+#else
+template <typename T, int NV>
+constexpr bool kPackedF32 = false;
+#endif
+
 template <typename T, int NV, int K, int EK, int RING, int AR>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
                                       int64_t t1, int lane) {
@@ -327,7 +500,8 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   const int64_t c0 = u0 - S::KA;
   const int64_t mycol = c0 + (int64_t)lane * V;
   const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
-  March<T, NV, K, EK, RING, AR> w;
+  using W = typename std::conditional<kPackedF32<T, NV>, MarchF32<K, EK, RING, AR>, March<T, NV, K, EK, RING, AR>>::type;
+  W w;
   // row base = column col_lo (= -cpad) of row 0; offsets are relative to it
   w.srow = reinterpret_cast<const char*>(src + a.col_lo);
   w.drow = reinterpret_cast<char*>(dst + a.col_lo);
@@ -350,10 +524,13 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   const bool useful = (mycol >= u0) && (mycol < ustop);
   w.st_off = useful && in_alloc ? off : kOob;
   if constexpr ((EK & 2) != 0) {
+    auto rcol = [&](int e) { return (mycol + e < 0 || mycol + e >= a.ncols) ? T(0) : r; };
+    if constexpr (kPackedF32<T, NV>) {
+      w.rl.a = {rcol(0), rcol(2)};
+      w.rl.b = {rcol(1), rcol(3)};
+    } else {
 #pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const int64_t c = mycol + e;
-      w.rl[e] = (c < 0 || c >= a.ncols) ? T(0) : r;
+      for (int e = 0; e < V; ++e) w.rl[e] = rcol(e);
     }
   }
   w.run();
@@ -382,8 +559,15 @@ __device__ __forceinline__ bool tb_item(const TbArgs& a, int64_t it, int64_t& st
 // frame-column strips — two code paths, fewer registers than the general
 // kernel (no per-level row tests, no corner selects). MAIN = false: the general
 // kernel classifies each item (edge kinds 0..3, see March).
+// Occupancy floor handed to the register allocator: the packed-fp32 MAIN
+// kernel with RING = 4 lands at 169 VGPRs for K = 16 (2 waves/SIMD) and fits
+// 168 (3 waves) without spilling when asked. Elsewhere a floor of 3 spills
+// (general kernels, RING = 6), so no floor there.
+template <typename T, int NV, int K, int RING, bool MAIN>
+constexpr int kMinWaves = (kPackedF32<T, NV> && MAIN && RING == 4 && K >= 11) ? 3 : 1;
+
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
-__global__ __launch_bounds__(256) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T, NV, K, RING, MAIN>))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
   using S = TbShape<T, NV, K>;
   const int lane = threadIdx.x & 63;
   // readfirstlane: make the wave id (and everything derived from it: strip, rows,

@@ -30,7 +30,7 @@ def build_parser():
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "cpu"])
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--ic", default=None)
-    ap.add_argument("--tb", type=int, default=8)
+    ap.add_argument("--tb", type=int, default=0, help="time steps per HBM pass (0: measured best per dtype)")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--copy-swap", action="store_true")
     ap.add_argument("--managed", action="store_true")
