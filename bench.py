@@ -37,7 +37,19 @@ sys.path.insert(0, _ROOT)
 REF_GPTS_PER_RANK = 50.0  # BASELINE.md derived ceiling, 1 MI250X GCD, fp64
 
 
+def _claim_stdout():
+    """Keep the driver's stdout for the ONE JSON line: RCCL (torch's and ours)
+    prints a version banner on stdout from C at communicator init, and C stdio
+    buffers flush at exit. Point fd 1 at stderr for the whole run and return a
+    private duplicate of the real stdout for the result line."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return fd
+
+
 def main():
+    out_fd = _claim_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=480)
@@ -157,7 +169,7 @@ def main():
             out["field_stats"] = stats
         if phases:
             out["phase_ms"] = phases
-        print(json.dumps(out), flush=True)
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
     s.close()
     tr.close()
     if world > 1:
