@@ -562,12 +562,18 @@ __device__ __forceinline__ bool tb_item(const TbArgs& a, int64_t it, int64_t& st
 // Occupancy floor handed to the register allocator: the packed-fp32 MAIN
 // kernel with RING = 4 lands at 169 VGPRs for K = 16 (2 waves/SIMD) and fits
 // 168 (3 waves) without spilling when asked. Elsewhere a floor of 3 spills
-// (general kernels, RING = 6), so no floor there.
-template <typename T, int NV, int K, int RING, bool MAIN>
-constexpr int kMinWaves = (kPackedF32<T, NV> && MAIN && RING == 4 && K >= 11) ? 3 : 1;
+// (general kernels, RING = 6), so no floor there. Checked per build with
+// ScratchSize = 0 in the ISA (tools/isa_report.py, tests/test_isa.py).
+// Likewise the fp64 fma interior kernel at K = 11..12 (129 -> 128 VGPRs: 4
+// waves/SIMD instead of 3); its exact-arithmetic twin would spill.
+template <typename T, int NV, int K, int RING, bool MAIN, int AR>
+constexpr int kMinWaves =
+    (kPackedF32<T, NV> && MAIN && RING == 4 && K >= 11)                                           ? 3
+    : (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K >= 11 && K <= 12) ? 4
+                                                                                               : 1;
 
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T, NV, K, RING, MAIN>))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T, NV, K, RING, MAIN, AR>))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
   using S = TbShape<T, NV, K>;
   const int lane = threadIdx.x & 63;
   // readfirstlane: make the wave id (and everything derived from it: strip, rows,

@@ -25,6 +25,10 @@ namespace io {
 inline int format_real(char* out, double v) {
   const double a = std::fabs(v);
   if (v == 0.0) return std::snprintf(out, 48, "   0.0000000000000000     ");
+  // an unstable run (r > 1/4) overflows: gfortran writes these words, and
+  // "%E" has no exponent to split (found by the UBSan build, tests/test_sanitizers.py)
+  if (std::isnan(v)) return std::snprintf(out, 48, "%25s", "NaN");
+  if (std::isinf(v)) return std::snprintf(out, 48, "%25s", v < 0 ? "-Infinity" : "Infinity");
   if (a >= 0.1 && a < 1e16) {
     const int d = (int)std::floor(std::log10(a)) + 1;  // digits left of the point (0 for [0.1,1))
     const int dec = std::max(0, 17 - std::max(d, 0));

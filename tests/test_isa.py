@@ -1,0 +1,50 @@
+"""ISA-level regression checks of the built gfx950 code objects (CPU only: the
+code objects are read out of _native/libheat2d.so, no GPU needed).
+
+* no temporal-blocked kernel spills to scratch;
+* the occupancy floors of tb_impl.hpp hold (fp32 interior K >= 11: 3
+  waves/SIMD; fp64 fma interior K = 11..12: 4 waves/SIMD);
+* the packed fp32 march stays compact (the element-wise one needed 209 VGPRs at
+  K = 10, profiles/packed_fp32.md)."""
+import os
+import shutil
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+import isa_report  # noqa: E402
+
+from heat2d.ops import _native as N  # noqa: E402
+
+pytestmark = pytest.mark.skipif(not (N.available() and os.path.exists(isa_report.READELF)),
+                                reason="native library or llvm-readelf missing")
+
+
+@pytest.fixture(scope="module")
+def tb():
+    ks = {}
+    for k in isa_report.kernels(N.LIB_PATH):
+        p = isa_report.tb_params(k["name"])
+        if p:
+            ks[p] = k
+    assert len(ks) == 256, len(ks)  # 2 dtypes x 2 rings x main/gen x 2 arith x K 1..16
+    return ks
+
+
+def test_no_scratch(tb):
+    spill = {p: k["scratch"] for p, k in tb.items() if k["scratch"]}
+    assert not spill, spill
+
+
+def test_occupancy_floors(tb):
+    for k in range(11, 17):
+        for ar in (0, 1):
+            assert tb[("fp32", 1, k, 4, True, ar)]["waves_per_simd"] >= 3, k
+    for k in (11, 12):
+        assert tb[("fp64", 1, k, 4, True, 1)]["waves_per_simd"] >= 4, k
+
+
+def test_packed_fp32_compact(tb):
+    assert tb[("fp32", 1, 10, 4, True, 1)]["vgpr"] <= 128
+    assert tb[("fp32", 1, 16, 4, True, 1)]["agpr"] == 0

@@ -1,0 +1,78 @@
+"""Host sanitizers: the native CLI's host code (runtime, CPU twin kernels,
+input.dat parser, I/O, checkpoint-free CLI paths) built with
+AddressSanitizer + UndefinedBehaviorSanitizer (`make -C csrc asan`, run by
+__graft_entry__.build()) and driven through its CPU path on every reference
+program variant, both dtypes, several temporal depths, the output writers and a
+set of malformed input.dat files. GPU ASan / xnack+ code objects are not
+available on the MI355X pool, so device code is covered by the NaN guard-band
+tests (tests/test_ops.py) instead. SURVEY.md §5 (race detection / sanitizers)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from heat2d.ops import _native as N
+
+ASAN_CLI = os.path.join(os.path.dirname(N.CLI_PATH), "asan", "heat2d")
+
+pytestmark = pytest.mark.skipif(not os.path.exists(ASAN_CLI), reason="sanitizer build missing (make -C csrc asan)")
+
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=99",
+           UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1:exitcode=98")
+
+
+def run(tmp_path, text, *args):
+    (tmp_path / "input.dat").write_text(text)
+    p = subprocess.run([ASAN_CLI, *args], cwd=tmp_path, env=ENV, capture_output=True, text=True, timeout=300)
+    bad = [w for w in ("AddressSanitizer", "LeakSanitizer", "runtime error:") if w in p.stderr + p.stdout]
+    assert not bad, p.stderr[-3000:]
+    assert p.returncode not in (98, 99), p.stderr[-3000:]
+    return p
+
+
+@pytest.mark.parametrize("args", [
+    ["--cpu", "--dtype", "fp64", "--tb", "1"],
+    ["--cpu", "--dtype", "fp64", "--tb", "7", "--arith", "fma"],
+    ["--cpu", "--dtype", "fp32", "--tb", "16"],
+    ["--cpu", "--variant", "serial"],
+    ["--cpu", "--variant", "cuda", "--output", "npy"],
+    ["--cpu", "--copy-swap"],
+    ["--cpu", "--check-every", "3", "--print-every", "4", "--json", "run.json", "--timers"],
+])
+def test_cli_cpu_paths_clean(tmp_path, args):
+    p = run(tmp_path, "67 0.25 0.05 2.0 23 1\n", *args)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "simulation completed" in p.stdout
+
+
+def test_outputs_match_uninstrumented(tmp_path):
+    """The instrumented build computes the same field as the regular CLI."""
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    run(a, "50 0.25 0.05 1.0 17 1\n", "--cpu", "--output", "npy", "--quiet")
+    (b / "input.dat").write_text("50 0.25 0.05 1.0 17 1\n")
+    subprocess.run([N.CLI_PATH, "--cpu", "--output", "npy", "--quiet"], cwd=b, check=True, capture_output=True)
+    fa = sorted(f for f in os.listdir(a) if f.endswith(".npy"))
+    assert fa and fa == sorted(f for f in os.listdir(b) if f.endswith(".npy"))
+    for f in fa:
+        assert np.array_equal(np.load(a / f), np.load(b / f))
+
+
+@pytest.mark.parametrize("text", ["", "64", "64 0.25 0.05", "abc def", "64 0.25 0.05 1.0 -3",
+                                  "0 0.25 0.05 1.0 5", "64,0.25,0.05,1.0d0,5,0\n", "64 0.25 0.05 1.0 5 0 extra junk",
+                                  "9" * 40 + " 0.25 0.05 1.0 5", "64 1e999 0.05 1.0 5"])
+def test_malformed_input_dat(tmp_path, text):
+    """Parser edge cases: a clean error (or a clean run), never a memory error."""
+    run(tmp_path, text, "--cpu", "--quiet")
+
+
+def test_unstable_run_writes_non_finite(tmp_path):
+    """sigma far above the 1/4 stability limit: the field overflows to inf/NaN
+    and the ASCII writers must still format it (they dereferenced a missing
+    exponent before the UBSan build caught it)."""
+    p = run(tmp_path, "16 40.0 0.05 1.0 400 1\n", "--cpu", "--quiet")
+    assert p.returncode == 0, p.stderr[-2000:]
+    txt = (tmp_path / "soln00000.dat").read_text()
+    assert "Infinity" in txt or "NaN" in txt
