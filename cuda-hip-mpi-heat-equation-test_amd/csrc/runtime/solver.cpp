@@ -286,29 +286,19 @@ const kern::SplitPlan& Solver::split_plan(int k) {
 }
 
 // Time candidate split plans (ring 4/6 x MAIN band counts) in the steady
-// state of the real loop — consecutive ping-pong cycles on the real buffers,
-// same stream/event protocol, no exchange — and keep the fastest. The
-// current field is backed up (one device copy) and restored afterwards, so
-// the solution is untouched; without room for the backup the default plan is
-// kept. Measured on MI355X the cycle time at 32768^2 swings by up to ~25%
+// state of the real loop — consecutive cycles on the real buffers, same
+// stream/event protocol, no exchange — and keep the fastest. Every trial
+// cycle reads the CURRENT buffer and writes the other one without swapping
+// (the same kernels and traffic as the ping-pong loop; the timing does not
+// depend on the values), so the solution is untouched and no backup copy is
+// needed — the full-HBM grid (two fields ~ 240 GB) is tuned too. Measured on MI355X the cycle time at 32768^2 swings by up to ~25%
 // between band counts of the same depth (DRAM page / channel locality of the
 // waves marching in lockstep, and the item-per-wave tail), which no static
 // rule captured; a single isolated cycle mispredicts the loop, hence the
 // steady-state measurement (profiles/autotune.md).
 void Solver::autotune_split(int k) {
   const int spare = tr_->exchanges() ? 8 : 0;
-  const size_t bytes = (size_t)L_.elems() * dtype_size(dtype());
   synchronize();
-  size_t free_b = 0, total_b = 0;
-  H2D_HIP(hipMemGetInfo(&free_b, &total_b));
-  if (free_b < bytes + (size_t(1) << 30)) return;  // no room for the backup: keep the default plan
-  void* backup = nullptr;
-  if (hipMalloc(&backup, bytes) != hipSuccess) {
-    (void)hipGetLastError();
-    return;
-  }
-  const int cur0 = cur_;
-  kern::launch_copy(backup, buf_[cur_], (int64_t)bytes, s_compute_);
   hipEvent_t e0, e1;
   H2D_HIP(hipEventCreate(&e0));
   H2D_HIP(hipEventCreate(&e1));
@@ -321,10 +311,9 @@ void Solver::autotune_split(int k) {
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_, cfg_.arith);
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
-    cur_ ^= 1;
   };
   auto time_plan = [&](const kern::SplitPlan& c) {
-    constexpr int kWarm = 1, kTimed = 3;
+    constexpr int kWarm = 1, kTimed = 4;
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
     for (int i = 0; i < kWarm; ++i) run_cycle(c);
@@ -363,12 +352,7 @@ void Solver::autotune_split(int k) {
       }
     }
   }
-  // restore the field into the buffer that was current
   synchronize();
-  cur_ = cur0;
-  kern::launch_copy(buf_[cur_], backup, (int64_t)bytes, s_compute_);
-  H2D_HIP(hipStreamSynchronize(s_compute_));
-  H2D_HIP(hipFree(backup));
   H2D_HIP(hipEventDestroy(e0));
   H2D_HIP(hipEventDestroy(e1));
   best.k = k;

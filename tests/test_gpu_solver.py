@@ -75,7 +75,7 @@ def test_hip_split_schedule_bitwise(gpu, native, dtype, tb, n):
 @pytest.mark.parametrize("dtype,tb", [("fp64", 12), ("fp32", 10)])
 def test_hip_autotune_keeps_state_bitwise(gpu, native, dtype, tb):
     """The split-plan autotuner runs trial cycles on the real buffers and
-    restores the field from a device backup: the solution must be untouched
+    writes only the non-current buffer (no swap): the solution must be untouched
     (bitwise vs the golden), and the chosen plan valid."""
     p = prob(1100, 29, "ghost", "sine")
     npdt = np.float64 if dtype == "fp64" else np.float32
