@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--steps", type=int, default=480)
     ap.add_argument("--warmup", type=int, default=48)
     ap.add_argument("--n", type=int, default=32768)
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: --n is the 1-GPU grid edge; the global square grid grows to n*sqrt(N) so "
+                         "every rank keeps ~n^2 points (e.g. --dtype fp32 --n 173056: the full-HBM 240 GB per GPU)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--tb", type=int, default=0,
                     help="time steps fused per HBM pass (0: measured best, fp64 12 / fp32 16; profiles/README.md)")
@@ -91,7 +94,11 @@ def main():
     from heat2d.models.heat2d import HeatSolver
     from heat2d.parallel.transport import RcclLoopTransport, RcclTransport, SelfTransport
 
-    inp = heat2d.InputDat(n=args.n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
+    n_glob = args.n
+    if args.weak:
+        import math
+        n_glob = int(round(args.n * math.sqrt(world)))
+    inp = heat2d.InputDat(n=n_glob, sigma=0.25, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     if world > 1:
         tr = RcclTransport(rank, world, local)
@@ -147,12 +154,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 6),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": round(gpts / (REF_GPTS_PER_RANK * world), 3),
             "dtype": args.dtype,
             "data": "synthetic (reference benchmark IC: T=2 interior, Dirichlet T=1 frame)",
             "config": {
-                "model": "heat2d FTCS 5-point, fortran/hip/input.dat (32768 0.25 0.05 1.0 25000 0)",
+                "model": ("heat2d FTCS 5-point, fortran/hip/input.dat (32768 0.25 0.05 1.0 25000 0)" if not args.weak else
+                          f"heat2d FTCS 5-point, weak scaling: {args.n}^2 points per GPU (global {n_glob}^2)"),
                 "grid": [rows or prob.n_owned, prob.n_owned],
                 "global_batch": 1,
                 "seq_len": prob.n_owned,
