@@ -56,6 +56,19 @@ int cu_count() {
 }
 
 int vec_elems(DType dt) { return dt == DType::F32 ? 4 : 2; }
+
+// XCD-aware wave numbering in tb_kernel (TbArgs::xcd_remap). Measured on
+// MI355X (profiles/README.md §8): it cuts the strip-halo over-fetch from 1.14x
+// to 1.07x of the field but costs 6 % (fp64) / 3 % (fp32) — the round-robin
+// numbering, where the waves in flight cover each row evenly from every XCD,
+// streams HBM better. Off by default; HEAT2D_XCD_REMAP=1 enables it.
+int xcd_remap() {
+  static const int v = [] {
+    const char* env = std::getenv("HEAT2D_XCD_REMAP");
+    return env ? (std::atoi(env) != 0 ? 1 : 0) : 0;
+  }();
+  return v;
+}
 // halo columns per strip side (whole lanes) and useful strip width; must match TbShape
 int halo_cols(DType dt, int k) {
   const int v = vec_elems(dt);
@@ -163,6 +176,7 @@ void launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int
   }
   if (q == 0) return;
   a.nrect = q;
+  a.xcd_remap = xcd_remap();
   a.nitems = items;
   a.nwaves = std::max<int64_t>(1, std::min<int64_t>(nwaves, items));
   const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
