@@ -35,6 +35,34 @@ struct Vec16<double> {
 __device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 __device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
+// Single fp32 adds as inline asm, for the two across-lane sums of the packed
+// march (MarchF32): written as plain C++ the backend re-packs them with other
+// scalar adds into v_pk_add_f32 on re-assembled register pairs (2 moves per
+// pair); as asm the two halves of a pair are produced in place. The DPP form
+// folds the wave shift into the add (v_add_f32_dpp, lanes without a source
+// read 0 = bound_ctrl); the s_nop gives the 2 wait states a DPP source read
+// needs after a VALU write of that VGPR (the hazard recognizer does not look
+// inside inline asm). fp add is commutative: x + a == a + x bitwise.
+__device__ __forceinline__ float asm_add(float a, float b) {
+  float r;
+  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float asm_add_from_upper(float a, float x) {  // a + x(lane + 1)
+  float r;
+  asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "=v"(r)
+      : "v"(x), "v"(a));
+  return r;
+}
+__device__ __forceinline__ float asm_add_from_lower(float a, float x) {  // a + x(lane - 1)
+  float r;
+  asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "=v"(r)
+      : "v"(x), "v"(a));
+  return r;
+}
+
 // DPP wave shifts (GFX9 family). wave_shr:1 -> lane i reads lane i-1;
 // wave_shl:1 -> lane i reads lane i+1. Lanes without a source get 0 (garbage
 // by construction: they lie in the strip's redundant halo columns).
@@ -374,14 +402,13 @@ struct MarchF32 {
 
   // part = S + E(C) (first partial sum of the reference order)
   static __device__ __forceinline__ Row partial(const Row& S, const Row& C) {
-    const F2 eb = {C.a.y, from_upper(C.a.x)};
-    return Row{S.a + C.b, S.b + eb};
+    return Row{S.a + C.b, F2{asm_add(S.b.x, C.a.y), asm_add_from_upper(S.b.y, C.a.x)}};
   }
   // sum - 4C (in) and the per-element r (re) of the update C + r*(sum - 4C)
   __device__ __forceinline__ void terms(const Row& part, const Row& C, const Row& N, int32_t row, Row& in,
                                         Row& re) const {
-    const F2 wa = {from_lower(C.b.y), C.b.x};
-    const Row sum = {(part.a + N.a) + wa, (part.b + N.b) + C.a};
+    const F2 ta = part.a + N.a;
+    const Row sum = {F2{asm_add_from_lower(ta.x, C.b.y), asm_add(ta.y, C.b.x)}, (part.b + N.b) + C.a};
     const F2 m4 = {-4.f, -4.f};
     in = Row{__builtin_elementwise_fma(m4, C.a, sum.a), __builtin_elementwise_fma(m4, C.b, sum.b)};
     const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
@@ -560,18 +587,14 @@ __device__ __forceinline__ bool tb_item(const TbArgs& a, int64_t it, int64_t& st
 // frame-column strips — two code paths, fewer registers than the general
 // kernel (no per-level row tests, no corner selects). MAIN = false: the general
 // kernel classifies each item (edge kinds 0..3, see March).
-// Occupancy floor handed to the register allocator: the packed-fp32 MAIN
-// kernel with RING = 4 lands at 169 VGPRs for K = 16 (2 waves/SIMD) and fits
-// 168 (3 waves) without spilling when asked. Elsewhere a floor of 3 spills
-// (general kernels, RING = 6), so no floor there. Checked per build with
-// ScratchSize = 0 in the ISA (tools/isa_report.py, tests/test_isa.py).
-// Likewise the fp64 fma interior kernel at K = 11..12 (129 -> 128 VGPRs: 4
-// waves/SIMD instead of 3); its exact-arithmetic twin would spill.
+// Occupancy floor handed to the register allocator: the fp64 fma interior
+// kernel at K = 11..12 lands at 129 VGPRs and fits 128 (4 waves/SIMD instead
+// of 3) without spilling; its exact-arithmetic twin would spill. (The packed
+// fp32 march with the asm across-lane adds spills under a 3-wave floor from
+// K = 12 on, so it has none.) Checked per build: ScratchSize = 0 in the ISA
+// (tools/isa_report.py, tests/test_isa.py).
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
-constexpr int kMinWaves =
-    (kPackedF32<T, NV> && MAIN && RING == 4 && K >= 11)                                           ? 3
-    : (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K >= 11 && K <= 12) ? 4
-                                                                                               : 1;
+constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K >= 11 && K <= 12) ? 4 : 1;
 
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T, NV, K, RING, MAIN, AR>))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
