@@ -54,7 +54,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=480)
     ap.add_argument("--warmup", type=int, default=48)
-    ap.add_argument("--n", type=int, default=32768)
+    ap.add_argument("--n", "--grid", dest="n", type=int, default=32768,
+                    help="grid edge (use --grid under torchrun: its parser takes --n as an abbreviation)")
     ap.add_argument("--weak", action="store_true",
                     help="weak scaling: --n is the 1-GPU grid edge; the global square grid grows to n*sqrt(N) so "
                          "every rank keeps ~n^2 points (e.g. --dtype fp32 --n 173056: the full-HBM 240 GB per GPU)")
@@ -71,6 +72,9 @@ def main():
                     help="record hipEvent phase timers in the timed region and report them (adds event records)")
     ap.add_argument("--rows", type=int, default=0,
                     help="with --rehearse-comm: rows of the slab (e.g. 4096 = one of 8 ranks of 32768)")
+    ap.add_argument("--backend", default="hip", choices=["hip", "cpu"],
+                    help="cpu: the same harness on the native CPU twin over gloo (CI rehearsal of the "
+                         "multi-process path: tests/test_bench_contract.py); not a performance number")
     ap.add_argument("--rehearse-comm", action="store_true",
                     help="1 GPU only: run the multi-GPU schedule (bands + RCCL self-exchange beside a CU-masked "
                          "interior) to measure its per-rank cost; not the headline (periodic halo)")
@@ -86,13 +90,22 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
+    hip = args.backend == "hip"
+    if hip:
+        torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if hip:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+
+    def sync():
+        if hip:
+            torch.cuda.synchronize()
 
     import heat2d
     from heat2d.models.heat2d import HeatSolver
-    from heat2d.parallel.transport import RcclLoopTransport, RcclTransport, SelfTransport
+    from heat2d.parallel.transport import RcclLoopTransport, RcclTransport, SelfTransport, TorchDistTransport
 
     n_glob = args.n
     if args.weak:
@@ -101,21 +114,21 @@ def main():
     inp = heat2d.InputDat(n=n_glob, sigma=0.25, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     if world > 1:
-        tr = RcclTransport(rank, world, local)
-    elif args.rehearse_comm:
+        tr = RcclTransport(rank, world, local) if hip else TorchDistTransport()
+    elif args.rehearse_comm and hip:
         tr = RcclLoopTransport(local)
     else:
         tr = SelfTransport()
     rows = args.rows if (args.rows and world == 1) else None
-    s = HeatSolver(prob, dtype=args.dtype, backend="hip", tb=args.tb, overlap=not args.no_overlap,
-                   tile_rows=args.tile_rows, transport=tr, device=local, rows=rows,
+    s = HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb, overlap=not args.no_overlap,
+                   tile_rows=args.tile_rows, transport=tr, device=local if hip else None, rows=rows,
                    comm_cus=args.comm_cus, arith=args.arith)
 
     def barrier():
         if world > 1:
-            tr_vals = torch.zeros(1, device="cuda")
+            tr_vals = torch.zeros(1, device="cuda" if hip else "cpu")
             dist.all_reduce(tr_vals)
-        torch.cuda.synchronize()
+        sync()
 
     s.prepare(args.steps)  # plan / autotune every depth the timed run uses (outside the timed region)
     s.step(args.warmup)
@@ -126,12 +139,12 @@ def main():
     t0 = time.perf_counter()
     s.step(args.steps)
     s.synchronize()
-    torch.cuda.synchronize()
+    sync()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cuda" if hip else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -159,8 +172,9 @@ def main():
             "dtype": args.dtype,
             "data": "synthetic (reference benchmark IC: T=2 interior, Dirichlet T=1 frame)",
             "config": {
-                "model": ("heat2d FTCS 5-point, fortran/hip/input.dat (32768 0.25 0.05 1.0 25000 0)" if not args.weak else
-                          f"heat2d FTCS 5-point, weak scaling: {args.n}^2 points per GPU (global {n_glob}^2)"),
+                "model": (f"heat2d FTCS 5-point, weak scaling: {args.n}^2 points per GPU (global {n_glob}^2)" if args.weak
+                          else "heat2d FTCS 5-point, fortran/hip/input.dat (32768 0.25 0.05 1.0 25000 0)" if n_glob == 32768
+                          else f"heat2d FTCS 5-point, {n_glob}^2 (sigma 0.25, nu 0.05, L 1.0)"),
                 "grid": [rows or prob.n_owned, prob.n_owned],
                 "global_batch": 1,
                 "seq_len": prob.n_owned,
@@ -168,7 +182,8 @@ def main():
                 "temporal_block": tb,
                 "arith": args.arith,
                 "overlap": not args.no_overlap,
-                "launch_plan": s.plan() if not args.no_overlap else None,
+                "launch_plan": s.plan() if (hip and not args.no_overlap) else None,
+                "backend": args.backend,
             },
             "hbm_gb_per_s_model": round(model_gbps, 1),
             "baseline_basis": "BASELINE.md derived ceiling 50 Gpts/s per MI250X GCD x n_gpus",

@@ -1,0 +1,53 @@
+"""The bench.py driver contract, rehearsed on CPU: the multi-process path the
+driver launches with torchrun on 2/4/8 GPUs (init, transport, prepare,
+barrier-bracketed timed region, MAX over ranks, rank 0 prints ONE JSON line on
+stdout — RCCL's version banners are kept off it) runs here with --backend cpu
+(gloo + the native CPU twin) and must produce exactly that line."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def run_bench(nproc, *args, port):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(nproc), "--backend", "cpu", *args]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("nproc,dtype", [(2, "fp64"), (3, "fp32")])
+def test_bench_json_line_multi_rank(nproc, dtype):
+    d = run_bench(nproc, "--grid", "100", "--steps", "24", "--warmup", "4", "--dtype", dtype, "--tb", "4",
+                  port=29560 + nproc)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == nproc and d["steps"] == 24 and d["warmup"] == 4 and d["dtype"] == dtype
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
+    assert d["scaling"] == "strong" and d["config"]["parallelism"] == f"slab{nproc}"
+    assert d["config"]["grid"] == [100, 100]
+
+
+def test_bench_weak_mode():
+    d = run_bench(2, "--grid", "64", "--weak", "--steps", "8", "--warmup", "2", "--tb", "4", port=29570)
+    assert d["scaling"] == "weak" and d["config"]["grid"] == [91, 91]  # round(64 * sqrt(2))
+
+
+def test_bench_single_process_cpu():
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--backend", "cpu", "--grid", "80", "--steps",
+                        "8", "--warmup", "2", "--tb", "4", "--check"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["field_stats"]["max"] <= 2.0
