@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "heat2d/capi.h"
+#include "heat2d/ckpt.hpp"
 #include "heat2d/config.hpp"
 #include "heat2d/runtime.hpp"
 
@@ -55,6 +56,9 @@ struct Args {
   bool timers = false;
   std::string engine = "tb";
   std::string arith = "exact";  // exact | fma (SolverConfig::arith)
+  std::string checkpoint;       // --checkpoint DIR (utils/checkpoint.py format)
+  int64_t checkpoint_every = 0;
+  std::string restart;          // --restart DIR (any writer rank count)
 };
 
 void usage() {
@@ -62,7 +66,8 @@ void usage() {
       "usage: heat2d [input.dat] [--variant mpi|serial|cuda] [--gpus N | --cpu] [--dtype fp64|fp32]\n"
       "              [--tb K] [--no-overlap] [--copy-swap] [--managed] [--graph] [--ic NAME]\n"
       "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
-      "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith exact|fma]\n");
+      "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith exact|fma]\n"
+      "              [--checkpoint DIR [--checkpoint-every N]] [--restart DIR]\n");
 }
 
 Args parse_args(int argc, char** argv) {
@@ -97,6 +102,9 @@ Args parse_args(int argc, char** argv) {
     else if (s == "--n") a.n = std::atoll(need("--n").c_str());
     else if (s == "--quiet") a.quiet = true;
     else if (s == "--timers") a.timers = true;
+    else if (s == "--checkpoint") a.checkpoint = need("--checkpoint");
+    else if (s == "--checkpoint-every") a.checkpoint_every = std::atoll(need("--checkpoint-every").c_str());
+    else if (s == "--restart") a.restart = need("--restart");
     else if (!s.empty() && s[0] != '-') a.input = s;
     else { std::fprintf(stderr, "unknown flag %s\n", s.c_str()); usage(); std::exit(2); }
   }
@@ -114,7 +122,30 @@ struct Shared {
   std::string err;
   double final_stats[6] = {0};
   int tb_used = 1;  // temporal depth the solver actually ran (jit / copy-swap force 1)
+  int64_t start_step = 0;  // > 0 after --restart
 };
+
+// Collective checkpoint (every rank its slab, then rank 0 publishes meta.json).
+void save_checkpoint(Shared& sh, Solver& s, Transport& tr, int rank, int64_t step) {
+  const Args& a = sh.args;
+  ckpt::write_rank(a.checkpoint, rank, s);
+  tr.barrier();
+  if (rank == 0) {
+    ckpt::Meta m;
+    m.step = step;
+    m.nranks = sh.nranks;
+    m.dtype = (int)s.dtype();
+    m.n_owned = sh.prob.n_owned;
+    m.n_input = sh.in.n;
+    m.convention = sh.prob.conv == Convention::Inclusive ? "inclusive" : "ghost";
+    m.sigma = sh.in.sigma;
+    m.nu = sh.in.nu;
+    m.dom_len = sh.in.dom_len;
+    m.r = sh.prob.r;
+    ckpt::write_meta(a.checkpoint, m);
+  }
+  tr.barrier();
+}
 
 std::string rank_file(int rank) {
   char b[32];
@@ -167,13 +198,28 @@ void run_rank(Shared& sh, int rank) {
     Solver s(cfg, tr);
     s.init(sh.prob.ic, sh.prob.x.data(), sh.prob.x.data());
     const bool inclusive = sh.prob.conv == Convention::Inclusive;
+    int64_t start = 0;
+    if (!a.restart.empty()) {  // resume (bitwise: FTCS carries no state besides the field)
+      const ckpt::Meta m = ckpt::read_meta(a.restart);
+      HEAT2D_REQUIRE(m.n_owned == sh.prob.n_owned, "checkpoint grid differs from input.dat's");
+      HEAT2D_REQUIRE(m.convention == (inclusive ? "inclusive" : "ghost"), "checkpoint grid convention differs");
+      const SlabLayout& L = s.layout();
+      std::vector<char> host((size_t)(L.nrows * L.ncols) * dtype_size(s.dtype()));
+      ckpt::read_rows(a.restart, m, L.row0, L.nrows, L.ncols, (int)s.dtype(), host.data());
+      s.upload(host.data(), L.ncols);  // + halo exchange
+      start = std::min<int64_t>(m.step, sh.in.ntime);
+      if (root) {
+        sh.start_step = start;
+        if (!a.quiet) std::printf(" restarted from %s at step %lld\n", a.restart.c_str(), (long long)start);
+      }
+    }
     if (root && !a.quiet) {
       if (P > 1 || sh.args.variant == "mpi") std::printf(" Automatic MPI decomposition: %12d  x 1\n", P);
       std::printf(" nx: %12lld\n", (long long)s.layout().nrows);
       std::printf(" ny: %12lld\n", (long long)s.layout().ncols);
       std::fflush(stdout);
     }
-    if (inclusive && a.output == "ascii") {  // int.dat: the IC (fortran/serial/heat.f90:50-55)
+    if (inclusive && a.output == "ascii" && start == 0) {  // int.dat: the IC (fortran/serial/heat.f90:50-55)
       for (int turn = 0; turn < P; ++turn) {
         if (turn == rank) write_inclusive(s, sh.prob, "int.dat", rank == 0, rank == P - 1, rank > 0);
         tr->barrier();
@@ -182,20 +228,20 @@ void run_rank(Shared& sh, int rank) {
 
     const int64_t ntime = sh.in.ntime;
     // plan / autotune every cycle depth the loop will use before the clock starts
-    s.prepare(ntime);
-    for (int64_t every : {a.print_every, a.check_every})
+    s.prepare(ntime - start);
+    for (int64_t every : {a.print_every, a.check_every, a.checkpoint_every})
       if (every > 0) s.prepare(std::min(every, ntime));
     if (a.timers) s.set_timing(true);
     tr->barrier();
     s.synchronize();
     const auto t0 = std::chrono::steady_clock::now();
-    int64_t done = 0;
-    const int64_t chunk_every = std::max<int64_t>(a.print_every, a.check_every);
+    int64_t done = start;
+    const bool ckpt_periodic = !a.checkpoint.empty() && a.checkpoint_every > 0;
     while (done < ntime) {
       int64_t chunk = ntime - done;
       if (a.print_every > 0) chunk = std::min(chunk, a.print_every - (done % a.print_every));
       if (a.check_every > 0) chunk = std::min(chunk, a.check_every - (done % a.check_every));
-      (void)chunk_every;
+      if (ckpt_periodic) chunk = std::min(chunk, a.checkpoint_every - (done % a.checkpoint_every));
       s.step(chunk);
       done += chunk;
       if (root && a.print_every > 0 && done % a.print_every == 0) std::printf(" time_it: %12lld\n", (long long)done);
@@ -207,6 +253,7 @@ void run_rank(Shared& sh, int rank) {
                       st[3], std::sqrt(st[4]));
         if (!std::isfinite(st[0])) fail(__FILE__, __LINE__, "non-finite temperature at step " + std::to_string(done));
       }
+      if (ckpt_periodic && done % a.checkpoint_every == 0 && done < ntime) save_checkpoint(sh, s, *tr, rank, done);
     }
     s.synchronize();
     tr->barrier();
@@ -219,6 +266,8 @@ void run_rank(Shared& sh, int rank) {
                   "exchange %.3f ms, cycle %.3f ms\n",
                   rank, (long long)ph[4], ph[0], ph[1], ph[2], ph[3]);
     }
+
+    if (!a.checkpoint.empty()) save_checkpoint(sh, s, *tr, rank, done);  // final state (outside the timed region)
 
     // outputs
     if (a.output != "none") {
@@ -299,7 +348,7 @@ int main(int argc, char** argv) {
   }
   double tmax = 0;
   for (double t : sh.t_elapsed) tmax = std::max(tmax, t);
-  const int64_t ntime = sh.in.ntime;
+  const int64_t ntime = sh.in.ntime - sh.start_step;  // steps this run executed
   const double pts = (double)sh.prob.n_owned * (double)sh.prob.n_owned;
   const double gpts = ntime > 0 && tmax > 0 ? pts * (double)ntime / tmax / 1e9 : 0.0;
   const int es = a.dtype == "fp32" ? 4 : 8;

@@ -1,0 +1,33 @@
+// Native checkpoint / restart (runtime/checkpoint.cpp): the Python driver's
+// on-disk format (utils/checkpoint.py), so either driver resumes the other's
+// checkpoints on any rank count.
+#pragma once
+
+#include <string>
+
+#include "heat2d/runtime.hpp"
+
+namespace heat2d {
+namespace ckpt {
+
+struct Meta {
+  int64_t step = 0;
+  int nranks = 1;
+  int dtype = 1;  // 0 fp32, 1 fp64
+  int64_t n_owned = 0, n_input = 0;
+  std::string convention = "ghost";  // ghost | inclusive
+  double sigma = 0, nu = 0, dom_len = 0, r = 0;
+};
+
+// Collective use: every rank writes its slab, then (after a barrier) rank 0
+// publishes meta.json atomically (temp file + rename), then a barrier.
+void write_rank(const std::string& dir, int rank, Solver& s);
+void write_meta(const std::string& dir, const Meta& m);
+Meta read_meta(const std::string& dir);
+// Global rows [row0, row0 + nrows) x ncols of the checkpointed field into `out`
+// (row-major, ld = ncols), gathered from however many writer files there are.
+void read_rows(const std::string& dir, const Meta& m, int64_t row0, int64_t nrows, int64_t ncols, int dtype,
+               void* out);
+
+}  // namespace ckpt
+}  // namespace heat2d

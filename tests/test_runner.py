@@ -11,6 +11,7 @@ import pytest
 
 import heat2d
 from heat2d.models import reference as R
+from heat2d.ops import _native as N
 from heat2d.utils import io
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -105,3 +106,42 @@ def test_io_roundtrip_and_npy(native, tmp_path):
     assert np.array_equal(T, T2) and np.array_equal(x, x2) and np.array_equal(y, y2)
     io.write_npy(str(tmp_path / "a.npy"), T.astype(np.float32))
     assert np.array_equal(np.load(tmp_path / "a.npy", allow_pickle=False), T.astype(np.float32))
+
+
+@pytest.mark.parametrize("writer,reader", [("cli", "cli"), ("py", "cli"), ("cli", "py")])
+def test_checkpoint_native_cli_interop(native, tmp_path, writer, reader):
+    """The native CLI's --checkpoint / --restart use the Python driver's format
+    (csrc/runtime/checkpoint.cpp): each driver resumes the other's checkpoints,
+    bitwise, on another rank count, and periodic checkpoints carry the step."""
+    (tmp_path / "input.dat").write_text("50 0.25 0.05 1.0 30 1\n")
+    cli = [N.CLI_PATH, "--cpu", "--quiet"]
+    if writer == "cli":
+        subprocess.run([*cli, "--ntime", "12", "--checkpoint", "ck", "--checkpoint-every", "5", "--output", "none"],
+                       cwd=tmp_path, check=True, capture_output=True)
+    else:
+        py(tmp_path, "--backend", "cpu", "--ntime", "12", "--checkpoint", "ck", "--output", "none", nproc=2)
+    meta = json.loads((tmp_path / "ck" / "meta.json").read_text())
+    assert meta["step"] == 12 and meta["format"] == "heat2d-checkpoint-v1"
+    if reader == "cli":
+        out = subprocess.run([*cli, "--restart", "ck"], cwd=tmp_path, check=True, capture_output=True, text=True)
+        assert out.returncode == 0
+        T = io.read_xyz(str(tmp_path / "soln00000.dat"))[2]
+    else:
+        py(tmp_path, "--backend", "cpu", "--restart", "ck", nproc=3)
+        T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
+
+
+def test_checkpoint_native_rejects_mismatch(native, tmp_path):
+    (tmp_path / "input.dat").write_text("40 0.25 0.05 1.0 10 0\n")
+    subprocess.run([N.CLI_PATH, "--cpu", "--quiet", "--checkpoint", "ck"], cwd=tmp_path, check=True,
+                   capture_output=True)
+    (tmp_path / "input.dat").write_text("41 0.25 0.05 1.0 10 0\n")
+    p = subprocess.run([N.CLI_PATH, "--cpu", "--quiet", "--restart", "ck"], cwd=tmp_path, capture_output=True,
+                       text=True)
+    assert p.returncode != 0 and "checkpoint grid differs" in p.stderr
+    (tmp_path / "input.dat").write_text("40 0.25 0.05 1.0 10 0\n")
+    p = subprocess.run([N.CLI_PATH, "--cpu", "--quiet", "--dtype", "fp32", "--restart", "ck"], cwd=tmp_path,
+                       capture_output=True, text=True)
+    assert p.returncode != 0 and "dtype" in p.stderr

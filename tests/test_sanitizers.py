@@ -39,11 +39,24 @@ def run(tmp_path, text, *args):
     ["--cpu", "--variant", "cuda", "--output", "npy"],
     ["--cpu", "--copy-swap"],
     ["--cpu", "--check-every", "3", "--print-every", "4", "--json", "run.json", "--timers"],
+    ["--cpu", "--checkpoint", "ck", "--checkpoint-every", "5"],
 ])
 def test_cli_cpu_paths_clean(tmp_path, args):
     p = run(tmp_path, "67 0.25 0.05 2.0 23 1\n", *args)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "simulation completed" in p.stdout
+
+
+def test_checkpoint_restart_clean(tmp_path):
+    """Native checkpoint writer + meta.json / .npy parsers under ASan/UBSan,
+    including a truncated rank file (clean error, no memory error)."""
+    run(tmp_path, "33 0.25 0.05 1.0 9 1\n", "--cpu", "--quiet", "--checkpoint", "ck")
+    p = run(tmp_path, "33 0.25 0.05 1.0 20 1\n", "--cpu", "--quiet", "--restart", "ck")
+    assert p.returncode == 0, p.stderr[-2000:]
+    f = tmp_path / "ck" / "rank00000.npy"
+    f.write_bytes(f.read_bytes()[:200])
+    p = run(tmp_path, "33 0.25 0.05 1.0 20 1\n", "--cpu", "--quiet", "--restart", "ck")
+    assert p.returncode != 0 and "truncated" in p.stderr
 
 
 def test_outputs_match_uninstrumented(tmp_path):
