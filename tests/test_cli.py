@@ -97,6 +97,19 @@ def test_cli_gpu_serial_variant(cli, gpu, tmp_path, extra):
     assert np.array_equal(a[:, 2], R.ftcs(prob).ravel())
 
 
+@pytest.mark.gpu
+def test_cli_gpu_checkpoint_restart(cli, gpu, tmp_path):
+    """GPU run checkpointed mid-way (HIP fields -> rank .npy), resumed on the GPU
+    and, separately, on the CPU twin: both finish bitwise equal to the golden."""
+    (tmp_path / "input.dat").write_text("300 0.25 0.05 1.0 40 1\n")
+    run_cli(tmp_path, "--gpus", "1", "--ntime", "17", "--checkpoint", "ck", "--output", "none", "--quiet")
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    ref = R.owned(R.ftcs(prob)).ravel()
+    for dev in (["--gpus", "1"], ["--cpu"]):
+        run_cli(tmp_path, *dev, "--restart", "ck", "--quiet")
+        assert np.array_equal(read_xyz(tmp_path / "soln00000.dat")[:, 2], ref), dev
+
+
 def test_cmake_configures(tmp_path):
     """The CMake build (alternative to csrc/Makefile) configures for gfx950."""
     import shutil
