@@ -35,34 +35,6 @@ struct Vec16<double> {
 __device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 __device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
-// Single fp32 adds as inline asm, for the two across-lane sums of the packed
-// march (MarchF32): written as plain C++ the backend re-packs them with other
-// scalar adds into v_pk_add_f32 on re-assembled register pairs (2 moves per
-// pair); as asm the two halves of a pair are produced in place. The DPP form
-// folds the wave shift into the add (v_add_f32_dpp, lanes without a source
-// read 0 = bound_ctrl); the s_nop gives the 2 wait states a DPP source read
-// needs after a VALU write of that VGPR (the hazard recognizer does not look
-// inside inline asm). fp add is commutative: x + a == a + x bitwise.
-__device__ __forceinline__ float asm_add(float a, float b) {
-  float r;
-  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ float asm_add_from_upper(float a, float x) {  // a + x(lane + 1)
-  float r;
-  asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-      : "=v"(r)
-      : "v"(x), "v"(a));
-  return r;
-}
-__device__ __forceinline__ float asm_add_from_lower(float a, float x) {  // a + x(lane - 1)
-  float r;
-  asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-      : "=v"(r)
-      : "v"(x), "v"(a));
-  return r;
-}
-
 // DPP wave shifts (GFX9 family). wave_shr:1 -> lane i reads lane i-1;
 // wave_shl:1 -> lane i reads lane i+1. Lanes without a source get 0 (garbage
 // by construction: they lie in the strip's redundant halo columns).
@@ -89,6 +61,22 @@ __device__ __forceinline__ double from_upper(double x) {
   const int hi = dpp_mov<kDppWaveShl1>((int)(b >> 32));
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+
+// Single fp32 adds for the two across-lane sums of the packed march
+// (MarchF32). Written plainly, the backend merges such scalar adds with their
+// neighbours into v_pk_add_f32 on re-assembled register pairs (2 extra moves
+// per pair); an empty asm that takes the sum as an in/out operand keeps each
+// add scalar, so the two halves of a pair are produced in place and the DPP
+// move folds into the add (v_add_f32_dpp, by the compiler's DPP combine, which
+// also inserts the DPP read hazard waits — a hand-written asm add needed an
+// s_nop per DPP and measured the same: profiles/packed_fp32.md).
+__device__ __forceinline__ float fence_v(float r) {
+  asm("" : "+v"(r));
+  return r;
+}
+__device__ __forceinline__ float asm_add(float a, float b) { return fence_v(a + b); }
+__device__ __forceinline__ float asm_add_from_upper(float a, float x) { return fence_v(a + from_upper(x)); }
+__device__ __forceinline__ float asm_add_from_lower(float a, float x) { return fence_v(a + from_lower(x)); }
 
 // Kernel arguments: the work is up to kMaxRects rectangles (output rows x
 // strips), each cut into `nb` row bands; a work item is one (band, strip) of
