@@ -74,9 +74,9 @@ __device__ __forceinline__ float fence_v(float r) {
   asm("" : "+v"(r));
   return r;
 }
-__device__ __forceinline__ float asm_add(float a, float b) { return fence_v(a + b); }
-__device__ __forceinline__ float asm_add_from_upper(float a, float x) { return fence_v(a + from_upper(x)); }
-__device__ __forceinline__ float asm_add_from_lower(float a, float x) { return fence_v(a + from_lower(x)); }
+__device__ __forceinline__ float sadd(float a, float b) { return fence_v(a + b); }
+__device__ __forceinline__ float sadd_from_upper(float a, float x) { return fence_v(a + from_upper(x)); }
+__device__ __forceinline__ float sadd_from_lower(float a, float x) { return fence_v(a + from_lower(x)); }
 
 // Kernel arguments: the work is up to kMaxRects rectangles (output rows x
 // strips), each cut into `nb` row bands; a work item is one (band, strip) of
@@ -390,13 +390,13 @@ struct MarchF32 {
 
   // part = S + E(C) (first partial sum of the reference order)
   static __device__ __forceinline__ Row partial(const Row& S, const Row& C) {
-    return Row{S.a + C.b, F2{asm_add(S.b.x, C.a.y), asm_add_from_upper(S.b.y, C.a.x)}};
+    return Row{S.a + C.b, F2{sadd(S.b.x, C.a.y), sadd_from_upper(S.b.y, C.a.x)}};
   }
   // sum - 4C (in) and the per-element r (re) of the update C + r*(sum - 4C)
   __device__ __forceinline__ void terms(const Row& part, const Row& C, const Row& N, int32_t row, Row& in,
                                         Row& re) const {
     const F2 ta = part.a + N.a;
-    const Row sum = {F2{asm_add_from_lower(ta.x, C.b.y), asm_add(ta.y, C.b.x)}, (part.b + N.b) + C.a};
+    const Row sum = {F2{sadd_from_lower(ta.x, C.b.y), sadd(ta.y, C.b.x)}, (part.b + N.b) + C.a};
     const F2 m4 = {-4.f, -4.f};
     in = Row{__builtin_elementwise_fma(m4, C.a, sum.a), __builtin_elementwise_fma(m4, C.b, sum.b)};
     const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
