@@ -616,13 +616,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
       else
         march<T, NV, K, 0, RING, AR>(src, dst, a, r, strip, t0, t1, lane);
     } else {
-#ifdef HEAT2D_AB_NO_EDGE  // timing experiments only (bench A/B builds): frame handling off, wrong numerics
-      const int ek = 0;
-      (void)c0;
-#else
       const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
                      (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
-#endif
       switch (ek) {
         case 0: march<T, NV, K, 0, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
         case 1: march<T, NV, K, 1, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
