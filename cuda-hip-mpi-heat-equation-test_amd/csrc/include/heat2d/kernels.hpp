@@ -54,7 +54,10 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 //   EDGE: the two boundary bands (all strips), general kernel.
 // The caller orders them with events (solver.cpp). valid = 0: slab too thin
 // or narrow for the split (use launch_tb on the whole slab); valid = 2: a
-// single-launch plan (plan_single).
+// single-launch plan (plan_single); valid = 3: the split run edge-first — the
+// band launch alone, then the interior, both on the compute stream, with the
+// halo exchange beside the interior (the autotuner's choice for slabs where
+// the interior would otherwise share the chip with the band waves).
 struct TbRect {
   int64_t r0, r1, s0, s1, nb;
 };

@@ -257,7 +257,8 @@ void Solver::phase_times(double out[5]) {
         phase_acc_[0] += el(pe.ev[0], pe.ev[1]);  // main (compute stream)
         phase_acc_[1] += el(pe.ev[2], pe.ev[3]);  // edge (comm stream, from its wait)
         phase_acc_[2] += el(pe.ev[3], pe.ev[5]);  // halo exchange
-        phase_acc_[3] += std::max(el(pe.ev[0], pe.ev[1]), el(pe.ev[2], pe.ev[5]));
+        // cycle: from the first record to the last (edge-first plans start with the bands)
+        phase_acc_[3] += std::max({el(pe.ev[0], pe.ev[1]), el(pe.ev[2], pe.ev[5]), el(pe.ev[2], pe.ev[1])});
       } else {
         phase_acc_[0] += el(pe.ev[0], pe.ev[4]);  // compute
         phase_acc_[2] += el(pe.ev[4], pe.ev[1]);  // exchange
@@ -281,6 +282,12 @@ const kern::SplitPlan& Solver::split_plan(int k) {
     p.k = k;
     const bool big = L_.nrows * L_.ncols >= (int64_t(1) << 24);
     if (p.valid && (cfg_.autotune > 0 || (cfg_.autotune < 0 && big))) autotune_split(k);
+    // HEAT2D_SPLIT_ORDER=edge-first | concurrent overrides the split's ordering (tests, A/B)
+    if (const char* env = std::getenv("HEAT2D_SPLIT_ORDER")) {
+      const std::string o = env;
+      if (o == "edge-first" && p.valid == 1) p.valid = 3;
+      if (o == "concurrent" && p.valid == 3) p.valid = 1;
+    }
   }
   return p;
 }
@@ -296,6 +303,9 @@ const kern::SplitPlan& Solver::split_plan(int k) {
 // waves marching in lockstep, and the item-per-wave tail), which no static
 // rule captured; a single isolated cycle mispredicts the loop, hence the
 // steady-state measurement (profiles/autotune.md).
+// smallest steady-state cycle (ms) for which edge-first split plans are tried
+constexpr float kEdgeFirstMinCycleMs = 0.4f;
+
 void Solver::autotune_split(int k) {
   const int spare = tr_->exchanges() ? 8 : 0;
   synchronize();
@@ -305,6 +315,14 @@ void Solver::autotune_split(int k) {
   auto run_cycle = [&](const kern::SplitPlan& c) {
     void* src = buf_[cur_];
     void* dst = buf_[cur_ ^ 1];
+    if (c.valid == 3) {  // edge-first: both parts in order on the compute stream
+      H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+      kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_compute_, cfg_.arith);
+      kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith);
+      H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+      H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+      return;
+    }
     H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
     H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
     kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith);
@@ -338,15 +356,27 @@ void Solver::autotune_split(int k) {
   // without an exchange to hide, a single general launch per cycle competes too
   const bool single_ok = !tr_->exchanges();
   const int64_t nb1 = single_ok ? kern::plan_single(dtype(), L_, k, compute_cus_, 0, 0, cfg_.arith).main.nb : 0;
-  for (int mode : {1, 2}) {
+  // mode 1: split, interior and bands concurrently on two streams; mode 2
+  // (no exchange): one general launch; mode 3 (exchange): edge-first split —
+  // the short band launch first on the whole chip, then the interior, with the
+  // exchange of the bands running beside the interior (valid = 3)
+  for (int mode : {1, 2, 3}) {
     if (mode == 2 && !single_ok) continue;
+    // the trials run without the exchange, which the edge-first order puts
+    // beside the WHOLE interior: only where the interior is long enough to
+    // hide it (measured on the 1-rank RCCL rehearsal, profiles/multi_gpu_rehearsal_v4.md:
+    // fp64 slabs of 4096-16384 rows +2-4 %; a 4096-row fp32 slab, whose
+    // interior cycle is 0.28 ms, lost 7 % to an exposed exchange)
+    if (mode == 3 && (single_ok || best.valid != 1 || timed.front().first < kEdgeFirstMinCycleMs)) continue;
     for (int ring : {4, 6}) {
       for (double f : {1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 1.25, 1.5, 2.0}) {
-        const int64_t nb = std::max<int64_t>(1, (int64_t)((mode == 1 ? nb0 : nb1) * f + 0.5));
+        const int64_t nb = std::max<int64_t>(1, (int64_t)((mode == 2 ? nb1 : nb0) * f + 0.5));
         if (mode == 1 && ring == best.ring && nb == best.main.nb) continue;
-        kern::SplitPlan c = mode == 1 ? kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, nb, cfg_.arith)
-                                      : kern::plan_single(dtype(), L_, k, compute_cus_, ring, nb, cfg_.arith);
+        kern::SplitPlan c = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, nb, cfg_.arith)
+                                      : kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, nb,
+                                                         cfg_.arith);  // spare: room for RCCL beside the interior
         if (!c.valid) continue;
+        if (mode == 3) c.valid = 3;
         if (mode == 1)  // more items than waves only via explicit band counts above the default
           c.main_waves = std::min<int64_t>(c.main_items, std::max<int64_t>(c.main_waves, best.main_waves));
         timed.emplace_back(time_plan(c, 4), c);
@@ -378,8 +408,29 @@ void Solver::cycle_overlap(int k) {
   void* src = buf_[cur_];
   void* dst = buf_[cur_ ^ 1];
   const kern::SplitPlan& sp = split_plan(k);
+  HEAT2D_REQUIRE(sp.valid != 2 || !tr_->exchanges(), "single-launch plan with a halo exchange");
   roctxRangePushA("heat2d.cycle.split");
   PhaseEvents* pe = timing_ ? phase_begin(0) : nullptr;
+  if (sp.valid == 3) {
+    // edge-first: compute stream = [exchange c-1 landed] bands(c) -> interior(c);
+    // comm stream = [bands(c) done] exchange(c), beside the interior.
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_compute_));
+    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_compute_, cfg_.arith);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[3], s_compute_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
+    kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_bnd_, 0));
+    exchange_on(dst, s_comm_);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[5], s_comm_));
+    H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
+    roctxRangePop();
+    cycle_swap();
+    return;
+  }
   H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));  // edge part c-1 (record not yet replaced)
   H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));     // main part c-1
   if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));

@@ -83,7 +83,7 @@ def test_hip_autotune_keeps_state_bitwise(gpu, native, dtype, tb):
     s.upload(R.owned(R.initial_field(p, npdt)))
     s.prepare(p.ntime)
     pl = s.plan()
-    assert pl["valid"] in (1, 2) and pl["tuned_ms"] > 0.0 and pl["ring"] in (4, 6)  # split or single launch
+    assert pl["valid"] in (1, 2, 3) and pl["tuned_ms"] > 0.0 and pl["ring"] in (4, 6)  # split or single launch
     s.step(p.ntime)
     ref = R.owned(R.ftcs(p, dtype=npdt))
     got = s.download()
@@ -207,3 +207,19 @@ def test_phase_timers(gpu, native):
     ph = s.phase_times()
     assert ph["cycles"] == 3 and ph["main_ms"] > 0 and ph["edge_ms"] == 0
     s.close()
+
+
+@pytest.mark.parametrize("order", ["edge-first", "concurrent"])
+@pytest.mark.parametrize("P,tb,dtype", [(2, 8, "fp64"), (4, 12, "fp64"), (3, 16, "fp32")])
+def test_split_orders_with_exchange_bitwise(gpu, native, order, P, tb, dtype, monkeypatch):
+    """Both orderings of the split cycle with a real halo exchange between
+    slabs (device-copy loopback): edge-first (valid = 3: bands, then interior,
+    exchange beside the interior) and concurrent (valid = 1): bitwise == golden."""
+    monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
+    p = prob(700, 53, "ghost", "uniform")
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    g = LoopbackGroup(p, P, dtype=dtype, backend="hip", tb=tb, device=0)
+    g.step(p.ntime)
+    got = g.download()
+    g.close()
+    assert np.array_equal(got, R.owned(R.ftcs(p, dtype=npdt)))
