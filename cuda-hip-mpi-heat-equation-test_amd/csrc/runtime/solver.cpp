@@ -544,7 +544,11 @@ void Solver::step(int64_t n) {
       steps_ += pairs * 2 * K;
       continue;
     }
-    const int k = (int)std::min<int64_t>(K, left);
+    // balanced depths: ceil(left / K) cycles of depth base or base + 1 rather
+    // than full-depth cycles plus one short remainder cycle (a K = 4 cycle runs
+    // ~3x slower per step than K = 12: 100 steps = 8 x 11 + 12, not 8 x 12 + 4)
+    const int64_t ncyc = (left + K - 1) / K;
+    const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
     if (cfg_.overlap && hip_) cycle_overlap(k);
     else cycle_serial(k);
     left -= k;
@@ -555,8 +559,11 @@ void Solver::step(int64_t n) {
 void Solver::prepare(int64_t n) {
   if (!hip_ || !cfg_.overlap || cfg_.copy_swap || n <= 0) return;
   const int K = cfg_.tb;
-  if (n >= K) (void)split_plan(K);
-  if (n % K) (void)split_plan((int)(n % K));
+  // the depths step(n) will use (see its balanced split)
+  const int64_t ncyc = (n + K - 1) / K;
+  const int64_t base = n / ncyc;
+  (void)split_plan((int)base);
+  if (n % ncyc) (void)split_plan((int)base + 1);
 }
 
 void Solver::synchronize() {
