@@ -558,12 +558,24 @@ void Solver::step(int64_t n) {
 
 void Solver::prepare(int64_t n) {
   if (!hip_ || !cfg_.overlap || cfg_.copy_swap || n <= 0) return;
+  // walk step(n)'s loop (graph pairs of depth K, then balanced eager cycles)
+  // and plan every depth it will launch
   const int K = cfg_.tb;
-  // the depths step(n) will use (see its balanced split)
-  const int64_t ncyc = (n + K - 1) / K;
-  const int64_t base = n / ncyc;
-  (void)split_plan((int)base);
-  if (n % ncyc) (void)split_plan((int)base + 1);
+  const bool multi = tr_->exchanges();
+  int par = cur_;
+  int64_t left = n;
+  while (left > 0) {
+    if (cfg_.use_graph && (!multi || tr_->capturable()) && left >= 2 * K && par == 0) {
+      (void)split_plan(K);
+      left -= left / (2 * K) * 2 * K;
+      continue;
+    }
+    const int64_t ncyc = (left + K - 1) / K;
+    const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
+    (void)split_plan(k);
+    left -= k;
+    par ^= 1;
+  }
 }
 
 void Solver::synchronize() {
