@@ -280,6 +280,10 @@ int heat2d_solver_prepare(void* s, int64_t n) {
   return guarded([&] { static_cast<Solver*>(s)->prepare(n); });
 }
 
+int heat2d_solver_plans_made(void* s, int64_t* out) {
+  return guarded([&] { *out = static_cast<Solver*>(s)->plans_made(); });
+}
+
 int heat2d_solver_plan(void* s, int k, heat2d_split_plan* out, float* tuned_ms) {
   return guarded([&] {
     Solver& sv = *static_cast<Solver*>(s);

@@ -129,6 +129,8 @@ int heat2d_solver_phase_times(void* s, double* out5);
 int heat2d_solver_prepare(void* s, int64_t n);
 /* split plan used for depth k (planned / autotuned on first use); tuned_ms = autotuned cycle time or 0 */
 int heat2d_solver_plan(void* s, int k, heat2d_split_plan* out, float* tuned_ms);
+/* number of split plans made so far (first uses of a depth; a prepare()d run adds none) */
+int heat2d_solver_plans_made(void* s, int64_t* out);
 int heat2d_solver_info(void* s, int32_t* tb, int64_t* band, int64_t* steps, void** field,
                        void** stream);
 

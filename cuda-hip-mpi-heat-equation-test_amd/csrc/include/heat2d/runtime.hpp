@@ -157,6 +157,8 @@ class Solver {
   // Split plan in use for depth k (planned / autotuned on first use).
   const kern::SplitPlan& plan_for(int k) { return split_plan(k); }
   float tuned_ms(int k) const { return k >= 0 && k <= kMaxTB ? tuned_ms_[k] : 0.f; }
+  // split plans planned so far (each a first use of a depth; autotuned on big slabs)
+  int64_t plans_made() const { return plans_made_; }
   // Phase timers (hipEvents on the GPU timeline) for every cycle while
   // enabled: [main ms, edge ms, exchange ms, whole-cycle ms (serial schedule),
   // cycles]. phase_times() synchronises, sums the recorded cycles and resets.
@@ -197,6 +199,7 @@ class Solver {
   int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all
   kern::SplitPlan split_[kMaxTB + 1] = {};  // per temporal depth (k == 0: not planned yet)
   float tuned_ms_[kMaxTB + 1] = {};           // autotuned cycle time (ms), 0 if not tuned
+  int64_t plans_made_ = 0;
   hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K
   int graph_k_ = 0;
   std::vector<char> host_stage_;  // CPU-backend / callback staging

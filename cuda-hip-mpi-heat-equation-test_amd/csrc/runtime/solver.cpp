@@ -280,6 +280,7 @@ const kern::SplitPlan& Solver::split_plan(int k) {
     const int spare = tr_->exchanges() ? 8 : 0;
     p = kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, 0, 0, cfg_.arith);
     p.k = k;
+    ++plans_made_;
     const bool big = L_.nrows * L_.ncols >= (int64_t(1) << 24);
     if (p.valid && (cfg_.autotune > 0 || (cfg_.autotune < 0 && big))) autotune_split(k);
     // HEAT2D_SPLIT_ORDER=edge-first | concurrent overrides the split's ordering (tests, A/B)

@@ -178,6 +178,14 @@ class HeatSolver:
                 "tuned_ms": ms.value}
 
     @property
+    def plans_made(self) -> int:
+        """Split plans made so far (each the first use of a depth; autotuned on
+        big slabs). After prepare(n), step(n) must not add any."""
+        v = C.c_int64()
+        N.call("heat2d_solver_plans_made", self._h, C.byref(v))
+        return v.value
+
+    @property
     def tb(self) -> int:
         return self.info()["tb"]
 

@@ -119,6 +119,7 @@ _SIGS = {
     "heat2d_jit_compile_check": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(_I64)]),
     "heat2d_solver_phase_times": (C.c_int, [_P, C.POINTER(C.c_double)]),
     "heat2d_solver_plan": (C.c_int, [_P, C.c_int, C.POINTER(SplitPlan), C.POINTER(C.c_float)]),
+    "heat2d_solver_plans_made": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "heat2d_tb": (C.c_int, [C.c_int, _P, _P, _LP, _I64, _I64, C.c_int, C.c_double, _P, _I64, C.c_int]),
     "heat2d_init_field": (C.c_int, [C.c_int, _P, _LP, C.POINTER(IcParams), _P, _P, _P]),
     "heat2d_stats": (C.c_int, [C.c_int, _P, _P, _LP, _P, _P, _P]),

@@ -223,3 +223,20 @@ def test_split_orders_with_exchange_bitwise(gpu, native, order, P, tb, dtype, mo
     got = g.download()
     g.close()
     assert np.array_equal(got, R.owned(R.ftcs(p, dtype=npdt)))
+
+
+@pytest.mark.parametrize("n,tb,graph", [(1000, 16, True), (1000, 16, False), (100, 12, False), (50, 12, True),
+                                        (13, 12, False), (480, 12, False)])
+def test_prepare_covers_every_depth(gpu, native, n, tb, graph):
+    """prepare(n) plans every cycle depth step(n) launches (graph pairs, then
+    balanced eager cycles), so no plan — and no autotuning — happens inside a
+    timed step(n)."""
+    p = prob(300, n, "ghost", "uniform")
+    s = HeatSolver(p, dtype="fp32", backend="hip", tb=tb, device=0, graph=graph)
+    s.prepare(n)
+    before = s.plans_made
+    s.step(n)
+    s.synchronize()
+    assert s.plans_made == before
+    assert np.array_equal(s.download(), R.owned(R.ftcs(p, dtype=np.float32)))
+    s.close()
