@@ -16,6 +16,7 @@
 // communicators; the halo exchange is RCCL send/recv over xGMI.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -228,9 +229,21 @@ void run_rank(Shared& sh, int rank) {
 
     const int64_t ntime = sh.in.ntime;
     // plan / autotune every cycle depth the loop will use before the clock starts
-    s.prepare(ntime - start);
-    for (int64_t every : {a.print_every, a.check_every, a.checkpoint_every})
-      if (every > 0) s.prepare(std::min(every, ntime));
+    {  // walk the chunking of the loop below and prepare each distinct chunk length
+      const bool ckpt_every = !a.checkpoint.empty() && a.checkpoint_every > 0;
+      std::vector<int64_t> seen;
+      for (int64_t d = start; d < ntime;) {
+        int64_t c = ntime - d;
+        if (a.print_every > 0) c = std::min(c, a.print_every - (d % a.print_every));
+        if (a.check_every > 0) c = std::min(c, a.check_every - (d % a.check_every));
+        if (ckpt_every) c = std::min(c, a.checkpoint_every - (d % a.checkpoint_every));
+        if (std::find(seen.begin(), seen.end(), c) == seen.end()) {
+          seen.push_back(c);
+          s.prepare(c);
+        }
+        d += c;
+      }
+    }
     if (a.timers) s.set_timing(true);
     tr->barrier();
     s.synchronize();

@@ -119,7 +119,17 @@ def run(argv=None) -> int:
     if var.outputs == "serial" and a.output == "ascii" and start_step == 0:
         _write_inclusive(s, prob, "int.dat", world)
 
-    s.prepare(nsteps - start_step)  # plan / autotune outside the timed region
+    # plan / autotune outside the timed region: every chunk length the loop below runs
+    rules = [v for v in (a.print_every, a.check_every, a.checkpoint_every) if v > 0]
+    d, seen = start_step, set()
+    while d < nsteps:
+        c = nsteps - d
+        for v in rules:
+            c = min(c, v - d % v)
+        if c not in seen:
+            seen.add(c)
+            s.prepare(c)
+        d += c
     _barrier(world)
     s.synchronize()
     t0 = time.perf_counter()
