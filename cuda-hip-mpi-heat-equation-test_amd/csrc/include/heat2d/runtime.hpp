@@ -159,6 +159,7 @@ class Solver {
   float tuned_ms(int k) const { return k >= 0 && k <= kMaxTB ? tuned_ms_[k] : 0.f; }
   // split plans planned so far (each a first use of a depth; autotuned on big slabs)
   int64_t plans_made() const { return plans_made_; }
+  int spare_waves() const;
   // Phase timers (hipEvents on the GPU timeline) for every cycle while
   // enabled: [main ms, edge ms, exchange ms, whole-cycle ms (serial schedule),
   // cycles]. phase_times() synchronises, sums the recorded cycles and resets.

@@ -277,7 +277,7 @@ const kern::SplitPlan& Solver::split_plan(int k) {
   kern::SplitPlan& p = split_[k];
   if (p.k != k) {
     // room for RCCL's workgroups beside the two stencil launches when exchanging
-    const int spare = tr_->exchanges() ? 8 : 0;
+    const int spare = spare_waves();
     p = kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, 0, 0, cfg_.arith);
     p.k = k;
     ++plans_made_;
@@ -304,11 +304,19 @@ const kern::SplitPlan& Solver::split_plan(int k) {
 // waves marching in lockstep, and the item-per-wave tail), which no static
 // rule captured; a single isolated cycle mispredicts the loop, hence the
 // steady-state measurement (profiles/autotune.md).
+// Wave slots the interior grid leaves free for RCCL's kernels when the slab
+// exchanges halos (HEAT2D_SPARE_WAVES overrides; A/B in profiles/).
+int Solver::spare_waves() const {
+  if (!tr_->exchanges()) return 0;
+  if (const char* env = std::getenv("HEAT2D_SPARE_WAVES")) return std::max(0, std::atoi(env));
+  return 8;
+}
+
 // smallest steady-state cycle (ms) for which edge-first split plans are tried
 constexpr float kEdgeFirstMinCycleMs = 0.4f;
 
 void Solver::autotune_split(int k) {
-  const int spare = tr_->exchanges() ? 8 : 0;
+  const int spare = spare_waves();
   synchronize();
   hipEvent_t e0, e1;
   H2D_HIP(hipEventCreate(&e0));
