@@ -503,6 +503,7 @@ void Solver::run_graph_cycles(int64_t npairs) {
       H2D_HIP(hipStreamWaitEvent(s_comm_, fork, 0));
       H2D_HIP(hipEventRecord(ev_int_, s_compute_));  // in-capture records replace the external ones
       H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+      H2D_HIP(hipEventRecord(ev_comm_, s_comm_));  // edge-first cycles wait on it
       const bool timing = timing_;
       timing_ = false;  // no timing events inside graphs
       cycle_overlap(K);

@@ -65,7 +65,12 @@ class RcclTransport final : public Transport {
   int rank() const override { return rank_; }
   int size() const override { return size_; }
   std::string name() const override { return loop_ ? "rccl-loop" : "rccl"; }
-  bool capturable() const override { return true; }
+  // Not captured into hipGraphs: capturing the grouped ncclSend/ncclRecv of
+  // the overlapped cycle segfaulted inside step() on the MI355X box (RCCL
+  // 2.26.6, tools/graph_rccl_probe.py, either split order), so --graph runs
+  // eager cycles whenever RCCL exchanges halos (single-rank runs still use
+  // graphs).
+  bool capturable() const override { return false; }
   bool exchanges() const override { return size_ > 1 || loop_; }
   void check() override {
     ncclResult_t st = ncclSuccess;

@@ -45,7 +45,9 @@ def test_rccl_single_rank(native, gpu):
         dist.destroy_process_group()
 
 
-def test_rccl_loop_rehearsal(native, gpu):
+@pytest.mark.parametrize("order,graph", [("auto", False), ("edge-first", False), ("edge-first", True),
+                                         ("concurrent", True)])
+def test_rccl_loop_rehearsal(native, gpu, order, graph, monkeypatch):
     """The 1-GPU rehearsal of the multi-GPU schedule: bands + RCCL self
     send/recv on the comm stream beside the CU-masked interior. The physics is
     periodic-ish (the frame rows are overwritten), so check what must hold:
@@ -54,10 +56,12 @@ def test_rccl_loop_rehearsal(native, gpu):
     from heat2d.models.heat2d import HeatSolver
     from heat2d.parallel.transport import RcclLoopTransport
 
+    if order != "auto":
+        monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
     tr = RcclLoopTransport(0)
     assert tr.name == "rccl-loop"
     p = heat2d.make_problem(heat2d.InputDat(n=400, sigma=0.25, nu=0.05, dom_len=1.0, ntime=40), "ghost", "sine")
-    s = HeatSolver(p, dtype="fp64", backend="hip", tb=8, transport=tr, device=0)
+    s = HeatSolver(p, dtype="fp64", backend="hip", tb=8, transport=tr, device=0, graph=graph)
     s.upload(R.owned(R.initial_field(p)))
     s.step(p.ntime)
     got = s.download()
