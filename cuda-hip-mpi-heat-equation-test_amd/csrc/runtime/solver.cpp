@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -70,7 +71,14 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
   int K = std::max(1, std::min<int>(cfg_.tb <= 0 ? tb_auto : cfg_.tb, kMaxTB));
   if (cfg_.copy_swap) K = 1;
   HEAT2D_REQUIRE(cfg_.engine == 0 || cfg_.engine == 1, "engine must be 0 (temporal-blocked) or 1 (jit)");
-  HEAT2D_REQUIRE(cfg_.arith == 0 || cfg_.arith == 1, "arith must be 0 (reference rounding) or 1 (fma)");
+  if (cfg_.arith < 0) {
+    // auto: the contracted form when it is bitwise identical to the reference
+    // rounding — r an exact power of two (sigma = 0.25 in every shipped
+    // input.dat), where r*x is exact (normal range) — else the reference form
+    int e = 0;
+    cfg_.arith = (cfg_.r > 0 && std::frexp(cfg_.r, &e) == 0.5) ? 1 : 0;
+  }
+  HEAT2D_REQUIRE(cfg_.arith == 0 || cfg_.arith == 1, "arith must be 0 (reference rounding), 1 (fma) or -1 (auto)");
   if (cfg_.engine == 1) {
     HEAT2D_REQUIRE(hip_, "the jit engine runs on the HIP backend");
     HEAT2D_REQUIRE(!cfg_.copy_swap, "the jit engine has no copy-swap mode");

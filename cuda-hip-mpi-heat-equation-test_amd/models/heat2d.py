@@ -78,7 +78,7 @@ class HeatSolver:
                  overlap: bool = True, copy_swap: bool = False, managed: bool = False, graph: bool = False,
                  tile_rows: int = 0, halo: int = 0, transport: Optional[T.Transport] = None,
                  device: Optional[int] = None, init: bool = True, rows: Optional[int] = None,
-                 comm_cus: int = 0, autotune: int = -1, engine: str = "tb", arith: str = "exact"):
+                 comm_cus: int = 0, autotune: int = -1, engine: str = "tb", arith: str = "auto"):
         self.problem = problem
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]
@@ -271,7 +271,7 @@ class LoopbackGroup:
     """
 
     def __init__(self, problem: Problem, nranks: int, *, dtype: str = "fp64", backend: str = "auto",
-                 tb: int = 0, tile_rows: int = 0, device: Optional[int] = None, arith: str = "exact"):
+                 tb: int = 0, tile_rows: int = 0, device: Optional[int] = None, arith: str = "auto"):
         self.problem = problem
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]

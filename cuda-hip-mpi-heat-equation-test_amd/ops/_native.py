@@ -27,7 +27,16 @@ CLI_PATH = os.path.join(NATIVE_DIR, "heat2d")
 
 F32, F64 = 0, 1
 # SolverConfig::arith: reference rounding (bitwise == NumPy golden) | contracted fma(r, sum - 4c, c)
-ARITH = {"exact": 0, "fma": 1}
+ARITH = {"exact": 0, "fma": 1, "auto": -1}
+
+
+def arith_code(arith: str, r: float) -> int:
+    """0 / 1 for the raw kernels; "auto" = fma iff r is an exact power of two
+    (then the contracted form is bitwise identical to the reference rounding)."""
+    import math
+    if arith == "auto":
+        return 1 if r > 0 and math.frexp(r)[0] == 0.5 else 0
+    return ARITH[arith]
 BACKEND_HIP, BACKEND_CPU = 0, 1
 
 

@@ -20,7 +20,7 @@ from .kernels import _check_field, _stream, dtype_code
 def render(dtype: int, layout: N.Layout, r: float, arith: str = "exact") -> str:
     """HIP source of one FTCS step specialised for ``layout`` and ``r``."""
     n = C.c_int64()
-    ar = N.ARITH[arith]
+    ar = N.arith_code(arith, r)
     N.call("heat2d_jit_render", dtype, C.byref(layout), float(r), ar, None, 0, C.byref(n))
     buf = C.create_string_buffer(n.value + 1)
     N.call("heat2d_jit_render", dtype, C.byref(layout), float(r), ar, buf, n.value + 1, C.byref(n))
@@ -45,7 +45,7 @@ class JitStencil:
         code = N.F32 if dtype == torch.float32 else N.F64
         dev = torch.cuda.current_device() if device is None else device
         h = C.c_void_p()
-        N.call("heat2d_jit_create", code, C.byref(layout), self.r, dev, N.ARITH[arith], C.byref(h))
+        N.call("heat2d_jit_create", code, C.byref(layout), self.r, dev, N.arith_code(arith, self.r), C.byref(h))
         self._h = h
         self.source = render(code, layout, self.r, arith)
 

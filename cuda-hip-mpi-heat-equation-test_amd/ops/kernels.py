@@ -96,7 +96,7 @@ def tb_step(src: torch.Tensor, dst: torch.Tensor, layout: N.Layout, k: int, r: f
     if src.data_ptr() == dst.data_ptr():
         raise ValueError("tb_step is out-of-place (ping-pong fields)")
     rb, re = (0, layout.nrows) if rows is None else rows
-    ar = N.ARITH[arith]
+    ar = N.arith_code(arith, r)
     if src.is_cuda:
         N.call("heat2d_tb", dtype_code(src), C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
                C.byref(layout), rb, re, k, r, _stream(src), tile_rows, ar)
