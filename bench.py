@@ -14,7 +14,7 @@ ranks. One "step" = one full time step of every grid point (temporal blocking
 fuses up to --tb steps per HBM pass; every point is still updated every step).
 Rank 0 prints one JSON line.
 
-Arithmetic (--arith, default fma): the update is the reference expression
+Arithmetic (--arith, default auto = fma here): the update is the reference expression
 c + r*(sum - 4c) (fortran/hip/heat_kernel.cpp:43) in fp64, contracted to
 fma(r, sum - 4c, c) — what hipcc's default -ffp-contract=fast makes of that
 line. With this config's r = 0.25 (a power of two) every rounding is the same
@@ -35,6 +35,14 @@ _ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, _ROOT)
 
 REF_GPTS_PER_RANK = 50.0  # BASELINE.md derived ceiling, 1 MI250X GCD, fp64
+
+
+def N_arith(r, arith):
+    """1 if the run uses the contracted update (see --arith)."""
+    import math
+    if arith == "auto":
+        return r > 0 and math.frexp(r)[0] == 0.5
+    return arith == "fma"
 
 
 def _claim_stdout():
@@ -63,8 +71,9 @@ def main():
     ap.add_argument("--tb", type=int, default=0,
                     help="time steps fused per HBM pass (0: measured best, fp64 12 / fp32 16; profiles/README.md)")
     ap.add_argument("--tile-rows", type=int, default=0)
-    ap.add_argument("--arith", default="fma", choices=["exact", "fma"],
-                    help="fma: contracted update (one op fewer per point); exact: every op rounded")
+    ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma"],
+                    help="fma: contracted update (one op fewer per point); exact: every op rounded; auto: fma when "
+                         "bitwise identical to exact (r a power of two, as here), else exact")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--comm-cus", type=int, default=0, help="CUs reserved for bands + RCCL (0: default, -1: none)")
     ap.add_argument("--check", action="store_true", help="print field statistics after the run")
@@ -180,7 +189,7 @@ def main():
                 "seq_len": prob.n_owned,
                 "parallelism": f"slab{world}" + ("-rehearsal" if args.rehearse_comm and world == 1 else ""),
                 "temporal_block": tb,
-                "arith": args.arith,
+                "arith": ("fma" if N_arith(prob.r, args.arith) else "exact") + (" (auto)" if args.arith == "auto" else ""),
                 "overlap": not args.no_overlap,
                 "launch_plan": s.plan() if (hip and not args.no_overlap) else None,
                 "backend": args.backend,
