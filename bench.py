@@ -69,7 +69,7 @@ def main():
                          "every rank keeps ~n^2 points (e.g. --dtype fp32 --n 173056: the full-HBM 240 GB per GPU)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--tb", type=int, default=0,
-                    help="time steps fused per HBM pass (0: measured best, fp64 12 / fp32 16; profiles/README.md)")
+                    help="time steps fused per HBM pass (0: measured best, fp64 14 / fp32 16; profiles/README.md)")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma"],
                     help="fma: contracted update (one op fewer per point); exact: every op rounded; auto: fma when "
@@ -89,7 +89,7 @@ def main():
                          "interior) to measure its per-rank cost; not the headline (periodic halo)")
     args = ap.parse_args()
     if args.tb <= 0:
-        args.tb = 12 if args.dtype == "fp64" else 16
+        args.tb = 14 if args.dtype == "fp64" else 16
 
     import torch
     import torch.distributed as dist

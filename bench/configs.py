@@ -67,8 +67,8 @@ def main():
         ("cpu-256-fp64", 256, "fp64", 200, 8, "cpu", 8, False),
         ("gpu-4096-fp32", 4096, "fp32", 1000, 64, "hip", 16, False),
         ("gpu-4096-fp32-graph", 4096, "fp32", 1000, 64, "hip", 16, True),
-        ("gpu-16384-fp64", 16384, "fp64", 480, 48, "hip", 12, False),
-        ("gpu-32768-fp64", 32768, "fp64", 480, 48, "hip", 12, False),
+        ("gpu-16384-fp64", 16384, "fp64", 480, 48, "hip", 14, False),
+        ("gpu-32768-fp64", 32768, "fp64", 480, 48, "hip", 14, False),
         ("gpu-32768-fp32", 32768, "fp32", 480, 48, "hip", 16, False),
         ("gpu-max-fp32", nmax, "fp32", 64, 16, "hip", 16, False),
     ]

@@ -65,9 +65,10 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
   HEAT2D_REQUIRE(cfg_.n_rows >= P, "fewer rows than ranks");
 
   // tb <= 0: the measured best depth of the HIP engine (bench.py sweeps on
-  // MI355X, profiles/README.md: fp64 12, fp32 16 with the packed fp32 march);
-  // 8 on the CPU twin.
-  const int tb_auto = hip_ ? (cfg_.dtype == 1 ? 12 : 16) : 8;
+  // MI355X, profiles/README.md §11: fp64 14 — equal to 12 on a whole 32768²
+  // grid, 3-6 % faster on the slabs of 2/4/8-rank runs — fp32 16 with the
+  // packed fp32 march); 8 on the CPU twin.
+  const int tb_auto = hip_ ? (cfg_.dtype == 1 ? 14 : 16) : 8;
   int K = std::max(1, std::min<int>(cfg_.tb <= 0 ? tb_auto : cfg_.tb, kMaxTB));
   if (cfg_.copy_swap) K = 1;
   HEAT2D_REQUIRE(cfg_.engine == 0 || cfg_.engine == 1, "engine must be 0 (temporal-blocked) or 1 (jit)");

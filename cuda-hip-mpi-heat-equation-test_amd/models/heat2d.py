@@ -48,7 +48,7 @@ class HeatSolver:
         dtype: "fp64" (reference precision) or "fp32".
         backend: "hip", "cpu" or "auto".
         tb: temporal-block depth K (time steps fused per HBM pass, 1..16; 0 = the
-            measured best: fp64 12 / fp32 16 on the HIP engine, 8 on the CPU twin).
+            measured best: fp64 14 / fp32 16 on the HIP engine, 8 on the CPU twin).
         overlap: boundary/interior split with the halo exchange on a comm stream.
         copy_swap: reference-parity schedule (full field copy every step, K=1).
         managed: allocate fields with hipMallocManaged.
