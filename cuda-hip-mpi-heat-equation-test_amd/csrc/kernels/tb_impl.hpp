@@ -339,10 +339,11 @@ struct March {
 // (columns c0..c3) is kept as an even/odd pair of register pairs
 // a = (c0, c2), b = (c1, c3), so the in-lane east/west neighbours of a whole
 // pair are the other pair (east of a is b, west of b is a) and only the
-// across-lane ones need a DPP move plus one pair assembly:
+// across-lane ones are built half by half with single fp32 adds (sadd*, the
+// DPP shift folded into v_add_f32_dpp):
 //   east of b = (c2, c0 of lane+1),   west of a = (c3 of lane-1, c1).
-// Per row and level: 10 packed ops + 2 DPP moves + 2 pair assemblies for 4
-// points. With the element-wise layout March<float> uses, the compiler had to
+// Per row and level: 8 packed ops + 4 single adds for 4 points (12 VALU ops).
+// With the element-wise layout March<float> uses, the compiler had to
 // rebuild misaligned pairs for every packed op (~4.9 VALU ops per point and
 // ~2x the registers: 209 VGPRs at K = 10). Same operation order and rounding
 // per element as March (bitwise identical); the loads / stores / ring /
@@ -578,7 +579,7 @@ __device__ __forceinline__ bool tb_item(const TbArgs& a, int64_t it, int64_t& st
 // Occupancy floor handed to the register allocator: the fp64 fma interior
 // kernel at K = 11..12 lands at 129 VGPRs and fits 128 (4 waves/SIMD instead
 // of 3) without spilling; its exact-arithmetic twin would spill. (The packed
-// fp32 march with the asm across-lane adds spills under a 3-wave floor from
+// fp32 march with the single across-lane adds spills under a 3-wave floor from
 // K = 12 on, so it has none.) Checked per build: ScratchSize = 0 in the ISA
 // (tools/isa_report.py, tests/test_isa.py).
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
