@@ -578,22 +578,28 @@ void Solver::step(int64_t n) {
 void Solver::prepare(int64_t n) {
   if (!hip_ || !cfg_.overlap || cfg_.copy_swap || n <= 0) return;
   // walk step(n)'s loop (graph pairs of depth K, then balanced eager cycles)
-  // and plan every depth it will launch
+  // and plan every depth it will launch. Graph pairs start only at buffer
+  // parity 0, so the depths depend on the parity step(n) starts from: walk
+  // both, since a warmup between prepare() and step(n) may flip it (4096^2
+  // fp32 graph, K = 6 / 14: an unplanned remainder depth autotuned inside the
+  // timed run cost 10 ms of 16).
   const int K = cfg_.tb;
   const bool multi = tr_->exchanges();
-  int par = cur_;
-  int64_t left = n;
-  while (left > 0) {
-    if (cfg_.use_graph && (!multi || tr_->capturable()) && left >= 2 * K && par == 0) {
-      (void)split_plan(K);
-      left -= left / (2 * K) * 2 * K;
-      continue;
+  for (int start = 0; start < 2; ++start) {
+    int par = start;
+    int64_t left = n;
+    while (left > 0) {
+      if (cfg_.use_graph && (!multi || tr_->capturable()) && left >= 2 * K && par == 0) {
+        (void)split_plan(K);
+        left -= left / (2 * K) * 2 * K;
+        continue;
+      }
+      const int64_t ncyc = (left + K - 1) / K;
+      const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
+      (void)split_plan(k);
+      left -= k;
+      par ^= 1;
     }
-    const int64_t ncyc = (left + K - 1) / K;
-    const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
-    (void)split_plan(k);
-    left -= k;
-    par ^= 1;
   }
 }
 

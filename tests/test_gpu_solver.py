@@ -240,3 +240,22 @@ def test_prepare_covers_every_depth(gpu, native, n, tb, graph):
     assert s.plans_made == before
     assert np.array_equal(s.download(), R.owned(R.ftcs(p, dtype=np.float32)))
     s.close()
+
+
+@pytest.mark.parametrize("tb", [6, 14])
+def test_prepare_covers_warmup_parity(gpu, native, tb):
+    """bench order: prepare(n), an untimed warmup that leaves the buffer parity
+    at 1, then step(n). Graph pairs start only at parity 0, so step(n) launches
+    other remainder depths than a walk from parity 0 would plan."""
+    n, warm = 1000, 64
+    p = prob(300, warm + n, "ghost", "uniform")
+    s = HeatSolver(p, dtype="fp32", backend="hip", tb=tb, device=0, graph=True)
+    s.prepare(n)
+    s.step(warm)
+    s.synchronize()
+    before = s.plans_made
+    s.step(n)
+    s.synchronize()
+    assert s.plans_made == before
+    assert np.array_equal(s.download(), R.owned(R.ftcs(p, dtype=np.float32)))
+    s.close()
