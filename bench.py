@@ -12,7 +12,14 @@ W untimed warm-up steps, then exactly K FTCS time steps, bracketed by a
 barrier + device synchronisation on both sides; the time is the MAX over
 ranks. One "step" = one full time step of every grid point (temporal blocking
 fuses up to --tb steps per HBM pass; every point is still updated every step).
-Rank 0 prints one JSON line.
+Rank 0 prints one JSON line. Without torchrun, --gpus N > 1 starts the N rank
+processes itself (and fails if fewer than N GPUs are visible).
+
+The JSON reports what the timed region launched: `cycles` (depth -> cycles),
+each depth's launch plan, and `hbm_gb_per_s_plan`, the DRAM traffic those
+plans move per second (utils/metrics.plan_hbm_bytes: strip halos and priming
+rows counted, no cache reuse assumed — an upper bound; rocprof cross-check in
+profiles/hbm_model_check.md).
 
 Arithmetic (--arith, default auto = fma here): the update is the reference expression
 c + r*(sum - 4c) (fortran/hip/heat_kernel.cpp:43) in fp64, contracted to
@@ -45,6 +52,56 @@ def N_arith(r, arith):
     return arith == "fma"
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _launch_ranks(n, backend):
+    """`python bench.py --gpus N` without torchrun: start N rank processes of
+    this script (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+    rendezvous on 127.0.0.1) and return the exit status. Rank 0 prints the
+    JSON line on the inherited stdout. If a rank fails, the others are
+    terminated (they would block in RCCL forever) and its status is returned.
+    Runs before this process touches the GPU: children are started, never
+    exec'd over a GPU-initialised process."""
+    import signal
+    import subprocess
+    if backend == "hip":
+        import torch  # device_count() does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the others", file=sys.stderr)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            try:
+                live[0].wait(timeout=0.2)
+            except subprocess.TimeoutExpired:
+                pass
+    return rc
+
+
 def _claim_stdout():
     """Keep the driver's stdout for the ONE JSON line: RCCL (torch's and ours)
     prints a version banner on stdout from C at communicator init, and C stdio
@@ -57,7 +114,6 @@ def _claim_stdout():
 
 
 def main():
-    out_fd = _claim_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=480)
@@ -90,6 +146,9 @@ def main():
     args = ap.parse_args()
     if args.tb <= 0:
         args.tb = 14 if args.dtype == "fp64" else 16
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_launch_ranks(args.gpus, args.backend))
+    out_fd = _claim_stdout()
 
     import torch
     import torch.distributed as dist
@@ -97,8 +156,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     hip = args.backend == "hip"
     if hip:
         torch.cuda.set_device(local)
@@ -142,6 +202,7 @@ def main():
     s.prepare(args.steps)  # plan / autotune every depth the timed run uses (outside the timed region)
     s.step(args.warmup)
     s.synchronize()
+    s.cycle_hist(reset=True)
     if args.phase_timers:
         s.set_timing(True)
     barrier()
@@ -162,8 +223,23 @@ def main():
     es = 8 if args.dtype == "fp64" else 4
     info = s.info()
     tb = info["tb"]
-    # model HBM traffic: one read + one write of the field per HBM pass (tb steps)
-    model_gbps = gpts * (2.0 * es / tb)
+    # what the timed region launched: cycles per depth (this rank), each depth's
+    # launch plan, and the DRAM traffic those plans move (strip halos W vs U and
+    # the 2k priming rows per band counted; no cache reuse assumed)
+    hist = s.cycle_hist()
+    assert sum(k * c for k, c in hist.items()) == args.steps, hist
+    plans, traffic = {}, 0.0
+    from heat2d.utils.metrics import plan_hbm_bytes
+    for k, c in sorted(hist.items()):
+        pl = s.plan(k) if hip else {"k": k, "valid": 0}
+        if hip:
+            plans[str(k)] = {kk: pl[kk] for kk in ("order", "ring", "main_bands", "main_waves", "edge_items",
+                                                    "tuned_ms")}
+        traffic += c * plan_hbm_bytes(pl, es, s.nrows, s.ncols)["total"]
+    if world > 1:
+        tt = torch.tensor([traffic], device="cuda" if hip else "cpu", dtype=torch.float64)
+        dist.all_reduce(tt)
+        traffic = float(tt.item())
     stats = s.stats() if args.check else None
     phases = s.phase_times() if args.phase_timers else None
     if rank == 0:
@@ -188,13 +264,14 @@ def main():
                 "global_batch": 1,
                 "seq_len": prob.n_owned,
                 "parallelism": f"slab{world}" + ("-rehearsal" if args.rehearse_comm and world == 1 else ""),
-                "temporal_block": tb,
+                "tb_max": tb,
+                "cycles": {str(k): c for k, c in sorted(hist.items())},
                 "arith": ("fma" if N_arith(prob.r, args.arith) else "exact") + (" (auto)" if args.arith == "auto" else ""),
                 "overlap": not args.no_overlap,
-                "launch_plan": s.plan() if (hip and not args.no_overlap) else None,
+                "launch_plans": plans or None,
                 "backend": args.backend,
             },
-            "hbm_gb_per_s_model": round(model_gbps, 1),
+            "hbm_gb_per_s_plan": round(traffic / elapsed / 1e9, 1),
             "baseline_basis": "BASELINE.md derived ceiling 50 Gpts/s per MI250X GCD x n_gpus",
         }
         if stats:

@@ -321,6 +321,25 @@ int heat2d_group_step(void* g, int64_t n) {
   return guarded([&] { static_cast<LoopbackGroup*>(g)->step(n); });
 }
 
+int heat2d_group_upload(void* g, const void* host, int64_t ld) {
+  return guarded([&] { static_cast<LoopbackGroup*>(g)->upload(host, ld); });
+}
+
+int heat2d_group_member(void* g, int i, void** solver) {
+  return guarded([&] {
+    auto* gr = static_cast<LoopbackGroup*>(g);
+    HEAT2D_REQUIRE(i >= 0 && i < gr->nranks(), "member index out of range");
+    *solver = &gr->member(i);
+  });
+}
+
+int heat2d_solver_cycle_hist(void* s, int64_t* out, int n, int reset) {
+  return guarded([&] {
+    HEAT2D_REQUIRE(n >= kMaxTB + 1, "cycle_hist needs kMaxTB + 1 slots");
+    static_cast<Solver*>(s)->cycle_hist(out, reset != 0);
+  });
+}
+
 int heat2d_group_download(void* g, void* host, int64_t ld) {
   return guarded([&] {
     auto* gr = static_cast<LoopbackGroup*>(g);

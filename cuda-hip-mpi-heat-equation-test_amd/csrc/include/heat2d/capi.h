@@ -140,6 +140,12 @@ int heat2d_group_free(void* g);
 int heat2d_group_init(void* g, const heat2d_ic* ic, const double* xg, const double* yg);
 int heat2d_group_step(void* g, int64_t n);
 int heat2d_group_download(void* g, void* host, int64_t ld);
+/* whole global owned region -> the members' slabs, then a loopback halo exchange */
+int heat2d_group_upload(void* g, const void* host, int64_t ld);
+/* member i's solver (borrowed handle: valid while the group lives; plan / info / hist queries) */
+int heat2d_group_member(void* g, int i, void** solver);
+/* cycles step() launched since the last reset, by depth: out[k], k = 0..heat2d_max_tb() (n >= max_tb + 1) */
+int heat2d_solver_cycle_hist(void* s, int64_t* out, int n, int reset);
 
 /* I/O (io.cpp). */
 int heat2d_write_xyz(const char* path, int dtype, const void* host, int64_t nrows, int64_t ncols,

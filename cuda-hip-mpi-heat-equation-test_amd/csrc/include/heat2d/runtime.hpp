@@ -73,9 +73,41 @@ class Transport {
   // Failure detection: raise if the fabric reported an asynchronous error
   // (RCCL: ncclCommGetAsyncError). Polled at every synchronisation point.
   virtual void check() {}
+  // Two-phase cycles (transports whose ranks share one process, e.g. the
+  // loopback): every rank post()s the field its cycle is writing and the
+  // event that marks that field's boundary bands written BEFORE any rank's
+  // exchange() of the same cycle is enqueued (LoopbackGroup drives this
+  // order). Fabrics with their own rendezvous (RCCL) ignore it.
+  virtual void post(void* /*field*/, const SlabLayout& /*L*/, hipEvent_t /*bands_ready*/) {}
 };
 
+// The messages of one halo exchange, shared by every transport (RCCL sends
+// and receives exactly these; the loopback copies them): k whole padded rows
+// per message, contiguous in the slab layout, so no pack / unpack.
+//   to / from rank-1: send rows [0, k),          receive into [-k, 0)
+//   to / from rank+1: send rows [nrows-k, nrows), receive into [nrows, nrows+k)
+// (the reference's two MPI_Sendrecv per step, fortran/hip/heat.F90:212-213)
+struct HaloMsg {
+  int peer;
+  int64_t send_row, recv_row;
+};
+inline int halo_msgs(int rank, int size, const SlabLayout& L, int64_t k, HaloMsg out[2]) {
+  int n = 0;
+  if (rank > 0) out[n++] = HaloMsg{rank - 1, 0, -k};
+  if (rank < size - 1) out[n++] = HaloMsg{rank + 1, L.nrows - k, L.nrows};
+  return n;
+}
+inline size_t halo_row_bytes(const SlabLayout& L, int64_t row, size_t es) {
+  return (size_t)((row + L.halo) * L.pitch) * es;
+}
+inline size_t halo_msg_bytes(const SlabLayout& L, int64_t k, size_t es) { return (size_t)(k * L.pitch) * es; }
+
 std::shared_ptr<Transport> make_self_transport();
+// P ranks of one process (one device, or host memory): halos move by
+// device-to-device copies on the receiving rank's exchange stream, ordered by
+// events against the neighbours' band kernels (transport.cpp). make_loopback_
+// transports returns the P member transports of one group.
+std::vector<std::shared_ptr<Transport>> make_loopback_transports(int nranks);
 // RCCL over xGMI. `uid` = 128-byte ncclUniqueId produced by rccl_unique_id()
 // on rank 0 and broadcast out of band (torch.distributed store, file, or a
 // shared variable for thread-per-GPU).
@@ -138,10 +170,20 @@ class Solver {
   // ghost/frame included) -> host.
   void download_region(int64_t r0, int64_t r1, int64_t c0, int64_t c1, void* host, int64_t ld);
 
-  // Phase API (used by the loopback group; step() drives these itself).
+  // Phase API. One cycle of depth k = cycle_launch(k) (kernels, the event
+  // that marks the bands written, Transport::post) then cycle_finish() (halo
+  // exchange of the new field, buffer swap). step() runs the two back to
+  // back; LoopbackGroup runs every member's launch before any member's finish.
+  void cycle_launch(int k);
+  void cycle_finish();
   void cycle_compute(int k);   // whole-slab compute cur -> nxt (no exchange)
   void cycle_swap();
+  void exchange_post();        // Transport::post of the current buffer (two-phase transports)
   void exchange_now();         // exchange halos of the current buffer on the compute stream
+  void upload_owned(const void* host, int64_t ld);  // upload() without the halo exchange
+  // Cycles launched by step() since the last reset, by depth: hist[k] for
+  // k = 0..kMaxTB (graph replays count their two cycles each).
+  void cycle_hist(int64_t out[kMaxTB + 1], bool reset);
 
   const SlabLayout& layout() const { return L_; }
   const SolverConfig& config() const { return cfg_; }
@@ -167,10 +209,10 @@ class Solver {
   void phase_times(double out[5]);
 
  private:
-  void cycle_overlap(int k);
+  void launch_overlap(int k);
+  void launch_serial(int k);
   const kern::SplitPlan& split_plan(int k);
   void autotune_split(int k);
-  void cycle_serial(int k);
   void cycle_copy_swap();
   void launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k);
   void exchange_on(void* field, hipStream_t s);
@@ -197,6 +239,12 @@ class Solver {
   std::vector<PhaseEvents> phase_pool_;  // reusable
   double phase_acc_[5] = {};
   PhaseEvents* phase_begin(int kind);
+  // the launched, not yet finished cycle (cycle_launch -> cycle_finish)
+  enum class Pending { None, Serial, Concurrent, EdgeFirst };
+  Pending pend_ = Pending::None;
+  int pend_k_ = 0;
+  int64_t pend_pe_ = -1;  // index into phase_ev_ (timing) or -1
+  int64_t hist_[kMaxTB + 1] = {};
   int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all
   kern::SplitPlan split_[kMaxTB + 1] = {};  // per temporal depth (k == 0: not planned yet)
   float tuned_ms_[kMaxTB + 1] = {};           // autotuned cycle time (ms), 0 if not tuned
@@ -207,9 +255,12 @@ class Solver {
   std::unique_ptr<JitStencil> jit_;  // engine 1
 };
 
-// P slabs of one domain on ONE device (or host), halos moved by device
-// copies: proves the decomposition, band split and exchange schedule without
-// a cluster (must be bitwise identical to P = 1).
+// P slabs of one domain on ONE device (or host), each a full Solver with its
+// own compute / comm streams, split plans and autotuner, exchanging halos
+// through the loopback transport (the same messages RCCL moves): the whole
+// multi-rank schedule — overlapped split cycles in either order, balanced
+// depths, the event protocol across streams — runs with real exchanges on one
+// GPU and must be bitwise identical to P = 1.
 class LoopbackGroup {
  public:
   LoopbackGroup(const SolverConfig& cfg, int nranks);
@@ -218,13 +269,11 @@ class LoopbackGroup {
   void step(int64_t n);
   void synchronize();
   void download(void* host, int64_t ld);  // whole global owned region
+  void upload(const void* host, int64_t ld);  // whole global owned region, then a halo exchange
   int nranks() const { return (int)members_.size(); }
   Solver& member(int i) { return *members_[i]; }
 
  private:
-  void exchange_all();
-  SolverConfig cfg_;
-  hipStream_t stream_ = nullptr;
   std::vector<std::unique_ptr<Solver>> members_;
 };
 

@@ -222,18 +222,64 @@ void Solver::cycle_swap() {
   cur_ ^= 1;
 }
 
+void Solver::exchange_post() {
+  if (!tr_->exchanges()) return;
+  if (hip_) H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+  tr_->post(buf_[cur_], L_, hip_ ? ev_bnd_ : nullptr);
+}
+
 void Solver::exchange_now() { exchange_on(buf_[cur_], s_compute_); }
 
-void Solver::cycle_serial(int k) {
+void Solver::cycle_launch(int k) {
+  HEAT2D_REQUIRE(pend_ == Pending::None, "cycle_launch: previous cycle not finished");
+  HEAT2D_REQUIRE(k >= 1 && k <= cfg_.tb, "cycle depth outside [1, tb]");
+  if (cfg_.overlap && hip_) launch_overlap(k);
+  else launch_serial(k);
+  pend_k_ = k;
+}
+
+void Solver::cycle_finish() {
+  HEAT2D_REQUIRE(pend_ != Pending::None, "cycle_finish without cycle_launch");
+  void* dst = buf_[cur_ ^ 1];
+  PhaseEvents* pe = pend_pe_ >= 0 ? &phase_ev_[(size_t)pend_pe_] : nullptr;
+  if (pend_ == Pending::Serial) {
+    exchange_on(dst, s_compute_);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
+  } else {
+    // both split orders: the exchange of the new bands runs on the comm
+    // stream (concurrent: right behind the EDGE launch there; edge-first:
+    // behind the bands, which ran first on the compute stream)
+    if (pend_ == Pending::EdgeFirst) H2D_HIP(hipStreamWaitEvent(s_comm_, ev_bnd_, 0));
+    exchange_on(dst, s_comm_);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[5], s_comm_));
+    H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
+  }
+  roctxRangePop();
+  pend_ = Pending::None;
+  pend_pe_ = -1;
+  steps_ += pend_k_;
+  hist_[pend_k_] += 1;
+  cycle_swap();
+}
+
+void Solver::cycle_hist(int64_t out[kMaxTB + 1], bool reset) {
+  for (int i = 0; i <= kMaxTB; ++i) out[i] = hist_[i];
+  if (reset)
+    for (auto& h : hist_) h = 0;
+}
+
+void Solver::launch_serial(int k) {
   roctxRangePushA("heat2d.cycle.serial");
   PhaseEvents* pe = (timing_ && hip_) ? phase_begin(1) : nullptr;
   if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
   cycle_compute(k);
   if (pe) H2D_HIP(hipEventRecord(pe->ev[4], s_compute_));
-  exchange_on(buf_[cur_ ^ 1], s_compute_);
-  if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
-  roctxRangePop();
-  cycle_swap();
+  if (tr_->exchanges()) {
+    if (hip_) H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+    tr_->post(buf_[cur_ ^ 1], L_, hip_ ? ev_bnd_ : nullptr);
+  }
+  pend_ = Pending::Serial;
+  pend_pe_ = pe ? (int64_t)phase_ev_.size() - 1 : -1;
 }
 
 Solver::PhaseEvents* Solver::phase_begin(int kind) {
@@ -422,31 +468,28 @@ void Solver::autotune_split(int k) {
   synchronize();
 }
 
-void Solver::cycle_overlap(int k) {
+void Solver::launch_overlap(int k) {
   void* src = buf_[cur_];
   void* dst = buf_[cur_ ^ 1];
   const kern::SplitPlan& sp = split_plan(k);
   HEAT2D_REQUIRE(sp.valid != 2 || !tr_->exchanges(), "single-launch plan with a halo exchange");
   roctxRangePushA("heat2d.cycle.split");
   PhaseEvents* pe = timing_ ? phase_begin(0) : nullptr;
+  pend_pe_ = pe ? (int64_t)phase_ev_.size() - 1 : -1;
   if (sp.valid == 3) {
     // edge-first: compute stream = [exchange c-1 landed] bands(c) -> interior(c);
-    // comm stream = [bands(c) done] exchange(c), beside the interior.
+    // comm stream (cycle_finish) = [bands(c) done] exchange(c), beside the interior.
     H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
     if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_compute_));
     kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_compute_, cfg_.arith);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[3], s_compute_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+    if (tr_->exchanges()) tr_->post(dst, L_, ev_bnd_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
     kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_bnd_, 0));
-    exchange_on(dst, s_comm_);
-    if (pe) H2D_HIP(hipEventRecord(pe->ev[5], s_comm_));
-    H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
-    roctxRangePop();
-    cycle_swap();
+    pend_ = Pending::EdgeFirst;
     return;
   }
   H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));  // edge part c-1 (record not yet replaced)
@@ -467,11 +510,8 @@ void Solver::cycle_overlap(int k) {
   }
   if (pe) H2D_HIP(hipEventRecord(pe->ev[3], s_comm_));
   H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
-  exchange_on(dst, s_comm_);
-  if (pe) H2D_HIP(hipEventRecord(pe->ev[5], s_comm_));
-  H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
-  roctxRangePop();
-  cycle_swap();
+  if (tr_->exchanges()) tr_->post(dst, L_, ev_bnd_);
+  pend_ = Pending::Concurrent;
 }
 
 void Solver::cycle_copy_swap() {
@@ -494,10 +534,13 @@ void Solver::run_graph_cycles(int64_t npairs) {
     if (graph_exec_) H2D_HIP(hipGraphExecDestroy(graph_exec_));
     hipGraph_t g = nullptr;
     const int saved = cur_;
+    const int64_t saved_steps = steps_, saved_hist = hist_[K];
     if (!ovl) {
       H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
-      cycle_serial(K);
-      cycle_serial(K);
+      for (int c = 0; c < 2; ++c) {
+        cycle_launch(K);
+        cycle_finish();
+      }
     } else {
       // Two-stream capture: fork the comm stream off the capture, record the
       // two overlapped cycles (their event protocol becomes graph edges), join.
@@ -515,8 +558,10 @@ void Solver::run_graph_cycles(int64_t npairs) {
       H2D_HIP(hipEventRecord(ev_comm_, s_comm_));  // edge-first cycles wait on it
       const bool timing = timing_;
       timing_ = false;  // no timing events inside graphs
-      cycle_overlap(K);
-      cycle_overlap(K);
+      for (int c = 0; c < 2; ++c) {
+        cycle_launch(K);
+        cycle_finish();
+      }
       timing_ = timing;
       H2D_HIP(hipEventRecord(join, s_comm_));
       H2D_HIP(hipStreamWaitEvent(s_compute_, join, 0));
@@ -525,6 +570,8 @@ void Solver::run_graph_cycles(int64_t npairs) {
       H2D_HIP(hipEventDestroy(join));
     }
     cur_ = saved;
+    steps_ = saved_steps;
+    hist_[K] = saved_hist;
     if (!g) H2D_HIP(hipStreamEndCapture(s_compute_, &g));
     H2D_HIP(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
     H2D_HIP(hipGraphDestroy(g));
@@ -536,6 +583,7 @@ void Solver::run_graph_cycles(int64_t npairs) {
   }
   // the graph was captured for buffer parity 0 -> 1 -> 0
   for (int64_t i = 0; i < npairs; ++i) H2D_HIP(hipGraphLaunch(graph_exec_, s_compute_));
+  hist_[K] += 2 * npairs;
   if (ovl) {  // eager cycles after the graph order against its end
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
@@ -568,10 +616,9 @@ void Solver::step(int64_t n) {
     // ~3x slower per step than K = 12: 100 steps = 8 x 11 + 12, not 8 x 12 + 4)
     const int64_t ncyc = (left + K - 1) / K;
     const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
-    if (cfg_.overlap && hip_) cycle_overlap(k);
-    else cycle_serial(k);
+    cycle_launch(k);
+    cycle_finish();
     left -= k;
-    steps_ += k;
   }
 }
 
@@ -655,6 +702,13 @@ void Solver::download_region(int64_t r0, int64_t r1, int64_t c0, int64_t c1, voi
 }
 
 void Solver::upload(const void* host, int64_t ld) {
+  upload_owned(host, ld);
+  exchange_post();
+  exchange_now();
+  synchronize();
+}
+
+void Solver::upload_owned(const void* host, int64_t ld) {
   const size_t es = dtype_size(dtype());
   char* dst = static_cast<char*>(buf_[cur_]) + (size_t)L_.origin() * es;
   if (hip_) {
@@ -666,96 +720,59 @@ void Solver::upload(const void* host, int64_t ld) {
       std::memcpy(dst + (size_t)(i * L_.pitch) * es, static_cast<const char*>(host) + (size_t)(i * ld) * es,
                   (size_t)L_.ncols * es);
   }
-  exchange_now();
-  synchronize();
 }
 
 // ------------------------------------------------------------------ loopback
 
-namespace {
-// Member transport: reports its rank within the group; the group moves halos.
-class GroupMemberTransport final : public Transport {
- public:
-  GroupMemberTransport(int r, int n) : r_(r), n_(n) {}
-  int rank() const override { return r_; }
-  int size() const override { return n_; }
-  void exchange(void*, const SlabLayout&, DType, int64_t, hipStream_t, bool) override {}
-  void allreduce(double*, int, int) override {}
-  void barrier() override {}
-  std::string name() const override { return "loopback"; }
-
- private:
-  int r_, n_;
-};
-}  // namespace
-
-LoopbackGroup::LoopbackGroup(const SolverConfig& cfg, int nranks) : cfg_(cfg) {
+LoopbackGroup::LoopbackGroup(const SolverConfig& cfg, int nranks) {
   HEAT2D_REQUIRE(nranks >= 1, "nranks >= 1");
-  const bool hip = cfg.backend == (int32_t)Backend::Hip;
-  if (hip) {
-    if (cfg.device >= 0) H2D_HIP(hipSetDevice(cfg.device));
-    H2D_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  }
-  for (int i = 0; i < nranks; ++i)
-    members_.emplace_back(new Solver(cfg, std::make_shared<GroupMemberTransport>(i, nranks), stream_));
+  // every member owns its streams, events, split plans and autotuner, exactly
+  // like one rank of a multi-GPU run; only the transport differs
+  auto trs = make_loopback_transports(nranks);
+  for (int i = 0; i < nranks; ++i) members_.emplace_back(new Solver(cfg, trs[(size_t)i]));
 }
 
 LoopbackGroup::~LoopbackGroup() {
-  members_.clear();
-  if (stream_) {
-    (void)hipStreamSynchronize(stream_);
-    (void)hipStreamDestroy(stream_);
+  try {
+    synchronize();
+  } catch (...) {
   }
+  members_.clear();
 }
 
 void LoopbackGroup::init(const kern::IcParams& ic, const double* xg, const double* yg) {
   for (auto& m : members_) m->init(ic, xg, yg);
 }
 
-void LoopbackGroup::exchange_all() {
-  const int P = nranks();
-  if (P == 1) return;
-  const bool hip = cfg_.backend == (int32_t)Backend::Hip;
-  for (int i = 0; i < P; ++i) {
-    Solver& me = *members_[i];
-    const SlabLayout& L = me.layout();
-    const int64_t B = me.band();
-    const size_t es = dtype_size(me.dtype());
-    const size_t bytes = (size_t)(B * L.pitch) * es;
-    char* mine = static_cast<char*>(me.field());
-    auto rowp = [&](char* base, const SlabLayout& LL, int64_t r) { return base + (size_t)((r + LL.halo) * LL.pitch) * es; };
-    if (i > 0) {
-      Solver& lo = *members_[i - 1];
-      const SlabLayout& LL = lo.layout();
-      char* src = rowp(static_cast<char*>(lo.field()), LL, LL.nrows - B);
-      char* dst = rowp(mine, L, -B);
-      if (hip) H2D_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream_));
-      else std::memcpy(dst, src, bytes);
-    }
-    if (i < P - 1) {
-      Solver& hi = *members_[i + 1];
-      const SlabLayout& LH = hi.layout();
-      char* src = rowp(static_cast<char*>(hi.field()), LH, 0);
-      char* dst = rowp(mine, L, L.nrows);
-      if (hip) H2D_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream_));
-      else std::memcpy(dst, src, bytes);
-    }
+// step()'s loop (balanced depths; no graphs: a capture cannot span the
+// members' streams) with the two phases of every cycle interleaved across
+// members: all launches (each posts its new field and band event), then all
+// exchanges — the order a multi-process run gets from RCCL's rendezvous.
+void LoopbackGroup::step(int64_t n) {
+  const int K = members_[0]->config().tb;
+  int64_t left = n;
+  while (left > 0) {
+    const int64_t ncyc = (left + K - 1) / K;
+    const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
+    for (auto& m : members_) m->cycle_launch(k);
+    for (auto& m : members_) m->cycle_finish();
+    left -= k;
   }
 }
 
-void LoopbackGroup::step(int64_t n) {
-  const int K = members_[0]->config().tb;
-  while (n > 0) {
-    const int k = (int)std::min<int64_t>(K, n);
-    for (auto& m : members_) m->cycle_compute(k);
-    for (auto& m : members_) m->cycle_swap();
-    exchange_all();
-    n -= k;
+void LoopbackGroup::upload(const void* host, int64_t ld) {
+  const size_t es = dtype_size(members_[0]->dtype());
+  for (auto& m : members_) {
+    m->synchronize();
+    m->upload_owned(static_cast<const char*>(host) + (size_t)(m->layout().row0 * ld) * es, ld);
   }
+  for (auto& m : members_) m->exchange_post();
+  for (auto& m : members_) m->exchange_now();
+  synchronize();
 }
 
 void LoopbackGroup::synchronize() {
-  if (stream_) H2D_HIP(hipStreamSynchronize(stream_));
+  for (auto& m : members_) m->synchronize();
 }
 
 void LoopbackGroup::download(void* host, int64_t ld) {

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -86,26 +87,21 @@ class RcclTransport final : public Transport {
     if ((size_ == 1 && !loop_) || k <= 0) return;
     const size_t es = dtype_size(dt);
     char* base = static_cast<char*>(field);
-    auto row_ptr = [&](int64_t i) { return base + (size_t)((i + L.halo) * L.pitch) * es; };
-    const size_t count = (size_t)(k * L.pitch);  // whole padded rows: contiguous, zero-copy
+    const size_t count = halo_msg_bytes(L, k, es) / es;  // whole padded rows: contiguous, zero-copy
     const ncclDataType_t t = dt == DType::F32 ? ncclFloat32 : ncclFloat64;
-    if (loop_) {  // periodic self-exchange (rehearsal): same message sizes and kernels as 2 peers
-      H2D_NCCL(ncclGroupStart());
-      H2D_NCCL(ncclSend(row_ptr(0), count, t, 0, comm_, stream));
-      H2D_NCCL(ncclRecv(row_ptr(L.nrows), count, t, 0, comm_, stream));
-      H2D_NCCL(ncclSend(row_ptr(L.nrows - k), count, t, 0, comm_, stream));
-      H2D_NCCL(ncclRecv(row_ptr(-k), count, t, 0, comm_, stream));
-      H2D_NCCL(ncclGroupEnd());
-      return;
+    HaloMsg msg[2];
+    int nmsg = 0;
+    if (loop_) {  // periodic self-exchange (rehearsal): the two messages of an interior rank, both to itself
+      nmsg = halo_msgs(1, 3, L, k, msg);
+      for (int i = 0; i < nmsg; ++i) msg[i].peer = 0;
+      std::swap(msg[0].recv_row, msg[1].recv_row);  // the wrap: row 0 lands above the top, the top below row 0
+    } else {
+      nmsg = halo_msgs(rank_, size_, L, k, msg);
     }
     H2D_NCCL(ncclGroupStart());
-    if (rank_ > 0) {
-      H2D_NCCL(ncclSend(row_ptr(0), count, t, rank_ - 1, comm_, stream));
-      H2D_NCCL(ncclRecv(row_ptr(-k), count, t, rank_ - 1, comm_, stream));
-    }
-    if (rank_ < size_ - 1) {
-      H2D_NCCL(ncclSend(row_ptr(L.nrows - k), count, t, rank_ + 1, comm_, stream));
-      H2D_NCCL(ncclRecv(row_ptr(L.nrows), count, t, rank_ + 1, comm_, stream));
+    for (int i = 0; i < nmsg; ++i) {
+      H2D_NCCL(ncclSend(base + halo_row_bytes(L, msg[i].send_row, es), count, t, msg[i].peer, comm_, stream));
+      H2D_NCCL(ncclRecv(base + halo_row_bytes(L, msg[i].recv_row, es), count, t, msg[i].peer, comm_, stream));
     }
     H2D_NCCL(ncclGroupEnd());
   }
@@ -197,9 +193,109 @@ class CallbackTransport final : public Transport {
   std::vector<char> stage_;
 };
 
+// ------------------------------------------------------------------ loopback
+// P ranks of one process, halos copied on the RECEIVING rank's exchange
+// stream (a pull): the messages are halo_msgs' — the ones RCCL moves — and the
+// cross-rank ordering RCCL's rendezvous provides is rebuilt from events:
+//   * a pull of cycle c waits for the peer's band event of cycle c (its post),
+//   * and for the peer's own pulls of cycle c-1 (done[(c-1) & 1]), which read
+//     this rank's band rows of the buffer this rank's bands of cycle c+1 will
+//     overwrite — those bands sit behind this exchange in stream order (on the
+//     comm stream, or, edge-first, behind ev_comm on the compute stream).
+// Both hold because LoopbackGroup posts every rank's cycle c before it
+// enqueues any rank's exchange of cycle c.
+struct LoopbackHub {
+  struct Slot {
+    void* field = nullptr;  // posted field of the current cycle
+    SlabLayout L{};
+    hipEvent_t ready = nullptr;  // the poster's band event (not owned)
+    hipEvent_t done[2] = {nullptr, nullptr};  // owned: pulls of cycle parity p done
+    int64_t posted = 0, pulled = 0;  // cycles posted / exchanged
+  };
+  explicit LoopbackHub(int n) : slot((size_t)n) {}
+  ~LoopbackHub() {
+    for (auto& s : slot)
+      for (auto& e : s.done)
+        if (e) (void)hipEventDestroy(e);
+  }
+  std::vector<Slot> slot;
+};
+
+class LoopbackTransport final : public Transport {
+ public:
+  LoopbackTransport(std::shared_ptr<LoopbackHub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int size() const override { return (int)hub_->slot.size(); }
+  std::string name() const override { return "loopback"; }
+  // the members share one host thread: collectives over them are the group's job
+  void allreduce(double*, int, int) override {}
+  void barrier() override {}
+
+  void post(void* field, const SlabLayout& L, hipEvent_t ready) override {
+    auto& me = hub_->slot[(size_t)rank_];
+    HEAT2D_REQUIRE(me.posted == me.pulled, "loopback: a cycle was posted twice without an exchange");
+    me.field = field;
+    me.L = L;
+    me.ready = ready;
+    ++me.posted;
+  }
+
+  void exchange(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
+                bool on_device) override {
+    if (size() == 1 || k <= 0) return;
+    auto& me = hub_->slot[(size_t)rank_];
+    HEAT2D_REQUIRE(me.posted == me.pulled + 1 && me.field == field,
+                   "loopback: exchange of a field that was not posted this cycle (drive members through LoopbackGroup)");
+    const int64_t c = me.pulled;
+    const size_t es = dtype_size(dt);
+    const size_t bytes = halo_msg_bytes(L, k, es);
+    HaloMsg msg[2];
+    const int nmsg = halo_msgs(rank_, size(), L, k, msg);
+    if (on_device) {
+      for (auto& e : me.done)
+        if (!e) H2D_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    for (int i = 0; i < nmsg; ++i) {
+      const auto& peer = hub_->slot[(size_t)msg[i].peer];
+      HEAT2D_REQUIRE(peer.posted == c + 1, "loopback: peer has not posted this cycle");
+      HEAT2D_REQUIRE(peer.L.pitch == L.pitch, "loopback: slabs of different pitch");
+      // the peer's message toward this rank: its send rows
+      HaloMsg pm[2];
+      const int np = halo_msgs(msg[i].peer, size(), peer.L, k, pm);
+      int64_t send_row = -1;
+      for (int j = 0; j < np; ++j)
+        if (pm[j].peer == rank_) send_row = pm[j].send_row;
+      HEAT2D_REQUIRE(send_row >= 0, "loopback: peer does not send to this rank");
+      const char* src = static_cast<const char*>(peer.field) + halo_row_bytes(peer.L, send_row, es);
+      char* dst = static_cast<char*>(field) + halo_row_bytes(L, msg[i].recv_row, es);
+      if (on_device) {
+        H2D_HIP(hipStreamWaitEvent(stream, peer.ready, 0));
+        if (c > 0 && peer.done[(c - 1) & 1]) H2D_HIP(hipStreamWaitEvent(stream, peer.done[(c - 1) & 1], 0));
+        H2D_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream));
+      } else {
+        std::memcpy(dst, src, bytes);
+      }
+    }
+    if (on_device) H2D_HIP(hipEventRecord(me.done[c & 1], stream));
+    ++me.pulled;
+  }
+
+ private:
+  std::shared_ptr<LoopbackHub> hub_;
+  int rank_;
+};
+
 }  // namespace
 
 std::shared_ptr<Transport> make_self_transport() { return std::make_shared<SelfTransport>(); }
+
+std::vector<std::shared_ptr<Transport>> make_loopback_transports(int nranks) {
+  HEAT2D_REQUIRE(nranks >= 1, "nranks >= 1");
+  auto hub = std::make_shared<LoopbackHub>(nranks);
+  std::vector<std::shared_ptr<Transport>> v;
+  for (int i = 0; i < nranks; ++i) v.push_back(std::make_shared<LoopbackTransport>(hub, i));
+  return v;
+}
 
 std::shared_ptr<Transport> make_rccl_transport(const void* uid, int rank, int size, int device) {
   return std::make_shared<RcclTransport>(uid, rank, size, device);

@@ -40,6 +40,24 @@ def resolve_backend(backend: str) -> str:
     return backend
 
 
+def _plan(h, k: int) -> dict:
+    p, ms = N.SplitPlan(), C.c_float()
+    N.call("heat2d_solver_plan", h, int(k), C.byref(p), C.byref(ms))
+    return {"k": p.k, "ring": p.ring, "valid": p.valid,
+            "order": {1: "concurrent", 2: "single", 3: "edge-first"}.get(p.valid, "serial"),
+            "main_bands": p.main.nb, "main_items": p.main_items, "main_waves": p.main_waves,
+            "edge_items": p.edge_items, "edge_waves": p.edge_waves, "tuned_ms": ms.value,
+            "main_rect": [p.main.r0, p.main.r1, p.main.s0, p.main.s1, p.main.nb],
+            "edge_rects": [[e.r0, e.r1, e.s0, e.s1, e.nb] for e in list(p.edge)[:p.nedge]]}
+
+
+def _cycle_hist(h, reset: bool) -> dict:
+    n = N.max_tb() + 1
+    out = (C.c_int64 * n)()
+    N.call("heat2d_solver_cycle_hist", h, out, n, int(bool(reset)))
+    return {k: int(out[k]) for k in range(n) if out[k]}
+
+
 class HeatSolver:
     """Distributed FTCS solver for one rank.
 
@@ -170,12 +188,11 @@ class HeatSolver:
 
     def plan(self, k: Optional[int] = None) -> dict:
         """The split plan (MAIN / EDGE launches) used for depth k (default: tb)."""
-        k = self.tb if k is None else k
-        p, ms = N.SplitPlan(), C.c_float()
-        N.call("heat2d_solver_plan", self._h, k, C.byref(p), C.byref(ms))
-        return {"k": p.k, "ring": p.ring, "valid": p.valid, "main_bands": p.main.nb, "main_items": p.main_items,
-                "main_waves": p.main_waves, "edge_items": p.edge_items, "edge_waves": p.edge_waves,
-                "tuned_ms": ms.value}
+        return _plan(self._h, self.tb if k is None else k)
+
+    def cycle_hist(self, reset: bool = False) -> dict:
+        """{depth: cycles} that step() launched since the last reset (graph replays count 2 each)."""
+        return _cycle_hist(self._h, reset)
 
     @property
     def plans_made(self) -> int:
@@ -264,14 +281,20 @@ class HeatSolver:
 
 
 class LoopbackGroup:
-    """P slabs of one domain on a single device (or host), halos moved by copies.
+    """P slabs of one domain on a single device (or host), exchanging halos
+    through the native loopback transport.
 
-    The decomposition / band-split / exchange schedule of the distributed solver
-    proven without a cluster: results must be bitwise identical to P = 1.
+    Every member is a full native solver with its own compute / comm streams,
+    split plans and autotuner — one rank of a multi-GPU run — and the halo
+    messages are the ones the RCCL transport sends (whole padded rows, shared
+    ``halo_msgs`` plan), copied device-to-device and ordered by events. So the
+    overlapped multi-rank schedule (both split orders, balanced depths) runs
+    with real exchanges on one GPU; results must be bitwise identical to P = 1.
     """
 
     def __init__(self, problem: Problem, nranks: int, *, dtype: str = "fp64", backend: str = "auto",
-                 tb: int = 0, tile_rows: int = 0, device: Optional[int] = None, arith: str = "auto"):
+                 tb: int = 0, tile_rows: int = 0, device: Optional[int] = None, arith: str = "auto",
+                 overlap: bool = True, autotune: int = -1, comm_cus: int = 0):
         self.problem = problem
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]
@@ -285,9 +308,13 @@ class LoopbackGroup:
         cfg.backend = N.BACKEND_HIP if self.backend == "hip" else N.BACKEND_CPU
         cfg.r = problem.r
         cfg.tb = tb
+        cfg.overlap = int(overlap)
+        cfg.autotune = autotune
+        cfg.comm_cus = comm_cus
         cfg.device = -1 if device is None else int(device)
         cfg.tile_rows = tile_rows
         cfg.arith = N.ARITH[arith]
+        self.nranks = nranks
         h = C.c_void_p()
         N.call("heat2d_group_create", C.byref(cfg), nranks, C.byref(h))
         self._h = h
@@ -299,11 +326,31 @@ class LoopbackGroup:
     def step(self, n: int) -> None:
         N.call("heat2d_group_step", self._h, int(n))
 
+    def upload(self, arr: np.ndarray) -> None:
+        """Whole owned grid -> the members' slabs, then a loopback halo exchange."""
+        m = self.problem.n_owned
+        a = np.ascontiguousarray(arr, dtype=NP_DTYPES[self.dtype])
+        if a.shape != (m, m):
+            raise ValueError(f"expected {(m, m)}, got {a.shape}")
+        N.call("heat2d_group_upload", self._h, a.ctypes.data_as(C.c_void_p), m)
+
     def download(self) -> np.ndarray:
         m = self.problem.n_owned
         out = np.empty((m, m), dtype=NP_DTYPES[self.dtype])
         N.call("heat2d_group_download", self._h, out.ctypes.data_as(C.c_void_p), m)
         return out
+
+    def _member(self, i: int):
+        h = C.c_void_p()
+        N.call("heat2d_group_member", self._h, int(i), C.byref(h))
+        return h
+
+    def plan(self, i: int, k: int) -> dict:
+        """Member i's split plan for depth k (as HeatSolver.plan)."""
+        return _plan(self._member(i), k)
+
+    def cycle_hist(self, i: int, reset: bool = False) -> dict:
+        return _cycle_hist(self._member(i), reset)
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -15,6 +15,38 @@ def model_bytes_per_point_step(dtype_bytes: int, tb: int, copy_swap: bool = Fals
     return 4.0 * dtype_bytes if copy_swap else 2.0 * dtype_bytes / max(1, tb)
 
 
+def strip_geometry(dtype_bytes: int, k: int) -> tuple:
+    """(W, U): columns a wave loads / stores per strip of the temporal-blocked
+    kernel at depth k (tb_impl.hpp TbShape: 16 B per lane, halo of whole lanes)."""
+    v = 16 // dtype_bytes
+    ka = (k + v - 1) // v * v
+    w = 64 * v
+    return w, w - 2 * ka
+
+
+def plan_hbm_bytes(plan: dict, dtype_bytes: int, nrows: int, ncols: int) -> dict:
+    """DRAM traffic of ONE cycle of a split plan, from its geometry alone: every
+    work item (one row band of one strip) loads its band rows plus 2k priming
+    rows at the strip's full width W (the k-column halos on both sides
+    included) and stores its useful U columns once. This counts no cache reuse
+    between neighbouring strips / bands (rocprof measured 1.13-1.19x the field
+    read per pass vs this model's W/U, profiles/hbm_model_check.md), so it is
+    an upper bound on the reads."""
+    k = int(plan["k"])
+    w, u = strip_geometry(dtype_bytes, k)
+    rects = [plan["main_rect"]] + list(plan.get("edge_rects", [])) if plan.get("valid", 0) else []
+    if not rects:  # unsplit launch over the whole slab (one band per strip)
+        nstrips = (ncols + u - 1) // u
+        rects = [[0, nrows, 0, nstrips, 1]]
+    rd = 0.0
+    for r0, r1, s0, s1, nb in rects:
+        if r1 <= r0 or s1 <= s0:
+            continue
+        rd += float((r1 - r0) + 2 * k * nb) * (s1 - s0) * w * dtype_bytes
+    wr = float(nrows) * ncols * dtype_bytes
+    return {"read": rd, "write": wr, "total": rd + wr}
+
+
 def record(n_owned: int, steps: int, seconds: float, nranks: int, dtype: str, tb: int, backend: str,
            copy_swap: bool = False, extra: Optional[dict] = None) -> dict:
     es = 8 if dtype == "fp64" else 4

@@ -51,3 +51,30 @@ def test_bench_single_process_cpu():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and d["field_stats"]["max"] <= 2.0
+
+
+def test_bench_launches_ranks_itself():
+    """`python bench.py --gpus N` without torchrun starts N rank processes
+    (never silently one): the driver's N-GPU command works either way."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--backend", "cpu", "--gpus", "4", "--grid",
+                        "100", "--steps", "8", "--warmup", "2", "--tb", "4"], capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "slab4"
+    # the timed region's cycles are reported, and they add up to the timed steps
+    assert sum(int(k) * c for k, c in d["config"]["cycles"].items()) == 8
+
+
+def test_bench_refuses_missing_gpus():
+    """More GPUs requested than visible: a non-zero exit, not a 1-GPU number."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "64", "--steps", "4"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode != 0 and p.stdout.strip() == ""
+    assert "GPU(s) visible" in p.stderr

@@ -210,19 +210,49 @@ def test_phase_timers(gpu, native):
 
 
 @pytest.mark.parametrize("order", ["edge-first", "concurrent"])
-@pytest.mark.parametrize("P,tb,dtype", [(2, 8, "fp64"), (4, 12, "fp64"), (3, 16, "fp32")])
-def test_split_orders_with_exchange_bitwise(gpu, native, order, P, tb, dtype, monkeypatch):
-    """Both orderings of the split cycle with a real halo exchange between
-    slabs (device-copy loopback): edge-first (valid = 3: bands, then interior,
-    exchange beside the interior) and concurrent (valid = 1): bitwise == golden."""
+@pytest.mark.parametrize("P,tb,dtype,n", [(2, 8, "fp64", 1100), (4, 12, "fp64", 1100), (3, 16, "fp32", 1300),
+                                          (5, 14, "fp64", 900)])
+def test_split_orders_with_exchange_bitwise(gpu, native, order, P, tb, dtype, n, monkeypatch):
+    """The overlapped multi-rank schedule with REAL halo exchanges on one GPU:
+    P member solvers, each with its own compute / comm streams and autotuned
+    split plans, exchange band rows through the loopback transport (RCCL's
+    messages, copied device-to-device, ordered by events). Both split orders —
+    edge-first (bands, then interior, exchange beside the interior) and
+    concurrent (interior beside bands + exchange) — on non-dyadic data must be
+    bitwise equal to the golden on ALL rows, and every member must really have
+    run the requested order."""
     monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
-    p = prob(700, 53, "ghost", "uniform")
+    steps = 3 * tb + 5  # full cycles and a balanced remainder
+    p = prob(n, steps, "ghost", "sine")
     npdt = np.float64 if dtype == "fp64" else np.float32
-    g = LoopbackGroup(p, P, dtype=dtype, backend="hip", tb=tb, device=0)
+    g = LoopbackGroup(p, P, dtype=dtype, backend="hip", tb=tb, device=0, autotune=1)
+    g.upload(R.owned(R.initial_field(p, npdt)))
+    g.step(p.ntime)
+    got = g.download()
+    want = 3 if order == "edge-first" else 1
+    for i in range(P):
+        hist = g.cycle_hist(i)
+        assert sum(k * c for k, c in hist.items()) == steps
+        for k in hist:
+            pl = g.plan(i, k)
+            assert pl["valid"] == want and pl["tuned_ms"] > 0, (i, k, pl)
+    g.close()
+    ref = R.owned(R.ftcs(p, dtype=npdt))
+    assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_loopback_serial_schedule_bitwise(gpu, native, P):
+    """overlap=False: one launch per cycle on the compute stream, exchange
+    behind it on the same stream (the two-phase post / pull protocol still
+    orders the ranks)."""
+    p = prob(600, 41, "ghost", "sine")
+    g = LoopbackGroup(p, P, dtype="fp64", backend="hip", tb=9, device=0, overlap=False)
+    g.upload(R.owned(R.initial_field(p)))
     g.step(p.ntime)
     got = g.download()
     g.close()
-    assert np.array_equal(got, R.owned(R.ftcs(p, dtype=npdt)))
+    assert np.array_equal(got, R.owned(R.ftcs(p)))
 
 
 @pytest.mark.parametrize("n,tb,graph", [(1000, 16, True), (1000, 16, False), (100, 12, False), (50, 12, True),
