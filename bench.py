@@ -125,7 +125,8 @@ def main():
                          "every rank keeps ~n^2 points (e.g. --dtype fp32 --n 173056: the full-HBM 240 GB per GPU)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--tb", type=int, default=0,
-                    help="time steps fused per HBM pass (0: measured best, fp64 14 / fp32 16; profiles/README.md)")
+                    help="largest time-step depth fused per HBM pass (0: every depth the kernels have, fp64 24 / "
+                         "fp32 16; prepare() picks the cycle schedule of the timed steps by measurement)")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma"],
                     help="fma: contracted update (one op fewer per point); exact: every op rounded; auto: fma when "
@@ -144,8 +145,6 @@ def main():
                     help="1 GPU only: run the multi-GPU schedule (bands + RCCL self-exchange beside a CU-masked "
                          "interior) to measure its per-rank cost; not the headline (periodic halo)")
     args = ap.parse_args()
-    if args.tb <= 0:
-        args.tb = 14 if args.dtype == "fp64" else 16
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_launch_ranks(args.gpus, args.backend))
     out_fd = _claim_stdout()
@@ -199,9 +198,14 @@ def main():
             dist.all_reduce(tr_vals)
         sync()
 
-    s.prepare(args.steps)  # plan / autotune every depth the timed run uses (outside the timed region)
     s.step(args.warmup)
     s.synchronize()
+    # plan / autotune every depth the timed run uses, pick its cycle schedule by
+    # measurement, and end on non-mutating trial cycles of that schedule (GPU
+    # clocks as in a long run) — outside the timed region, after the warmup
+    tp = time.perf_counter()
+    s.prepare(args.steps)
+    prepare_s = time.perf_counter() - tp
     s.cycle_hist(reset=True)
     if args.phase_timers:
         s.set_timing(True)
@@ -266,6 +270,8 @@ def main():
                 "parallelism": f"slab{world}" + ("-rehearsal" if args.rehearse_comm and world == 1 else ""),
                 "tb_max": tb,
                 "cycles": {str(k): c for k, c in sorted(hist.items())},
+                "schedule": "measured" if s.schedule(args.steps) else "balanced",
+                "prepare_s": round(prepare_s, 2),
                 "arith": ("fma" if N_arith(prob.r, args.arith) else "exact") + (" (auto)" if args.arith == "auto" else ""),
                 "overlap": not args.no_overlap,
                 "launch_plans": plans or None,

@@ -340,6 +340,15 @@ int heat2d_solver_cycle_hist(void* s, int64_t* out, int n, int reset) {
   });
 }
 
+int heat2d_solver_schedule(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len) {
+  return guarded([&] {
+    const std::vector<int>* v = static_cast<Solver*>(s)->schedule(n);
+    *len = v ? (int64_t)v->size() : -1;
+    if (v && out)
+      for (int64_t i = 0; i < std::min<int64_t>(cap, (int64_t)v->size()); ++i) out[i] = (*v)[(size_t)i];
+  });
+}
+
 int heat2d_group_download(void* g, void* host, int64_t ld) {
   return guarded([&] {
     auto* gr = static_cast<LoopbackGroup*>(g);

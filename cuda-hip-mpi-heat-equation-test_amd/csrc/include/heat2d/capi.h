@@ -146,6 +146,9 @@ int heat2d_group_upload(void* g, const void* host, int64_t ld);
 int heat2d_group_member(void* g, int i, void** solver);
 /* cycles step() launched since the last reset, by depth: out[k], k = 0..heat2d_max_tb() (n >= max_tb + 1) */
 int heat2d_solver_cycle_hist(void* s, int64_t* out, int n, int reset);
+/* the measured cycle schedule prepare(n) chose for step(n): depths in out[0..min(cap, len)); len = -1 if none
+   (step(n) then runs balanced cycles of the preferred depth) */
+int heat2d_solver_schedule(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len);
 
 /* I/O (io.cpp). */
 int heat2d_write_xyz(const char* path, int dtype, const void* host, int64_t nrows, int64_t ncols,

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <functional>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -157,8 +158,19 @@ class Solver {
   // Advance n time steps (asynchronous on the HIP backend).
   void step(int64_t n);
   // Plan (and autotune, if enabled) every cycle depth a step(n) will use, so
-  // that no planning happens inside a timed step(n).
+  // that no planning happens inside a timed step(n). On slabs whose split
+  // plans are autotuned it also picks step(n)'s cycle schedule by
+  // measurement: the number of cycles c (depths balanced within c) with the
+  // smallest sum of measured cycle times — the max over ranks, so every rank
+  // runs the same schedule. E.g. 20 steps at 32768^2 fp64: one depth-20 pass
+  // (6.4 ms) instead of two depth-10 passes (7.6 ms).
   void prepare(int64_t n);
+  // The measured schedule step(n) will run (nullptr: balanced cycles of
+  // pref_depth()).
+  const std::vector<int>* schedule(int64_t n) const;
+  // depth of the balanced cycles when no measured schedule applies (the
+  // steady-state best: fp64 14, fp32 16 unless --tb is given)
+  int pref_depth() const { return k_pref_; }
   void synchronize();
   // Global statistics over all ranks: sum, sum_sq, min, max, and residual
   // terms vs the previous buffer (valid right after a step()).
@@ -217,6 +229,10 @@ class Solver {
   void launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k);
   void exchange_on(void* field, hipStream_t s);
   void run_graph_cycles(int64_t npairs);
+  bool measured_schedules() const;
+  void trial_cycle(const kern::SplitPlan& c);
+  float depth_ms(int k);
+  std::vector<int> choose_schedule(int64_t n);
 
   SolverConfig cfg_;
   std::shared_ptr<Transport> tr_;
@@ -245,6 +261,9 @@ class Solver {
   int pend_k_ = 0;
   int64_t pend_pe_ = -1;  // index into phase_ev_ (timing) or -1
   int64_t hist_[kMaxTB + 1] = {};
+  int k_pref_ = 1;
+  std::map<int64_t, std::vector<int>> sched_;  // measured schedules by step count
+  float depth_ms_[kMaxTB + 1] = {};            // cycle ms per depth, max over ranks (schedule search)
   int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all
   kern::SplitPlan split_[kMaxTB + 1] = {};  // per temporal depth (k == 0: not planned yet)
   float tuned_ms_[kMaxTB + 1] = {};           // autotuned cycle time (ms), 0 if not tuned

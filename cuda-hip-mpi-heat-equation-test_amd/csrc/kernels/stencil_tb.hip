@@ -120,10 +120,10 @@ void dispatch_t(int ring, bool main, int arith, int k, unsigned nblocks, const T
   else dispatch_ar<T, 0>(ring, main, k, nblocks, s, d, a, r, st);
 }
 
-void check_layout(const SlabLayout& L, int k) {
-  HEAT2D_REQUIRE(k >= 1 && k <= kMaxTB, "k must be in [1, kMaxTB]");
+void check_layout(DType dt, const SlabLayout& L, int k) {
+  HEAT2D_REQUIRE(k >= 1 && k <= max_tb(dt), "k must be in [1, max_tb(dtype)] (fp64 24, fp32 16)");
   HEAT2D_REQUIRE(k <= L.halo, "temporal depth exceeds the halo depth");
-  HEAT2D_REQUIRE(L.cpad >= 16, "column padding too small for the strip halo");
+  HEAT2D_REQUIRE(L.cpad >= (k + 1) / 2 * 2 + 4, "column padding too small for the strip halo");
   // the march keeps row indices in 32 bits (scalar compares)
   HEAT2D_REQUIRE(L.nrows_global + 2 * L.halo < (int64_t(1) << 31) && L.row0 < (int64_t(1) << 31),
                  "row count exceeds the 32-bit row index of the stencil kernel");
@@ -195,7 +195,7 @@ void launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int
 
 TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k, int64_t tile_rows,
                int cus, int arith) {
-  check_layout(L, k);
+  check_layout(dt, L, k);
   HEAT2D_REQUIRE(row_begin >= 0 && row_end <= L.nrows && row_begin < row_end, "bad row range");
   TbPlan p{};
   p.k = k;
@@ -232,7 +232,7 @@ void launch_tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_
 
 void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t rb0, int64_t re0, int64_t rb1,
                 int64_t re1, int k, double r, hipStream_t stream, int64_t tile_rows, int cus, int arith) {
-  check_layout(L, k);
+  check_layout(dt, L, k);
   const int64_t n0 = std::max<int64_t>(0, re0 - rb0), n1 = std::max<int64_t>(0, re1 - rb1);
   if (n0 + n1 == 0) return;
   // plan over the concatenated rows, then give each range its share of bands
@@ -249,7 +249,7 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 
 SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus, int spare_waves,
                      int ring_override, int64_t main_bands, int arith) {
-  check_layout(L, k);
+  check_layout(dt, L, k);
   SplitPlan p{};
   p.k = k;
   p.ring = (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k);
@@ -282,7 +282,7 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
 }
 
 SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_override, int64_t bands, int arith) {
-  check_layout(L, k);
+  check_layout(dt, L, k);
   SplitPlan p{};
   p.k = k;
   p.ring = (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k);

@@ -1,11 +1,11 @@
 // Instantiation unit (contracted arithmetic, AR = 1): temporal-blocked stencil, double, 16 B per lane, ring of
-// 6 level-0 rows, interior-only (MAIN) kernel, K = 1..16 (see tb_impl.hpp).
+// 6 level-0 rows, interior-only (MAIN) kernel, K = 1..24 (see tb_impl.hpp).
 #include "tb_impl.hpp"
 
 namespace heat2d {
 namespace kern {
 namespace tbimpl {
-H2D_TB_UNIT(double, 6, true, 1)
+H2D_TB_UNIT_F64(double, 6, true, 1)
 }  // namespace tbimpl
 }  // namespace kern
 }  // namespace heat2d

@@ -674,12 +674,18 @@ int occupancy_blocks(int k);
   M(T, RING, MAIN, AR, 5) M(T, RING, MAIN, AR, 6) M(T, RING, MAIN, AR, 7) M(T, RING, MAIN, AR, 8)       \
   M(T, RING, MAIN, AR, 9) M(T, RING, MAIN, AR, 10) M(T, RING, MAIN, AR, 11) M(T, RING, MAIN, AR, 12)    \
   M(T, RING, MAIN, AR, 13) M(T, RING, MAIN, AR, 14) M(T, RING, MAIN, AR, 15) M(T, RING, MAIN, AR, 16)
-#define H2D_TB_UNIT(T, RING, MAIN, AR)                                                                  \
+// fp64 only: K = 17..24 (kMaxTB; fp32 stops at kMaxTBF32 = 16, common.hpp)
+#define H2D_TB_CASES_DEEP(M, T, RING, MAIN, AR)                                                        \
+  M(T, RING, MAIN, AR, 17) M(T, RING, MAIN, AR, 18) M(T, RING, MAIN, AR, 19) M(T, RING, MAIN, AR, 20)   \
+  M(T, RING, MAIN, AR, 21) M(T, RING, MAIN, AR, 22) M(T, RING, MAIN, AR, 23) M(T, RING, MAIN, AR, 24)
+#define H2D_NO_CASES(M, T, RING, MAIN, AR)
+#define H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, DEEP)                                                       \
   template <>                                                                                           \
   void dispatch<T, RING, MAIN, AR>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, \
                                    hipStream_t s) {                                                     \
     switch (k) {                                                                                        \
       H2D_TB_CASES(H2D_TB_CASE, T, RING, MAIN, AR)                                                      \
+      DEEP(H2D_TB_CASE, T, RING, MAIN, AR)                                                              \
       default:                                                                                          \
         break;                                                                                          \
     }                                                                                                   \
@@ -689,11 +695,14 @@ int occupancy_blocks(int k);
   int occupancy_blocks<T, RING, MAIN, AR>(int k) {                                                      \
     switch (k) {                                                                                        \
       H2D_TB_CASES(H2D_OCC_CASE, T, RING, MAIN, AR)                                                     \
+      DEEP(H2D_OCC_CASE, T, RING, MAIN, AR)                                                             \
       default:                                                                                          \
         break;                                                                                          \
     }                                                                                                   \
     return 1;                                                                                           \
   }
+#define H2D_TB_UNIT(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_NO_CASES)
+#define H2D_TB_UNIT_F64(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_DEEP)
 
 }  // namespace tbimpl
 }  // namespace kern

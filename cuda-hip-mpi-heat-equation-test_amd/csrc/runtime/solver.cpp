@@ -68,8 +68,13 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
   // MI355X, profiles/README.md §11: fp64 14 — equal to 12 on a whole 32768²
   // grid, 3-6 % faster on the slabs of 2/4/8-rank runs — fp32 16 with the
   // packed fp32 march); 8 on the CPU twin.
-  const int tb_auto = hip_ ? (cfg_.dtype == 1 ? 14 : 16) : 8;
-  int K = std::max(1, std::min<int>(cfg_.tb <= 0 ? tb_auto : cfg_.tb, kMaxTB));
+  // tb <= 0 on the HIP engine: depths up to max_tb (fp64 24, fp32 16) are
+  // available to the measured schedules of prepare(); the balanced fallback
+  // uses the steady-state best.
+  const bool tb_given = cfg_.tb > 0;
+  const int tb_pref = hip_ ? (cfg_.dtype == 1 ? 14 : 16) : 8;
+  const int tb_auto = hip_ ? max_tb(dtype()) : 8;
+  int K = std::max(1, std::min<int>(tb_given ? cfg_.tb : tb_auto, max_tb(dtype())));
   if (cfg_.copy_swap) K = 1;
   HEAT2D_REQUIRE(cfg_.engine == 0 || cfg_.engine == 1, "engine must be 0 (temporal-blocked) or 1 (jit)");
   if (cfg_.arith < 0) {
@@ -89,6 +94,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
   K = (int)std::min<int64_t>(K, cfg_.n_rows / P);
   cfg_.tb = K;
   band_ = K;
+  k_pref_ = tb_given ? K : std::min(K, tb_pref);
   const int64_t halo = cfg_.halo > 0 ? cfg_.halo : kDefaultHalo;
   HEAT2D_REQUIRE(halo >= K, "halo must be >= temporal depth");
   const SlabRange sr = decompose(cfg_.n_rows, P, rank);
@@ -370,30 +376,35 @@ int Solver::spare_waves() const {
 // smallest steady-state cycle (ms) for which edge-first split plans are tried
 constexpr float kEdgeFirstMinCycleMs = 0.4f;
 
+// One trial cycle of plan c (autotuner, prepare's clock warm-up): the real
+// kernels and traffic of a cycle, reading the CURRENT buffer and writing the
+// other one without a swap or an exchange, so the solution is untouched.
+void Solver::trial_cycle(const kern::SplitPlan& c) {
+  void* src = buf_[cur_];
+  void* dst = buf_[cur_ ^ 1];
+  if (c.valid == 3) {  // edge-first: both parts in order on the compute stream
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+    kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_compute_, cfg_.arith);
+    kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith);
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+    return;
+  }
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+  H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
+  kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith);
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_, cfg_.arith);
+  H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+}
+
 void Solver::autotune_split(int k) {
   const int spare = spare_waves();
   synchronize();
   hipEvent_t e0, e1;
   H2D_HIP(hipEventCreate(&e0));
   H2D_HIP(hipEventCreate(&e1));
-  auto run_cycle = [&](const kern::SplitPlan& c) {
-    void* src = buf_[cur_];
-    void* dst = buf_[cur_ ^ 1];
-    if (c.valid == 3) {  // edge-first: both parts in order on the compute stream
-      H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
-      kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_compute_, cfg_.arith);
-      kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith);
-      H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-      H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
-      return;
-    }
-    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
-    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
-    kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith);
-    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-    kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_, cfg_.arith);
-    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
-  };
+  auto run_cycle = [&](const kern::SplitPlan& c) { trial_cycle(c); };
   auto time_plan = [&](const kern::SplitPlan& c, int kTimed) {
     constexpr int kWarm = 1;
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
@@ -527,7 +538,7 @@ void Solver::cycle_copy_swap() {
 }
 
 void Solver::run_graph_cycles(int64_t npairs) {
-  const int K = cfg_.tb;
+  const int K = k_pref_;
   const bool ovl = cfg_.overlap != 0;
   if (ovl) (void)split_plan(K);  // plan / autotune (synchronising) before any capture
   if (!graph_exec_ || graph_k_ != K) {
@@ -600,7 +611,14 @@ void Solver::step(int64_t n) {
     steps_ += n;
     return;
   }
-  const int K = cfg_.tb;
+  if (auto it = sched_.find(n); it != sched_.end()) {
+    for (int k : it->second) {
+      cycle_launch(k);
+      cycle_finish();
+    }
+    return;
+  }
+  const int K = k_pref_;
   const bool multi = tr_->exchanges();
   int64_t left = n;
   while (left > 0) {
@@ -622,15 +640,92 @@ void Solver::step(int64_t n) {
   }
 }
 
+bool Solver::measured_schedules() const {
+  if (!hip_ || !cfg_.overlap || cfg_.copy_swap || cfg_.use_graph || jit_) return false;
+  const bool big = L_.nrows * L_.ncols >= (int64_t(1) << 24);
+  return cfg_.autotune > 0 || (cfg_.autotune < 0 && big);
+}
+
+// Autotuned steady-state cycle time of depth k, max over ranks (0: no tuned
+// split plan for this depth, e.g. a slab too thin to split).
+float Solver::depth_ms(int k) {
+  if (depth_ms_[k] == 0.f) {
+    (void)split_plan(k);
+    double v = tuned_ms_[k];
+    tr_->allreduce(&v, 1, 1);
+    depth_ms_[k] = v > 0 ? (float)v : -1.f;
+  }
+  return depth_ms_[k];
+}
+
+// Cycle schedule of n steps from measured cycle times. The cycle time t(k) is
+// flat while a pass is HBM-bound and grows ~linearly once it is VALU-bound
+// (profiles/depth_schedule.md), i.e. convex, so for c cycles the balanced
+// depths (n/c, rounded) are the best split; scan c upward from ceil(n/Kmax)
+// and stop once the base depth's per-step cost is 25 % worse than the best
+// seen (deeper into the HBM-bound region it only gets worse).
+std::vector<int> Solver::choose_schedule(int64_t n) {
+  const int Kmax = cfg_.tb;
+  double best = 1e300, best_step = 1e300;
+  int64_t best_c = 0;
+  for (int64_t c = (n + Kmax - 1) / Kmax; c <= n; ++c) {
+    const int kb = (int)(n / c);
+    const int64_t rem = n % c;
+    const float tb = depth_ms(kb);
+    const float t1 = rem ? depth_ms(kb + 1) : 0.f;
+    if (tb < 0 || t1 < 0) return {};
+    const double cost = (double)(c - rem) * tb + (double)rem * t1;
+    if (cost < best) {
+      best = cost;
+      best_c = c;
+    }
+    best_step = std::min(best_step, (double)tb / kb);
+    if (kb <= 1 || (double)tb / kb > 1.25 * best_step) break;
+  }
+  std::vector<int> sched;
+  const int kb = (int)(n / best_c);
+  const int64_t rem = n % best_c;
+  for (int64_t i = 0; i < best_c; ++i) sched.push_back(i < rem ? kb + 1 : kb);
+  return sched;
+}
+
+const std::vector<int>* Solver::schedule(int64_t n) const {
+  auto it = sched_.find(n);
+  return it == sched_.end() ? nullptr : &it->second;
+}
+
 void Solver::prepare(int64_t n) {
   if (!hip_ || !cfg_.overlap || cfg_.copy_swap || n <= 0) return;
+  if (measured_schedules() && !sched_.count(n)) {
+    std::vector<int> s = choose_schedule(n);
+    if (!s.empty()) sched_[n] = std::move(s);
+  }
+  if (const std::vector<int>* s = schedule(n)) {
+    // Leave the GPU in the schedule's steady state: the search ends on its
+    // shallowest (HBM-bound) depths, and a VALU-bound cycle that follows
+    // HBM-bound work or an idle gap runs at lower clocks (32768^2 fp64, one
+    // depth-20 pass: 6.4 ms after a compute-bound cycle, 6.8 ms after a
+    // depth-5 one, 7.5 ms after 0.5 s idle; profiles/depth_schedule.md).
+    // Trial cycles of its first depths (>= 3 cycles and ~20 ms), state untouched.
+    synchronize();
+    float ms = 0.f;
+    for (size_t i = 0; i < 64 && (i < 3 || ms < 20.f); ++i) {
+      const int k = (*s)[i % s->size()];
+      trial_cycle(split_plan(k));
+      ms += depth_ms(k);
+    }
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+    synchronize();
+    return;
+  }
   // walk step(n)'s loop (graph pairs of depth K, then balanced eager cycles)
   // and plan every depth it will launch. Graph pairs start only at buffer
   // parity 0, so the depths depend on the parity step(n) starts from: walk
   // both, since a warmup between prepare() and step(n) may flip it (4096^2
   // fp32 graph, K = 6 / 14: an unplanned remainder depth autotuned inside the
   // timed run cost 10 ms of 16).
-  const int K = cfg_.tb;
+  const int K = k_pref_;
   const bool multi = tr_->exchanges();
   for (int start = 0; start < 2; ++start) {
     int par = start;
@@ -749,7 +844,7 @@ void LoopbackGroup::init(const kern::IcParams& ic, const double* xg, const doubl
 // members: all launches (each posts its new field and band event), then all
 // exchanges — the order a multi-process run gets from RCCL's rendezvous.
 void LoopbackGroup::step(int64_t n) {
-  const int K = members_[0]->config().tb;
+  const int K = members_[0]->pref_depth();
   int64_t left = n;
   while (left > 0) {
     const int64_t ncyc = (left + K - 1) / K;

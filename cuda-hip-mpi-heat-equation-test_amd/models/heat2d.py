@@ -65,8 +65,10 @@ class HeatSolver:
         problem: resolved :class:`~utils.config.Problem`.
         dtype: "fp64" (reference precision) or "fp32".
         backend: "hip", "cpu" or "auto".
-        tb: temporal-block depth K (time steps fused per HBM pass, 1..16; 0 = the
-            measured best: fp64 14 / fp32 16 on the HIP engine, 8 on the CPU twin).
+        tb: largest temporal-block depth K (time steps fused per HBM pass; fp64
+            1..24, fp32 1..16). 0: all depths up to that limit for the measured
+            schedules of prepare() (autotuned slabs), balanced cycles of the
+            steady-state best (fp64 14 / fp32 16) otherwise; 8 on the CPU twin.
         overlap: boundary/interior split with the halo exchange on a comm stream.
         copy_swap: reference-parity schedule (full field copy every step, K=1).
         managed: allocate fields with hipMallocManaged.
@@ -189,6 +191,17 @@ class HeatSolver:
     def plan(self, k: Optional[int] = None) -> dict:
         """The split plan (MAIN / EDGE launches) used for depth k (default: tb)."""
         return _plan(self._h, self.tb if k is None else k)
+
+    def schedule(self, n: int):
+        """Depths of the measured cycle schedule prepare(n) chose for step(n), or None
+        (balanced cycles of the preferred depth)."""
+        ln = C.c_int64()
+        N.call("heat2d_solver_schedule", self._h, int(n), None, 0, C.byref(ln))
+        if ln.value < 0:
+            return None
+        out = (C.c_int32 * max(1, ln.value))()
+        N.call("heat2d_solver_schedule", self._h, int(n), out, ln.value, C.byref(ln))
+        return [int(v) for v in out[:ln.value]]
 
     def cycle_hist(self, reset: bool = False) -> dict:
         """{depth: cycles} that step() launched since the last reset (graph replays count 2 each)."""

@@ -289,3 +289,43 @@ def test_prepare_covers_warmup_parity(gpu, native, tb):
     assert s.plans_made == before
     assert np.array_equal(s.download(), R.owned(R.ftcs(p, dtype=np.float32)))
     s.close()
+
+
+@pytest.mark.parametrize("dtype,n,steps", [("fp64", 1100, 20), ("fp32", 1100, 37), ("fp64", 700, 45)])
+def test_measured_schedule(gpu, native, dtype, n, steps):
+    """prepare(n) on an autotuned slab picks step(n)'s cycle schedule from
+    measured cycle times (balanced depths for the best cycle count, up to
+    max_tb: fp64 24, fp32 16); step(n) runs exactly that schedule, plans
+    nothing new, and stays bitwise equal to the golden."""
+    from collections import Counter
+    p = prob(n, steps, "ghost", "sine")
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    s = HeatSolver(p, dtype=dtype, backend="hip", device=0, autotune=1)
+    assert s.tb == (24 if dtype == "fp64" else 16)
+    s.upload(R.owned(R.initial_field(p, npdt)))
+    s.prepare(steps)
+    sched = s.schedule(steps)
+    assert sched and sum(sched) == steps and max(sched) - min(sched) <= 1 and max(sched) <= s.tb
+    before = s.plans_made
+    s.cycle_hist(reset=True)
+    s.step(steps)
+    s.synchronize()
+    assert s.plans_made == before
+    assert s.cycle_hist() == dict(Counter(sched))
+    got = s.download()
+    ref = R.owned(R.ftcs(p, dtype=npdt))
+    assert np.array_equal(got, ref), np.abs(got.astype(np.float64) - ref).max()
+    s.close()
+
+
+@pytest.mark.parametrize("k", [17, 20, 24])
+def test_deep_fp64_bitwise(gpu, native, k):
+    """fp64 depths 17..24 (one-pass short runs): both kernels (split + single) bitwise."""
+    p = prob(1100, 2 * k + 3, "ghost", "sine")
+    for overlap in (True, False):
+        s = HeatSolver(p, dtype="fp64", backend="hip", tb=k, device=0, overlap=overlap)
+        s.upload(R.owned(R.initial_field(p)))
+        s.step(p.ntime)
+        got = s.download()
+        s.close()
+        assert np.array_equal(got, R.owned(R.ftcs(p))), (k, overlap)

@@ -28,7 +28,8 @@ def tb():
         p = isa_report.tb_params(k["name"])
         if p:
             ks[p] = k
-    assert len(ks) == 256, len(ks)  # 2 dtypes x 2 rings x main/gen x 2 arith x K 1..16
+    # 2 rings x main/gen x 2 arith x (fp32 K 1..16 + fp64 K 1..24)
+    assert len(ks) == 8 * (16 + 24), len(ks)
     return ks
 
 
@@ -43,6 +44,15 @@ def test_occupancy_floors(tb):
     for k in range(1, 12):  # the packed fp32 interior kernel keeps >= 3 waves/SIMD up to K = 11
         for ar in (0, 1):
             assert tb[("fp32", 1, k, 4, True, ar)]["waves_per_simd"] >= 3, k
+
+
+def test_deep_fp64_interior_two_waves(tb):
+    """fp64 K = 17..24 exist for one-pass short runs: the interior (MAIN) kernel
+    must keep 2 waves/SIMD with ring 4 there (the general one may drop to 1)."""
+    for k in range(17, 25):
+        for ar in (0, 1):
+            assert tb[("fp64", 1, k, 4, True, ar)]["waves_per_simd"] >= 2, k
+    assert not any(p[0] == "fp32" and p[2] > 16 for p in tb)
 
 
 def test_packed_fp32_compact(tb):
