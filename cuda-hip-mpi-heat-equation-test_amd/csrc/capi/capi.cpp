@@ -340,6 +340,14 @@ int heat2d_solver_cycle_hist(void* s, int64_t* out, int n, int reset) {
   });
 }
 
+int heat2d_solver_pref_depth(void* s, int32_t* out) {
+  return guarded([&] { *out = static_cast<Solver*>(s)->pref_depth(); });
+}
+
+int heat2d_solver_step_stats(void* s, int64_t n, double* out6) {
+  return guarded([&] { static_cast<Solver*>(s)->step_stats(n, out6); });
+}
+
 int heat2d_solver_schedule(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len) {
   return guarded([&] {
     const std::vector<int>* v = static_cast<Solver*>(s)->schedule(n);

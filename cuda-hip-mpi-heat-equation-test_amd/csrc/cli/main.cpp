@@ -230,12 +230,16 @@ void run_rank(Shared& sh, int rank) {
 
     const int64_t ntime = sh.in.ntime;
     // plan / autotune every cycle depth the loop will use before the clock starts
+    // time_it lines (fortran/hip/heat.F90:241 prints one per step) do not cut
+    // the run into cycles shorter than the preferred depth: chunks of
+    // max(print_every, pref_depth) steps, every due line printed after its chunk
+    const int64_t print_chunk = a.print_every > 0 ? std::max<int64_t>(a.print_every, s.pref_depth()) : 0;
     {  // walk the chunking of the loop below and prepare each distinct chunk length
       const bool ckpt_every = !a.checkpoint.empty() && a.checkpoint_every > 0;
       std::vector<int64_t> seen;
       for (int64_t d = start; d < ntime;) {
         int64_t c = ntime - d;
-        if (a.print_every > 0) c = std::min(c, a.print_every - (d % a.print_every));
+        if (print_chunk > 0) c = std::min(c, print_chunk - (d % print_chunk));
         if (a.check_every > 0) c = std::min(c, a.check_every - (d % a.check_every));
         if (ckpt_every) c = std::min(c, a.checkpoint_every - (d % a.checkpoint_every));
         if (std::find(seen.begin(), seen.end(), c) == seen.end()) {
@@ -253,18 +257,22 @@ void run_rank(Shared& sh, int rank) {
     const bool ckpt_periodic = !a.checkpoint.empty() && a.checkpoint_every > 0;
     while (done < ntime) {
       int64_t chunk = ntime - done;
-      if (a.print_every > 0) chunk = std::min(chunk, a.print_every - (done % a.print_every));
+      if (print_chunk > 0) chunk = std::min(chunk, print_chunk - (done % print_chunk));
       if (a.check_every > 0) chunk = std::min(chunk, a.check_every - (done % a.check_every));
       if (ckpt_periodic) chunk = std::min(chunk, a.checkpoint_every - (done % a.checkpoint_every));
-      s.step(chunk);
+      const bool check = a.check_every > 0 && (done + chunk) % a.check_every == 0;
+      double st[6];
+      if (check) s.step_stats(chunk, st);  // statistics + one-step residual fused into the last cycle
+      else s.step(chunk);
+      const int64_t before = done;
       done += chunk;
-      if (root && a.print_every > 0 && done % a.print_every == 0) std::printf(" time_it: %12lld\n", (long long)done);
-      if (a.check_every > 0 && done % a.check_every == 0) {
-        double st[6];
-        s.stats(st, true);
+      if (root && a.print_every > 0)
+        for (int64_t t = (before / a.print_every + 1) * a.print_every; t <= done; t += a.print_every)
+          std::printf(" time_it: %12lld\n", (long long)t);
+      if (check) {
         if (root)
-          std::printf(" step %lld: sum=%.17g min=%.6g max=%.6g residual_l2=%.6e\n", (long long)done, st[0], st[2],
-                      st[3], std::sqrt(st[4]));
+          std::printf(" step %lld: sum=%.17g min=%.6g max=%.6g residual_l2=%.6e residual_max=%.6e\n", (long long)done,
+                      st[0], st[2], st[3], std::sqrt(st[4]), st[5]);
         if (!std::isfinite(st[0])) fail(__FILE__, __LINE__, "non-finite temperature at step " + std::to_string(done));
       }
       if (ckpt_periodic && done % a.checkpoint_every == 0 && done < ntime) save_checkpoint(sh, s, *tr, rank, done);

@@ -111,6 +111,11 @@ int heat2d_solver_create(const heat2d_config* cfg, void* transport, void** out);
 int heat2d_solver_free(void* s);
 int heat2d_solver_init(void* s, const heat2d_ic* ic, const double* xg, const double* yg);
 int heat2d_solver_step(void* s, int64_t n);
+/* step(n) with the global statistics of T_n and its one-step residual fused into the last cycle:
+   out6 = {sum, sum_sq, min, max, sum (T_n - T_{n-1})^2, max |T_n - T_{n-1}|} */
+int heat2d_solver_step_stats(void* s, int64_t n, double* out6);
+/* depth of the balanced cycles step() runs when no measured schedule applies */
+int heat2d_solver_pref_depth(void* s, int32_t* out);
 int heat2d_solver_sync(void* s);
 int heat2d_solver_stats(void* s, double* out6, int residual);
 int heat2d_solver_download(void* s, void* host, int64_t ld);

@@ -111,6 +111,18 @@ int64_t stats_work_elems();
 void launch_stats(DType dt, const void* field, const void* other, const SlabLayout& L,
                   double* work, double* out, hipStream_t stream);
 
+// One cycle of k steps over the whole slab (one general launch, like
+// plan_single) that also reduces the statistics of the NEW field and its
+// one-step residual T_k - T_{k-1} — [sum, sum_sq, min, max, sum_sq_diff,
+// max_abs_diff], the launch_stats layout — fused into the march's stored
+// level (no extra pass over the field): per-wave partials in `partials`
+// (>= kNStat * max_stats_waves() doubles), then a fixed-order reduce into
+// out6 (device). Deterministic for a given slab and device.
+int64_t max_stats_waves();
+void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, int k, double r, double* partials,
+                     double* out6, hipStream_t stream, int arith = 0);
+void launch_reduce_partials(const double* partials, int64_t nparts, double* out6, hipStream_t stream);
+
 // Vectorised streaming copy / read (bandwidth roof probes; copy-swap mode).
 void launch_copy(void* dst, const void* src, int64_t bytes, hipStream_t stream, int blocks = 0);
 void launch_read(const void* src, int64_t bytes, unsigned* sink, hipStream_t stream, int blocks = 0);

@@ -172,9 +172,16 @@ class Solver {
   // steady-state best: fp64 14, fp32 16 unless --tb is given)
   int pref_depth() const { return k_pref_; }
   void synchronize();
-  // Global statistics over all ranks: sum, sum_sq, min, max, and residual
-  // terms vs the previous buffer (valid right after a step()).
+  // Global statistics over all ranks: sum, sum_sq, min, max of the current
+  // field (a separate pass over it); residual = true adds sum (T_n - T_{n-1})^2
+  // and max |T_n - T_{n-1}| when the last cycle had depth 1 (the other buffer
+  // then holds T_{n-1}), else NaN — use step_stats for a residual at any depth.
   void stats(double out[6], bool residual);
+  // step(n), with the statistics of T_n and its ONE-STEP residual T_n - T_{n-1}
+  // (layout of stats()) fused into the last cycle's stencil launch — no extra
+  // pass over the field (HIP engine; the CPU twin, copy-swap and jit modes run
+  // n-1 steps, one step, and stats(residual)). Reduced over ranks.
+  void step_stats(int64_t n, double out[6]);
   // Owned region <-> host (rows x n_cols, leading dimension ld elements).
   void download(void* host, int64_t ld);
   void upload(const void* host, int64_t ld);  // followed by a halo exchange
@@ -223,6 +230,8 @@ class Solver {
  private:
   void launch_overlap(int k);
   void launch_serial(int k);
+  void launch_stats_cycle(int k);
+  void reduce_global(const double loc[6], double out[6]);
   const kern::SplitPlan& split_plan(int k);
   void autotune_split(int k);
   void cycle_copy_swap();
@@ -262,6 +271,9 @@ class Solver {
   int64_t pend_pe_ = -1;  // index into phase_ev_ (timing) or -1
   int64_t hist_[kMaxTB + 1] = {};
   int k_pref_ = 1;
+  int last_k_ = 0;            // depth of the last finished cycle
+  bool stats_next_ = false;   // the next cycle_launch is the fused-statistics cycle
+  double* d_part_ = nullptr;  // fused statistics: per-wave partials
   std::map<int64_t, std::vector<int>> sched_;  // measured schedules by step count
   float depth_ms_[kMaxTB + 1] = {};            // cycle ms per depth, max over ranks (schedule search)
   int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all

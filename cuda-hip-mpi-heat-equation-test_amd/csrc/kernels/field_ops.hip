@@ -112,17 +112,19 @@ __global__ __launch_bounds__(kStatsThreads) void stats_pass1(const T* __restrict
   if (threadIdx.x < kNStat) work[threadIdx.x * kStatsBlocks + blockIdx.x] = red[threadIdx.x][0];
 }
 
-__global__ __launch_bounds__(kStatsThreads) void stats_pass2(const double* __restrict__ work,
+// Pass 2 (also the reduce of the stencil's fused per-wave statistics):
+// work[j * n + b], b < n, reduced in a fixed order.
+__global__ __launch_bounds__(kStatsThreads) void stats_pass2(const double* __restrict__ work, int64_t n,
                                                              double* __restrict__ out) {
   __shared__ double red[kNStat][kStatsThreads];
   double acc[kNStat] = {0.0, 0.0, DBL_MAX, -DBL_MAX, 0.0, 0.0};
-  for (int b = threadIdx.x; b < kStatsBlocks; b += blockDim.x) {
-    acc[0] += work[0 * kStatsBlocks + b];
-    acc[1] += work[1 * kStatsBlocks + b];
-    acc[2] = fmin(acc[2], work[2 * kStatsBlocks + b]);
-    acc[3] = fmax(acc[3], work[3 * kStatsBlocks + b]);
-    acc[4] += work[4 * kStatsBlocks + b];
-    acc[5] = fmax(acc[5], work[5 * kStatsBlocks + b]);
+  for (int64_t b = threadIdx.x; b < n; b += blockDim.x) {
+    acc[0] += work[0 * n + b];
+    acc[1] += work[1 * n + b];
+    acc[2] = fmin(acc[2], work[2 * n + b]);
+    acc[3] = fmax(acc[3], work[3 * n + b]);
+    acc[4] += work[4 * n + b];
+    acc[5] = fmax(acc[5], work[5 * n + b]);
   }
   for (int k = 0; k < kNStat; ++k) red[k][threadIdx.x] = acc[k];
   __syncthreads();
@@ -227,8 +229,14 @@ void launch_stats(DType dt, const void* field, const void* other, const SlabLayo
     hipLaunchKernelGGL(stats_pass1<double>, dim3(kStatsBlocks), dim3(kStatsThreads), 0, stream,
                        static_cast<const double*>(field), static_cast<const double*>(other), L, work);
   check_launch("stats_pass1");
-  hipLaunchKernelGGL(stats_pass2, dim3(1), dim3(kStatsThreads), 0, stream, work, out);
+  hipLaunchKernelGGL(stats_pass2, dim3(1), dim3(kStatsThreads), 0, stream, work, (int64_t)kStatsBlocks, out);
   check_launch("stats_pass2");
+}
+
+void launch_reduce_partials(const double* partials, int64_t nparts, double* out, hipStream_t stream) {
+  HEAT2D_REQUIRE(nparts >= 1, "no partials to reduce");
+  hipLaunchKernelGGL(stats_pass2, dim3(1), dim3(kStatsThreads), 0, stream, partials, nparts, out);
+  check_launch("stats_pass2 (fused partials)");
 }
 
 void launch_copy(void* dst, const void* src, int64_t bytes, hipStream_t stream, int blocks) {

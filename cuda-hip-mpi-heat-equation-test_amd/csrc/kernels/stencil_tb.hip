@@ -94,6 +94,12 @@ int occupancy_t(int ring, bool main, int k) {
   return main ? occupancy_blocks<T, 6, true, AR>(k) : occupancy_blocks<T, 6, false, AR>(k);
 }
 
+int occupancy_stats(DType dt, int k, int arith) {
+  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 (exact) or 1 (fma)");
+  if (dt == DType::F32) return arith ? occupancy_blocks_stats<float, 1>(k) : occupancy_blocks_stats<float, 0>(k);
+  return arith ? occupancy_blocks_stats<double, 1>(k) : occupancy_blocks_stats<double, 0>(k);
+}
+
 int occupancy(DType dt, int ring, bool main, int k, int arith) {
   HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 (exact) or 1 (fma)");
   if (dt == DType::F32) return arith ? occupancy_t<float, 1>(ring, main, k) : occupancy_t<float, 0>(ring, main, k);
@@ -154,8 +160,10 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t slots, int k) {
 }
 
 // Launch `rects` (item counts from their nb and strip ranges) on `nwaves` waves.
-void launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
-                  const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith) {
+// partials != nullptr: the fused-statistics kernel (general, ring 4); returns the waves launched
+int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
+                     const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith,
+                     double* partials = nullptr) {
   HEAT2D_REQUIRE(nrect >= 1 && nrect <= kMaxRects, "bad rect count");
   TbArgs a{};
   a.pitch = L.pitch;
@@ -174,21 +182,35 @@ void launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int
     items += R.nb * (R.s1 - R.s0);
     ++q;
   }
-  if (q == 0) return;
+  if (q == 0) return 0;
   a.nrect = q;
   a.xcd_remap = xcd_remap();
   a.nitems = items;
   a.nwaves = std::max<int64_t>(1, std::min<int64_t>(nwaves, items));
+  a.partials = partials;
   const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
   const int64_t o = L.origin();
-  if (dt == DType::F32)
+  if (partials) {
+    HEAT2D_REQUIRE(a.nwaves <= max_stats_waves(), "statistics partials buffer too small");
+    const float* s32 = static_cast<const float*>(src) + o;
+    const double* s64 = static_cast<const double*>(src) + o;
+    if (dt == DType::F32) {
+      if (arith) dispatch_stats<float, 1>(k, nblocks, s32, static_cast<float*>(dst) + o, a, (float)r, stream);
+      else dispatch_stats<float, 0>(k, nblocks, s32, static_cast<float*>(dst) + o, a, (float)r, stream);
+    } else {
+      if (arith) dispatch_stats<double, 1>(k, nblocks, s64, static_cast<double*>(dst) + o, a, r, stream);
+      else dispatch_stats<double, 0>(k, nblocks, s64, static_cast<double*>(dst) + o, a, r, stream);
+    }
+  } else if (dt == DType::F32) {
     dispatch_t<float>(ring, main, arith, k, nblocks, static_cast<const float*>(src) + o, static_cast<float*>(dst) + o, a,
                       (float)r, stream);
-  else
+  } else {
     dispatch_t<double>(ring, main, arith, k, nblocks, static_cast<const double*>(src) + o, static_cast<double*>(dst) + o,
                        a, r, stream);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("tb_kernel launch: ") + hipGetErrorString(e));
+  return a.nwaves;
 }
 
 }  // namespace
@@ -298,6 +320,21 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   p.nedge = 0;
   p.valid = 2;
   return p;
+}
+
+int64_t max_stats_waves() { return (int64_t)cu_count() * 32; }  // 8 x 256-thread blocks per CU
+
+void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, int k, double r, double* partials,
+                     double* out6, hipStream_t stream, int arith) {
+  check_layout(dt, L, k);
+  HEAT2D_REQUIRE(partials && out6, "statistics buffers required");
+  const int64_t U = useful_width(dt, k);
+  const int64_t ns = (L.ncols + U - 1) / U;
+  const int64_t slots = (int64_t)cu_count() * occupancy_stats(dt, k, arith) * 4;
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(choose_bands(L.nrows, ns, slots, k), L.nrows));
+  const TbRect rect{0, L.nrows, 0, ns, nb};
+  const int64_t nw = launch_rects(dt, src, dst, L, k, 4, false, &rect, 1, slots, r, stream, arith, partials);
+  launch_reduce_partials(partials, nw, out6, stream);
 }
 
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,

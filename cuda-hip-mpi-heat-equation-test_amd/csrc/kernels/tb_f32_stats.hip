@@ -1,0 +1,11 @@
+// Instantiation unit: temporal-blocked stencil with fused statistics of the stored level
+// (float, ring 4, general kernel, reference arithmetic AR = 0; see tb_impl.hpp StatAcc).
+#include "tb_impl.hpp"
+
+namespace heat2d {
+namespace kern {
+namespace tbimpl {
+H2D_ST_UNIT(float, 0, H2D_NO_CASES)
+}  // namespace tbimpl
+}  // namespace kern
+}  // namespace heat2d

@@ -99,6 +99,26 @@ struct TbArgs {
   int32_t nrect;
   int32_t xcd_remap;  // 1: XCD-aware block -> wave-id mapping (tb_kernel)
   TbRectArg rect[kMaxRects];
+  double* partials;   // ST kernels: per-wave statistics, partials[j * nwaves + wave] (kNStatFused = 6 values)
+};
+
+// Fused statistics of the stored (last) level (ST kernels): sum T, sum T^2,
+// min T, max T, sum (T_K - T_{K-1})^2, max |T_K - T_{K-1}| over the owned
+// points — T_K - T_{K-1} is the one-step residual of the cycle's last step,
+// whatever the depth. Accumulated in fp64 per lane, reduced per wave with a
+// fixed butterfly, one partial per wave: deterministic for a given plan.
+constexpr int kNStatFused = 6;
+struct StatAcc {
+  double s = 0.0, ss = 0.0, mn = __builtin_huge_val(), mx = -__builtin_huge_val(), dd = 0.0, md = 0.0;
+  __device__ __forceinline__ void add(bool ok, double v, double c) {
+    const double d = v - c;
+    s += ok ? v : 0.0;
+    ss += ok ? v * v : 0.0;
+    mn = fmin(mn, ok ? v : __builtin_huge_val());
+    mx = fmax(mx, ok ? v : -__builtin_huge_val());
+    dd += ok ? d * d : 0.0;
+    md = fmax(md, ok ? fabs(d) : 0.0);
+  }
 };
 
 template <typename T, int NV, int K>
@@ -163,7 +183,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uin
 // fewer per point (5 fp64 ops + 2 DPP moves instead of 6 + 2) for a kernel that
 // is VALU-co-bound. When r is a power of two (sigma = 0.25 in every shipped
 // input) r*x is exact and both forms round identically (normal range).
-template <typename T, int NV, int K, int EK, int RING, int AR>
+template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false>
 struct March {
   using S = TbShape<T, NV, K>;
   static constexpr int V = S::V;
@@ -187,6 +207,8 @@ struct March {
 
   T X[2][KX][V];     // levels 1..K-1: X[parity][level-1][elem]
   VT Lb[RING][NV];   // level 0: load ring
+  StatAcc acc;       // ST: statistics of the stored rows
+  uint32_t colmask;  // ST: bit e = element e is an owned output column of this lane
 
   __device__ __forceinline__ void load_row(int32_t m, VT (&out)[NV]) const {
     const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + (int64_t)m * pitch_b, nrec);
@@ -284,7 +306,14 @@ struct March {
 #pragma unroll
         for (int e = 0; e < V; ++e) part[e] = nxtpart[e];
       } else {
-        store_row(m + s, m + s < t1 && m + s >= t0, out);
+        const bool live = m + s < t1 && m + s >= t0;  // wave-uniform
+        store_row(m + s, live, out);
+        if constexpr (ST) {
+          if (live) {
+#pragma unroll
+            for (int e = 0; e < V; ++e) acc.add((colmask >> e) & 1u, (double)out[e], (double)C[e]);
+          }
+        }
       }
     }
   }
@@ -348,7 +377,7 @@ struct March {
 // ~2x the registers: 209 VGPRs at K = 10). Same operation order and rounding
 // per element as March (bitwise identical); the loads / stores / ring /
 // descriptors / edge kinds are March's.
-template <int K, int EK, int RING, int AR>
+template <int K, int EK, int RING, int AR, bool ST = false>
 struct MarchF32 {
   using F2 = float __attribute__((ext_vector_type(2)));
   using VT = float __attribute__((ext_vector_type(4)));
@@ -372,6 +401,8 @@ struct MarchF32 {
   Row rl;  // EK & 2: r per element (0 in Dirichlet / pad columns)
 
   Row X[2][KX];
+  StatAcc acc;       // ST: statistics of the stored rows
+  uint32_t colmask;  // ST: bit e = element e (memory order) is an owned output column
   // Level-0 ring. A slot holds a row in memory order (a = (c0, c1),
   // b = (c2, c3)) from its load until its first use (as the north row), where
   // it is rearranged IN PLACE to the even/odd form: one swap per row instead
@@ -458,7 +489,17 @@ struct MarchF32 {
         X[P][i] = update(part, C, N, m + s);
         part = nxtpart;
       } else {
-        store_row(m + s, m + s < t1 && m + s >= t0, update_last(part, C, N, m + s));
+        const bool live = m + s < t1 && m + s >= t0;  // wave-uniform
+        const VT w = update_last(part, C, N, m + s);
+        store_row(m + s, live, w);
+        if constexpr (ST) {
+          if (live) {  // C in even/odd form: a = (c0, c2), b = (c1, c3)
+            acc.add(colmask & 1u, (double)w.x, (double)C.a.x);
+            acc.add((colmask >> 1) & 1u, (double)w.y, (double)C.b.x);
+            acc.add((colmask >> 2) & 1u, (double)w.z, (double)C.a.y);
+            acc.add((colmask >> 3) & 1u, (double)w.w, (double)C.b.y);
+          }
+        }
       }
     }
   }
@@ -507,9 +548,9 @@ template <typename T, int NV>
 constexpr bool kPackedF32 = false;
 #endif
 
-template <typename T, int NV, int K, int EK, int RING, int AR>
+template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
-                                      int64_t t1, int lane) {
+                                      int64_t t1, int lane, StatAcc* acc = nullptr) {
   using S = TbShape<T, NV, K>;
   constexpr int V = S::V;
   constexpr int ES = (int)sizeof(T);
@@ -517,7 +558,8 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   const int64_t c0 = u0 - S::KA;
   const int64_t mycol = c0 + (int64_t)lane * V;
   const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
-  using W = typename std::conditional<kPackedF32<T, NV>, MarchF32<K, EK, RING, AR>, March<T, NV, K, EK, RING, AR>>::type;
+  using W = typename std::conditional<kPackedF32<T, NV>, MarchF32<K, EK, RING, AR, ST>,
+                                      March<T, NV, K, EK, RING, AR, ST>>::type;
   W w;
   // row base = column col_lo (= -cpad) of row 0; offsets are relative to it
   w.srow = reinterpret_cast<const char*>(src + a.col_lo);
@@ -550,7 +592,17 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
       for (int e = 0; e < V; ++e) w.rl[e] = rcol(e);
     }
   }
-  w.run();
+  if constexpr (ST) {
+    uint32_t mask = 0;
+#pragma unroll
+    for (int e = 0; e < V; ++e) mask |= (useful && mycol + e >= 0 && mycol + e < a.ncols) ? (1u << e) : 0u;
+    w.colmask = mask;
+    w.acc = *acc;
+    w.run();
+    *acc = w.acc;
+  } else {
+    w.run();
+  }
 }
 
 // Decode work item `it` -> (strip, output rows [t0, t1)); false if empty.
@@ -585,8 +637,27 @@ __device__ __forceinline__ bool tb_item(const TbArgs& a, int64_t it, int64_t& st
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
 constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K >= 11 && K <= 12) ? 4 : 1;
 
-template <typename T, int NV, int K, int RING, bool MAIN, int AR>
+// wave-wide sum / min / max (fixed xor butterfly: every lane ends with the
+// same bits, lane 0's are written)
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+template <typename T, int NV, int K, int RING, bool MAIN, int AR, bool ST = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T, NV, K, RING, MAIN, AR>))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
+  static_assert(!ST || !MAIN, "fused statistics use the general kernel");
   using S = TbShape<T, NV, K>;
   const int lane = threadIdx.x & 63;
   // readfirstlane: make the wave id (and everything derived from it: strip, rows,
@@ -607,11 +678,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
   // Items are band-major within a rect: consecutive waves take adjacent strips
   // of the same band, so the waves in flight stream whole contiguous rows (HBM
   // page locality) and all march in step.
+  StatAcc acc;
   for (int64_t it = wid; it < a.nitems; it += a.nwaves) {
     int64_t strip, t0, t1;
     if (!tb_item(a, it, strip, t0, t1)) continue;
     const int64_t c0 = strip * S::U - S::KA;
-    if constexpr (MAIN) {
+    if constexpr (ST) {
+      const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
+                     (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
+      switch (ek) {
+        case 0: march<T, NV, K, 0, RING, AR, true>(src, dst, a, r, strip, t0, t1, lane, &acc); break;
+        case 1: march<T, NV, K, 1, RING, AR, true>(src, dst, a, r, strip, t0, t1, lane, &acc); break;
+        case 2: march<T, NV, K, 2, RING, AR, true>(src, dst, a, r, strip, t0, t1, lane, &acc); break;
+        default: march<T, NV, K, 3, RING, AR, true>(src, dst, a, r, strip, t0, t1, lane, &acc); break;
+      }
+    } else if constexpr (MAIN) {
       if ((c0 < 0) || (c0 + S::W > a.ncols))
         march<T, NV, K, 2, RING, AR>(src, dst, a, r, strip, t0, t1, lane);
       else
@@ -627,15 +708,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
       }
     }
   }
+  if constexpr (ST) {
+    const double v[kNStatFused] = {wave_sum(acc.s), wave_sum(acc.ss), wave_min(acc.mn),
+                                   wave_max(acc.mx), wave_sum(acc.dd), wave_max(acc.md)};
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < kNStatFused; ++j) a.partials[j * a.nwaves + wid] = v[j];
+    }
+  }
 }
 
-template <typename T, int NV, int K, int RING, bool MAIN, int AR>
+template <typename T, int NV, int K, int RING, bool MAIN, int AR, bool ST = false>
 constexpr auto kernel_ptr() {
-  return &tb_kernel<T, NV, K, RING, MAIN, AR>;
+  return &tb_kernel<T, NV, K, RING, MAIN, AR, ST>;
 }
 
 // Resident 256-thread workgroups per CU for one kernel instance (occupancy API).
-template <typename T, int NV, int K, int RING, bool MAIN, int AR>
+template <typename T, int NV, int K, int RING, bool MAIN, int AR, bool ST = false>
 int blocks_per_cu() {
   static std::mutex mu;
   static std::map<int, int> cache;  // device -> blocks/CU
@@ -645,7 +734,7 @@ int blocks_per_cu() {
   auto it = cache.find(dev);
   if (it != cache.end()) return it->second;
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, RING, MAIN, AR>()),
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, RING, MAIN, AR, ST>()),
                                                    256, 0) != hipSuccess ||
       nb <= 0)
     nb = 1;
@@ -659,6 +748,11 @@ template <typename T, int RING, bool MAIN, int AR>
 void dispatch(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
 template <typename T, int RING, bool MAIN, int AR>
 int occupancy_blocks(int k);
+// fused-statistics kernels: general kernel, ring 4 (tb_<dtype>_stats.hip)
+template <typename T, int AR>
+void dispatch_stats(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
+template <typename T, int AR>
+int occupancy_blocks_stats(int k);
 
 #define H2D_TB_CASE(T, RING, MAIN, AR, KK)                                                                    \
   case KK:                                                                                                    \
@@ -702,6 +796,35 @@ int occupancy_blocks(int k);
     return 1;                                                                                           \
   }
 #define H2D_TB_UNIT(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_NO_CASES)
+#define H2D_ST_CASE(T, RING, MAIN, AR, KK)                                                                         \
+  case KK:                                                                                                         \
+    hipLaunchKernelGGL((tb_kernel<T, 1, KK, 4, false, AR, true>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
+    return;
+#define H2D_ST_OCC_CASE(T, RING, MAIN, AR, KK) \
+  case KK:                                     \
+    return blocks_per_cu<T, 1, KK, 4, false, AR, true>();
+#define H2D_ST_UNIT(T, AR, DEEP)                                                                              \
+  template <>                                                                                                 \
+  void dispatch_stats<T, AR>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r,             \
+                             hipStream_t s) {                                                                 \
+    switch (k) {                                                                                              \
+      H2D_TB_CASES(H2D_ST_CASE, T, 4, false, AR)                                                              \
+      DEEP(H2D_ST_CASE, T, 4, false, AR)                                                                      \
+      default:                                                                                                \
+        break;                                                                                                \
+    }                                                                                                         \
+    HEAT2D_REQUIRE(false, "temporal depth not instantiated for the statistics kernel");                       \
+  }                                                                                                           \
+  template <>                                                                                                 \
+  int occupancy_blocks_stats<T, AR>(int k) {                                                                  \
+    switch (k) {                                                                                              \
+      H2D_TB_CASES(H2D_ST_OCC_CASE, T, 4, false, AR)                                                          \
+      DEEP(H2D_ST_OCC_CASE, T, 4, false, AR)                                                                  \
+      default:                                                                                                \
+        break;                                                                                                \
+    }                                                                                                         \
+    return 1;                                                                                                 \
+  }
 #define H2D_TB_UNIT_F64(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_DEEP)
 
 }  // namespace tbimpl

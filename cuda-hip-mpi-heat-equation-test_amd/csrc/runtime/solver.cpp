@@ -109,6 +109,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
       else H2D_HIP(hipMalloc(&buf_[b], bytes));
     }
     H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_work_), (size_t)(kern::stats_work_elems() + 8) * sizeof(double)));
+    H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_part_), (size_t)(6 * kern::max_stats_waves()) * sizeof(double)));
     if (external_stream) {
       s_compute_ = s_comm_ = external_stream;
       cfg_.overlap = 0;
@@ -169,6 +170,7 @@ Solver::~Solver() {
     for (auto& b : buf_)
       if (b) (void)hipFree(b);
     if (d_work_) (void)hipFree(d_work_);
+    if (d_part_) (void)hipFree(d_part_);
     if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
     if (ev_int_) (void)hipEventDestroy(ev_int_);
@@ -239,9 +241,29 @@ void Solver::exchange_now() { exchange_on(buf_[cur_], s_compute_); }
 void Solver::cycle_launch(int k) {
   HEAT2D_REQUIRE(pend_ == Pending::None, "cycle_launch: previous cycle not finished");
   HEAT2D_REQUIRE(k >= 1 && k <= cfg_.tb, "cycle depth outside [1, tb]");
-  if (cfg_.overlap && hip_) launch_overlap(k);
+  if (stats_next_ && hip_ && !jit_) launch_stats_cycle(k);
+  else if (cfg_.overlap && hip_) launch_overlap(k);
   else launch_serial(k);
+  stats_next_ = false;
   pend_k_ = k;
+}
+
+// The fused-statistics cycle: one general launch over the whole slab on the
+// compute stream, after the previous cycle's EDGE and exchange (ev_bnd /
+// ev_comm), the per-wave partials reduced right behind it into the tail of
+// d_work_; the exchange of its bands follows on the comm stream (overlap) or
+// the compute stream (serial), as for an edge-first / serial cycle.
+void Solver::launch_stats_cycle(int k) {
+  roctxRangePushA("heat2d.cycle.stats");
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
+  kern::launch_tb_stats(dtype(), buf_[cur_], buf_[cur_ ^ 1], L_, k, cfg_.r, d_part_,
+                        d_work_ + kern::stats_work_elems(), s_compute_, cfg_.arith);
+  H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  if (tr_->exchanges()) tr_->post(buf_[cur_ ^ 1], L_, ev_bnd_);
+  pend_ = (cfg_.overlap && s_comm_ != s_compute_) ? Pending::EdgeFirst : Pending::Serial;
+  pend_pe_ = -1;
 }
 
 void Solver::cycle_finish() {
@@ -265,6 +287,7 @@ void Solver::cycle_finish() {
   pend_pe_ = -1;
   steps_ += pend_k_;
   hist_[pend_k_] += 1;
+  last_k_ = pend_k_;
   cycle_swap();
 }
 
@@ -595,6 +618,7 @@ void Solver::run_graph_cycles(int64_t npairs) {
   // the graph was captured for buffer parity 0 -> 1 -> 0
   for (int64_t i = 0; i < npairs; ++i) H2D_HIP(hipGraphLaunch(graph_exec_, s_compute_));
   hist_[K] += 2 * npairs;
+  if (npairs > 0) last_k_ = K;
   if (ovl) {  // eager cycles after the graph order against its end
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
@@ -753,17 +777,40 @@ void Solver::synchronize() {
   tr_->check();
 }
 
-void Solver::stats(double out[6], bool residual) {
-  double loc[6];
-  const void* other = residual ? buf_[cur_ ^ 1] : nullptr;
-  if (hip_) {
-    synchronize();
-    kern::launch_stats(dtype(), buf_[cur_], other, L_, d_work_, d_work_ + kern::stats_work_elems(), s_compute_);
-    H2D_HIP(hipMemcpyAsync(loc, d_work_ + kern::stats_work_elems(), sizeof(loc), hipMemcpyDeviceToHost, s_compute_));
-    H2D_HIP(hipStreamSynchronize(s_compute_));
-  } else {
-    cpu::stats(dtype(), buf_[cur_], other, L_, loc);
+void Solver::step_stats(int64_t n, double out[6]) {
+  HEAT2D_REQUIRE(n >= 1, "step_stats needs n >= 1");
+  if (hip_) H2D_HIP(hipSetDevice(cfg_.device));
+  if (!hip_ || jit_ || cfg_.copy_swap) {
+    step(n - 1);
+    step(1);
+    stats(out, true);
+    return;
   }
+  // the cycles step(n) would run (the measured schedule, else balanced cycles
+  // of the preferred depth), eagerly, the last one with the fused statistics
+  std::vector<int> seq;
+  if (const std::vector<int>* sc = schedule(n)) {
+    seq = *sc;
+  } else {
+    for (int64_t left = n; left > 0;) {
+      const int64_t ncyc = (left + k_pref_ - 1) / k_pref_;
+      const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
+      seq.push_back(k);
+      left -= k;
+    }
+  }
+  for (size_t i = 0; i < seq.size(); ++i) {
+    stats_next_ = i + 1 == seq.size();
+    cycle_launch(seq[i]);
+    cycle_finish();
+  }
+  double loc[6];
+  H2D_HIP(hipMemcpyAsync(loc, d_work_ + kern::stats_work_elems(), sizeof(loc), hipMemcpyDeviceToHost, s_compute_));
+  synchronize();
+  reduce_global(loc, out);
+}
+
+void Solver::reduce_global(const double loc[6], double out[6]) {
   double sums[3] = {loc[0], loc[1], loc[4]};
   double maxs[3] = {loc[3], loc[5], -loc[2]};
   tr_->allreduce(sums, 3, 0);
@@ -774,6 +821,23 @@ void Solver::stats(double out[6], bool residual) {
   out[3] = maxs[0];
   out[4] = sums[2];
   out[5] = maxs[1];
+}
+
+void Solver::stats(double out[6], bool residual) {
+  double loc[6];
+  // the other buffer holds T_{n-1} only after a depth-1 cycle (or a copy-swap step)
+  const bool one_step = cfg_.copy_swap || last_k_ == 1;
+  const void* other = residual && one_step ? buf_[cur_ ^ 1] : nullptr;
+  if (hip_) {
+    synchronize();
+    kern::launch_stats(dtype(), buf_[cur_], other, L_, d_work_, d_work_ + kern::stats_work_elems(), s_compute_);
+    H2D_HIP(hipMemcpyAsync(loc, d_work_ + kern::stats_work_elems(), sizeof(loc), hipMemcpyDeviceToHost, s_compute_));
+    H2D_HIP(hipStreamSynchronize(s_compute_));
+  } else {
+    cpu::stats(dtype(), buf_[cur_], other, L_, loc);
+  }
+  reduce_global(loc, out);
+  if (residual && !one_step) out[4] = out[5] = std::nan("");
 }
 
 void Solver::download(void* host, int64_t ld) { download_region(0, L_.nrows, 0, L_.ncols, host, ld); }

@@ -135,6 +135,14 @@ class RcclTransport final : public Transport {
 class CallbackTransport final : public Transport {
  public:
   CallbackTransport(const CallbackOps& ops, int rank, int size) : ops_(ops), rank_(rank), size_(size) {}
+  ~CallbackTransport() override {
+    if (ev_) {
+      (void)hipEventSynchronize(ev_);
+      (void)hipEventDestroy(ev_);
+    }
+    if (d_stage_) (void)hipFree(d_stage_);
+    if (h_stage_) (void)hipHostFree(h_stage_);
+  }
   int rank() const override { return rank_; }
   int size() const override { return size_; }
   std::string name() const override { return "callback"; }
@@ -144,31 +152,41 @@ class CallbackTransport final : public Transport {
     if (size_ == 1 || k <= 0) return;
     const size_t es = dtype_size(dt);
     const int64_t count = k * L.ncols;
-    stage_.resize((size_t)(4 * count) * es);
-    char* s_lo = stage_.data();
-    char* s_hi = s_lo + count * es;
-    char* r_lo = s_hi + count * es;
-    char* r_hi = r_lo + count * es;
+    const size_t bytes = (size_t)(4 * count) * es;
     const bool has_lo = rank_ > 0, has_hi = rank_ < size_ - 1;
     if (on_device) {
-      // device -> host staging (the reference's path, kept for generic transports)
-      void* d = nullptr;
-      H2D_HIP(hipMallocAsync(&d, (size_t)(2 * count) * es, stream));
-      char* dlo = static_cast<char*>(d);
-      char* dhi = dlo + count * es;
-      if (has_lo) kern::launch_pack_rows(dt, field, L, 0, k, dlo, stream);
-      if (has_hi) kern::launch_pack_rows(dt, field, L, L.nrows - k, k, dhi, stream);
-      H2D_HIP(hipMemcpyAsync(s_lo, d, (size_t)(2 * count) * es, hipMemcpyDeviceToHost, stream));
+      // device -> pinned host staging (the reference's path, kept for generic
+      // transports): buffers grow once and are reused; the previous
+      // exchange's H2D copies must have drained before the host reuses them
+      if (ev_) H2D_HIP(hipEventSynchronize(ev_));
+      else H2D_HIP(hipEventCreateWithFlags(&ev_, hipEventDisableTiming));
+      if (bytes > cap_) {
+        if (d_stage_) H2D_HIP(hipFree(d_stage_));
+        if (h_stage_) H2D_HIP(hipHostFree(h_stage_));
+        H2D_HIP(hipMalloc(&d_stage_, bytes));
+        H2D_HIP(hipHostMalloc(&h_stage_, bytes, hipHostMallocDefault));
+        cap_ = bytes;
+      }
+      char* h = static_cast<char*>(h_stage_);
+      char* d = static_cast<char*>(d_stage_);
+      const size_t half = (size_t)(2 * count) * es;  // [send_lo | send_hi | recv_lo | recv_hi]
+      if (has_lo) kern::launch_pack_rows(dt, field, L, 0, k, d, stream);
+      if (has_hi) kern::launch_pack_rows(dt, field, L, L.nrows - k, k, d + count * es, stream);
+      H2D_HIP(hipMemcpyAsync(h, d, half, hipMemcpyDeviceToHost, stream));
       H2D_HIP(hipStreamSynchronize(stream));
-      int rc = ops_.exchange(ops_.ctx, has_lo ? s_lo : nullptr, has_hi ? s_hi : nullptr,
-                             has_lo ? r_lo : nullptr, has_hi ? r_hi : nullptr, count, (int32_t)dt);
+      int rc = ops_.exchange(ops_.ctx, has_lo ? h : nullptr, has_hi ? h + count * es : nullptr,
+                             has_lo ? h + half : nullptr, has_hi ? h + half + count * es : nullptr, count, (int32_t)dt);
       HEAT2D_REQUIRE(rc == 0, "exchange callback failed");
-      H2D_HIP(hipMemcpyAsync(d, r_lo, (size_t)(2 * count) * es, hipMemcpyHostToDevice, stream));
-      if (has_lo) kern::launch_unpack_rows(dt, field, L, -k, k, dlo, stream);
-      if (has_hi) kern::launch_unpack_rows(dt, field, L, L.nrows, k, dhi, stream);
-      H2D_HIP(hipFreeAsync(d, stream));
-      H2D_HIP(hipStreamSynchronize(stream));
+      H2D_HIP(hipMemcpyAsync(d + half, h + half, half, hipMemcpyHostToDevice, stream));
+      if (has_lo) kern::launch_unpack_rows(dt, field, L, -k, k, d + half, stream);
+      if (has_hi) kern::launch_unpack_rows(dt, field, L, L.nrows, k, d + half + count * es, stream);
+      H2D_HIP(hipEventRecord(ev_, stream));  // no host sync: the next exchange waits on it
     } else {
+      stage_.resize(bytes);
+      char* s_lo = stage_.data();
+      char* s_hi = s_lo + count * es;
+      char* r_lo = s_hi + count * es;
+      char* r_hi = r_lo + count * es;
       if (has_lo) cpu::pack_rows(dt, field, L, 0, k, s_lo);
       if (has_hi) cpu::pack_rows(dt, field, L, L.nrows - k, k, s_hi);
       int rc = ops_.exchange(ops_.ctx, has_lo ? s_lo : nullptr, has_hi ? s_hi : nullptr,
@@ -190,7 +208,11 @@ class CallbackTransport final : public Transport {
  private:
   CallbackOps ops_;
   int rank_, size_;
-  std::vector<char> stage_;
+  std::vector<char> stage_;      // host fields
+  void* d_stage_ = nullptr;      // device fields: [send_lo | send_hi | recv_lo | recv_hi]
+  void* h_stage_ = nullptr;      // pinned host mirror of d_stage_
+  size_t cap_ = 0;
+  hipEvent_t ev_ = nullptr;      // end of the last exchange's H2D copies
 };
 
 // ------------------------------------------------------------------ loopback

@@ -217,7 +217,15 @@ class HeatSolver:
 
     @property
     def tb(self) -> int:
+        """Largest temporal depth this solver may run (the halo / band depth)."""
         return self.info()["tb"]
+
+    @property
+    def pref_depth(self) -> int:
+        """Depth of the balanced cycles when no measured schedule applies."""
+        v = C.c_int32()
+        N.call("heat2d_solver_pref_depth", self._h, C.byref(v))
+        return v.value
 
     @property
     def steps_done(self) -> int:
@@ -234,6 +242,16 @@ class HeatSolver:
         """Advance n time steps (asynchronous on the GPU)."""
         N.call("heat2d_solver_step", self._h, int(n))
 
+    def step_stats(self, n: int) -> dict:
+        """step(n), returning the global statistics of the new field and its
+        one-step residual T_n - T_{n-1}, fused into the last cycle's stencil
+        launch on the HIP engine (no extra pass over the field)."""
+        out = (C.c_double * 6)()
+        N.call("heat2d_solver_step_stats", self._h, int(n), out)
+        s = list(out)
+        return {"sum": s[0], "sum_sq": s[1], "min": s[2], "max": s[3], "residual_l2": float(np.sqrt(s[4])),
+                "residual_max": s[5]}
+
     def run(self, ntime: Optional[int] = None) -> None:
         self.step(self.problem.ntime if ntime is None else ntime)
 
@@ -241,12 +259,14 @@ class HeatSolver:
         N.call("heat2d_solver_sync", self._h)
 
     def stats(self, residual: bool = False) -> dict:
-        """Global (all-rank) statistics of the current field."""
+        """Global (all-rank) statistics of the current field (a separate pass).
+        residual=True: the one-step residual, available only right after a
+        depth-1 cycle (else NaN) — step_stats(n) gives it at any depth."""
         out = (C.c_double * 6)()
         N.call("heat2d_solver_stats", self._h, out, int(residual))
         s = list(out)
         d = {"sum": s[0], "sum_sq": s[1], "min": s[2], "max": s[3]}
-        if residual:
+        if residual:  # NaN unless the last cycle had depth 1 (see step_stats)
             d["residual_l2"] = float(np.sqrt(s[4]))
             d["residual_max"] = s[5]
         return d

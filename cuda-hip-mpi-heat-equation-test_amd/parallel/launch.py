@@ -119,8 +119,12 @@ def run(argv=None) -> int:
     if var.outputs == "serial" and a.output == "ascii" and start_step == 0:
         _write_inclusive(s, prob, "int.dat", world)
 
+    # time_it lines (fortran/hip/heat.F90:241: one per step) do not cut the run
+    # into cycles shorter than the preferred depth: chunks of
+    # max(print_every, pref_depth) steps, every due line printed after its chunk
+    print_chunk = max(a.print_every, s.pref_depth) if a.print_every > 0 else 0
     # plan / autotune outside the timed region: every chunk length the loop below runs
-    rules = [v for v in (a.print_every, a.check_every, a.checkpoint_every) if v > 0]
+    rules = [v for v in (print_chunk, a.check_every, a.checkpoint_every) if v > 0]
     d, seen = start_step, set()
     while d < nsteps:
         c = nsteps - d
@@ -134,20 +138,20 @@ def run(argv=None) -> int:
     s.synchronize()
     t0 = time.perf_counter()
     done = start_step
-    chunk_rules = [v for v in (a.print_every, a.check_every, a.checkpoint_every) if v > 0]
     while done < nsteps:
         chunk = nsteps - done
-        for v in chunk_rules:
+        for v in rules:
             chunk = min(chunk, v - done % v)
-        s.step(chunk)
-        done += chunk
-        if root and a.print_every and done % a.print_every == 0:
-            print(f" time_it: {done:12d}")
-        if a.check_every and done % a.check_every == 0:
-            st = s.stats(residual=True)
+        check = a.check_every > 0 and (done + chunk) % a.check_every == 0
+        st = s.step_stats(chunk) if check else s.step(chunk)  # stats + one-step residual fused into the last cycle
+        before, done = done, done + chunk
+        if root and a.print_every:
+            for t in range((before // a.print_every + 1) * a.print_every, done + 1, a.print_every):
+                print(f" time_it: {t:12d}")
+        if check:
             if root:
                 print(f" step {done}: sum={st['sum']:.17g} min={st['min']:.6g} max={st['max']:.6g} "
-                      f"residual_l2={st['residual_l2']:.6e}", flush=True)
+                      f"residual_l2={st['residual_l2']:.6e} residual_max={st['residual_max']:.6e}", flush=True)
             if not np.isfinite(st["sum"]):
                 raise FloatingPointError(f"non-finite temperature at step {done}")
         if a.checkpoint and a.checkpoint_every and done % a.checkpoint_every == 0 and done < nsteps:

@@ -71,6 +71,24 @@ def test_cli_flags_and_json(cli, tmp_path):
     assert r["n"] == 48 and r["steps"] == 9 and r["dtype"] == "fp32" and r["backend"] == "cpu"
 
 
+def test_cli_time_it_every_step_keeps_deep_cycles(cli, tmp_path):
+    """--print-every 1: one time_it line per step, in order (the reference,
+    fortran/hip/heat.F90:241), without cutting the run into depth-1 cycles:
+    lines are printed after each cycle of pref_depth steps; the result stays
+    bitwise; --check-every prints the fused one-step residual."""
+    (tmp_path / "input.dat").write_text("64 0.25 0.05 1.0 29 0\n")
+    out = run_cli(tmp_path, "--cpu", "--tb", "8", "--print-every", "1", "--check-every", "16", "--output", "npy")
+    steps = [int(l.split()[1]) for l in out.splitlines() if l.strip().startswith("time_it:")]
+    assert steps == list(range(1, 30))
+    checks = [l for l in out.splitlines() if l.strip().startswith("step 16:")]
+    assert len(checks) == 1 and "residual_l2=" in checks[0] and "residual_max=" in checks[0]
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    T16, T15 = R.owned(R.ftcs(prob, 16)), R.owned(R.ftcs(prob, 15))
+    rl2 = float(checks[0].split("residual_l2=")[1].split()[0])
+    assert np.isclose(rl2, np.sqrt(((T16 - T15) ** 2).sum()), rtol=1e-6)
+    assert np.array_equal(np.load(tmp_path / "soln00000.npy"), R.owned(R.ftcs(prob)))
+
+
 def test_cli_bad_input(cli, tmp_path):
     (tmp_path / "input.dat").write_text("10 0.25\n")
     out = subprocess.run([N.CLI_PATH, "--cpu"], cwd=tmp_path, capture_output=True, text=True)

@@ -85,7 +85,26 @@ def test_stats_cpu(native):
     T = R.owned(R.ftcs(p))
     assert np.isclose(st["sum"], T.sum(), rtol=1e-13)
     assert st["max"] == T.max() and st["min"] == T.min()
-    assert st["residual_l2"] > 0
+    # the last cycle had depth 2: the other buffer is T_4, not T_5 -> no residual claimed
+    assert np.isnan(st["residual_l2"]) and np.isnan(st["residual_max"])
+    s.close()
+
+
+@pytest.mark.parametrize("tb,n", [(1, 6), (2, 7), (8, 19)])
+def test_step_stats_cpu(native, tb, n):
+    """step_stats: global statistics + the one-step residual T_n - T_{n-1} at any depth."""
+    p = prob(40, n, "ghost", "sine")
+    s = HeatSolver(p, dtype="fp64", backend="cpu", tb=tb)
+    s.upload(R.owned(R.initial_field(p)))
+    st = s.step_stats(n)
+    T = R.owned(R.ftcs(p))
+    d = T - R.owned(R.ftcs(p, n - 1))
+    assert np.isclose(st["sum"], T.sum(), rtol=1e-13, atol=1e-12)
+    assert st["max"] == T.max() and st["min"] == T.min()
+    assert np.isclose(st["residual_l2"], np.sqrt((d * d).sum()), rtol=1e-12)
+    assert st["residual_max"] == np.abs(d).max()
+    assert np.array_equal(s.download(), T)
+    s.close()
 
 
 def test_upload_download_cpu(native):

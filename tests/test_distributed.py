@@ -50,15 +50,25 @@ def run_world(tmp_path, world, args, timeout=240):
     return got, meta
 
 
-def golden(args):
+def golden(args, steps=None):
     inp = heat2d.InputDat(n=args["n"], sigma=0.25, nu=0.05, dom_len=args.get("dom", 1.0), ntime=args["steps"])
     prob = heat2d.make_problem(inp, args.get("conv", "ghost"), args.get("ic", "uniform"))
     dt = np.float64 if args.get("dtype", "fp64") == "fp64" else np.float32
     if args.get("random"):
         sys.path.insert(0, HERE)
         from dist_worker import random_field
-        return R.owned(R.ftcs(prob, dtype=dt, T0=random_field(prob, args.get("dtype", "fp64"))))
-    return R.owned(R.ftcs(prob, dtype=dt))
+        return R.owned(R.ftcs(prob, steps, dtype=dt, T0=random_field(prob, args.get("dtype", "fp64"))))
+    return R.owned(R.ftcs(prob, steps, dtype=dt))
+
+
+def check_stats(st, args):
+    """Global statistics + one-step residual reduced over the ranks (step_stats)."""
+    T = golden(args).astype(np.float64)
+    d = T - golden(args, args["steps"] - 1).astype(np.float64)
+    assert np.isclose(st["sum"], T.sum(), rtol=1e-12, atol=0)
+    assert st["min"] == T.min() and st["max"] == T.max()
+    assert np.isclose(st["residual_l2"], np.sqrt((d * d).sum()), rtol=1e-10)
+    assert st["residual_max"] == np.abs(d).max()
 
 
 @pytest.mark.parametrize("world,tb", [(2, 1), (2, 8), (3, 3), (4, 5)])
@@ -67,6 +77,7 @@ def test_gloo_cpu_bitwise(native, tmp_path, world, tb):
     got, meta = run_world(tmp_path, world, args)
     assert np.array_equal(got, golden(args))
     assert meta["info"]["size"] == world
+    check_stats(meta["stats"], args)
 
 
 def test_gloo_cpu_inclusive_fp32(native, tmp_path):
@@ -77,12 +88,20 @@ def test_gloo_cpu_inclusive_fp32(native, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,tb,overlap,n", [(2, 8, True, 301), (3, 4, True, 301), (2, 6, False, 301),
-                                                (4, 8, True, 301), (4, 8, True, 60), (2, 10, True, 1500)])
-def test_gloo_hip_ranks_share_gpu(native, gpu, tmp_path, world, tb, overlap, n):
+@pytest.mark.parametrize("world,tb,overlap,n,order", [(2, 8, True, 301, None), (3, 4, True, 301, None),
+                                                      (2, 6, False, 301, None), (4, 8, True, 301, None),
+                                                      (4, 8, True, 60, None), (2, 10, True, 1500, None),
+                                                      (2, 10, True, 1500, "edge-first"),
+                                                      (3, 8, True, 900, "edge-first")])
+def test_gloo_hip_ranks_share_gpu(native, gpu, tmp_path, world, tb, overlap, n, order, monkeypatch):
     """Overlapped schedule (interior on the compute stream, bands + exchange on
-    the comm stream) on random data; n=60 at 4 ranks makes every slab thinner
-    than its two bands (the all-on-comm-stream branch)."""
+    the comm stream; or edge-first) on random data, P processes on the one GPU;
+    n=60 at 4 ranks makes every slab thinner than its two bands (the
+    all-on-comm-stream branch). The last chunk runs with the fused statistics
+    (one general launch, then the exchange), reduced over the ranks."""
+    if order:
+        monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)  # run_world copies os.environ
     args = {"n": n, "steps": 37, "tb": tb, "backend": "hip", "overlap": overlap, "random": True}
     got, meta = run_world(tmp_path, world, args)
     assert np.array_equal(got, golden(args))
+    check_stats(meta["stats"], args)

@@ -158,6 +158,32 @@ def test_graph_split_schedule_bitwise(gpu, native, dtype):
     s.close()
 
 
+@pytest.mark.parametrize("dtype,tb,overlap", [("fp64", 1, True), ("fp64", 8, True), ("fp64", 14, True),
+                                               ("fp64", 14, False), ("fp64", 20, True), ("fp32", 8, True),
+                                               ("fp32", 16, False)])
+def test_step_stats_fused(gpu, native, dtype, tb, overlap):
+    """Statistics of T_n and the ONE-STEP residual T_n - T_{n-1} fused into the
+    last cycle's stencil launch, at any depth, against NumPy; the field itself
+    stays bitwise, and the run continues correctly after the stats cycle."""
+    p = prob(1100, 3 * tb + 2, "ghost", "sine")
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, overlap=overlap)
+    s.upload(R.owned(R.initial_field(p, npdt)))
+    n1 = p.ntime - tb
+    st = s.step_stats(n1)
+    T = R.owned(R.ftcs(p, n1, dtype=npdt)).astype(np.float64)
+    d = T - R.owned(R.ftcs(p, n1 - 1, dtype=npdt)).astype(np.float64)
+    assert np.isclose(st["sum"], T.sum(), rtol=1e-12, atol=1e-9)
+    assert np.isclose(st["sum_sq"], (T * T).sum(), rtol=1e-12)
+    assert st["min"] == T.min() and st["max"] == T.max()
+    assert np.isclose(st["residual_l2"], np.sqrt((d * d).sum()), rtol=1e-10)
+    assert st["residual_max"] == np.abs(d).max()
+    s.step(tb)
+    got = s.download()
+    assert np.array_equal(got, R.owned(R.ftcs(p, dtype=npdt)))
+    s.close()
+
+
 def test_stats_and_residual(gpu, native):
     p = prob(300, 10, "ghost", "uniform")
     s = HeatSolver(p, dtype="fp64", backend="hip", tb=1, device=0)
