@@ -162,10 +162,14 @@ def main():
     if hip:
         torch.cuda.set_device(local)
     if world > 1:
+        # a dead peer fails the run instead of hanging it: torch's own collectives
+        # time out, and the native RCCL transport's watchdog uses the same limit
+        from datetime import timedelta
+        to = timedelta(seconds=float(os.environ.get("HEAT2D_COMM_TIMEOUT", "600")))
         if hip:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=to)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=to)
 
     def sync():
         if hip:

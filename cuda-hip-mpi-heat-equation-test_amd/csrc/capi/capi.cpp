@@ -4,12 +4,17 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <string>
 
 #include "heat2d/config.hpp"
 #include "heat2d/runtime.hpp"
+#include "heat2d/watchdog.hpp"
 
 extern "C" int heat2d_io_write_xyz_impl(const char*, int, const void*, int64_t, int64_t, int64_t,
                                         const double*, const double*, int);
@@ -338,6 +343,53 @@ int heat2d_solver_cycle_hist(void* s, int64_t* out, int n, int reset) {
     HEAT2D_REQUIRE(n >= kMaxTB + 1, "cycle_hist needs kMaxTB + 1 slots");
     static_cast<Solver*>(s)->cycle_hist(out, reset != 0);
   });
+}
+
+int heat2d_watchdog_selftest(double timeout_s, int mode, int progress_polls, double wait_s, double* fired_after_s,
+                             char* reason, int64_t cap) {
+  return guarded([&] {
+    // mode 0: progress for `progress_polls` polls, then pending forever (a hang);
+    // 1: idle forever (nothing outstanding: must never fire); 2: a fabric error
+    std::atomic<int> polls{0};
+    std::atomic<bool> fired{false};
+    const auto t0 = std::chrono::steady_clock::now();
+    double after = -1.0;
+    std::mutex mu;
+    std::string why;
+    {
+      Watchdog wd(
+          timeout_s, 0.02,
+          [&](std::string* d) {
+            const int i = polls++;
+            if (mode == 1) return Watchdog::Idle;
+            if (mode == 2) {
+              *d = "injected";
+              return Watchdog::Error;
+            }
+            if (i < progress_polls) return Watchdog::Progress;
+            *d = "selftest op pending";
+            return Watchdog::Pending;
+          },
+          [&](const std::string& r) {
+            std::lock_guard<std::mutex> g(mu);
+            after = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            why = r;
+            fired = true;
+          });
+      while (!fired && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < wait_s)
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    }
+    *fired_after_s = after;
+    if (reason && cap > 0) {
+      const size_t n = std::min<size_t>((size_t)cap - 1, why.size());
+      std::memcpy(reason, why.data(), n);
+      reason[n] = 0;
+    }
+  });
+}
+
+int heat2d_transport_abort(void* t, const char* reason) {
+  return guarded([&] { static_cast<TransportHandle*>(t)->t->abort(reason ? reason : "aborted by the caller"); });
 }
 
 int heat2d_solver_pref_depth(void* s, int32_t* out) {

@@ -21,7 +21,9 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -120,7 +122,10 @@ struct Shared {
   unsigned char uid[128];
   std::vector<double> t_elapsed;
   std::atomic<int> failed{0};
+  std::mutex mu;  // err, trs
   std::string err;
+  std::vector<std::shared_ptr<Transport>> trs;  // every rank's transport (fail-fast abort)
+  std::vector<std::shared_ptr<Transport>> cpu_trs;  // --cpu with P > 1: the host-thread transports
   double final_stats[6] = {0};
   int tb_used = 1;  // temporal depth the solver actually ran (jit / copy-swap force 1)
   int64_t start_step = 0;  // > 0 after --restart
@@ -177,7 +182,14 @@ void run_rank(Shared& sh, int rank) {
       if (hipSetDevice(rank) != hipSuccess) fail(__FILE__, __LINE__, "hipSetDevice failed");
       if (!a.quiet && (root || P > 1)) std::printf(" MPI rank %12d using GPU %12d\n", rank, rank);
     }
-    tr = P > 1 ? make_rccl_transport(sh.uid, rank, P, a.cpu ? -1 : rank) : make_self_transport();
+    if (P == 1) tr = make_self_transport();
+    else if (a.cpu) tr = sh.cpu_trs[(size_t)rank];  // host threads (the reference's `make mpi`)
+    else tr = make_rccl_transport(sh.uid, rank, P, rank);
+    {
+      std::lock_guard<std::mutex> g(sh.mu);
+      sh.trs[(size_t)rank] = tr;
+      if (sh.failed) tr->abort("another rank failed first");
+    }
 
     SolverConfig cfg{};
     cfg.n_rows = sh.prob.n_owned;
@@ -233,6 +245,12 @@ void run_rank(Shared& sh, int rank) {
     // time_it lines (fortran/hip/heat.F90:241 prints one per step) do not cut
     // the run into cycles shorter than the preferred depth: chunks of
     // max(print_every, pref_depth) steps, every due line printed after its chunk
+    // fault injection for the fail-fast tests: rank HEAT2D_FAIL_RANK throws
+    // once it has run HEAT2D_FAIL_STEP steps (tests/test_cli.py)
+    const char* fr = std::getenv("HEAT2D_FAIL_RANK");
+    const int fail_rank = fr ? std::atoi(fr) : -1;
+    const char* fs = std::getenv("HEAT2D_FAIL_STEP");
+    const int64_t fail_step = fs ? std::atoll(fs) : 0;
     const int64_t print_chunk = a.print_every > 0 ? std::max<int64_t>(a.print_every, s.pref_depth()) : 0;
     {  // walk the chunking of the loop below and prepare each distinct chunk length
       const bool ckpt_every = !a.checkpoint.empty() && a.checkpoint_every > 0;
@@ -260,6 +278,8 @@ void run_rank(Shared& sh, int rank) {
       if (print_chunk > 0) chunk = std::min(chunk, print_chunk - (done % print_chunk));
       if (a.check_every > 0) chunk = std::min(chunk, a.check_every - (done % a.check_every));
       if (ckpt_periodic) chunk = std::min(chunk, a.checkpoint_every - (done % a.checkpoint_every));
+      if (fail_rank == rank && done >= fail_step)  // fault injection (HEAT2D_FAIL_RANK / HEAT2D_FAIL_STEP)
+        fail(__FILE__, __LINE__, "injected failure at step " + std::to_string(done));
       const bool check = a.check_every > 0 && (done + chunk) % a.check_every == 0;
       double st[6];
       if (check) s.step_stats(chunk, st);  // statistics + one-step residual fused into the last cycle
@@ -324,8 +344,14 @@ void run_rank(Shared& sh, int rank) {
       sh.tb_used = s.config().tb;
     }
   } catch (const std::exception& e) {
+    // fail fast: the first error is reported; every rank's communicator is
+    // aborted so that the others, blocked in an exchange or a barrier with
+    // this rank, return with an error instead of hanging in join()
+    std::lock_guard<std::mutex> g(sh.mu);
+    if (!sh.failed) sh.err = "rank " + std::to_string(rank) + ": " + e.what();
     sh.failed = 1;
-    if (sh.err.empty()) sh.err = e.what();
+    for (auto& t : sh.trs)
+      if (t) t->abort("rank " + std::to_string(rank) + " failed: " + e.what());
   }
 }
 
@@ -353,13 +379,14 @@ int main(int argc, char** argv) {
     }
     sh.nranks = a.cpu ? std::max(1, a.gpus) : (a.gpus > 0 ? a.gpus : 1);
     if (!a.cpu && sh.nranks > ndev) fail(__FILE__, __LINE__, "more GPUs requested than present");
-    if (a.cpu && sh.nranks > 1) fail(__FILE__, __LINE__, "--cpu runs one rank (use the Python launcher for CPU multi-rank)");
-    if (sh.nranks > 1) rccl_unique_id(sh.uid);
+    if (a.cpu && sh.nranks > 1) sh.cpu_trs = make_thread_transports(sh.nranks);
+    else if (sh.nranks > 1) rccl_unique_id(sh.uid);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "heat2d: %s\n", e.what());
     return 1;
   }
   sh.t_elapsed.assign((size_t)sh.nranks, 0.0);
+  sh.trs.assign((size_t)sh.nranks, nullptr);
   std::vector<std::thread> th;
   for (int r = 1; r < sh.nranks; ++r) th.emplace_back(run_rank, std::ref(sh), r);
   run_rank(sh, 0);

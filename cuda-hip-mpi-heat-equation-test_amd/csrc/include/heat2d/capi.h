@@ -105,6 +105,12 @@ int heat2d_transport_rccl_loop(int device, void** out);
 int heat2d_transport_callback(heat2d_exchange_fn ex, heat2d_allreduce_fn ar, heat2d_barrier_fn br,
                               void* ctx, int rank, int size, void** out);
 int heat2d_transport_free(void* t);
+/* fail fast: abort the transport's fabric (RCCL: ncclCommAbort); its solver's next synchronisation raises */
+int heat2d_transport_abort(void* t, const char* reason);
+/* watchdog mechanism self-test (no GPU): mode 0 = progress for progress_polls polls then a hang,
+   1 = idle (must not fire), 2 = fabric error. fired_after_s = -1 if it did not fire within wait_s. */
+int heat2d_watchdog_selftest(double timeout_s, int mode, int progress_polls, double wait_s, double* fired_after_s,
+                             char* reason, int64_t cap);
 
 /* Solver. */
 int heat2d_solver_create(const heat2d_config* cfg, void* transport, void** out);

@@ -80,6 +80,12 @@ class Transport {
   // exchange() of the same cycle is enqueued (LoopbackGroup drives this
   // order). Fabrics with their own rendezvous (RCCL) ignore it.
   virtual void post(void* /*field*/, const SlabLayout& /*L*/, hipEvent_t /*bands_ready*/) {}
+  // Fail fast: abort the fabric (RCCL: ncclCommAbort) so that every blocked
+  // operation of this rank returns, and make check() raise `reason`. Called by
+  // the transport's own watchdog (hang / async error) or by a driver whose
+  // other rank failed. Thread-safe, idempotent.
+  virtual void abort(const std::string& /*reason*/) {}
+  virtual bool aborted() const { return false; }
 };
 
 // The messages of one halo exchange, shared by every transport (RCCL sends
@@ -109,6 +115,10 @@ std::shared_ptr<Transport> make_self_transport();
 // events against the neighbours' band kernels (transport.cpp). make_loopback_
 // transports returns the P member transports of one group.
 std::vector<std::shared_ptr<Transport>> make_loopback_transports(int nranks);
+// P ranks as host threads of one process, host-memory fields (CPU backend):
+// barrier-synchronised zero-copy row exchange, fixed-order all-reduce;
+// barriers time out (HEAT2D_COMM_TIMEOUT) and abort() wakes every waiter.
+std::vector<std::shared_ptr<Transport>> make_thread_transports(int nranks);
 // RCCL over xGMI. `uid` = 128-byte ncclUniqueId produced by rccl_unique_id()
 // on rank 0 and broadcast out of band (torch.distributed store, file, or a
 // shared variable for thread-per-GPU).

@@ -29,7 +29,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -772,8 +774,23 @@ void Solver::prepare(int64_t n) {
 void Solver::synchronize() {
   if (!hip_) return;
   H2D_HIP(hipSetDevice(cfg_.device));
-  H2D_HIP(hipStreamSynchronize(s_compute_));
-  if (s_comm_ != s_compute_) H2D_HIP(hipStreamSynchronize(s_comm_));
+  if (!tr_->exchanges()) {
+    H2D_HIP(hipStreamSynchronize(s_compute_));
+    if (s_comm_ != s_compute_) H2D_HIP(hipStreamSynchronize(s_comm_));
+    tr_->check();
+    return;
+  }
+  // exchanging ranks: poll, so that a transport abort (its watchdog, or a
+  // failed peer in the same process) ends the wait with an error instead of a hang
+  for (hipStream_t st : {s_compute_, s_comm_}) {
+    hipError_t q;
+    int spins = 0;
+    while ((q = hipStreamQuery(st)) == hipErrorNotReady) {
+      if (tr_->aborted()) tr_->check();
+      if (++spins > 1000) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    H2D_HIP(q);
+  }
   tr_->check();
 }
 

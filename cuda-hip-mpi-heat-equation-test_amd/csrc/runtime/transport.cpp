@@ -12,10 +12,18 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "heat2d/runtime.hpp"
+#include "heat2d/watchdog.hpp"
 
 namespace heat2d {
 
@@ -46,6 +54,12 @@ class SelfTransport final : public Transport {
 };
 
 // ------------------------------------------------------------------ RCCL
+// Failure detection: every exchange / all-reduce records a completion event;
+// a Watchdog thread polls them and ncclCommGetAsyncError. Outstanding
+// exchanges with none completing for HEAT2D_COMM_TIMEOUT seconds (default
+// 600), or an RCCL async error, abort the communicator (ncclCommAbort: the
+// blocked RCCL kernels and host waits return) and the next check() — every
+// Solver::synchronize — raises with the rank and the reason.
 class RcclTransport final : public Transport {
  public:
   RcclTransport(const void* uid, int rank, int size, int device, bool loop = false)
@@ -57,9 +71,16 @@ class RcclTransport final : public Transport {
     H2D_NCCL(ncclCommInitRank(&comm_, size, id, rank));
     H2D_HIP(hipStreamCreateWithFlags(&aux_, hipStreamNonBlocking));
     H2D_HIP(hipMalloc(&d_scratch_, 64 * sizeof(double)));
+    const double timeout = Watchdog::env_timeout(600.0);
+    if (timeout > 0 && (size_ > 1 || loop_))
+      wd_.reset(new Watchdog(
+          timeout, 0.05, [this](std::string* d) { return poll(d); }, [this](const std::string& r) { abort(r); }));
   }
   ~RcclTransport() override {
+    wd_.reset();  // stop the watchdog before anything it polls goes away
     if (comm_) ncclCommDestroy(comm_);
+    for (auto& p : pend_) (void)hipEventDestroy(p.ev);
+    for (auto e : pool_) (void)hipEventDestroy(e);
     if (d_scratch_) (void)hipFree(d_scratch_);
     if (aux_) (void)hipStreamDestroy(aux_);
   }
@@ -73,12 +94,34 @@ class RcclTransport final : public Transport {
   // graphs).
   bool capturable() const override { return false; }
   bool exchanges() const override { return size_ > 1 || loop_; }
+  bool aborted() const override { return aborted_.load(); }
+
   void check() override {
+    if (aborted_) fail_aborted();
+    std::unique_lock<std::timed_mutex> lk(cmu_);
     ncclResult_t st = ncclSuccess;
     H2D_NCCL(ncclCommGetAsyncError(comm_, &st));
     if (st != ncclSuccess && st != ncclInProgress)
       fail(__FILE__, __LINE__, std::string("RCCL communicator failed asynchronously: ") + ncclGetErrorString(st) +
                                    " (rank " + std::to_string(rank_) + " of " + std::to_string(size_) + ")");
+  }
+
+  void abort(const std::string& reason) override {
+    bool expect = false;
+    if (!aborted_.compare_exchange_strong(expect, true)) return;
+    {
+      std::lock_guard<std::mutex> g(pmu_);
+      abort_reason_ = reason;
+    }
+    // the comm lock keeps a host thread from entering RCCL on a freed
+    // communicator; if the host thread is itself stuck inside an RCCL call
+    // (holding it), abort anyway: that is the hang being broken
+    std::unique_lock<std::timed_mutex> lk(cmu_, std::defer_lock);
+    (void)lk.try_lock_for(std::chrono::seconds(2));
+    if (comm_) {
+      (void)ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
   }
 
   void exchange(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
@@ -98,12 +141,17 @@ class RcclTransport final : public Transport {
     } else {
       nmsg = halo_msgs(rank_, size_, L, k, msg);
     }
-    H2D_NCCL(ncclGroupStart());
-    for (int i = 0; i < nmsg; ++i) {
-      H2D_NCCL(ncclSend(base + halo_row_bytes(L, msg[i].send_row, es), count, t, msg[i].peer, comm_, stream));
-      H2D_NCCL(ncclRecv(base + halo_row_bytes(L, msg[i].recv_row, es), count, t, msg[i].peer, comm_, stream));
+    {
+      std::unique_lock<std::timed_mutex> lk(cmu_);
+      live();
+      H2D_NCCL(ncclGroupStart());
+      for (int i = 0; i < nmsg; ++i) {
+        H2D_NCCL(ncclSend(base + halo_row_bytes(L, msg[i].send_row, es), count, t, msg[i].peer, comm_, stream));
+        H2D_NCCL(ncclRecv(base + halo_row_bytes(L, msg[i].recv_row, es), count, t, msg[i].peer, comm_, stream));
+      }
+      H2D_NCCL(ncclGroupEnd());
     }
-    H2D_NCCL(ncclGroupEnd());
+    track(stream, "halo exchange");
   }
 
   void allreduce(double* vals, int n, int op) override {
@@ -111,9 +159,21 @@ class RcclTransport final : public Transport {
     H2D_HIP(hipSetDevice(device_));
     H2D_HIP(hipMemcpyAsync(d_scratch_, vals, n * sizeof(double), hipMemcpyHostToDevice, aux_));
     const ncclRedOp_t o = op == 0 ? ncclSum : (op == 1 ? ncclMax : ncclMin);
-    H2D_NCCL(ncclAllReduce(d_scratch_, d_scratch_, n, ncclFloat64, o, comm_, aux_));
+    {
+      std::unique_lock<std::timed_mutex> lk(cmu_);
+      live();
+      H2D_NCCL(ncclAllReduce(d_scratch_, d_scratch_, n, ncclFloat64, o, comm_, aux_));
+    }
+    track(aux_, "all-reduce");
     H2D_HIP(hipMemcpyAsync(vals, d_scratch_, n * sizeof(double), hipMemcpyDeviceToHost, aux_));
-    H2D_HIP(hipStreamSynchronize(aux_));
+    // poll instead of blocking, so an abort by the watchdog ends the wait
+    hipError_t q;
+    while ((q = hipStreamQuery(aux_)) == hipErrorNotReady) {
+      if (aborted_) check();
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    H2D_HIP(q);
+    check();
   }
   void barrier() override {
     double v = 0.0;
@@ -121,12 +181,90 @@ class RcclTransport final : public Transport {
   }
 
  private:
+  [[noreturn]] void fail_aborted() {
+    std::string why;
+    {
+      std::lock_guard<std::mutex> g(pmu_);
+      why = abort_reason_;
+    }
+    fail(__FILE__, __LINE__, "RCCL communicator aborted (rank " + std::to_string(rank_) + " of " +
+                                 std::to_string(size_) + "): " + why);
+  }
+  void live() {  // with cmu_ held
+    if (aborted_ || !comm_) fail_aborted();
+  }
+  // record a completion event of the operation just enqueued on `s` (watchdog)
+  void track(hipStream_t s, const char* what) {
+    if (!wd_) return;
+    std::lock_guard<std::mutex> g(pmu_);
+    if (pend_.size() >= 4096) return;  // the host is far ahead: the oldest ones tell the story
+    hipEvent_t e = nullptr;
+    if (!pool_.empty()) {
+      e = pool_.back();
+      pool_.pop_back();
+    } else {
+      H2D_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    H2D_HIP(hipEventRecord(e, s));
+    pend_.push_back(Pend{e, ++nops_, what});
+  }
+  // watchdog thread: completions since the last poll
+  Watchdog::Status poll(std::string* detail) {
+    if (aborted_) return Watchdog::Idle;
+    static thread_local int dev_set = -1;
+    if (dev_set != device_) {
+      (void)hipSetDevice(device_);
+      dev_set = device_;
+    }
+    {
+      std::unique_lock<std::timed_mutex> lk(cmu_, std::defer_lock);
+      if (lk.try_lock_for(std::chrono::milliseconds(10)) && comm_) {
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(comm_, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress) {
+          *detail = std::string("ncclCommGetAsyncError: ") + ncclGetErrorString(st);
+          return Watchdog::Error;
+        }
+      }
+    }
+    std::lock_guard<std::mutex> g(pmu_);
+    int done = 0;
+    while (!pend_.empty()) {
+      const hipError_t q = hipEventQuery(pend_.front().ev);
+      if (q == hipErrorNotReady) break;
+      if (q != hipSuccess) {
+        *detail = std::string("hipEventQuery: ") + hipGetErrorString(q);
+        return Watchdog::Error;
+      }
+      pool_.push_back(pend_.front().ev);
+      pend_.pop_front();
+      ++done;
+    }
+    if (done) return Watchdog::Progress;
+    if (pend_.empty()) return Watchdog::Idle;
+    *detail = std::string(pend_.front().what) + " #" + std::to_string(pend_.front().seq) + " of rank " +
+              std::to_string(rank_) + " of " + std::to_string(size_) + " still pending";
+    return Watchdog::Pending;
+  }
+
+  struct Pend {
+    hipEvent_t ev;
+    int64_t seq;
+    const char* what;
+  };
   int rank_, size_;
   bool loop_ = false;
   int device_ = 0;
   ncclComm_t comm_ = nullptr;
   hipStream_t aux_ = nullptr;
   double* d_scratch_ = nullptr;
+  std::timed_mutex cmu_;  // comm_ vs the watchdog's abort
+  std::mutex pmu_;        // pend_ / pool_ / abort_reason_
+  std::deque<Pend> pend_;
+  std::vector<hipEvent_t> pool_;
+  int64_t nops_ = 0;
+  std::atomic<bool> aborted_{false};
+  std::string abort_reason_;
+  std::unique_ptr<Watchdog> wd_;
 };
 
 // ------------------------------------------------------------------ callbacks
@@ -307,9 +445,136 @@ class LoopbackTransport final : public Transport {
   int rank_;
 };
 
+// ------------------------------------------------------------------ host threads
+// P ranks as host threads of one process with host-memory fields (the CPU
+// twin): the native CLI's `--cpu --gpus P`, the reference's `make mpi` CPU
+// MPI build (fortran/mpi+cuda/makefile:1-2). An exchange publishes this
+// rank's field, meets the others at a barrier, copies its ghost rows straight
+// out of the neighbours' fields (halo_msgs, as RCCL), and meets them again
+// before anyone overwrites a field. Barriers time out after
+// HEAT2D_COMM_TIMEOUT seconds and can be aborted (a failed rank), so a dead
+// or failed thread never leaves the others blocked.
+struct ThreadHub {
+  explicit ThreadHub(int n) : n(n), field((size_t)n), layout((size_t)n), vals((size_t)n * 64) {
+    timeout = Watchdog::env_timeout(600.0);
+  }
+  void barrier(int rank) {
+    std::unique_lock<std::mutex> lk(mu);
+    if (aborted) throw_aborted(rank);
+    const int64_t g = gen;
+    if (++count == n) {
+      count = 0;
+      ++gen;
+      cv.notify_all();
+      return;
+    }
+    const auto pred = [&] { return gen != g || aborted; };
+    if (timeout > 0) {
+      if (!cv.wait_for(lk, std::chrono::duration<double>(timeout), pred)) {
+        aborted = true;
+        reason = "rank " + std::to_string(rank) + " waited " + std::to_string(timeout) +
+                 " s at a barrier (HEAT2D_COMM_TIMEOUT): a peer rank is dead or hung";
+        cv.notify_all();
+      }
+    } else {
+      cv.wait(lk, pred);
+    }
+    if (aborted) throw_aborted(rank);
+  }
+  void abort(const std::string& why) {
+    std::lock_guard<std::mutex> g(mu);
+    if (!aborted) reason = why;
+    aborted = true;
+    cv.notify_all();
+  }
+  [[noreturn]] void throw_aborted(int rank) {
+    fail(__FILE__, __LINE__, "host-thread transport aborted (rank " + std::to_string(rank) + " of " +
+                                 std::to_string(n) + "): " + reason);
+  }
+  const int n;
+  double timeout = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int64_t gen = 0;
+  int count = 0;
+  bool aborted = false;
+  std::string reason;
+  std::vector<char*> field;
+  std::vector<SlabLayout> layout;
+  std::vector<double> vals;  // allreduce slots, 64 per rank
+};
+
+class ThreadTransport final : public Transport {
+ public:
+  ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int size() const override { return hub_->n; }
+  std::string name() const override { return "host-threads"; }
+  void abort(const std::string& reason) override { hub_->abort(reason); }
+  bool aborted() const override {
+    std::lock_guard<std::mutex> g(hub_->mu);
+    return hub_->aborted;
+  }
+  void check() override {
+    std::unique_lock<std::mutex> lk(hub_->mu);
+    if (hub_->aborted) hub_->throw_aborted(rank_);
+  }
+
+  void exchange(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t, bool on_device) override {
+    HEAT2D_REQUIRE(!on_device, "the host-thread transport moves host-memory fields (CPU backend)");
+    if (size() == 1 || k <= 0) return;
+    hub_->field[(size_t)rank_] = static_cast<char*>(field);
+    hub_->layout[(size_t)rank_] = L;
+    hub_->barrier(rank_);  // every rank's new field is published
+    const size_t es = dtype_size(dt);
+    HaloMsg msg[2];
+    const int nmsg = halo_msgs(rank_, size(), L, k, msg);
+    for (int i = 0; i < nmsg; ++i) {
+      const int p = msg[i].peer;
+      const SlabLayout& PL = hub_->layout[(size_t)p];
+      HEAT2D_REQUIRE(PL.pitch == L.pitch, "slabs of different pitch");
+      HaloMsg pm[2];
+      const int np = halo_msgs(p, size(), PL, k, pm);
+      for (int j = 0; j < np; ++j)
+        if (pm[j].peer == rank_)
+          std::memcpy(static_cast<char*>(field) + halo_row_bytes(L, msg[i].recv_row, es),
+                      hub_->field[(size_t)p] + halo_row_bytes(PL, pm[j].send_row, es), halo_msg_bytes(L, k, es));
+    }
+    hub_->barrier(rank_);  // nobody moves on (and overwrites its field) before all copies are done
+  }
+  void allreduce(double* vals, int n, int op) override {
+    HEAT2D_REQUIRE(n <= 64, "allreduce too large");
+    if (size() == 1) return;
+    std::copy(vals, vals + n, hub_->vals.begin() + (ptrdiff_t)rank_ * 64);
+    hub_->barrier(rank_);
+    for (int j = 0; j < n; ++j) {  // same fixed order on every rank: identical results
+      double a = hub_->vals[(size_t)j];
+      for (int r = 1; r < size(); ++r) {
+        const double b = hub_->vals[(size_t)r * 64 + j];
+        a = op == 0 ? a + b : (op == 1 ? std::max(a, b) : std::min(a, b));
+      }
+      vals[j] = a;
+    }
+    hub_->barrier(rank_);
+  }
+  void barrier() override { hub_->barrier(rank_); }
+
+ private:
+  std::shared_ptr<ThreadHub> hub_;
+  int rank_;
+};
+
 }  // namespace
 
 std::shared_ptr<Transport> make_self_transport() { return std::make_shared<SelfTransport>(); }
+
+std::vector<std::shared_ptr<Transport>> make_thread_transports(int nranks) {
+  HEAT2D_REQUIRE(nranks >= 1, "nranks >= 1");
+  auto hub = std::make_shared<ThreadHub>(nranks);
+  std::vector<std::shared_ptr<Transport>> v;
+  for (int i = 0; i < nranks; ++i) v.push_back(std::make_shared<ThreadTransport>(hub, i));
+  return v;
+}
 
 std::vector<std::shared_ptr<Transport>> make_loopback_transports(int nranks) {
   HEAT2D_REQUIRE(nranks >= 1, "nranks >= 1");

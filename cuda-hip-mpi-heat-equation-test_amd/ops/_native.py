@@ -166,6 +166,9 @@ _SIGS = {
     "heat2d_group_upload": (C.c_int, [_P, _P, _I64]),
     "heat2d_group_member": (C.c_int, [_P, C.c_int, C.POINTER(_P)]),
     "heat2d_solver_cycle_hist": (C.c_int, [_P, C.POINTER(C.c_int64), C.c_int, C.c_int]),
+    "heat2d_transport_abort": (C.c_int, [_P, C.c_char_p]),
+    "heat2d_watchdog_selftest": (C.c_int, [C.c_double, C.c_int, C.c_int, C.c_double, C.POINTER(C.c_double),
+                                           C.c_char_p, _I64]),
     "heat2d_solver_pref_depth": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "heat2d_solver_step_stats": (C.c_int, [_P, _I64, C.POINTER(C.c_double)]),
     "heat2d_solver_schedule": (C.c_int, [_P, _I64, C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64)]),

@@ -62,10 +62,12 @@ def _dist_setup(backend: str):
     if backend == "hip":
         torch.cuda.set_device(local)
     if world > 1 and not dist.is_initialized():
+        from datetime import timedelta
+        to = timedelta(seconds=float(os.environ.get("HEAT2D_COMM_TIMEOUT", "600")))  # dead peer -> error, not hang
         if backend == "hip":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=to)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=to)
     return rank, world, local
 
 

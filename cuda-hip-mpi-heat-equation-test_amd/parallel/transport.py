@@ -39,6 +39,11 @@ class Transport:
     def handle(self):
         return self._h
 
+    def abort(self, reason: str = "aborted by the caller") -> None:
+        """Fail fast (RCCL: ncclCommAbort): blocked exchanges return and the
+        solver's next synchronisation raises ``reason``."""
+        N.call("heat2d_transport_abort", self._h, reason.encode())
+
     def close(self) -> None:
         if self._h:
             N.call("heat2d_transport_free", self._h)
@@ -59,7 +64,11 @@ class SelfTransport(Transport):
 
 
 class RcclTransport(Transport):
-    """RCCL communicator created from an ncclUniqueId (collective over all ranks)."""
+    """RCCL communicator created from an ncclUniqueId (collective over all ranks).
+
+    A watchdog thread aborts the communicator when outstanding exchanges stop
+    completing for ``$HEAT2D_COMM_TIMEOUT`` seconds (default 600, 0 = off) or
+    RCCL reports an async error; the rank then raises instead of hanging."""
 
     def __init__(self, rank: int, size: int, device: int, uid: Optional[bytes] = None, group=None):
         if uid is None:

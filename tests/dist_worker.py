@@ -33,7 +33,10 @@ def main():
     from heat2d.models.heat2d import HeatSolver
     from heat2d.parallel.transport import TorchDistTransport
 
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    from datetime import timedelta
+    timeout = float(os.environ.get("HEAT2D_COMM_TIMEOUT", "600"))
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=timedelta(seconds=timeout))
     inp = heat2d.InputDat(n=args["n"], sigma=0.25, nu=0.05, dom_len=args.get("dom", 1.0), ntime=args["steps"])
     prob = heat2d.make_problem(inp, args.get("conv", "ghost"), args.get("ic", "uniform"))
     backend = args.get("backend", "cpu")
@@ -50,6 +53,10 @@ def main():
     # split the stepping to exercise restarts of the cycle schedule
     first = args["steps"] // 3
     s.step(first)
+    if args.get("die_rank") == rank:  # failure injection: this rank dies mid-run (tests/test_watchdog.py)
+        s.step(args.get("die_after", 0))
+        sys.stdout.flush()
+        os._exit(3)
     # the rest with the global statistics + one-step residual of the final field
     st = s.step_stats(args["steps"] - first)
     full = s.gather()

@@ -89,6 +89,38 @@ def test_cli_time_it_every_step_keeps_deep_cycles(cli, tmp_path):
     assert np.array_equal(np.load(tmp_path / "soln00000.npy"), R.owned(R.ftcs(prob)))
 
 
+@pytest.mark.parametrize("P", [2, 3])
+def test_cli_cpu_multirank(cli, tmp_path, P):
+    """`heat2d --cpu --gpus P`: P host-thread ranks of the CPU twin exchanging
+    halos through the host-thread transport (the reference's `make mpi` CPU
+    MPI build): per-rank soln%05d.dat, bitwise the golden, and the global sum
+    all-reduced over the ranks."""
+    (tmp_path / "input.dat").write_text("67 0.25 0.05 1.0 23 1\n")
+    out = run_cli(tmp_path, "--cpu", "--gpus", str(P), "--tb", "4", "--check-every", "23")
+    assert f"Automatic MPI decomposition: {P:12d}  x 1" in out
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    T = R.owned(R.ftcs(prob))
+    parts = [read_xyz(tmp_path / f"soln{r:05d}.dat")[:, 2] for r in range(P)]
+    assert np.array_equal(np.concatenate(parts), T.ravel())
+    line = [l for l in out.splitlines() if l.strip().startswith("step 23:")][0]
+    assert np.isclose(float(line.split("sum=")[1].split()[0]), T.sum(), rtol=1e-13)
+
+
+def test_cli_failing_rank_fails_fast(cli, tmp_path):
+    """One rank fails mid-run (fault injection): the others, blocked exchanging
+    with it, are aborted and the process exits non-zero at once naming the
+    failed rank — no hang in join()."""
+    import time
+    (tmp_path / "input.dat").write_text("64 0.25 0.05 1.0 400 0\n")
+    env = dict(os.environ, HEAT2D_FAIL_RANK="1", HEAT2D_FAIL_STEP="8", HEAT2D_COMM_TIMEOUT="60")
+    t0 = time.time()
+    p = subprocess.run([N.CLI_PATH, "--cpu", "--gpus", "3", "--tb", "4", "--print-every", "4"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode != 0
+    assert "rank 1" in p.stderr and "injected failure" in p.stderr, p.stderr
+    assert time.time() - t0 < 30
+
+
 def test_cli_bad_input(cli, tmp_path):
     (tmp_path / "input.dat").write_text("10 0.25\n")
     out = subprocess.run([N.CLI_PATH, "--cpu"], cwd=tmp_path, capture_output=True, text=True)

@@ -40,6 +40,7 @@ def run(tmp_path, text, *args):
     ["--cpu", "--copy-swap"],
     ["--cpu", "--check-every", "3", "--print-every", "4", "--json", "run.json", "--timers"],
     ["--cpu", "--checkpoint", "ck", "--checkpoint-every", "5"],
+    ["--cpu", "--gpus", "3", "--tb", "4", "--check-every", "6"],  # host-thread ranks: exchange + all-reduce
 ])
 def test_cli_cpu_paths_clean(tmp_path, args):
     p = run(tmp_path, "67 0.25 0.05 2.0 23 1\n", *args)
