@@ -134,7 +134,7 @@ struct Shared {
 // Collective checkpoint (every rank its slab, then rank 0 publishes meta.json).
 void save_checkpoint(Shared& sh, Solver& s, Transport& tr, int rank, int64_t step) {
   const Args& a = sh.args;
-  ckpt::write_rank(a.checkpoint, rank, s);
+  ckpt::write_rank(a.checkpoint, rank, step, s);
   tr.barrier();
   if (rank == 0) {
     ckpt::Meta m;
@@ -219,7 +219,7 @@ void run_rank(Shared& sh, int rank) {
       HEAT2D_REQUIRE(m.convention == (inclusive ? "inclusive" : "ghost"), "checkpoint grid convention differs");
       const SlabLayout& L = s.layout();
       std::vector<char> host((size_t)(L.nrows * L.ncols) * dtype_size(s.dtype()));
-      ckpt::read_rows(a.restart, m, L.row0, L.nrows, L.ncols, (int)s.dtype(), host.data());
+      ckpt::read_rows(m, L.row0, L.nrows, L.ncols, (int)s.dtype(), host.data());
       s.upload(host.data(), L.ncols);  // + halo exchange
       start = std::min<int64_t>(m.step, sh.in.ntime);
       if (root) {

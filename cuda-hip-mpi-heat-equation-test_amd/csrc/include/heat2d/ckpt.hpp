@@ -17,17 +17,24 @@ struct Meta {
   int64_t n_owned = 0, n_input = 0;
   std::string convention = "ghost";  // ghost | inclusive
   double sigma = 0, nu = 0, dom_len = 0, r = 0;
+  std::string dir;  // read_meta: the directory holding this step's files
 };
 
-// Collective use: every rank writes its slab, then (after a barrier) rank 0
-// publishes meta.json atomically (temp file + rename), then a barrier.
-void write_rank(const std::string& dir, int rank, Solver& s);
+// Layout (v2): DIR/step-NNNNNNNNNNNN/{rankNNNNN.npy, meta.json} + DIR/latest,
+// a one-line pointer to the newest COMPLETE step directory. Collective use:
+// every rank writes its slab into the step's own directory; after a barrier
+// rank 0 writes meta.json there, then republishes DIR/latest (temp file +
+// rename, atomic) and prunes all but the two newest step directories. A crash
+// at any point leaves `latest` on a complete checkpoint; rank files of two
+// steps can never be mixed. read_meta also accepts a step directory itself
+// and the v1 flat layout (DIR/meta.json + DIR/rank*.npy).
+void write_rank(const std::string& dir, int rank, int64_t step, Solver& s);
 void write_meta(const std::string& dir, const Meta& m);
 Meta read_meta(const std::string& dir);
 // Global rows [row0, row0 + nrows) x ncols of the checkpointed field into `out`
-// (row-major, ld = ncols), gathered from however many writer files there are.
-void read_rows(const std::string& dir, const Meta& m, int64_t row0, int64_t nrows, int64_t ncols, int dtype,
-               void* out);
+// (row-major, ld = ncols), gathered from however many writer files there are
+// (their shapes checked against the writer's decomposition).
+void read_rows(const Meta& m, int64_t row0, int64_t nrows, int64_t ncols, int dtype, void* out);
 
 }  // namespace ckpt
 }  // namespace heat2d

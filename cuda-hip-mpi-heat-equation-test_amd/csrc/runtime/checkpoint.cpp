@@ -1,7 +1,8 @@
 // Checkpoint / restart for the native CLI, in the SAME on-disk format as the
-// Python driver (utils/checkpoint.py, "heat2d-checkpoint-v1"):
-//   DIR/meta.json          problem + solver parameters + completed step count
-//   DIR/rankNNNNN.npy      each rank's owned rows (NumPy v1 header, C order)
+// Python driver (utils/checkpoint.py, "heat2d-checkpoint-v2", ckpt.hpp):
+//   DIR/step-NNNNNNNNNNNN/rankNNNNN.npy  each rank's owned rows (NumPy v1 header, C order)
+//   DIR/step-NNNNNNNNNNNN/meta.json      problem + solver parameters + completed step count
+//   DIR/latest                           the newest complete step (atomic commit point)
 // so a run can checkpoint from `heat2d --gpus 8` and resume under torchrun
 // (or the other way round), on any rank count: restart reads each writer
 // file's row range that overlaps this rank's slab. The reference has no
@@ -13,7 +14,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <dirent.h>
 #include <sys/stat.h>
+#include <unistd.h>
 #include <vector>
 
 #include "heat2d/capi.h"
@@ -25,9 +28,30 @@ namespace ckpt {
 
 namespace {
 
-constexpr const char* kFormat = "heat2d-checkpoint-v1";
+constexpr const char* kFormat = "heat2d-checkpoint-v2";
+constexpr const char* kFormatV1 = "heat2d-checkpoint-v1";  // flat layout, still readable
 
 std::string join(const std::string& dir, const std::string& name) { return dir + "/" + name; }
+
+std::string step_name(int64_t step) {
+  char b[32];
+  std::snprintf(b, sizeof(b), "step-%012lld", (long long)step);
+  return b;
+}
+
+bool exists(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0;
+}
+
+void write_atomic(const std::string& path, const std::string& text) {
+  const std::string tmp = path + ".tmp";
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  HEAT2D_REQUIRE(f != nullptr, "cannot write " + tmp);
+  const bool ok = std::fwrite(text.data(), 1, text.size(), f) == text.size();
+  HEAT2D_REQUIRE(std::fclose(f) == 0 && ok, "error writing " + tmp);
+  HEAT2D_REQUIRE(std::rename(tmp.c_str(), path.c_str()) == 0, "cannot publish " + path);
+}
 
 std::string rank_file(const std::string& dir, int rank) {
   char b[32];
@@ -121,33 +145,61 @@ NpyInfo npy_header(FILE* f, const std::string& path) {
 
 }  // namespace
 
-void write_rank(const std::string& dir, int rank, Solver& s) {
+void write_rank(const std::string& dir, int rank, int64_t step, Solver& s) {
   ::mkdir(dir.c_str(), 0755);  // all ranks may race on it: EEXIST is fine
+  const std::string sd = join(dir, step_name(step));
+  ::mkdir(sd.c_str(), 0755);
   const SlabLayout& L = s.layout();
   std::vector<char> host((size_t)(L.nrows * L.ncols) * dtype_size(s.dtype()));
   s.download(host.data(), L.ncols);
-  if (heat2d_write_npy(rank_file(dir, rank).c_str(), (int)s.dtype(), host.data(), L.nrows, L.ncols, L.ncols))
+  if (heat2d_write_npy(rank_file(sd, rank).c_str(), (int)s.dtype(), host.data(), L.nrows, L.ncols, L.ncols))
     fail(__FILE__, __LINE__, heat2d_last_error());
 }
 
 void write_meta(const std::string& dir, const Meta& m) {
-  const std::string tmp = join(dir, "meta.json.tmp");
-  FILE* f = std::fopen(tmp.c_str(), "wb");
-  HEAT2D_REQUIRE(f != nullptr, "cannot write " + tmp);
-  std::fprintf(f,
-               "{\n \"format\": \"%s\",\n \"step\": %lld,\n \"nranks\": %d,\n \"dtype\": \"%s\",\n"
-               " \"n_owned\": %lld,\n \"n_input\": %lld,\n \"convention\": \"%s\",\n \"sigma\": %.17g,\n"
-               " \"nu\": %.17g,\n \"dom_len\": %.17g,\n \"r\": %.17g,\n \"rows\": [],\n \"writer\": \"heat2d-cli\"\n}\n",
-               kFormat, (long long)m.step, m.nranks, m.dtype == 0 ? "fp32" : "fp64", (long long)m.n_owned,
-               (long long)m.n_input, m.convention.c_str(), m.sigma, m.nu, m.dom_len, m.r);
-  HEAT2D_REQUIRE(std::fclose(f) == 0, "error writing " + tmp);
-  HEAT2D_REQUIRE(std::rename(tmp.c_str(), join(dir, "meta.json").c_str()) == 0, "cannot publish meta.json");
+  const std::string name = step_name(m.step);
+  char buf[1024];
+  std::snprintf(buf, sizeof(buf),
+                "{\n \"format\": \"%s\",\n \"step\": %lld,\n \"nranks\": %d,\n \"dtype\": \"%s\",\n"
+                " \"n_owned\": %lld,\n \"n_input\": %lld,\n \"convention\": \"%s\",\n \"sigma\": %.17g,\n"
+                " \"nu\": %.17g,\n \"dom_len\": %.17g,\n \"r\": %.17g,\n \"writer\": \"heat2d-cli\"\n}\n",
+                kFormat, (long long)m.step, m.nranks, m.dtype == 0 ? "fp32" : "fp64", (long long)m.n_owned,
+                (long long)m.n_input, m.convention.c_str(), m.sigma, m.nu, m.dom_len, m.r);
+  write_atomic(join(join(dir, name), "meta.json"), buf);
+  write_atomic(join(dir, "latest"), name + "\n");  // the commit point
+  // prune: keep the two newest complete steps (names sort by step)
+  std::vector<std::string> steps;
+  if (DIR* d = ::opendir(dir.c_str())) {
+    while (dirent* e = ::readdir(d))
+      if (std::strncmp(e->d_name, "step-", 5) == 0) steps.push_back(e->d_name);
+    ::closedir(d);
+  }
+  std::sort(steps.begin(), steps.end());
+  const auto cur = std::find(steps.begin(), steps.end(), name);
+  for (auto it = steps.begin(); cur != steps.end() && it + 1 < cur; ++it) {
+    const std::string sd = join(dir, *it);
+    if (DIR* d = ::opendir(sd.c_str())) {
+      while (dirent* e = ::readdir(d))
+        if (e->d_name[0] != '.') ::unlink(join(sd, e->d_name).c_str());
+      ::closedir(d);
+    }
+    ::rmdir(sd.c_str());
+  }
 }
 
 Meta read_meta(const std::string& dir) {
-  const std::string js = read_text(join(dir, "meta.json"));
-  HEAT2D_REQUIRE(json_value(js, "format") == kFormat, dir + ": not a " + kFormat + " checkpoint");
+  std::string sd = dir;
+  if (exists(join(dir, "latest"))) {
+    std::string name = read_text(join(dir, "latest"));
+    while (!name.empty() && (name.back() == '\n' || name.back() == ' ')) name.pop_back();
+    sd = join(dir, name);
+  }
+  HEAT2D_REQUIRE(exists(join(sd, "meta.json")), dir + ": no checkpoint (neither latest nor meta.json)");
+  const std::string js = read_text(join(sd, "meta.json"));
+  const std::string fmt = json_value(js, "format");
+  HEAT2D_REQUIRE(fmt == kFormat || fmt == kFormatV1, dir + ": not a heat2d checkpoint (" + fmt + ")");
   Meta m;
+  m.dir = sd;
   m.step = std::atoll(json_value(js, "step").c_str());
   m.nranks = std::atoi(json_value(js, "nranks").c_str());
   m.dtype = json_value(js, "dtype") == "fp32" ? 0 : 1;
@@ -162,17 +214,18 @@ Meta read_meta(const std::string& dir) {
   return m;
 }
 
-void read_rows(const std::string& dir, const Meta& m, int64_t row0, int64_t nrows, int64_t ncols, int dtype,
-               void* out) {
+void read_rows(const Meta& m, int64_t row0, int64_t nrows, int64_t ncols, int dtype, void* out) {
   HEAT2D_REQUIRE(dtype == m.dtype, "checkpoint dtype differs from the run's --dtype");
   const size_t es = dtype == 0 ? 4 : 8;
   int64_t start = 0;  // global row of the current writer file's first row
   for (int r = 0; r < m.nranks; ++r) {
-    const std::string path = rank_file(dir, r);
+    const std::string path = rank_file(m.dir, r);
     File file(path, "rb");
     FILE* f = file.f;
     const NpyInfo info = npy_header(f, path);
     HEAT2D_REQUIRE(info.cols == ncols && info.dtype == dtype, path + ": shape / dtype differ from the run");
+    HEAT2D_REQUIRE(info.rows == decompose(m.n_owned, m.nranks, r).nrows,
+                   path + ": row count differs from the writer's decomposition");
     const int64_t a = std::max(row0, start), b = std::min(row0 + nrows, start + info.rows);
     if (a < b) {
       const long off = info.data_off + (long)((a - start) * ncols * (int64_t)es);
@@ -183,7 +236,7 @@ void read_rows(const std::string& dir, const Meta& m, int64_t row0, int64_t nrow
     }
     start += info.rows;
   }
-  HEAT2D_REQUIRE(start == m.n_owned, dir + ": rank files do not cover the grid");
+  HEAT2D_REQUIRE(start == m.n_owned, m.dir + ": rank files do not cover the grid");
 }
 
 }  // namespace ckpt

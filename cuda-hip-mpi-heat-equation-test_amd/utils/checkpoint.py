@@ -1,9 +1,16 @@
 """Checkpoint / restart (absent in the reference: its only dumps, int.dat /
 soln.dat / soln%05d.dat, are never read back — SURVEY.md §5).
 
-Layout of a checkpoint directory:
-    meta.json           problem + solver parameters + completed step count
-    rank00000.npy ...   each rank's owned rows (plain .npy, loaded with allow_pickle=False)
+Layout (v2, shared with the native CLI, csrc/runtime/checkpoint.cpp):
+    DIR/step-NNNNNNNNNNNN/rank00000.npy ...  each rank's owned rows (plain .npy, allow_pickle=False)
+    DIR/step-NNNNNNNNNNNN/meta.json          problem + solver parameters + completed step count
+    DIR/latest                               the newest COMPLETE step directory (atomic commit point)
+
+Every step is written into its own directory; only after all rank files and
+meta.json are there does rank 0 republish ``latest`` (temp file + rename) and
+prune all but the two newest steps. A crash at any point leaves ``latest`` on a
+complete checkpoint — rank files of two different steps are never mixed.
+Readers also accept a step directory itself and the v1 flat layout.
 
 Restart re-decomposes: a run on P ranks can resume a checkpoint written by Q
 ranks (each rank memory-maps the rank files and copies its own row range), so
@@ -14,45 +21,74 @@ from __future__ import annotations
 
 import json
 import os
+import shutil
 from typing import Optional
 
 import numpy as np
 
-FORMAT = "heat2d-checkpoint-v1"
+FORMAT = "heat2d-checkpoint-v2"
+FORMATS = (FORMAT, "heat2d-checkpoint-v1")
+
+
+def step_dir(directory: str, step: int) -> str:
+    return os.path.join(directory, f"step-{int(step):012d}")
+
+
+def _write_atomic(path: str, text: str) -> None:
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        f.write(text)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
 
 
 def save(solver, directory: str, step: Optional[int] = None, extra: Optional[dict] = None) -> None:
-    """Collective: every rank writes its slab; rank 0 writes meta.json last."""
-    os.makedirs(directory, exist_ok=True)
+    """Collective: every rank writes its slab into the step's directory; rank 0
+    then writes meta.json there and atomically republishes ``latest``."""
+    step = int(solver.steps_done if step is None else step)
+    sd = step_dir(directory, step)
+    os.makedirs(sd, exist_ok=True)
     local = solver.download()
-    np.save(os.path.join(directory, f"rank{solver.rank:05d}.npy"), local, allow_pickle=False)
+    np.save(os.path.join(sd, f"rank{solver.rank:05d}.npy"), local, allow_pickle=False)
     _barrier(solver)
     if solver.rank == 0:
         p = solver.problem
         meta = {
             "format": FORMAT,
-            "step": int(solver.steps_done if step is None else step),
+            "step": step,
             "nranks": solver.size,
             "dtype": "fp64" if local.dtype == np.float64 else "fp32",
             "n_owned": p.n_owned,
             "n_input": p.n_input,
             "convention": p.convention,
             "sigma": p.sigma, "nu": p.nu, "dom_len": p.dom_len, "r": p.r,
-            "rows": [],
         }
         meta.update(extra or {})
-        tmp = os.path.join(directory, "meta.json.tmp")
-        with open(tmp, "w") as f:
-            json.dump(meta, f, indent=1)
-        os.replace(tmp, os.path.join(directory, "meta.json"))
+        _write_atomic(os.path.join(sd, "meta.json"), json.dumps(meta, indent=1))
+        _write_atomic(os.path.join(directory, "latest"), os.path.basename(sd) + "\n")  # the commit point
+        steps = sorted(d for d in os.listdir(directory) if d.startswith("step-"))
+        for d in steps[:max(0, steps.index(os.path.basename(sd)) - 1)]:  # keep the two newest
+            shutil.rmtree(os.path.join(directory, d), ignore_errors=True)
     _barrier(solver)
 
 
+def resolve(directory: str) -> str:
+    """The directory holding the newest complete checkpoint under `directory`."""
+    latest = os.path.join(directory, "latest")
+    if os.path.exists(latest):
+        with open(latest) as f:
+            return os.path.join(directory, f.read().strip())
+    return directory  # a step directory itself, or the v1 flat layout
+
+
 def load_meta(directory: str) -> dict:
-    with open(os.path.join(directory, "meta.json")) as f:
+    sd = resolve(directory)
+    with open(os.path.join(sd, "meta.json")) as f:
         meta = json.load(f)
-    if meta.get("format") != FORMAT:
-        raise ValueError(f"{directory}: not a {FORMAT} checkpoint")
+    if meta.get("format") not in FORMATS:
+        raise ValueError(f"{directory}: not a heat2d checkpoint")
+    meta["dir"] = sd
     return meta
 
 
@@ -63,8 +99,16 @@ def load(solver, directory: str) -> dict:
         raise ValueError(f"checkpoint grid {meta['n_owned']} != solver grid {solver.problem.n_owned}")
     if meta["convention"] != solver.problem.convention:
         raise ValueError("checkpoint grid convention differs")
-    parts = [np.load(os.path.join(directory, f"rank{r:05d}.npy"), mmap_mode="r", allow_pickle=False)
+    want = "fp64" if solver.np_dtype == np.float64 else "fp32"
+    if meta["dtype"] != want:
+        raise ValueError(f"checkpoint dtype {meta['dtype']} != solver dtype {want}")
+    parts = [np.load(os.path.join(meta["dir"], f"rank{r:05d}.npy"), mmap_mode="r", allow_pickle=False)
              for r in range(meta["nranks"])]
+    for r, part in enumerate(parts):
+        base, rem = divmod(meta["n_owned"], meta["nranks"])  # the writer's decomposition (common.hpp)
+        rows = base + (1 if r < rem else 0)
+        if part.shape != (rows, solver.ncols) or part.dtype != solver.np_dtype:
+            raise ValueError(f"rank file {r}: {part.shape} {part.dtype}, expected {(rows, solver.ncols)} {want}")
     starts = np.cumsum([0] + [p.shape[0] for p in parts])
     r0, r1 = solver.row0, solver.row0 + solver.nrows
     out = np.empty((solver.nrows, solver.ncols), dtype=solver.np_dtype)

@@ -69,12 +69,18 @@ def test_torchrun_gloo_mpi_variant_and_merge(native, tmp_path):
     assert np.array_equal(x, prob.x[1:-1])
 
 
+def ck_meta(ck):
+    """meta.json of the newest complete checkpoint (DIR/latest -> DIR/step-N/)."""
+    name = (ck / "latest").read_text().strip()
+    return json.loads((ck / name / "meta.json").read_text())
+
+
 @pytest.mark.parametrize("p_write,p_read", [(2, 1), (1, 3), (3, 2)])
 def test_checkpoint_restart_changes_rank_count(native, tmp_path, p_write, p_read):
     (tmp_path / "input.dat").write_text("50 0.25 0.05 1.0 30 1\n")
     # run 12 steps with a checkpoint, then resume to 30 steps on a different rank count
     py(tmp_path, "--backend", "cpu", "--ntime", "12", "--checkpoint", "ck", "--output", "none", nproc=p_write)
-    meta = json.loads((tmp_path / "ck" / "meta.json").read_text())
+    meta = ck_meta(tmp_path / "ck")
     assert meta["step"] == 12 and meta["nranks"] == p_write
     for f in tmp_path.glob("soln*.dat"):
         f.unlink()
@@ -120,8 +126,8 @@ def test_checkpoint_native_cli_interop(native, tmp_path, writer, reader):
                        cwd=tmp_path, check=True, capture_output=True)
     else:
         py(tmp_path, "--backend", "cpu", "--ntime", "12", "--checkpoint", "ck", "--output", "none", nproc=2)
-    meta = json.loads((tmp_path / "ck" / "meta.json").read_text())
-    assert meta["step"] == 12 and meta["format"] == "heat2d-checkpoint-v1"
+    meta = ck_meta(tmp_path / "ck")
+    assert meta["step"] == 12 and meta["format"] == "heat2d-checkpoint-v2"
     if reader == "cli":
         out = subprocess.run([*cli, "--restart", "ck"], cwd=tmp_path, check=True, capture_output=True, text=True)
         assert out.returncode == 0
@@ -145,3 +151,50 @@ def test_checkpoint_native_rejects_mismatch(native, tmp_path):
     p = subprocess.run([N.CLI_PATH, "--cpu", "--quiet", "--dtype", "fp32", "--restart", "ck"], cwd=tmp_path,
                        capture_output=True, text=True)
     assert p.returncode != 0 and "dtype" in p.stderr
+
+
+def test_checkpoint_torn_write_resumes_last_complete(native, tmp_path):
+    """Periodic checkpoints go to per-step directories behind an atomic
+    `latest` pointer: a crash while writing step 15 (a partial rank file, no
+    meta.json, `latest` not moved) resumes bitwise from step 10; only the two
+    newest complete steps are kept."""
+    (tmp_path / "input.dat").write_text("50 0.25 0.05 1.0 30 1\n")
+    cli = [N.CLI_PATH, "--cpu", "--quiet", "--gpus", "2", "--tb", "3"]
+    subprocess.run([*cli, "--ntime", "12", "--checkpoint", "ck", "--checkpoint-every", "5", "--output", "none"],
+                   cwd=tmp_path, check=True, capture_output=True)
+    ck = tmp_path / "ck"
+    assert sorted(d.name for d in ck.iterdir() if d.name.startswith("step-")) == [
+        "step-000000000010", "step-000000000012"]
+    (ck / "latest").write_text("step-000000000010\n")  # as if step 12's publish had not happened
+    torn = ck / "step-000000000012"
+    (torn / "meta.json").unlink()
+    with open(torn / "rank00000.npy", "r+b") as f:
+        f.truncate(100)
+    subprocess.run([*cli, "--restart", "ck"], cwd=tmp_path, check=True, capture_output=True)
+    T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
+
+
+def test_checkpoint_python_load_checks(native, tmp_path):
+    """Python loader: a dtype mismatch raises (no silent cast); the v1 flat
+    layout of round-1 checkpoints still loads."""
+    from heat2d.models.heat2d import HeatSolver
+    from heat2d.utils import checkpoint
+    p = heat2d.make_problem(heat2d.InputDat(n=40, sigma=0.25, nu=0.05, dom_len=1.0, ntime=7), "ghost", "uniform")
+    s = HeatSolver(p, dtype="fp64", backend="cpu", tb=2)
+    s.step(7)
+    checkpoint.save(s, str(tmp_path / "ck"))
+    s32 = HeatSolver(p, dtype="fp32", backend="cpu", tb=2)
+    with pytest.raises(ValueError, match="dtype"):
+        checkpoint.load(s32, str(tmp_path / "ck"))
+    # v1: flat directory
+    v1 = tmp_path / "v1"
+    v1.mkdir()
+    m = ck_meta(tmp_path / "ck")
+    m["format"] = "heat2d-checkpoint-v1"
+    (v1 / "meta.json").write_text(json.dumps(m))
+    np.save(v1 / "rank00000.npy", s.download(), allow_pickle=False)
+    s2 = HeatSolver(p, dtype="fp64", backend="cpu", tb=2)
+    assert checkpoint.load(s2, str(v1))["step"] == 7
+    assert np.array_equal(s2.download(), R.owned(R.ftcs(p)))
