@@ -54,7 +54,7 @@ def test_checkpoint_restart_clean(tmp_path):
     run(tmp_path, "33 0.25 0.05 1.0 9 1\n", "--cpu", "--quiet", "--checkpoint", "ck")
     p = run(tmp_path, "33 0.25 0.05 1.0 20 1\n", "--cpu", "--quiet", "--restart", "ck")
     assert p.returncode == 0, p.stderr[-2000:]
-    f = tmp_path / "ck" / "rank00000.npy"
+    f = tmp_path / "ck" / (tmp_path / "ck" / "latest").read_text().strip() / "rank00000.npy"
     f.write_bytes(f.read_bytes()[:200])
     p = run(tmp_path, "33 0.25 0.05 1.0 20 1\n", "--cpu", "--quiet", "--restart", "ck")
     assert p.returncode != 0 and "truncated" in p.stderr
