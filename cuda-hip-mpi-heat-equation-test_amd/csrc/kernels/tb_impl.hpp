@@ -9,6 +9,7 @@
 #include <map>
 #include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "heat2d/kernels.hpp"
 
@@ -183,7 +184,58 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uin
 // fewer per point (5 fp64 ops + 2 DPP moves instead of 6 + 2) for a kernel that
 // is VALU-co-bound. When r is a power of two (sigma = 0.25 in every shipped
 // input) r*x is exact and both forms round identically (normal range).
-template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false>
+// Dependency chains of the march (CL levels per chain). Level s computes
+// row m + off(s) while the march is at level-0 row m. Inside a chain (delta 1)
+// level s reads level s-1's row of THIS iteration — a serial dependency, K
+// levels deep per row in the single-chain march (CL = K). At a chain boundary
+// (delta 2: s = 1 + j*CL, j >= 1) level s reads only rows of level s-1 from the
+// three previous iterations, so the K/CL chains of an iteration are
+// independent: instruction-level parallelism for a wave that is alone on its
+// SIMD (small grids, thin-slab boundary bands), paid with one more register
+// row for the level below each boundary (a 3-slot ring) and one more march
+// row per boundary. Same operations, same order per point: bitwise identical.
+// Measured: profiles/chained_march.md.
+template <int K, int CL>
+struct ChainShape {
+  static constexpr int delta(int s) { return (s > 1 && (s - 1) % CL == 0) ? 2 : 1; }
+  static constexpr int off(int s) { return s + (s >= 1 ? (s - 1) / CL : 0); }
+  // ring size of stored level j (1 .. K-1): 2 rows, 3 below a boundary
+  static constexpr int ring(int j) { return (j >= 1 && j < K) ? delta(j + 1) + 1 : 2; }
+  static constexpr int boundaries = K >= 1 ? (K - 1) / CL : 0;
+  // loop-body length: whole level-0 rings and whole 2- (and 3-) slot level rings
+  static constexpr int unroll(int ring0) {
+    return boundaries == 0 ? ring0 : (ring0 % 3 == 0 ? (ring0 % 2 == 0 ? ring0 : 2 * ring0) : (ring0 % 2 == 0 ? 3 * ring0 : 6 * ring0));
+  }
+  // slot of the row level j computed `back` iterations before phase ph
+  static constexpr int slot(int ph, int back, int j) { return ((ph - back) % ring(j) + ring(j)) % ring(j); }
+};
+
+// Default chain length per dtype (build flags HEAT2D_CHAIN_F32 / _F64; 0 = one
+// chain of K levels) for depths >= HEAT2D_CHAIN_MIN_K. Measured with fixed
+// plans (profiles/chained_march.md): chains of 4 speed up the deep fp64 passes
+// (32768^2 K = 20: 6.78 -> 6.56 ms per cycle), are neutral for fp64 K = 14
+// and fp32 K = 16 on big grids, and cost 6 % on the 4096^2 fp32 grid — so only
+// fp64 K = 17..20 (the one-pass depths of short runs) uses them.
+#ifndef HEAT2D_CHAIN_F32
+#define HEAT2D_CHAIN_F32 0
+#endif
+#ifndef HEAT2D_CHAIN_F64
+#define HEAT2D_CHAIN_F64 4
+#endif
+#ifndef HEAT2D_CHAIN_MIN_K
+#define HEAT2D_CHAIN_MIN_K 17
+#endif
+// above K = 20 the chains' extra rows push the fp64 interior kernel to 1 wave/SIMD
+#ifndef HEAT2D_CHAIN_MAX_K
+#define HEAT2D_CHAIN_MAX_K 20
+#endif
+template <typename T, int K>
+constexpr int chain_len() {
+  constexpr int c = std::is_same<T, float>::value ? HEAT2D_CHAIN_F32 : HEAT2D_CHAIN_F64;
+  return (c <= 0 || c >= K || K < HEAT2D_CHAIN_MIN_K || K > HEAT2D_CHAIN_MAX_K) ? K : c;
+}
+
+template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, int CL = K>
 struct March {
   using S = TbShape<T, NV, K>;
   static constexpr int V = S::V;
@@ -200,12 +252,15 @@ struct March {
   T r;
   int32_t t0, t1;    // output rows [t0, t1)
   int32_t fixed_lo, fixed_hi;  // EK & 1: rows outside [fixed_lo, fixed_hi) are frame rows
-  int32_t mlo;       // lowest level-0 row (t0 - K)
+  int32_t mlo;       // lowest march row (t0 - off(K))
+  int32_t mload;     // lowest level-0 row loaded (t0 - K)
   int32_t ld_off;    // per-lane load byte offset (kOob outside the allocation)
   int32_t st_off;    // per-lane vector store offset (kOob unless the lane holds output columns)
   T rl[(EK & 2) ? V : 1];  // EK & 2: r per element, 0 in Dirichlet / pad columns
 
-  T X[2][KX][V];     // levels 1..K-1: X[parity][level-1][elem]
+  using Ch = ChainShape<K, CL>;
+  static constexpr int L = Ch::unroll(RING);  // march rows per loop body
+  T X[3][KX][V];     // levels 1..K-1: X[slot][level-1][elem] (slot 2 only below chain boundaries)
   VT Lb[RING][NV];   // level 0: load ring
   StatAcc acc;       // ST: statistics of the stored rows
   uint32_t colmask;  // ST: bit e = element e is an owned output column of this lane
@@ -269,10 +324,12 @@ struct March {
     }
   }
 
+  // One march row at phase PH (0 .. L-1; level-0 ring slot PH % RING, level-j
+  // ring slot PH % ring(j)).
   template <int PH>
   __device__ __forceinline__ void step(int32_t m) {
-    constexpr int P = PH & 1, Q = P ^ 1;  // level rings: P = oldest row (-> new row), Q = centre
-    constexpr int sN = PH, sC = (PH + RING - 1) % RING, sS = (PH + RING - 2) % RING;  // level-0 slots
+    constexpr int P0 = PH % RING;
+    constexpr int sN = P0, sC = (P0 + RING - 1) % RING, sS = (P0 + RING - 2) % RING;  // level-0 slots
     T part[V];
     T C0[V], N0[V];
     {
@@ -287,27 +344,34 @@ struct March {
       // latch (which waits for the load and serialises the ring).
       const int32_t nxt = m + 2 - RING;
       __builtin_amdgcn_sched_barrier(0);
-      load_row(nxt >= mlo ? nxt : mlo, Lb[sS]);
+      load_row(nxt >= mload ? nxt : mload, Lb[sS]);
     }
     unpack(Lb[sN], N0);
 #pragma unroll
     for (int s = 1; s <= K; ++s) {
       T C[V], N[V], out[V], nxtpart[V];
+      const int d = Ch::delta(s);
+      const int j = s > 1 ? s - 1 : 1;  // the level read (s - 1), when stored
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        C[e] = s == 1 ? C0[e] : X[Q][s > 1 ? s - 2 : 0][e];  // row m+s   (centre)
-        N[e] = s == 1 ? N0[e] : X[P][s > 1 ? s - 2 : 0][e];  // row m+s-1 (north, x-1; fresh)
+        // delta 1: N = level s-1's row of this iteration (fresh), C one back;
+        // delta 2: N one back, C two back (independent of this iteration)
+        C[e] = s == 1 ? C0[e] : X[Ch::slot(PH, d, j)][j - 1][e];
+        N[e] = s == 1 ? N0[e] : X[Ch::slot(PH, d - 1, j)][j - 1][e];
       }
-      if (s < K) partial(X[P][s - 1], X[Q][s - 1], nxtpart);  // level s+1's S+E, before level s's new row lands
-      update(part, C, N, m + s, out);
+      const int ps = Ch::slot(PH, 0, s < K ? s : 1);  // this level's slot of this iteration
+      // level s+1's S+E from level s's S (the slot about to be overwritten) and C
+      if (s < K) partial(X[ps][s - 1], X[Ch::slot(PH, Ch::delta(s + 1), s)][s - 1], nxtpart);
+      update(part, C, N, m + Ch::off(s), out);
       if (s < K) {
 #pragma unroll
-        for (int e = 0; e < V; ++e) X[P][s - 1][e] = out[e];
+        for (int e = 0; e < V; ++e) X[ps][s - 1][e] = out[e];
 #pragma unroll
         for (int e = 0; e < V; ++e) part[e] = nxtpart[e];
       } else {
-        const bool live = m + s < t1 && m + s >= t0;  // wave-uniform
-        store_row(m + s, live, out);
+        const int32_t row = m + Ch::off(K);
+        const bool live = row < t1 && row >= t0;  // wave-uniform
+        store_row(row, live, out);
         if constexpr (ST) {
           if (live) {
 #pragma unroll
@@ -318,47 +382,43 @@ struct March {
     }
   }
 
-  // March rows m = t1+K-1 down to t0-K (level-0 rows [t0-K, t1+K)). Level K
-  // row m+K is an output row once m+K < t1: the first 2K iterations only prime
-  // the levels (their stores are dropped by the descriptor). The trip count is
-  // rounded up to whole RING-phase bodies (the extra rows re-read row t0-K and
-  // their stores are dropped too): a loop body with a single exit, so no
-  // load can be sunk past a mid-body exit (which would serialise the ring).
+  template <int... I>
+  __device__ __forceinline__ void body(int32_t m, std::integer_sequence<int, I...>) {
+    (step<I>(m - I), ...);
+  }
+
+  // March rows m = t1+K-1 down to t0-off(K) (level-0 rows [t0-K, t1+K) are
+  // loaded; below t0-K the loads are clamped: those rows only feed priming
+  // values). Level K row m+off(K) is an output row once it is < t1: the first
+  // iterations only prime the levels (their stores are dropped by the
+  // descriptor). The trip count is rounded up to whole L-row bodies (the
+  // extra rows' stores are dropped too): a loop body with a single exit, so
+  // no load can be sunk past a mid-body exit (which would serialise the ring).
   __device__ __forceinline__ void run() {
-    mlo = t0 - K;
+    mload = t0 - K;
+    mlo = t0 - Ch::off(K);
     const int32_t mtop = t1 + K - 1;
     // slots 0..RING-3: rows mtop, mtop-1, ...; slots RING-2 / RING-1 stand for
     // rows mtop+2 / mtop+1 (priming only: their results are never stored)
 #pragma unroll
-    for (int q = 0; q < RING - 2; ++q) load_row(mtop - q >= mlo ? mtop - q : mlo, Lb[q]);
+    for (int q = 0; q < RING - 2; ++q) load_row(mtop - q >= mload ? mtop - q : mload, Lb[q]);
 #pragma unroll
     for (int q = RING - 2; q < RING; ++q)
 #pragma unroll
       for (int v = 0; v < NV; ++v) Lb[q][v] = VT{};
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 3; ++p)
 #pragma unroll
       for (int s = 0; s < KX; ++s)
 #pragma unroll
         for (int e = 0; e < V; ++e) X[p][s][e] = T(0);
     const int32_t iters = mtop - mlo + 1;
-    const int32_t bodies = (iters + RING - 1) / RING;
+    const int32_t bodies = (iters + L - 1) / L;
     int32_t m = mtop;
 #pragma unroll 1
     for (int32_t b = 0; b < bodies; ++b) {
-      step<0>(m);
-      step<1>(m - 1);
-      step<2>(m - 2);
-      step<3>(m - 3);
-      if constexpr (RING >= 6) {
-        step<4 % RING>(m - 4);
-        step<5 % RING>(m - 5);
-      }
-      if constexpr (RING >= 8) {
-        step<6 % RING>(m - 6);
-        step<7 % RING>(m - 7);
-      }
-      m -= RING;
+      body(m, std::make_integer_sequence<int, L>{});
+      m -= L;
     }
   }
 };
@@ -377,7 +437,7 @@ struct March {
 // ~2x the registers: 209 VGPRs at K = 10). Same operation order and rounding
 // per element as March (bitwise identical); the loads / stores / ring /
 // descriptors / edge kinds are March's.
-template <int K, int EK, int RING, int AR, bool ST = false>
+template <int K, int EK, int RING, int AR, bool ST = false, int CL = K>
 struct MarchF32 {
   using F2 = float __attribute__((ext_vector_type(2)));
   using VT = float __attribute__((ext_vector_type(4)));
@@ -395,12 +455,15 @@ struct MarchF32 {
   float r;
   int32_t t0, t1;
   int32_t fixed_lo, fixed_hi;
-  int32_t mlo;
+  int32_t mlo;    // lowest march row (t0 - off(K))
+  int32_t mload;  // lowest level-0 row loaded (t0 - K)
   int32_t ld_off;
   int32_t st_off;
   Row rl;  // EK & 2: r per element (0 in Dirichlet / pad columns)
 
-  Row X[2][KX];
+  using Ch = ChainShape<K, CL>;
+  static constexpr int L = Ch::unroll(RING);
+  Row X[3][KX];  // slot 2 only below chain boundaries (see March)
   StatAcc acc;       // ST: statistics of the stored rows
   uint32_t colmask;  // ST: bit e = element e (memory order) is an owned output column
   // Level-0 ring. A slot holds a row in memory order (a = (c0, c1),
@@ -468,30 +531,34 @@ struct MarchF32 {
 
   template <int PH>
   __device__ __forceinline__ void step(int32_t m) {
-    constexpr int P = PH & 1, Q = P ^ 1;
-    constexpr int sN = PH, sC = (PH + RING - 1) % RING, sS = (PH + RING - 2) % RING;
+    constexpr int P0 = PH % RING;
+    constexpr int sN = P0, sC = (P0 + RING - 1) % RING, sS = (P0 + RING - 2) % RING;
     const Row C0 = Lb[sC];
     Row part = partial(Lb[sS], C0);
     {
       const int32_t nxt = m + 2 - RING;
       __builtin_amdgcn_sched_barrier(0);
-      load_row(nxt >= mlo ? nxt : mlo, Lb[sS]);
+      load_row(nxt >= mload ? nxt : mload, Lb[sS]);
     }
     Lb[sN] = split(Lb[sN]);  // first use of this row: to even/odd form, in place
     const Row N0 = Lb[sN];
 #pragma unroll
     for (int s = 1; s <= K; ++s) {
-      const Row C = s == 1 ? C0 : X[Q][s > 1 ? s - 2 : 0];
-      const Row N = s == 1 ? N0 : X[P][s > 1 ? s - 2 : 0];
+      const int d = Ch::delta(s);
+      const int j = s > 1 ? s - 1 : 1;
+      const Row C = s == 1 ? C0 : X[Ch::slot(PH, d, j)][j - 1];
+      const Row N = s == 1 ? N0 : X[Ch::slot(PH, d - 1, j)][j - 1];
       if (s < K) {
         const int i = s < K ? s - 1 : 0;
-        const Row nxtpart = partial(X[P][i], X[Q][i]);
-        X[P][i] = update(part, C, N, m + s);
+        const int ps = Ch::slot(PH, 0, s < K ? s : 1);
+        const Row nxtpart = partial(X[ps][i], X[Ch::slot(PH, Ch::delta(s + 1), s < K ? s : 1)][i]);
+        X[ps][i] = update(part, C, N, m + Ch::off(s));
         part = nxtpart;
       } else {
-        const bool live = m + s < t1 && m + s >= t0;  // wave-uniform
-        const VT w = update_last(part, C, N, m + s);
-        store_row(m + s, live, w);
+        const int32_t row = m + Ch::off(K);
+        const bool live = row < t1 && row >= t0;  // wave-uniform
+        const VT w = update_last(part, C, N, row);
+        store_row(row, live, w);
         if constexpr (ST) {
           if (live) {  // C in even/odd form: a = (c0, c2), b = (c1, c3)
             acc.add(colmask & 1u, (double)w.x, (double)C.a.x);
@@ -504,35 +571,30 @@ struct MarchF32 {
     }
   }
 
+  template <int... I>
+  __device__ __forceinline__ void body(int32_t m, std::integer_sequence<int, I...>) {
+    (step<I>(m - I), ...);
+  }
+
   __device__ __forceinline__ void run() {
-    mlo = t0 - K;
+    mload = t0 - K;
+    mlo = t0 - Ch::off(K);
     const int32_t mtop = t1 + K - 1;
 #pragma unroll
-    for (int q = 0; q < RING - 2; ++q) load_row(mtop - q >= mlo ? mtop - q : mlo, Lb[q]);
+    for (int q = 0; q < RING - 2; ++q) load_row(mtop - q >= mload ? mtop - q : mload, Lb[q]);
 #pragma unroll
     for (int q = RING - 2; q < RING; ++q) Lb[q] = Row{F2{0.f, 0.f}, F2{0.f, 0.f}};
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 3; ++p)
 #pragma unroll
       for (int s = 0; s < KX; ++s) X[p][s] = Row{F2{0.f, 0.f}, F2{0.f, 0.f}};
     const int32_t iters = mtop - mlo + 1;
-    const int32_t bodies = (iters + RING - 1) / RING;
+    const int32_t bodies = (iters + L - 1) / L;
     int32_t m = mtop;
 #pragma unroll 1
     for (int32_t b = 0; b < bodies; ++b) {
-      step<0>(m);
-      step<1>(m - 1);
-      step<2>(m - 2);
-      step<3>(m - 3);
-      if constexpr (RING >= 6) {
-        step<4 % RING>(m - 4);
-        step<5 % RING>(m - 5);
-      }
-      if constexpr (RING >= 8) {
-        step<6 % RING>(m - 6);
-        step<7 % RING>(m - 7);
-      }
-      m -= RING;
+      body(m, std::make_integer_sequence<int, L>{});
+      m -= L;
     }
   }
 };
@@ -558,8 +620,11 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   const int64_t c0 = u0 - S::KA;
   const int64_t mycol = c0 + (int64_t)lane * V;
   const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
-  using W = typename std::conditional<kPackedF32<T, NV>, MarchF32<K, EK, RING, AR, ST>,
-                                      March<T, NV, K, EK, RING, AR, ST>>::type;
+  // the fused-statistics variant keeps one chain: its accumulators on top of
+  // the chains' extra rows spill at fp64 K >= 21
+  constexpr int CL = ST ? K : chain_len<T, K>();
+  using W = typename std::conditional<kPackedF32<T, NV>, MarchF32<K, EK, RING, AR, ST, CL>,
+                                      March<T, NV, K, EK, RING, AR, ST, CL>>::type;
   W w;
   // row base = column col_lo (= -cpad) of row 0; offsets are relative to it
   w.srow = reinterpret_cast<const char*>(src + a.col_lo);
