@@ -140,8 +140,11 @@ void check_layout(DType dt, const SlabLayout& L, int k) {
 // per wave when ns divides the slots well; several rounds when the strips
 // alone leave many slots idle (e.g. 734 strips on 2048 slots: 1 band idles
 // 28 % of the chip, 11 bands lose 1.4 %).
-int64_t choose_bands(int64_t rows, int64_t ns, int64_t slots, int k) {
-  const int64_t min_rows = std::max<int64_t>(4 * (int64_t)k, 16);
+// prime_rows: march rows of overhead per band (2k; the fp32 interior kernel
+// skips the levels its priming rows do not need, which costs ~k - 1).
+int64_t choose_bands(int64_t rows, int64_t ns, int64_t slots, int k, int64_t prime_rows = -1) {
+  if (prime_rows < 0) prime_rows = 2 * (int64_t)k;
+  const int64_t min_rows = std::max<int64_t>(2 * prime_rows, 16);
   const int64_t nb_max = std::max<int64_t>(1, std::min<int64_t>(rows / min_rows, 64 * slots / std::max<int64_t>(ns, 1) + 1));
   int64_t best = 1;
   double best_cost = 1e300;
@@ -149,7 +152,7 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t slots, int k) {
     const int64_t items = nb * ns;
     const int64_t rounds = (items + slots - 1) / slots;
     const double idle = (double)(rounds * slots) / (double)items;
-    const double prime = 1.0 + 2.0 * k * (double)nb / (double)rows;
+    const double prime = 1.0 + (double)prime_rows * (double)nb / (double)rows;
     const double cost = idle * prime;
     if (cost < best_cost - 1e-9) {
       best_cost = cost;
@@ -284,7 +287,8 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   const int bpc = occupancy(dt, p.ring, true, k, arith);
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
   const int64_t mw = std::max<int64_t>(4, slots - std::max(0, spare_waves));
-  int64_t nb_m = choose_bands(rows_m, ns, mw, k);
+  // the fp32 interior kernel skips unneeded priming levels (tb_impl.hpp run<PS>)
+  int64_t nb_m = choose_bands(rows_m, ns, mw, k, dt == DType::F32 ? std::max(1, k - 1) : -1);
   if (main_bands > 0) nb_m = std::min<int64_t>(main_bands, std::max<int64_t>(1, rows_m / (2 * (int64_t)k)));
   p.main = TbRect{B, n - B, 0, ns, nb_m};
   p.main_items = nb_m * ns;

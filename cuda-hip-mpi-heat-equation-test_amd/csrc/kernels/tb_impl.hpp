@@ -208,6 +208,18 @@ struct ChainShape {
   }
   // slot of the row level j computed `back` iterations before phase ph
   static constexpr int slot(int ph, int back, int j) { return ((ph - back) % ring(j) + ring(j)) % ring(j); }
+  // Priming: at march iteration i (0 = the top row), level s computes row
+  // mtop - i + off(s), which some output needs only once i >= off(s) + s; in
+  // the first iterations the deep levels would compute rows above the band's
+  // dependency cone (about K^2 wasted level-rows per work item, 18 % of a
+  // 64-row item at K = 16). Levels needed at iteration i:
+  static __device__ __forceinline__ int32_t levels_at(int32_t i) {
+    int32_t n = 0;
+#pragma unroll
+    for (int s = 1; s <= K; ++s) n += (off(s) + s <= i) ? 1 : 0;
+    return n;
+  }
+  static constexpr int prime_iters = off(K) + K;  // from here on every level is needed
 };
 
 // Default chain length per dtype (build flags HEAT2D_CHAIN_F32 / _F64; 0 = one
@@ -326,8 +338,9 @@ struct March {
 
   // One march row at phase PH (0 .. L-1; level-0 ring slot PH % RING, level-j
   // ring slot PH % ring(j)).
-  template <int PH>
-  __device__ __forceinline__ void step(int32_t m) {
+  // PRIME: only levels 1..nl (levels_at of this iteration) are computed.
+  template <int PH, bool PRIME = false>
+  __device__ __forceinline__ void step(int32_t m, int32_t nl = K) {
     constexpr int P0 = PH % RING;
     constexpr int sN = P0, sC = (P0 + RING - 1) % RING, sS = (P0 + RING - 2) % RING;  // level-0 slots
     T part[V];
@@ -349,6 +362,9 @@ struct March {
     unpack(Lb[sN], N0);
 #pragma unroll
     for (int s = 1; s <= K; ++s) {
+      // PRIME: deeper levels are not needed yet (wave-uniform guard; a `break`
+      // here would keep the loop from unrolling into constant register indices)
+      if (PRIME && s > nl) continue;
       T C[V], N[V], out[V], nxtpart[V];
       const int d = Ch::delta(s);
       const int j = s > 1 ? s - 1 : 1;  // the level read (s - 1), when stored
@@ -386,6 +402,10 @@ struct March {
   __device__ __forceinline__ void body(int32_t m, std::integer_sequence<int, I...>) {
     (step<I>(m - I), ...);
   }
+  template <int... I>
+  __device__ __forceinline__ void body_prime(int32_t m, int32_t i, std::integer_sequence<int, I...>) {
+    (step<I, true>(m - I, Ch::levels_at(i + I)), ...);
+  }
 
   // March rows m = t1+K-1 down to t0-off(K) (level-0 rows [t0-K, t1+K) are
   // loaded; below t0-K the loads are clamped: those rows only feed priming
@@ -394,6 +414,10 @@ struct March {
   // descriptor). The trip count is rounded up to whole L-row bodies (the
   // extra rows' stores are dropped too): a loop body with a single exit, so
   // no load can be sunk past a mid-body exit (which would serialise the ring).
+  // PS: skip the levels the first march rows do not need (priming). Only the
+  // fp32 interior kernel uses it: the guarded priming body costs the fp64 and
+  // general kernels an occupancy level (profiles/priming_skip.md).
+  template <bool PS = false>
   __device__ __forceinline__ void run() {
     mload = t0 - K;
     mlo = t0 - Ch::off(K);
@@ -414,9 +438,17 @@ struct March {
         for (int e = 0; e < V; ++e) X[p][s][e] = T(0);
     const int32_t iters = mtop - mlo + 1;
     const int32_t bodies = (iters + L - 1) / L;
+    // priming bodies (deep levels skipped while not needed), then the steady loop
+    const int32_t pb = PS ? min(bodies, (int32_t)((Ch::prime_iters + L - 1) / L)) : 0;
     int32_t m = mtop;
+    int32_t b = 0;
 #pragma unroll 1
-    for (int32_t b = 0; b < bodies; ++b) {
+    for (; b < pb; ++b) {
+      body_prime(m, b * L, std::make_integer_sequence<int, L>{});
+      m -= L;
+    }
+#pragma unroll 1
+    for (; b < bodies; ++b) {
       body(m, std::make_integer_sequence<int, L>{});
       m -= L;
     }
@@ -529,8 +561,8 @@ struct MarchF32 {
               fin(re.b.y, in.b.y, C.b.y)};
   }
 
-  template <int PH>
-  __device__ __forceinline__ void step(int32_t m) {
+  template <int PH, bool PRIME = false>
+  __device__ __forceinline__ void step(int32_t m, int32_t nl = K) {
     constexpr int P0 = PH % RING;
     constexpr int sN = P0, sC = (P0 + RING - 1) % RING, sS = (P0 + RING - 2) % RING;
     const Row C0 = Lb[sC];
@@ -544,6 +576,7 @@ struct MarchF32 {
     const Row N0 = Lb[sN];
 #pragma unroll
     for (int s = 1; s <= K; ++s) {
+      if (PRIME && s > nl) continue;  // wave-uniform guard (see March)
       const int d = Ch::delta(s);
       const int j = s > 1 ? s - 1 : 1;
       const Row C = s == 1 ? C0 : X[Ch::slot(PH, d, j)][j - 1];
@@ -575,7 +608,15 @@ struct MarchF32 {
   __device__ __forceinline__ void body(int32_t m, std::integer_sequence<int, I...>) {
     (step<I>(m - I), ...);
   }
+  template <int... I>
+  __device__ __forceinline__ void body_prime(int32_t m, int32_t i, std::integer_sequence<int, I...>) {
+    (step<I, true>(m - I, Ch::levels_at(i + I)), ...);
+  }
 
+  // PS: skip the levels the first march rows do not need (priming). Only the
+  // fp32 interior kernel uses it: the guarded priming body costs the fp64 and
+  // general kernels an occupancy level (profiles/priming_skip.md).
+  template <bool PS = false>
   __device__ __forceinline__ void run() {
     mload = t0 - K;
     mlo = t0 - Ch::off(K);
@@ -590,9 +631,17 @@ struct MarchF32 {
       for (int s = 0; s < KX; ++s) X[p][s] = Row{F2{0.f, 0.f}, F2{0.f, 0.f}};
     const int32_t iters = mtop - mlo + 1;
     const int32_t bodies = (iters + L - 1) / L;
+    // priming bodies (deep levels skipped while not needed), then the steady loop
+    const int32_t pb = PS ? min(bodies, (int32_t)((Ch::prime_iters + L - 1) / L)) : 0;
     int32_t m = mtop;
+    int32_t b = 0;
 #pragma unroll 1
-    for (int32_t b = 0; b < bodies; ++b) {
+    for (; b < pb; ++b) {
+      body_prime(m, b * L, std::make_integer_sequence<int, L>{});
+      m -= L;
+    }
+#pragma unroll 1
+    for (; b < bodies; ++b) {
       body(m, std::make_integer_sequence<int, L>{});
       m -= L;
     }
@@ -610,7 +659,7 @@ template <typename T, int NV>
 constexpr bool kPackedF32 = false;
 #endif
 
-template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false>
+template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, bool PS = false>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
                                       int64_t t1, int lane, StatAcc* acc = nullptr) {
   using S = TbShape<T, NV, K>;
@@ -666,7 +715,7 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
     w.run();
     *acc = w.acc;
   } else {
-    w.run();
+    w.template run<PS>();
   }
 }
 
@@ -758,10 +807,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
         default: march<T, NV, K, 3, RING, AR, true>(src, dst, a, r, strip, t0, t1, lane, &acc); break;
       }
     } else if constexpr (MAIN) {
+      constexpr bool PS = std::is_same<T, float>::value;  // priming skip: fp32 interior kernel only
       if ((c0 < 0) || (c0 + S::W > a.ncols))
-        march<T, NV, K, 2, RING, AR>(src, dst, a, r, strip, t0, t1, lane);
+        march<T, NV, K, 2, RING, AR, false, PS>(src, dst, a, r, strip, t0, t1, lane);
       else
-        march<T, NV, K, 0, RING, AR>(src, dst, a, r, strip, t0, t1, lane);
+        march<T, NV, K, 0, RING, AR, false, PS>(src, dst, a, r, strip, t0, t1, lane);
     } else {
       const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
                      (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
