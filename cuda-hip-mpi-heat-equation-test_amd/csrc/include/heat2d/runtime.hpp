@@ -248,8 +248,12 @@ class Solver {
   void launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k);
   void exchange_on(void* field, hipStream_t s);
   void run_graph_cycles(int64_t npairs);
+  void ensure_pair_graph();
   bool measured_schedules() const;
   void trial_cycle(const kern::SplitPlan& c);
+  bool schedule_graphs() const;
+  void capture_schedule(int64_t n);
+  void run_schedule_graph(int64_t n);
   float depth_ms(int k);
   std::vector<int> choose_schedule(int64_t n);
 
@@ -285,6 +289,9 @@ class Solver {
   bool stats_next_ = false;   // the next cycle_launch is the fused-statistics cycle
   double* d_part_ = nullptr;  // fused statistics: per-wave partials
   std::map<int64_t, std::vector<int>> sched_;  // measured schedules by step count
+  // use_graph + a capturable transport: each measured schedule captured whole
+  // (both streams), keyed by (steps, starting buffer parity)
+  std::map<std::pair<int64_t, int>, hipGraphExec_t> sched_graph_;
   float depth_ms_[kMaxTB + 1] = {};            // cycle ms per depth, max over ranks (schedule search)
   int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all
   kern::SplitPlan split_[kMaxTB + 1] = {};  // per temporal depth (k == 0: not planned yet)

@@ -135,14 +135,25 @@ void check_layout(DType dt, const SlabLayout& L, int k) {
                  "row count exceeds the 32-bit row index of the stencil kernel");
 }
 
-// Row-band count for `rows` x `ns` strips on `slots` resident waves: minimise
-// (idle wave-slots of the last round) x (2k priming rows per band). One item
-// per wave when ns divides the slots well; several rounds when the strips
-// alone leave many slots idle (e.g. 734 strips on 2048 slots: 1 band idles
-// 28 % of the chip, 11 bands lose 1.4 %).
+// Row-band count for `rows` x `ns` strips on `simds` balance units: minimise
+// (rounds of items per SIMD, the most-loaded SIMD sets the launch time) x
+// (band rows + priming rows). Balanced per SIMD, not per resident-wave slot:
+// one march wave keeps its SIMD's VALU ~80 % busy, so a second wave on the
+// same SIMD adds little throughput (rocprofv3 SQ counters, 4096^2 fp32:
+// profiles/small_grid/) — 1197 items on 1024 SIMDs ran 1.5x slower than 1007
+// would. fp64 balances over resident wave slots instead: there 2-3 waves per
+// SIMD do add throughput (A/B: profiles/band_balance.md). Several rounds when
+// the strips alone leave many units idle.
 // prime_rows: march rows of overhead per band (2k; the fp32 interior kernel
 // skips the levels its priming rows do not need, which costs ~k - 1).
-int64_t choose_bands(int64_t rows, int64_t ns, int64_t slots, int k, int64_t prime_rows = -1) {
+// units the band chooser balances items over: SIMDs for fp32, resident wave slots for fp64
+int64_t balance_units(DType dt, int cus, int bpc) {
+  const int64_t c = (int64_t)(cus > 0 ? cus : cu_count());
+  return dt == DType::F32 ? c * 4 : c * bpc * 4;
+}
+
+int64_t choose_bands(int64_t rows, int64_t ns, int64_t simds, int k, int64_t prime_rows = -1) {
+  const int64_t slots = std::max<int64_t>(simds, 1);
   if (prime_rows < 0) prime_rows = 2 * (int64_t)k;
   const int64_t min_rows = std::max<int64_t>(2 * prime_rows, 16);
   const int64_t nb_max = std::max<int64_t>(1, std::min<int64_t>(rows / min_rows, 64 * slots / std::max<int64_t>(ns, 1) + 1));
@@ -163,7 +174,7 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t slots, int k, int64_t pri
 }
 
 // Launch `rects` (item counts from their nb and strip ranges) on `nwaves` waves.
-// partials != nullptr: the fused-statistics kernel (general, ring 4); returns the waves launched
+// partials != nullptr: the fused-statistics kernel (general, ring 4). Returns the waves launched.
 int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
                      const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith,
                      double* partials = nullptr) {
@@ -239,7 +250,7 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
   if (tile_rows > 0) {
     nbands = (rows + tile_rows - 1) / tile_rows;
   } else {
-    nbands = choose_bands(rows, p.nstrips, std::max<int64_t>(slots, 1), k);
+    nbands = choose_bands(rows, p.nstrips, balance_units(dt, cus, bpc), k);
   }
   nbands = std::max<int64_t>(1, std::min<int64_t>(nbands, rows));
   const int64_t items = nbands * p.nstrips;
@@ -288,7 +299,8 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
   const int64_t mw = std::max<int64_t>(4, slots - std::max(0, spare_waves));
   // the fp32 interior kernel skips unneeded priming levels (tb_impl.hpp run<PS>)
-  int64_t nb_m = choose_bands(rows_m, ns, mw, k, dt == DType::F32 ? std::max(1, k - 1) : -1);
+  int64_t nb_m = choose_bands(rows_m, ns, dt == DType::F32 ? balance_units(dt, cus, bpc) : mw, k,
+                              dt == DType::F32 ? std::max(1, k - 1) : -1);
   if (main_bands > 0) nb_m = std::min<int64_t>(main_bands, std::max<int64_t>(1, rows_m / (2 * (int64_t)k)));
   p.main = TbRect{B, n - B, 0, ns, nb_m};
   p.main_items = nb_m * ns;
@@ -316,7 +328,7 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   const int64_t ns = (L.ncols + U - 1) / U;
   const int bpc = occupancy(dt, p.ring, false, k, arith);
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
-  int64_t nb = choose_bands(L.nrows, ns, slots, k);
+  int64_t nb = choose_bands(L.nrows, ns, balance_units(dt, cus, bpc), k);
   if (bands > 0) nb = std::min<int64_t>(bands, std::max<int64_t>(1, L.nrows / (2 * (int64_t)k)));
   p.main = TbRect{0, L.nrows, 0, ns, nb};
   p.main_items = nb * ns;
@@ -335,7 +347,8 @@ void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, 
   const int64_t U = useful_width(dt, k);
   const int64_t ns = (L.ncols + U - 1) / U;
   const int64_t slots = (int64_t)cu_count() * occupancy_stats(dt, k, arith) * 4;
-  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(choose_bands(L.nrows, ns, slots, k), L.nrows));
+  const int64_t nb = std::max<int64_t>(
+      1, std::min<int64_t>(choose_bands(L.nrows, ns, balance_units(dt, 0, occupancy_stats(dt, k, arith)), k), L.nrows));
   const TbRect rect{0, L.nrows, 0, ns, nb};
   const int64_t nw = launch_rects(dt, src, dst, L, k, 4, false, &rect, 1, slots, r, stream, arith, partials);
   launch_reduce_partials(partials, nw, out6, stream);

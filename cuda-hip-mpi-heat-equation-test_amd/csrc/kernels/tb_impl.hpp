@@ -659,7 +659,7 @@ template <typename T, int NV>
 constexpr bool kPackedF32 = false;
 #endif
 
-template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, bool PS = false>
+template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, bool PS = false, int CLX = 0>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
                                       int64_t t1, int lane, StatAcc* acc = nullptr) {
   using S = TbShape<T, NV, K>;
@@ -671,7 +671,8 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
   // the fused-statistics variant keeps one chain: its accumulators on top of
   // the chains' extra rows spill at fp64 K >= 21
-  constexpr int CL = ST ? K : chain_len<T, K>();
+  // (CLX > 0: an explicit chain length — the boundary-band kernel)
+  constexpr int CL = CLX > 0 ? (CLX < K ? CLX : K) : (ST ? K : chain_len<T, K>());
   using W = typename std::conditional<kPackedF32<T, NV>, MarchF32<K, EK, RING, AR, ST, CL>,
                                       March<T, NV, K, EK, RING, AR, ST, CL>>::type;
   W w;
@@ -769,9 +770,16 @@ __device__ __forceinline__ double wave_max(double v) {
   return v;
 }
 
-template <typename T, int NV, int K, int RING, bool MAIN, int AR, bool ST = false>
+// Kernel variants (VAR): 0 plain; 1 fused statistics (StatAcc; general kernel).
+// (A third, latency-oriented variant for the boundary-band launch — priming
+// skip + dependency chains — measured slower everywhere and was removed:
+// profiles/edge_kernel.md.)
+constexpr int kVarPlain = 0, kVarStats = 1;
+
+template <typename T, int NV, int K, int RING, bool MAIN, int AR, int VAR = kVarPlain>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T, NV, K, RING, MAIN, AR>))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
-  static_assert(!ST || !MAIN, "fused statistics use the general kernel");
+  constexpr bool ST = VAR == kVarStats;
+  static_assert(VAR == kVarPlain || !MAIN, "the statistics variant uses the general kernel");
   using S = TbShape<T, NV, K>;
   const int lane = threadIdx.x & 63;
   // readfirstlane: make the wave id (and everything derived from it: strip, rows,
@@ -833,13 +841,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
   }
 }
 
-template <typename T, int NV, int K, int RING, bool MAIN, int AR, bool ST = false>
+template <typename T, int NV, int K, int RING, bool MAIN, int AR, int VAR = kVarPlain>
 constexpr auto kernel_ptr() {
-  return &tb_kernel<T, NV, K, RING, MAIN, AR, ST>;
+  return &tb_kernel<T, NV, K, RING, MAIN, AR, VAR>;
 }
 
 // Resident 256-thread workgroups per CU for one kernel instance (occupancy API).
-template <typename T, int NV, int K, int RING, bool MAIN, int AR, bool ST = false>
+template <typename T, int NV, int K, int RING, bool MAIN, int AR, int VAR = kVarPlain>
 int blocks_per_cu() {
   static std::mutex mu;
   static std::map<int, int> cache;  // device -> blocks/CU
@@ -849,7 +857,7 @@ int blocks_per_cu() {
   auto it = cache.find(dev);
   if (it != cache.end()) return it->second;
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, RING, MAIN, AR, ST>()),
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_ptr<T, NV, K, RING, MAIN, AR, VAR>()),
                                                    256, 0) != hipSuccess ||
       nb <= 0)
     nb = 1;
@@ -868,7 +876,6 @@ template <typename T, int AR>
 void dispatch_stats(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
 template <typename T, int AR>
 int occupancy_blocks_stats(int k);
-
 #define H2D_TB_CASE(T, RING, MAIN, AR, KK)                                                                    \
   case KK:                                                                                                    \
     hipLaunchKernelGGL((tb_kernel<T, 1, KK, RING, MAIN, AR>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
@@ -911,13 +918,15 @@ int occupancy_blocks_stats(int k);
     return 1;                                                                                           \
   }
 #define H2D_TB_UNIT(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_NO_CASES)
-#define H2D_ST_CASE(T, RING, MAIN, AR, KK)                                                                         \
-  case KK:                                                                                                         \
-    hipLaunchKernelGGL((tb_kernel<T, 1, KK, 4, false, AR, true>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
+#define H2D_TB_UNIT_F64(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_DEEP)
+#define H2D_ST_CASE(T, RING, MAIN, AR, KK)                                                                        \
+  case KK:                                                                                                        \
+    hipLaunchKernelGGL((tb_kernel<T, 1, KK, 4, false, AR, kVarStats>), dim3(nblocks), dim3(256), 0, s, src, dst, a, \
+                       r);                                                                                        \
     return;
 #define H2D_ST_OCC_CASE(T, RING, MAIN, AR, KK) \
   case KK:                                     \
-    return blocks_per_cu<T, 1, KK, 4, false, AR, true>();
+    return blocks_per_cu<T, 1, KK, 4, false, AR, kVarStats>();
 #define H2D_ST_UNIT(T, AR, DEEP)                                                                              \
   template <>                                                                                                 \
   void dispatch_stats<T, AR>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r,             \
@@ -940,7 +949,7 @@ int occupancy_blocks_stats(int k);
     }                                                                                                         \
     return 1;                                                                                                 \
   }
-#define H2D_TB_UNIT_F64(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_DEEP)
+
 
 }  // namespace tbimpl
 }  // namespace kern

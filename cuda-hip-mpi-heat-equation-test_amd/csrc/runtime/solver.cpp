@@ -169,6 +169,7 @@ Solver::~Solver() {
     if (s_compute_) (void)hipStreamSynchronize(s_compute_);
     if (s_comm_ && s_comm_ != s_compute_) (void)hipStreamSynchronize(s_comm_);
     if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
+    for (auto& g : sched_graph_) (void)hipGraphExecDestroy(g.second);
     for (auto& b : buf_)
       if (b) (void)hipFree(b);
     if (d_work_) (void)hipFree(d_work_);
@@ -369,11 +370,16 @@ const kern::SplitPlan& Solver::split_plan(int k) {
     ++plans_made_;
     const bool big = L_.nrows * L_.ncols >= (int64_t(1) << 24);
     if (p.valid && (cfg_.autotune > 0 || (cfg_.autotune < 0 && big))) autotune_split(k);
-    // HEAT2D_SPLIT_ORDER=edge-first | concurrent overrides the split's ordering (tests, A/B)
+    // HEAT2D_SPLIT_ORDER=edge-first | concurrent overrides the split's ordering (tests, A/B);
+    // HEAT2D_SPLIT_ORDER=single forces one general launch per cycle (no exchange only)
     if (const char* env = std::getenv("HEAT2D_SPLIT_ORDER")) {
       const std::string o = env;
       if (o == "edge-first" && p.valid == 1) p.valid = 3;
       if (o == "concurrent" && p.valid == 3) p.valid = 1;
+      if (o == "single" && !tr_->exchanges()) {
+        p = kern::plan_single(dtype(), L_, k, compute_cus_, 0, 0, cfg_.arith);
+        p.k = k;
+      }
     }
   }
   return p;
@@ -563,6 +569,29 @@ void Solver::cycle_copy_swap() {
 }
 
 void Solver::run_graph_cycles(int64_t npairs) {
+  ensure_pair_graph();
+  const int K = k_pref_;
+  const bool ovl = cfg_.overlap != 0;
+  if (ovl) {  // the graph starts only when the eager work on both streams is done
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
+  }
+  // the graph was captured for buffer parity 0 -> 1 -> 0
+  for (int64_t i = 0; i < npairs; ++i) H2D_HIP(hipGraphLaunch(graph_exec_, s_compute_));
+  hist_[K] += 2 * npairs;
+  if (npairs > 0) last_k_ = K;
+  if (ovl) {  // eager cycles after the graph order against its end
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+    H2D_HIP(hipEventRecord(ev_comm_, s_compute_));
+    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_comm_, 0));
+  }
+}
+
+// Capture + instantiate the two-cycle graph of depth pref_depth (parity 0 ->
+// 1 -> 0) unless it exists: called by prepare(), so that instantiation (~ms)
+// stays out of timed step()s.
+void Solver::ensure_pair_graph() {
   const int K = k_pref_;
   const bool ovl = cfg_.overlap != 0;
   if (ovl) (void)split_plan(K);  // plan / autotune (synchronising) before any capture
@@ -612,20 +641,11 @@ void Solver::run_graph_cycles(int64_t npairs) {
     H2D_HIP(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
     H2D_HIP(hipGraphDestroy(g));
     graph_k_ = K;
-  }
-  if (ovl) {  // the graph starts only when the eager work on both streams is done
-    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
-    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
-  }
-  // the graph was captured for buffer parity 0 -> 1 -> 0
-  for (int64_t i = 0; i < npairs; ++i) H2D_HIP(hipGraphLaunch(graph_exec_, s_compute_));
-  hist_[K] += 2 * npairs;
-  if (npairs > 0) last_k_ = K;
-  if (ovl) {  // eager cycles after the graph order against its end
-    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-    H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
-    H2D_HIP(hipEventRecord(ev_comm_, s_compute_));
-    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_comm_, 0));
+    if (ovl) {  // the events were recorded inside the capture only: re-establish them
+      H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+      H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+      H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
+    }
   }
 }
 
@@ -638,6 +658,10 @@ void Solver::step(int64_t n) {
     return;
   }
   if (auto it = sched_.find(n); it != sched_.end()) {
+    if (schedule_graphs()) {
+      run_schedule_graph(n);
+      return;
+    }
     for (int k : it->second) {
       cycle_launch(k);
       cycle_finish();
@@ -667,7 +691,8 @@ void Solver::step(int64_t n) {
 }
 
 bool Solver::measured_schedules() const {
-  if (!hip_ || !cfg_.overlap || cfg_.copy_swap || cfg_.use_graph || jit_) return false;
+  if (!hip_ || !cfg_.overlap || cfg_.copy_swap || jit_) return false;
+  if (cfg_.use_graph && tr_->exchanges() && !tr_->capturable()) return false;  // graphs of the pair kind
   const bool big = L_.nrows * L_.ncols >= (int64_t(1) << 24);
   return cfg_.autotune > 0 || (cfg_.autotune < 0 && big);
 }
@@ -715,6 +740,82 @@ std::vector<int> Solver::choose_schedule(int64_t n) {
   return sched;
 }
 
+bool Solver::schedule_graphs() const {
+  return cfg_.use_graph && hip_ && cfg_.overlap && (!tr_->exchanges() || tr_->capturable());
+}
+
+// Capture the whole measured schedule of n steps, from the current buffer
+// parity, as one graph: both streams (the comm stream forked off the capture),
+// the cycles' event protocol as graph edges. Replayed by step(n) with no
+// host launches between cycles (small grids: the ~12 us gaps between the
+// cross-stream launches are a quarter of a 4096^2 fp32 cycle).
+void Solver::capture_schedule(int64_t n) {
+  const std::vector<int>& sc = sched_.at(n);
+  for (int k : sc) (void)split_plan(k);  // plan / autotune (synchronising) before the capture
+  synchronize();
+  const int saved = cur_;
+  const int64_t saved_steps = steps_;
+  int64_t saved_hist[kMaxTB + 1];
+  std::copy(hist_, hist_ + kMaxTB + 1, saved_hist);
+  hipEvent_t fork = nullptr, join = nullptr;
+  H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+  H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  hipGraph_t g = nullptr;
+  H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
+  H2D_HIP(hipEventRecord(fork, s_compute_));
+  H2D_HIP(hipStreamWaitEvent(s_comm_, fork, 0));
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));  // in-capture records replace the external ones
+  H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+  H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
+  const bool timing = timing_;
+  timing_ = false;
+  for (int k : sc) {
+    cycle_launch(k);
+    cycle_finish();
+  }
+  timing_ = timing;
+  H2D_HIP(hipEventRecord(join, s_comm_));
+  H2D_HIP(hipStreamWaitEvent(s_compute_, join, 0));
+  H2D_HIP(hipStreamEndCapture(s_compute_, &g));
+  H2D_HIP(hipEventDestroy(fork));
+  H2D_HIP(hipEventDestroy(join));
+  cur_ = saved;
+  steps_ = saved_steps;
+  std::copy(saved_hist, saved_hist + kMaxTB + 1, hist_);
+  hipGraphExec_t ge = nullptr;
+  H2D_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  H2D_HIP(hipGraphDestroy(g));
+  sched_graph_[{n, cur_}] = ge;
+  // the events were recorded inside the capture only: re-establish them
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+  H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
+}
+
+void Solver::run_schedule_graph(int64_t n) {
+  auto it = sched_graph_.find({n, cur_});
+  if (it == sched_graph_.end()) {
+    capture_schedule(n);
+    it = sched_graph_.find({n, cur_});
+  }
+  const std::vector<int>& sc = sched_.at(n);
+  // the graph starts when the eager work on both streams is done
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
+  H2D_HIP(hipGraphLaunch(it->second, s_compute_));
+  // eager cycles after the graph order against its end
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_comm_, s_compute_));
+  H2D_HIP(hipStreamWaitEvent(s_comm_, ev_comm_, 0));
+  for (int k : sc) {
+    hist_[k] += 1;
+    steps_ += k;
+  }
+  last_k_ = sc.back();
+  if (sc.size() % 2) cycle_swap();
+}
+
 const std::vector<int>* Solver::schedule(int64_t n) const {
   auto it = sched_.find(n);
   return it == sched_.end() ? nullptr : &it->second;
@@ -725,6 +826,15 @@ void Solver::prepare(int64_t n) {
   if (measured_schedules() && !sched_.count(n)) {
     std::vector<int> s = choose_schedule(n);
     if (!s.empty()) sched_[n] = std::move(s);
+  }
+  if (schedule(n) && schedule_graphs()) {
+    // both buffer parities (a warmup between prepare and step(n) may flip it);
+    // a capture only records the launches, so flipping cur_ around it is safe
+    for (int p = 0; p < 2; ++p) {
+      cur_ ^= p;
+      if (!sched_graph_.count({n, cur_})) capture_schedule(n);
+      cur_ ^= p;
+    }
   }
   if (const std::vector<int>* s = schedule(n)) {
     // Leave the GPU in the schedule's steady state: the search ends on its
@@ -758,7 +868,7 @@ void Solver::prepare(int64_t n) {
     int64_t left = n;
     while (left > 0) {
       if (cfg_.use_graph && (!multi || tr_->capturable()) && left >= 2 * K && par == 0) {
-        (void)split_plan(K);
+        ensure_pair_graph();
         left -= left / (2 * K) * 2 * K;
         continue;
       }

@@ -355,3 +355,29 @@ def test_deep_fp64_bitwise(gpu, native, k):
         got = s.download()
         s.close()
         assert np.array_equal(got, R.owned(R.ftcs(p))), (k, overlap)
+
+
+@pytest.mark.parametrize("dtype,n,steps,warm", [("fp32", 1100, 61, 0), ("fp32", 1100, 61, 3), ("fp64", 900, 45, 5)])
+def test_measured_schedule_graph(gpu, native, dtype, n, steps, warm):
+    """graph=True + a measured schedule: prepare(n) captures the whole schedule
+    (both streams, both buffer parities) as one hipGraph; step(n) replays it
+    with nothing planned or captured inside; bitwise, also after a warmup
+    that flips the parity, and when replayed twice."""
+    p = prob(n, warm + 2 * steps, "ghost", "sine")
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    s = HeatSolver(p, dtype=dtype, backend="hip", device=0, autotune=1, graph=True)
+    s.upload(R.owned(R.initial_field(p, npdt)))
+    s.step(warm)
+    s.prepare(steps)
+    assert s.schedule(steps)
+    before = s.plans_made
+    s.cycle_hist(reset=True)
+    s.step(steps)
+    s.step(steps)
+    s.synchronize()
+    assert s.plans_made == before and s.steps_done == warm + 2 * steps
+    assert sum(k * c for k, c in s.cycle_hist().items()) == 2 * steps
+    got = s.download()
+    ref = R.owned(R.ftcs(p, dtype=npdt))
+    assert np.array_equal(got, ref), np.abs(got.astype(np.float64) - ref).max()
+    s.close()

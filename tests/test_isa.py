@@ -31,7 +31,7 @@ def tb():
     # 2 rings x main/gen x 2 arith x (fp32 K 1..16 + fp64 K 1..24), plus the
     # fused-statistics variants (general, ring 4, 2 arith)
     assert sum(len(p) == 6 for p in ks) == 8 * (16 + 24), len(ks)
-    assert sum(len(p) == 7 for p in ks) == 2 * (16 + 24), len(ks)
+    assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 2 * (16 + 24), len(ks)
     return ks
 
 

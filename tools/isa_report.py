@@ -62,7 +62,7 @@ def kernels(so_path):
     return out
 
 
-_TB = re.compile(r"tb_kernelI([df])Li(\d+)ELi(\d+)ELi(\d+)ELb([01])ELi(\d+)E(?:Lb([01])E)?")
+_TB = re.compile(r"tb_kernelI([df])Li(\d+)ELi(\d+)ELi(\d+)ELb([01])ELi(\d+)E(?:Li(\d)E)?")
 
 
 def tb_params(mangled):
@@ -72,7 +72,8 @@ def tb_params(mangled):
         return None
     p = ("fp64" if m.group(1) == "d" else "fp32", int(m.group(2)), int(m.group(3)), int(m.group(4)),
          m.group(5) == "1", int(m.group(6)))
-    return p + ("stats",) if m.group(7) == "1" else p  # fused-statistics variant: a 7th field
+    var = m.group(7) or "0"  # kernel variant (tb_impl.hpp): 1 fused statistics
+    return p + ("stats",) if var == "1" else p
 
 
 def main():
