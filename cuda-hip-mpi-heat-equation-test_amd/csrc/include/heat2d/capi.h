@@ -160,6 +160,8 @@ int heat2d_solver_cycle_hist(void* s, int64_t* out, int n, int reset);
 /* the measured cycle schedule prepare(n) chose for step(n): depths in out[0..min(cap, len)); len = -1 if none
    (step(n) then runs balanced cycles of the preferred depth) */
 int heat2d_solver_schedule(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len);
+/* the schedule search itself on given cycle times t_ms[k] (k = 1..kmax; t_ms[0] unused): depths in out */
+int heat2d_cycle_schedule(int64_t n, int kmax, const double* t_ms, int32_t* out, int64_t cap, int64_t* len);
 
 /* I/O (io.cpp). */
 int heat2d_write_xyz(const char* path, int dtype, const void* host, int64_t nrows, int64_t ncols,

@@ -155,6 +155,13 @@ int num_threads();
 
 // ---------------------------------------------------------------- solver
 
+// Cycle schedule of n steps from per-depth cycle times t(k), k <= kmax (the
+// search of Solver::prepare, exposed for tests): balanced depths for the
+// cycle count c with the smallest sum of t over its cycles, c scanned upward
+// from ceil(n / kmax) until the base depth's per-step time is 25 % above the
+// best seen. Empty if t(k) < 0 for a depth it needs.
+std::vector<int> cycle_schedule(int64_t n, int kmax, const std::function<double(int)>& t);
+
 class Solver {
  public:
   Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream_t external_stream = nullptr);

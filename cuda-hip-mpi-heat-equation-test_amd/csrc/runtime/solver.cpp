@@ -716,22 +716,26 @@ float Solver::depth_ms(int k) {
 // and stop once the base depth's per-step cost is 25 % worse than the best
 // seen (deeper into the HBM-bound region it only gets worse).
 std::vector<int> Solver::choose_schedule(int64_t n) {
-  const int Kmax = cfg_.tb;
+  return cycle_schedule(n, cfg_.tb, [this](int k) { return (double)depth_ms(k); });
+}
+
+std::vector<int> cycle_schedule(int64_t n, int kmax, const std::function<double(int)>& t) {
+  HEAT2D_REQUIRE(n >= 1 && kmax >= 1, "cycle_schedule needs n >= 1, kmax >= 1");
   double best = 1e300, best_step = 1e300;
   int64_t best_c = 0;
-  for (int64_t c = (n + Kmax - 1) / Kmax; c <= n; ++c) {
+  for (int64_t c = (n + kmax - 1) / kmax; c <= n; ++c) {
     const int kb = (int)(n / c);
     const int64_t rem = n % c;
-    const float tb = depth_ms(kb);
-    const float t1 = rem ? depth_ms(kb + 1) : 0.f;
+    const double tb = t(kb);
+    const double t1 = rem ? t(kb + 1) : 0.0;
     if (tb < 0 || t1 < 0) return {};
     const double cost = (double)(c - rem) * tb + (double)rem * t1;
     if (cost < best) {
       best = cost;
       best_c = c;
     }
-    best_step = std::min(best_step, (double)tb / kb);
-    if (kb <= 1 || (double)tb / kb > 1.25 * best_step) break;
+    best_step = std::min(best_step, tb / kb);
+    if (kb <= 1 || tb / kb > 1.25 * best_step) break;
   }
   std::vector<int> sched;
   const int kb = (int)(n / best_c);

@@ -1,0 +1,61 @@
+"""The measured-schedule search (Solver::prepare -> cycle_schedule), on CPU with
+synthetic cycle-time curves: it must find the cheapest cut of n steps into
+cycles of at most kmax steps among balanced splits, which for the convex t(k)
+the hardware shows (flat while a pass is HBM-bound, then linear in k) is the
+global optimum — checked against brute force over all compositions."""
+import ctypes as C
+
+import pytest
+
+from heat2d.ops import _native as N
+
+
+def schedule(n, kmax, t):
+    tm = (C.c_double * (kmax + 1))(*([0.0] + [t(k) for k in range(1, kmax + 1)]))
+    out = (C.c_int32 * max(1, n))()
+    ln = C.c_int64()
+    N.call("heat2d_cycle_schedule", n, kmax, tm, out, n, C.byref(ln))
+    return [int(v) for v in out[:ln.value]]
+
+
+def brute(n, kmax, t):
+    """Cheapest cut of n steps into cycles of <= kmax steps, over ALL compositions (DP)."""
+    best = [0.0] + [float("inf")] * n
+    for m in range(1, n + 1):
+        best[m] = min(t(k) + best[m - k] for k in range(1, min(kmax, m) + 1))
+    return best[n]
+
+
+def mi355x_fp64(k):  # measured shape at 32768^2 fp64 (profiles/depth_schedule.md): ms per cycle
+    return max(3.61, 0.30 * k - 0.05) + 0.02
+
+
+CURVES = {
+    "measured-fp64": mi355x_fp64,
+    "hbm-flat-then-linear": lambda k: max(1.0, 0.12 * k),
+    "pure-linear": lambda k: 0.2 * k + 0.05,
+    "launch-bound": lambda k: 0.05 + 0.004 * k,
+}
+
+
+@pytest.mark.parametrize("curve", sorted(CURVES))
+@pytest.mark.parametrize("n,kmax", [(20, 24), (480, 24), (37, 16), (7, 24), (1, 24), (100, 14), (25000, 24)])
+def test_schedule_optimal(native, curve, n, kmax):
+    t = CURVES[curve]
+    s = schedule(n, kmax, t)
+    assert sum(s) == n and max(s) <= kmax and max(s) - min(s) <= 1
+    cost = sum(t(k) for k in s)
+    if n <= 30000:
+        assert cost <= brute(n, kmax, t) * (1 + 1e-9)
+
+
+def test_schedule_examples(native):
+    assert schedule(20, 24, mi355x_fp64) == [20]  # one pass beats 2 x 10 (profiles/depth_schedule.md)
+    assert schedule(20, 14, mi355x_fp64) == [10, 10]
+    s = schedule(480, 24, mi355x_fp64)
+    assert set(s) <= {13, 14, 15, 16} and sum(s) == 480
+
+
+def test_schedule_missing_depth(native):
+    """A depth without a tuned time (t < 0, e.g. a slab too thin to split) aborts the search."""
+    assert schedule(20, 24, lambda k: -1.0 if k == 20 else 1.0) == []
