@@ -28,7 +28,8 @@ struct TbPlan {
 };
 
 // Plan a launch that advances rows [row_begin, row_end) of the slab by k steps.
-// tile_rows <= 0 selects the occupancy-driven default; cus > 0 plans for a
+// tile_rows == 0 selects the occupancy-driven row bands, > 0 bands of that many
+// rows, < 0 -tile_rows segments (TbRect nb < 0; ntiles = -segments); cus > 0 plans for a
 // stream restricted to that many CUs (comm-reserving CU mask).
 // arith: 0 = reference arithmetic (every op rounded), 1 = contracted fma form
 // (tb_impl.hpp, March); every launcher below takes it last.
@@ -58,6 +59,9 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 // band launch alone, then the interior, both on the compute stream, with the
 // halo exchange beside the interior (the autotuner's choice for slabs where
 // the interior would otherwise share the chip with the band waves).
+// nb > 0: nb row bands per strip (nb x strips work items); nb < 0: -nb equal
+// segments of the strip-major row sequence (one work item each, crossing strip
+// ends where they fall: equal rows per wave for any strip count).
 struct TbRect {
   int64_t r0, r1, s0, s1, nb;
 };
@@ -67,7 +71,8 @@ struct SplitPlan {
   TbRect edge[4];
   int64_t main_waves, edge_waves, main_items, edge_items;
 };
-// ring_override: 4 | 6 (0: default); main_bands: MAIN row bands (0: persistent default)
+// ring_override: 4 | 6 (0: default); main_bands: MAIN row bands (0: persistent default;
+// < 0: -main_bands segments, TbRect)
 SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus = 0, int spare_waves = 0,
                      int ring_override = 0, int64_t main_bands = 0, int arith = 0);
 // The alternative the autotuner weighs against the split (valid = 2): ONE

@@ -190,10 +190,13 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   int q = 0;
   for (int i = 0; i < nrect; ++i) {
     const TbRect& R = rects[i];
-    if (R.r1 <= R.r0 || R.s1 <= R.s0 || R.nb <= 0) continue;
+    if (R.r1 <= R.r0 || R.s1 <= R.s0 || R.nb == 0) continue;
     HEAT2D_REQUIRE(R.r0 >= 0 && R.r1 <= L.nrows, "rect rows outside the slab");
     a.rect[q] = TbRectArg{R.r0, R.r1, R.s0, R.s1, R.nb, items};
-    items += R.nb * (R.s1 - R.s0);
+    // nb < 0: -nb segments of the strip-major row sequence (tb_range)
+    HEAT2D_REQUIRE(R.nb > 0 || -R.nb <= (R.r1 - R.r0) * (R.s1 - R.s0), "more segments than strip rows");
+    HEAT2D_REQUIRE((R.r1 - R.r0) * (R.s1 - R.s0) < (int64_t(1) << 31), "rect exceeds 2^31 strip rows");
+    items += R.nb > 0 ? R.nb * (R.s1 - R.s0) : -R.nb;
     ++q;
   }
   if (q == 0) return 0;
@@ -246,6 +249,14 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
   const int bpc = occupancy(dt, p.prefetch, false, k, arith);
   p.blocks_per_cu = bpc;
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;  // resident waves
+  if (tile_rows < 0) {  // -tile_rows segments of the strip-major row sequence (TbRect nb < 0)
+    const int64_t nseg = std::min<int64_t>(-tile_rows, rows * p.nstrips);
+    p.ntiles = -nseg;
+    p.nwaves = std::min<int64_t>(nseg, std::max<int64_t>(slots, 1));
+    p.tile_rows = (rows * p.nstrips + nseg - 1) / nseg;
+    p.nblocks = (p.nwaves + 3) / 4;
+    return p;
+  }
   int64_t nbands;
   if (tile_rows > 0) {
     nbands = (rows + tile_rows - 1) / tile_rows;
@@ -275,6 +286,14 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
   const TbPlan p = plan_tb(dt, L, 0, std::min<int64_t>(n0 + n1, L.nrows), k, tile_rows, cus, arith);
   TbRect rects[2];
   int nr = 0;
+  if (p.ntiles < 0) {  // segments, shared out over the two ranges by rows
+    const int64_t ns = -p.ntiles;
+    const int64_t s0 = n1 == 0 ? ns : (n0 == 0 ? 0 : std::max<int64_t>(1, (ns * n0 + (n0 + n1) / 2) / (n0 + n1)));
+    if (n0 > 0) rects[nr++] = TbRect{rb0, re0, 0, p.nstrips, -std::min<int64_t>(s0, n0 * p.nstrips)};
+    if (n1 > 0) rects[nr++] = TbRect{rb1, re1, 0, p.nstrips, -std::min<int64_t>(std::max<int64_t>(1, ns - s0), n1 * p.nstrips)};
+    launch_rects(dt, src, dst, L, k, p.prefetch, false, rects, nr, p.nwaves, r, stream, arith);
+    return;
+  }
   const int64_t nb = std::max<int64_t>(p.ntiles, (n0 > 0) + (n1 > 0));
   const int64_t nb0 = n1 == 0 ? nb : (n0 == 0 ? 0 : std::min<int64_t>(nb - 1, std::max<int64_t>(1, (nb * n0 + (n0 + n1) / 2) / (n0 + n1))));
   if (n0 > 0) rects[nr++] = TbRect{rb0, re0, 0, p.nstrips, std::min<int64_t>(nb0, n0)};
@@ -302,8 +321,9 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   int64_t nb_m = choose_bands(rows_m, ns, dt == DType::F32 ? balance_units(dt, cus, bpc) : mw, k,
                               dt == DType::F32 ? std::max(1, k - 1) : -1);
   if (main_bands > 0) nb_m = std::min<int64_t>(main_bands, std::max<int64_t>(1, rows_m / (2 * (int64_t)k)));
+  if (main_bands < 0) nb_m = -std::min<int64_t>(-main_bands, std::max<int64_t>(1, rows_m * ns / (2 * (int64_t)k)));
   p.main = TbRect{B, n - B, 0, ns, nb_m};
-  p.main_items = nb_m * ns;
+  p.main_items = nb_m > 0 ? nb_m * ns : -nb_m;
   p.main_waves = std::min<int64_t>(p.main_items, mw);  // > one item per wave if main_bands asks for it
   // EDGE: the two boundary bands (one band each), general kernel. Short
   // (B + 2k march rows per item): beside MAIN where wave slots allow, else
@@ -330,8 +350,9 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
   int64_t nb = choose_bands(L.nrows, ns, balance_units(dt, cus, bpc), k);
   if (bands > 0) nb = std::min<int64_t>(bands, std::max<int64_t>(1, L.nrows / (2 * (int64_t)k)));
+  if (bands < 0) nb = -std::min<int64_t>(-bands, std::max<int64_t>(1, L.nrows * ns / (2 * (int64_t)k)));
   p.main = TbRect{0, L.nrows, 0, ns, nb};
-  p.main_items = nb * ns;
+  p.main_items = nb > 0 ? nb * ns : -nb;
   p.main_waves = std::min<int64_t>(p.main_items, slots);
   p.nedge = 0;
   p.valid = 2;

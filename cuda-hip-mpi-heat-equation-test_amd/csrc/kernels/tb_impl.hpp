@@ -720,8 +720,23 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   }
 }
 
-// Decode work item `it` -> (strip, output rows [t0, t1)); false if empty.
-__device__ __forceinline__ bool tb_item(const TbArgs& a, int64_t it, int64_t& strip, int64_t& t0, int64_t& t1) {
+// Work item `it` -> a range [lin, lin_end) of its rect's strip-major row
+// sequence (lin = strip_local * rows + row_local), marched piece by piece, one
+// piece per strip it touches.
+//   nb > 0: row bands — item = (band, strip), band-major; one piece.
+//   nb < 0: -nb equal segments of the whole sequence — item = segment; a
+//           segment may cross strip ends (1-2 pieces when segments are shorter
+//           than a strip). Every wave gets the same row count whatever the
+//           strip count, which bands (whole rows x whole strips) cannot give a
+//           thin slab: profiles/thin_slab.md.
+// Only (it, lin) are carried across a march (the rest is recomputed from the
+// kernarg per piece): more loop-carried SGPRs spill into VGPR lanes and cost
+// the deep fp64 interior kernels a wave per SIMD. lin < 2^31 (host-checked).
+struct TbSpan {
+  int32_t lin, lin_end, rows;
+  int64_t r0, s0;
+};
+__device__ __forceinline__ TbSpan tb_span(const TbArgs& a, int64_t it) {
   // select the rect with constant indices only (a dynamic index into the
   // by-value kernarg struct would be lowered to a private-memory copy)
   TbRectArg R = a.rect[0];
@@ -730,12 +745,30 @@ __device__ __forceinline__ bool tb_item(const TbArgs& a, int64_t it, int64_t& st
     if (i < a.nrect && it >= a.rect[i].item0) R = a.rect[i];
   const int64_t local = it - R.item0;
   const int64_t ns = R.s1 - R.s0;
-  const int64_t band = local / ns;
-  strip = R.s0 + (local - band * ns);
   const int64_t rows = R.r1 - R.r0;
-  t0 = R.r0 + band * rows / R.nb;
-  t1 = R.r0 + (band + 1) * rows / R.nb;
-  return t1 > t0;
+  TbSpan g{0, 0, (int32_t)rows, R.r0, R.s0};
+  if (R.nb > 0) {
+    const int64_t band = local / ns, sl = local - band * ns;
+    g.lin = (int32_t)(sl * rows + band * rows / R.nb);
+    g.lin_end = (int32_t)(sl * rows + (band + 1) * rows / R.nb);
+  } else {
+    const int64_t total = ns * rows, nseg = -R.nb;
+    g.lin = (int32_t)(local * total / nseg);
+    g.lin_end = (int32_t)((local + 1) * total / nseg);
+  }
+  return g;
+}
+// The piece of item `it` starting at lin -> (strip, output rows [t0, t1));
+// false when lin is past the item. Advance with lin += t1 - t0.
+__device__ __forceinline__ bool tb_piece(const TbArgs& a, int64_t it, int32_t lin, int64_t& strip, int64_t& t0,
+                                         int64_t& t1) {
+  const TbSpan g = tb_span(a, it);
+  if (lin >= g.lin_end) return false;
+  const int32_t sl = lin / g.rows, row = lin - sl * g.rows;
+  strip = g.s0 + sl;
+  t0 = g.r0 + row;
+  t1 = t0 + min(g.rows - row, g.lin_end - lin);
+  return true;
 }
 
 // MAIN = true: the caller guarantees no item reaches a frame ROW (the slab
@@ -797,13 +830,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
   }
   const int64_t wid = (int64_t)blk * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (wid >= a.nwaves) return;  // whole wave exits; no barriers in this kernel
-  // Items are band-major within a rect: consecutive waves take adjacent strips
-  // of the same band, so the waves in flight stream whole contiguous rows (HBM
-  // page locality) and all march in step.
+  // Band items are band-major within a rect: consecutive waves take adjacent
+  // strips of the same band, so the waves in flight stream whole contiguous
+  // rows (HBM page locality) and all march in step.
   StatAcc acc;
-  for (int64_t it = wid; it < a.nitems; it += a.nwaves) {
+  // one flat loop over the pieces of items wid, wid + nwaves, ... (a nested
+  // piece loop around the march costs the deep fp64 kernels registers)
+  int64_t it = wid;
+  int32_t lin = tb_span(a, it).lin;
+  while (it < a.nitems) {
     int64_t strip, t0, t1;
-    if (!tb_item(a, it, strip, t0, t1)) continue;
+    if (!tb_piece(a, it, lin, strip, t0, t1)) {
+      it += a.nwaves;
+      if (it < a.nitems) lin = tb_span(a, it).lin;
+      continue;
+    }
+    lin += (int32_t)(t1 - t0);
     const int64_t c0 = strip * S::U - S::KA;
     if constexpr (ST) {
       const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |

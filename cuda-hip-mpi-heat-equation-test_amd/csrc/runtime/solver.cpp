@@ -381,6 +381,18 @@ const kern::SplitPlan& Solver::split_plan(int k) {
         p.k = k;
       }
     }
+    // HEAT2D_SEGMENTS=n re-plans the interior (or the single launch) as n
+    // segment work items, keeping the order and ring (tests, A/B)
+    if (const char* env = std::getenv("HEAT2D_SEGMENTS")) {
+      const int64_t nseg = std::atoll(env);
+      if (nseg > 0 && p.valid) {
+        const int valid = p.valid, ring = p.ring;
+        p = valid == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, -nseg, cfg_.arith)
+                       : kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, -nseg, cfg_.arith);
+        if (p.valid) p.valid = valid;
+        p.k = k;
+      }
+    }
   }
   return p;
 }
@@ -480,11 +492,25 @@ void Solver::autotune_split(int k) {
         if (mode == 1 && ring == best.ring && nb == best.main.nb) continue;
         kern::SplitPlan c = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, nb, cfg_.arith)
                                       : kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, nb,
-                                                         cfg_.arith);  // spare: room for RCCL beside the interior
+                                                         cfg_.arith);
         if (!c.valid) continue;
         if (mode == 3) c.valid = 3;
         if (mode == 1)  // more items than waves only via explicit band counts above the default
           c.main_waves = std::min<int64_t>(c.main_items, std::max<int64_t>(c.main_waves, best.main_waves));
+        timed.emplace_back(time_plan(c, 4), c);
+      }
+      // segment work items (TbRect nb < 0): the interior cut into equal runs of
+      // strip rows, 1/2 .. 2 per persistent wave — balanced whatever the strip
+      // count (thin slabs: profiles/thin_slab.md)
+      const int64_t w0 = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, 0, cfg_.arith).main_waves
+                                   : best.main_waves;
+      for (double f : {0.5, 1.0, 1.5, 2.0}) {
+        const int64_t nseg = std::max<int64_t>(1, (int64_t)(w0 * f + 0.5));
+        kern::SplitPlan c = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, -nseg, cfg_.arith)
+                                      : kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, -nseg,
+                                                         cfg_.arith);
+        if (!c.valid) continue;
+        if (mode == 3) c.valid = 3;
         timed.emplace_back(time_plan(c, 4), c);
       }
     }

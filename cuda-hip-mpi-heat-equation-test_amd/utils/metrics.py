@@ -24,9 +24,21 @@ def strip_geometry(dtype_bytes: int, k: int) -> tuple:
     return w, w - 2 * ka
 
 
+def work_pieces(rows: int, nstrips: int, nb: int) -> int:
+    """Marches (each with its own 2k priming rows) of one rect of the
+    temporal-blocked kernel: nb > 0 row bands -> nb per strip; nb < 0 -> -nb
+    equal segments of the strip-major row sequence, cut again at strip ends
+    (tb_impl.hpp tb_range / tb_piece)."""
+    if nb > 0:
+        return nb * nstrips
+    total, nseg = rows * nstrips, -nb
+    cuts = {j * total // nseg for j in range(nseg + 1)} | {s * rows for s in range(nstrips + 1)}
+    return len(cuts) - 1
+
+
 def plan_hbm_bytes(plan: dict, dtype_bytes: int, nrows: int, ncols: int) -> dict:
     """DRAM traffic of ONE cycle of a split plan, from its geometry alone: every
-    work item (one row band of one strip) loads its band rows plus 2k priming
+    march (a row band or a segment piece of one strip) loads its rows plus 2k priming
     rows at the strip's full width W (the k-column halos on both sides
     included) and stores its useful U columns once. This counts no cache reuse
     between neighbouring strips / bands (rocprof measured 1.13-1.19x the field
@@ -42,7 +54,7 @@ def plan_hbm_bytes(plan: dict, dtype_bytes: int, nrows: int, ncols: int) -> dict
     for r0, r1, s0, s1, nb in rects:
         if r1 <= r0 or s1 <= s0:
             continue
-        rd += float((r1 - r0) + 2 * k * nb) * (s1 - s0) * w * dtype_bytes
+        rd += float((r1 - r0) * (s1 - s0) + 2 * k * work_pieces(r1 - r0, s1 - s0, nb)) * w * dtype_bytes
     wr = float(nrows) * ncols * dtype_bytes
     return {"read": rd, "write": wr, "total": rd + wr}
 

@@ -100,7 +100,9 @@ def test_hip_sizes(gpu, native, n):
     s.close()
 
 
-@pytest.mark.parametrize("tile_rows", [1, 7, 64, 512])
+# negative: -tile_rows segment work items (TbRect nb < 0); 300 x 300 fp64 at
+# depth 6 is 3 strips = 900 strip rows, so -5000 clamps to one-row segments
+@pytest.mark.parametrize("tile_rows", [1, 7, 64, 512, -1, -7, -250, -5000])
 def test_hip_tile_rows(gpu, native, tile_rows):
     p = prob(300, 19, "inclusive", "hat-cuda", dom=2.0)
     s = HeatSolver(p, dtype="fp64", backend="hip", tb=6, tile_rows=tile_rows, device=0)
@@ -263,6 +265,40 @@ def test_split_orders_with_exchange_bitwise(gpu, native, order, P, tb, dtype, n,
             pl = g.plan(i, k)
             assert pl["valid"] == want and pl["tuned_ms"] > 0, (i, k, pl)
     g.close()
+    ref = R.owned(R.ftcs(p, dtype=npdt))
+    assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
+
+
+@pytest.mark.parametrize("order,nseg", [("edge-first", 37), ("concurrent", 1000), ("single", 5), ("single", 4097)])
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+def test_segment_plans_bitwise(gpu, native, order, nseg, dtype, monkeypatch):
+    """Interior / single launches cut into segment work items (HEAT2D_SEGMENTS,
+    TbRect nb < 0 — runs of the strip-major row sequence crossing strip ends)
+    are bitwise equal to the golden: split orders with real loopback
+    exchanges, and the single launch of an unsplit grid."""
+    monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
+    monkeypatch.setenv("HEAT2D_SEGMENTS", str(nseg))
+    tb = 12 if dtype == "fp64" else 16
+    p = prob(1100, 2 * tb + 3, "ghost", "sine")
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    if order == "single":
+        s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0)
+        s.upload(R.owned(R.initial_field(p, npdt)))
+        s.step(p.ntime)
+        got = s.download()
+        pl = s.plan(tb)
+        s.close()
+        plans = [pl]
+    else:
+        g = LoopbackGroup(p, 3, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0)
+        g.upload(R.owned(R.initial_field(p, npdt)))
+        g.step(p.ntime)
+        got = g.download()
+        plans = [g.plan(i, tb) for i in range(3)]
+        g.close()
+    for pl in plans:
+        assert pl["main_bands"] == -pl["main_items"] and 0 < pl["main_items"] <= nseg, pl
+        assert pl["valid"] == {"edge-first": 3, "concurrent": 1, "single": 2}[order], pl
     ref = R.owned(R.ftcs(p, dtype=npdt))
     assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
 

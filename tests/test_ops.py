@@ -85,6 +85,27 @@ def test_stats_cpu(native):
     assert st["sum"] == 2.0 * 900 and st["min"] == 2.0 and st["max"] == 2.0
 
 
+def test_work_pieces():
+    """Marches per rect: bands -> nb per strip; segments -> cut again at strip ends."""
+    from heat2d.utils.metrics import work_pieces
+    assert work_pieces(100, 3, 4) == 12
+    assert work_pieces(100, 3, -1) == 3        # one segment over all strips
+    assert work_pieces(100, 3, -3) == 3        # aligned with the strips
+    assert work_pieces(100, 3, -2) == 4        # the middle strip cut once
+    assert work_pieces(100, 3, -300) == 300    # one-row segments
+    assert work_pieces(4096, 147, -1020) == 1020 + 146 - sum(
+        1 for s in range(1, 147) if (s * 4096 * 1020) % (4096 * 147) == 0)
+
+
+def test_plan_segments(native):
+    from heat2d.ops import _native as N
+    L = K.make_layout(4096, 32768, halo=16)
+    pl = N.plan_tb(N.F32, L, 0, 4096, 16, -1000)
+    assert pl.ntiles == -1000 and pl.nwaves == 1000
+    pl = N.plan_tb(N.F32, L, 0, 10, 16, -10 ** 9)      # clamped to one strip row each
+    assert pl.ntiles == -10 * pl.nstrips
+
+
 def test_plan_fills_chip(native):
     from heat2d.ops import _native as N
     L = K.make_layout(32768, 32768, halo=16)
@@ -96,7 +117,7 @@ def test_plan_fills_chip(native):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-@pytest.mark.parametrize("k,tile_rows", [(1, 0), (3, 0), (8, 0), (8, 5), (13, 0), (16, 0)])
+@pytest.mark.parametrize("k,tile_rows", [(1, 0), (3, 0), (8, 0), (8, 5), (13, 0), (16, 0), (8, -3), (16, -77)])
 def test_guard_gpu(native, gpu, dtype, k, tile_rows):
     run_guard("cuda", dtype, 203, k, (0, 201), tile_rows=tile_rows)
     run_guard("cuda", dtype, 203, k, (17, 61), row0=40, nrows=100, tile_rows=tile_rows)
