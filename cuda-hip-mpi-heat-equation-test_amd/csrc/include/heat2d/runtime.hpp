@@ -69,6 +69,9 @@ class Transport {
   virtual void barrier() = 0;
   virtual std::string name() const = 0;
   virtual bool capturable() const { return false; }  // safe inside hipGraph capture
+  // a graph with this transport's exchanges captured in it was launched on `stream`
+  // (failure detection tracks the replay as a whole)
+  virtual void graph_launched(hipStream_t /*stream*/) {}
   // true if exchange() moves data (size > 1, or a 1-rank periodic rehearsal)
   virtual bool exchanges() const { return size() > 1; }
   // Failure detection: raise if the fabric reported an asynchronous error

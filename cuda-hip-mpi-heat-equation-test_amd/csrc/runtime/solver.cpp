@@ -604,6 +604,7 @@ void Solver::run_graph_cycles(int64_t npairs) {
   }
   // the graph was captured for buffer parity 0 -> 1 -> 0
   for (int64_t i = 0; i < npairs; ++i) H2D_HIP(hipGraphLaunch(graph_exec_, s_compute_));
+  if (npairs > 0 && tr_->exchanges()) tr_->graph_launched(s_compute_);
   hist_[K] += 2 * npairs;
   if (npairs > 0) last_k_ = K;
   if (ovl) {  // eager cycles after the graph order against its end
@@ -833,6 +834,7 @@ void Solver::run_schedule_graph(int64_t n) {
   H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
   H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
   H2D_HIP(hipGraphLaunch(it->second, s_compute_));
+  if (tr_->exchanges()) tr_->graph_launched(s_compute_);
   // eager cycles after the graph order against its end
   H2D_HIP(hipEventRecord(ev_int_, s_compute_));
   H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));

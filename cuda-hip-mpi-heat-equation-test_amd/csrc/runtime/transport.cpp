@@ -15,6 +15,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -88,11 +89,14 @@ class RcclTransport final : public Transport {
   int size() const override { return size_; }
   std::string name() const override { return loop_ ? "rccl-loop" : "rccl"; }
   // Not captured into hipGraphs: capturing the grouped ncclSend/ncclRecv of
-  // the overlapped cycle segfaulted inside step() on the MI355X box (RCCL
-  // 2.26.6, tools/graph_rccl_probe.py, either split order), so --graph runs
-  // eager cycles whenever RCCL exchanges halos (single-rank runs still use
-  // graphs).
+  // the overlapped cycle segfaults inside step() on the MI355X box (RCCL
+  // 2.26.6, 1-rank self-loop, tools/graph_rccl_probe.py, either split order),
+  // also with the watchdog's event tracking kept out of the capture (track()
+  // skips capturing streams) — the fault is inside RCCL's captured send/recv
+  // path. --graph therefore runs eager cycles whenever RCCL exchanges halos
+  // (single-rank runs use graphs).
   bool capturable() const override { return false; }
+  void graph_launched(hipStream_t stream) override { track(stream, "graph replay"); }
   bool exchanges() const override { return size_ > 1 || loop_; }
   bool aborted() const override { return aborted_.load(); }
 
@@ -196,6 +200,9 @@ class RcclTransport final : public Transport {
   // record a completion event of the operation just enqueued on `s` (watchdog)
   void track(hipStream_t s, const char* what) {
     if (!wd_) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    H2D_HIP(hipStreamIsCapturing(s, &cs));
+    if (cs != hipStreamCaptureStatusNone) return;  // inside a capture: the replay is tracked
     std::lock_guard<std::mutex> g(pmu_);
     if (pend_.size() >= 4096) return;  // the host is far ahead: the oldest ones tell the story
     hipEvent_t e = nullptr;
