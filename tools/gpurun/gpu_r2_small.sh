@@ -1,13 +1,14 @@
 #!/bin/bash
-# Small grid (BASELINE config 2: 4096^2 fp32, 1000 steps) and the headline benches after the priming skip.
+# 4096^2 fp32 K=16, single launch over 1007 segments (the autotuner's plan): kernel trace + SQ/GRBM counters.
 set -o pipefail
-O=gpurun_out/small
+O=gpurun_out/small2
 mkdir -p $O
-export PYTHONUNBUFFERED=1
-timeout -k 10 600 python -u -m pytest tests/test_gpu_solver.py -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
-tail -1 $O/pytest.log
-show() { python -c "import json,sys;d=json.load(open(sys.argv[1]));c=d['config'];print(sys.argv[1].split('/')[-1], d['value'], d['ms_per_step'], c['cycles'], {k:(v['order'],v['main_bands'],v['main_waves']) for k,v in (c['launch_plans'] or {}).items()})" $1; }
-timeout -k 10 300 python bench.py --grid 4096 --dtype fp32 --steps 1000 --warmup 10 > $O/s4096.json || exit 1; show $O/s4096.json
-timeout -k 10 300 python bench.py --grid 4096 --dtype fp32 --steps 1000 --warmup 10 > $O/s4096b.json || exit 1; show $O/s4096b.json
-timeout -k 10 300 python bench.py --dtype fp32 --steps 480 --warmup 5 > $O/f32.json || exit 1; show $O/f32.json
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/b20.json || exit 1; show $O/b20.json
+export HEAT2D_SPLIT_ORDER=single HEAT2D_SEGMENTS=1007 HEAT2D_TB_RING=6
+timeout -k 10 120 python tools/cycle_probe.py fp32 4096 16 40 1 0 > $O/eager.json || exit 1
+timeout -k 10 120 python tools/cycle_probe.py fp32 4096 16 40 1 1 > $O/graph.json || exit 1
+timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d $O/trace -- python tools/cycle_probe.py fp32 4096 16 40 1 1 > /dev/null || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace --output-format csv -d $O/sq -- python tools/cycle_probe.py fp32 4096 16 10 1 0 > /dev/null || exit 1
+python tools/prof_summary.py trace $O/trace > $O/trace.txt || exit 1
+python tools/prof_summary.py sq $O/sq > $O/sq.txt || exit 1
+for f in $O/eager.json $O/graph.json; do python -c "import json;d=json.load(open('$f'));print('$f', round(d['gpts']), round(d['ms']/d['cycles']*1e3,1),'us/cycle')"; done
+tail -8 $O/trace.txt; cat $O/sq.txt | head -40

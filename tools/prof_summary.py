@@ -58,7 +58,15 @@ def sq(d):
             acc[r["Counter_Name"]] += float(r["Counter_Value"])
             n += 1
     wc = acc["SQ_WAVE_CYCLES"] or 1
-    return {"SQ_totals": {k: v for k, v in sorted(acc.items())},
+    # dispatches / mean duration of the same run's tb_kernel dispatches (kernel
+    # trace beside the counters): GRBM_GUI_ACTIVE per dispatch / duration = clock
+    ks = [r for r in rows(d, "kernel_trace") if "tb_kernel" in r["Kernel_Name"]]
+    dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in ks]
+    extra = {}
+    if dur and acc.get("GRBM_GUI_ACTIVE"):
+        extra = {"dispatches": len(dur), "mean_us": round(sum(dur) / len(dur) / 1e3, 2),
+                 "clock_GHz": round(acc["GRBM_GUI_ACTIVE"] / sum(dur), 3)}
+    return {**extra, "SQ_totals": {k: v for k, v in sorted(acc.items())},
             "wait_any/wave_cycles": round(acc["SQ_WAIT_ANY"] / wc, 3),
             "wait_inst_any/wave_cycles": round(acc["SQ_WAIT_INST_ANY"] / wc, 3),
             "active_inst_any/wave_cycles": round(acc["SQ_ACTIVE_INST_ANY"] / wc, 3),
