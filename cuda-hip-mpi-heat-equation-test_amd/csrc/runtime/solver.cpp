@@ -416,6 +416,14 @@ int Solver::spare_waves() const {
   return 8;
 }
 
+static bool tune_segments() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_TUNE_SEGMENTS");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 // smallest steady-state cycle (ms) for which edge-first split plans are tried
 constexpr float kEdgeFirstMinCycleMs = 0.4f;
 
@@ -501,7 +509,11 @@ void Solver::autotune_split(int k) {
       }
       // segment work items (TbRect nb < 0): the interior cut into equal runs of
       // strip rows, 1/2 .. 2 per persistent wave — balanced whatever the strip
-      // count (thin slabs: profiles/thin_slab.md)
+      // count (thin slabs: profiles/thin_slab.md); HEAT2D_TUNE_SEGMENTS=0 skips them.
+      // fp32: single launches only — split plans over segments won 4-cycle trials
+      // by noise and then ran 1.7 % slower than bands on 32768^2 (interleaved A/B,
+      // profiles/thin_slab.md §4), while single launches over segments win 4096^2
+      if (!tune_segments() || (dtype() == DType::F32 && mode != 2)) continue;
       const int64_t w0 = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, 0, cfg_.arith).main_waves
                                    : best.main_waves;
       for (double f : {0.5, 1.0, 1.5, 2.0}) {
