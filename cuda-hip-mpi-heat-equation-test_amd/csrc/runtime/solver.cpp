@@ -381,11 +381,14 @@ const kern::SplitPlan& Solver::split_plan(int k) {
         p.k = k;
       }
     }
-    // HEAT2D_SEGMENTS=n re-plans the interior (or the single launch) as n
-    // segment work items, keeping the order and ring (tests, A/B)
-    if (const char* env = std::getenv("HEAT2D_SEGMENTS")) {
-      const int64_t nseg = std::atoll(env);
-      if (nseg > 0 && p.valid) {
+    // HEAT2D_SEGMENTS=n / HEAT2D_BANDS=n re-plan the interior (or the single
+    // launch) as n segment work items / n row bands, keeping the order and ring
+    // (tests, A/B)
+    const char* env_seg = std::getenv("HEAT2D_SEGMENTS");
+    const char* env_bands = std::getenv("HEAT2D_BANDS");
+    if (env_seg || env_bands) {
+      const int64_t nseg = env_seg ? std::atoll(env_seg) : -std::atoll(env_bands);  // < 0: bands
+      if (nseg != 0 && p.valid) {
         const int valid = p.valid, ring = p.ring;
         p = valid == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, -nseg, cfg_.arith)
                        : kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, -nseg, cfg_.arith);
