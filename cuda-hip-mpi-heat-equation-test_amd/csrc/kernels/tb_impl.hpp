@@ -247,6 +247,17 @@ constexpr int chain_len() {
   return (c <= 0 || c >= K || K < HEAT2D_CHAIN_MIN_K || K > HEAT2D_CHAIN_MAX_K) ? K : c;
 }
 
+// Cache-policy bits of the march's 16-B row stores: 2 = nt (streaming). The
+// output rows are written once and read by the next pass only, so marking them
+// streaming leaves more of the XCD's L2 to the halo columns neighbouring strips
+// re-read: rocprof FETCH_SIZE per pass 1.160 -> 1.138x the field (fp64 32768^2,
+// K = 16), 1.130 -> 1.124x (fp32); 480-step fp64 bench +0.7 % in 6 of 6
+// interleaved pairs (profiles/hbm_model_check.md). Build with
+// -DHEAT2D_STORE_AUX=0 for the default policy.
+#ifndef HEAT2D_STORE_AUX
+#define HEAT2D_STORE_AUX 2
+#endif
+
 template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, int CL = K>
 struct March {
   using S = TbShape<T, NV, K>;
@@ -294,7 +305,7 @@ struct March {
       VT w;
 #pragma unroll
       for (int e = 0; e < VM; ++e) w[e] = out[v * VM + e];
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off + v * 16, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off + v * 16, 0, HEAT2D_STORE_AUX);
     }
   }
 
@@ -511,7 +522,7 @@ struct MarchF32 {
   }
   __device__ __forceinline__ void store_row(int32_t row, bool live, const VT& w) const {
     const __amdgpu_buffer_rsrc_t rs = row_rsrc(drow + (int64_t)row * pitch_b, live ? nrec : 0u);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off, 0, HEAT2D_STORE_AUX);
   }
   static __device__ __forceinline__ Row split(const Row& v) { return Row{F2{v.a.x, v.b.x}, F2{v.a.y, v.b.y}}; }
 
