@@ -24,29 +24,41 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def run(name, n, dtype, steps, warmup, backend, tb, graph=False):
     import heat2d
     from heat2d.models.heat2d import HeatSolver
+    from heat2d.utils.metrics import plan_hbm_bytes
     inp = heat2d.InputDat(n=n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=steps, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     t_init = time.perf_counter()
     s = HeatSolver(prob, dtype=dtype, backend=backend, tb=tb, graph=graph, device=0 if backend == "hip" else None)
     s.synchronize()
     t_init = time.perf_counter() - t_init
-    s.prepare(steps)  # plan / autotune outside the timed region
+    # as bench.py: warm-up, then plan / autotune / pick the cycle schedule of the
+    # timed run by measurement, outside the timed region
     s.step(warmup)
     s.synchronize()
+    tp = time.perf_counter()
+    s.prepare(steps)
+    prepare_s = time.perf_counter() - tp
+    s.cycle_hist(reset=True)
     t0 = time.perf_counter()
     s.step(steps)
     s.synchronize()
     dt = time.perf_counter() - t0
     st = s.stats()
     es = 8 if dtype == "fp64" else 4
-    k = s.tb
     gpts = float(n) * n * steps / dt / 1e9
-    rec = {"config": name, "n": n, "dtype": dtype, "backend": backend, "tb": k, "graph": graph, "steps": steps,
-           "s": round(dt, 6), "ms_per_step": round(dt / steps * 1e3, 5), "gpts": round(gpts, 2),
-           "model_gbps": round(gpts * 2 * es / k, 1), "field_gb": round(s.layout.elems() * es / 1e9, 2),
-           "init_s": round(t_init, 3), "finite": bool(math.isfinite(st["sum"]))}
+    hist = s.cycle_hist()
+    rec = {"config": name, "n": n, "dtype": dtype, "backend": backend, "tb_max": s.tb, "graph": graph,
+           "steps": steps, "s": round(dt, 6), "ms_per_step": round(dt / steps * 1e3, 5), "gpts": round(gpts, 2),
+           "cycles": {str(k): c for k, c in sorted(hist.items())}, "field_gb": round(s.layout.elems() * es / 1e9, 2),
+           "init_s": round(t_init, 3), "prepare_s": round(prepare_s, 2), "finite": bool(math.isfinite(st["sum"]))}
     if backend == "hip":
-        rec["launch_plan"] = s.plan()
+        plans, traffic = {}, 0.0
+        for k, c in sorted(hist.items()):
+            pl = s.plan(k)
+            plans[str(k)] = {kk: pl[kk] for kk in ("order", "ring", "main_bands", "main_waves", "tuned_ms")}
+            traffic += c * plan_hbm_bytes(pl, es, n, n)["total"]
+        rec["launch_plans"] = plans
+        rec["hbm_gb_per_s_plan"] = round(traffic / dt / 1e9, 1)
     s.close()
     return rec
 
@@ -64,13 +76,14 @@ def main():
     nmax = int(math.sqrt(a.max_gb * 1e9 / (2 * es32)))
     nmax = nmax // 1024 * 1024
     plan = [
+        # tb 0: depths up to the dtype's maximum, chosen per run by measurement
         ("cpu-256-fp64", 256, "fp64", 200, 8, "cpu", 8, False),
-        ("gpu-4096-fp32", 4096, "fp32", 1000, 64, "hip", 16, False),
-        ("gpu-4096-fp32-graph", 4096, "fp32", 1000, 64, "hip", 16, True),
-        ("gpu-16384-fp64", 16384, "fp64", 480, 48, "hip", 14, False),
-        ("gpu-32768-fp64", 32768, "fp64", 480, 48, "hip", 14, False),
-        ("gpu-32768-fp32", 32768, "fp32", 480, 48, "hip", 16, False),
-        ("gpu-max-fp32", nmax, "fp32", 64, 16, "hip", 16, False),
+        ("gpu-4096-fp32", 4096, "fp32", 1000, 64, "hip", 0, False),
+        ("gpu-4096-fp32-graph", 4096, "fp32", 1000, 64, "hip", 0, True),
+        ("gpu-16384-fp64", 16384, "fp64", 480, 48, "hip", 0, False),
+        ("gpu-32768-fp64", 32768, "fp64", 480, 48, "hip", 0, False),
+        ("gpu-32768-fp32", 32768, "fp32", 480, 48, "hip", 0, False),
+        ("gpu-max-fp32", nmax, "fp32", 64, 16, "hip", 0, False),
     ]
     for name, n, dt, steps, warm, be, tb, graph in plan:
         if a.only and not any(name.startswith(o) for o in a.only):
