@@ -269,15 +269,17 @@ def test_split_orders_with_exchange_bitwise(gpu, native, order, P, tb, dtype, n,
     assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
 
 
-@pytest.mark.parametrize("order,nseg", [("edge-first", 37), ("concurrent", 1000), ("single", 5), ("single", 4097)])
+@pytest.mark.parametrize("order,nseg", [("edge-first", 37), ("concurrent", 1000), ("single", 5), ("single", 4097),
+                                        ("concurrent", -3), ("single", -40)])
 @pytest.mark.parametrize("dtype", ["fp64", "fp32"])
 def test_segment_plans_bitwise(gpu, native, order, nseg, dtype, monkeypatch):
     """Interior / single launches cut into segment work items (HEAT2D_SEGMENTS,
     TbRect nb < 0 — runs of the strip-major row sequence crossing strip ends)
-    are bitwise equal to the golden: split orders with real loopback
-    exchanges, and the single launch of an unsplit grid."""
+    or forced row-band counts (HEAT2D_BANDS, nseg < 0 here) are bitwise equal
+    to the golden: split orders with real loopback exchanges, and the single
+    launch of an unsplit grid."""
     monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
-    monkeypatch.setenv("HEAT2D_SEGMENTS", str(nseg))
+    monkeypatch.setenv("HEAT2D_SEGMENTS" if nseg > 0 else "HEAT2D_BANDS", str(abs(nseg)))
     tb = 12 if dtype == "fp64" else 16
     p = prob(1100, 2 * tb + 3, "ghost", "sine")
     npdt = np.float64 if dtype == "fp64" else np.float32
@@ -297,7 +299,10 @@ def test_segment_plans_bitwise(gpu, native, order, nseg, dtype, monkeypatch):
         plans = [g.plan(i, tb) for i in range(3)]
         g.close()
     for pl in plans:
-        assert pl["main_bands"] == -pl["main_items"] and 0 < pl["main_items"] <= nseg, pl
+        if nseg > 0:
+            assert pl["main_bands"] == -pl["main_items"] and 0 < pl["main_items"] <= nseg, pl
+        else:
+            assert 0 < pl["main_bands"] <= -nseg, pl
         assert pl["valid"] == {"edge-first": 3, "concurrent": 1, "single": 2}[order], pl
     ref = R.owned(R.ftcs(p, dtype=npdt))
     assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
