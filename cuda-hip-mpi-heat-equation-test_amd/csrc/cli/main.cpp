@@ -127,7 +127,8 @@ struct Shared {
   std::vector<std::shared_ptr<Transport>> trs;  // every rank's transport (fail-fast abort)
   std::vector<std::shared_ptr<Transport>> cpu_trs;  // --cpu with P > 1: the host-thread transports
   double final_stats[6] = {0};
-  int tb_used = 1;  // temporal depth the solver actually ran (jit / copy-swap force 1)
+  int tb_used = 1;  // largest temporal depth the solver may run (jit / copy-swap force 1)
+  int64_t hist[kMaxTB + 1] = {0};  // cycles per depth of the timed loop (rank 0)
   int64_t start_step = 0;  // > 0 after --restart
 };
 
@@ -268,6 +269,10 @@ void run_rank(Shared& sh, int rank) {
       }
     }
     if (a.timers) s.set_timing(true);
+    {
+      int64_t h[kMaxTB + 1];
+      s.cycle_hist(h, true);  // count the timed loop's cycles only
+    }
     tr->barrier();
     s.synchronize();
     const auto t0 = std::chrono::steady_clock::now();
@@ -342,6 +347,7 @@ void run_rank(Shared& sh, int rank) {
     if (root) {
       std::memcpy(sh.final_stats, st, sizeof(st));
       sh.tb_used = s.config().tb;
+      s.cycle_hist(sh.hist, false);
     }
   } catch (const std::exception& e) {
     // fail fast: the first error is reported; every rank's communicator is
@@ -402,25 +408,37 @@ int main(int argc, char** argv) {
   const double gpts = ntime > 0 && tmax > 0 ? pts * (double)ntime / tmax / 1e9 : 0.0;
   const int es = a.dtype == "fp32" ? 4 : 8;
   const int K = sh.tb_used;
-  // model bytes/pt/step: one read + one write per HBM pass (K steps); copy mode adds the copy
-  const double bpp = a.copy_swap ? 4.0 * es : 2.0 * es / K;
+  // passes (cycles) the timed loop launched, and their depths: the measured
+  // schedule / balanced cycles decide them, not K alone
+  int64_t passes = 0;
+  std::string depths;
+  for (int k = 1; k <= kMaxTB; ++k) {
+    if (!sh.hist[k]) continue;
+    passes += sh.hist[k];
+    depths += (depths.empty() ? "" : ", ") + std::string("\"") + std::to_string(k) + "\": " + std::to_string(sh.hist[k]);
+  }
+  // model bytes/pt/step: one read + one write of the field per HBM pass; copy mode adds the copy
+  const double bpp = a.copy_swap ? 4.0 * es
+                                 : (passes > 0 && ntime > 0 ? 2.0 * es * (double)passes / (double)ntime : 2.0 * es / K);
   std::printf(" simulation completed!!!!\n");
   if (a.variant == "mpi")
     std::printf(" Average time: %24.16g\n", ntime > 0 ? tmax / (double)ntime : 0.0);
   else
     std::printf(" total time: %24.16g\n", tmax);
   if (!a.quiet)
-    std::printf(" heat2d: n=%lld P=%d %s K=%d steps=%lld wall=%.6f s  %.3f Gpts/s  %.1f GB/s(model)  sum(T)=%.17g\n",
-                (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, (long long)ntime, tmax, gpts,
-                gpts * bpp, sh.final_stats[0]);
+    std::printf(" heat2d: n=%lld P=%d %s K<=%d passes=%lld steps=%lld wall=%.6f s  %.3f Gpts/s  %.1f GB/s(model)  "
+                "sum(T)=%.17g\n",
+                (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, (long long)passes, (long long)ntime, tmax,
+                gpts, gpts * bpp, sh.final_stats[0]);
   if (!a.json.empty()) {
     FILE* f = std::fopen(a.json.c_str(), "w");
     if (f) {
       std::fprintf(f,
-                   "{\"n\": %lld, \"nranks\": %d, \"dtype\": \"%s\", \"tb\": %d, \"steps\": %lld, \"wall_s\": %.9g, "
+                   "{\"n\": %lld, \"nranks\": %d, \"dtype\": \"%s\", \"tb\": %d, \"cycles\": {%s}, \"steps\": %lld, \"wall_s\": %.9g, "
                    "\"gpts_per_s\": %.9g, \"model_gb_per_s\": %.9g, \"sum\": %.17g, \"min\": %.17g, \"max\": %.17g, "
                    "\"backend\": \"%s\", \"variant\": \"%s\", \"arith\": \"%s\"}\n",
-                   (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, (long long)ntime, tmax, gpts, gpts * bpp,
+                   (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, depths.c_str(), (long long)ntime, tmax,
+                   gpts, gpts * bpp,
                    sh.final_stats[0], sh.final_stats[2], sh.final_stats[3], a.cpu ? "cpu" : "hip", a.variant.c_str(),
                    a.arith.c_str());
       std::fclose(f);

@@ -136,6 +136,7 @@ def run(argv=None) -> int:
             seen.add(c)
             s.prepare(c)
         d += c
+    s.cycle_hist(reset=True)  # count the timed loop's cycles only
     _barrier(world)
     s.synchronize()
     t0 = time.perf_counter()
@@ -163,6 +164,7 @@ def run(argv=None) -> int:
     elapsed = time.perf_counter() - t0
     elapsed = _max_over_ranks(elapsed, world, backend)
     ran = nsteps - start_step
+    cycles = s.cycle_hist()
 
     if a.checkpoint:
         checkpoint.save(s, a.checkpoint, step=done)
@@ -188,9 +190,11 @@ def run(argv=None) -> int:
         else:
             print(f" total time: {elapsed:24.16g}")
         rec = metrics.record(prob.n_owned, ran, elapsed, world, a.dtype, s.tb, backend, a.copy_swap,
-                             {"variant": var.name, "arith": a.arith, "sum": st["sum"], "min": st["min"], "max": st["max"]})
+                             {"variant": var.name, "arith": a.arith, "sum": st["sum"], "min": st["min"], "max": st["max"]},
+                             cycles=cycles)
         if not a.quiet:
-            print(f" heat2d: n={prob.n_owned} P={world} {a.dtype} K={s.tb} steps={ran} wall={elapsed:.6f} s  "
+            print(f" heat2d: n={prob.n_owned} P={world} {a.dtype} K<={s.tb} passes={sum(cycles.values())} "
+                  f"steps={ran} wall={elapsed:.6f} s  "
                   f"{rec['gpts_per_s']:.3f} Gpts/s  {rec['model_hbm_gb_per_s']:.1f} GB/s(model)  "
                   f"sum(T)={st['sum']:.17g}", flush=True)
         if a.json:

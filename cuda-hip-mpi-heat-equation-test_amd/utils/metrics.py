@@ -60,14 +60,23 @@ def plan_hbm_bytes(plan: dict, dtype_bytes: int, nrows: int, ncols: int) -> dict
 
 
 def record(n_owned: int, steps: int, seconds: float, nranks: int, dtype: str, tb: int, backend: str,
-           copy_swap: bool = False, extra: Optional[dict] = None) -> dict:
+           copy_swap: bool = False, extra: Optional[dict] = None, cycles: Optional[dict] = None) -> dict:
+    """Run record. cycles: {depth: count} the timed loop launched (Solver.cycle_hist);
+    with it the model counts one read + one write per pass actually run
+    instead of assuming depth tb throughout."""
     es = 8 if dtype == "fp64" else 4
     pts = float(n_owned) * float(n_owned)
     gpts = pts * steps / seconds / 1e9 if seconds > 0 and steps > 0 else 0.0
+    passes = sum(cycles.values()) if cycles else 0
+    if passes and steps and not copy_swap:
+        bpp = 2.0 * es * passes / steps
+    else:
+        bpp = model_bytes_per_point_step(es, tb, copy_swap)
     r = {
         "n": n_owned, "steps": steps, "wall_s": seconds, "nranks": nranks, "dtype": dtype, "tb": tb,
+        "cycles": {str(k): v for k, v in sorted((cycles or {}).items())},
         "backend": backend, "gpts_per_s": gpts,
-        "model_hbm_gb_per_s": gpts * model_bytes_per_point_step(es, tb, copy_swap),
+        "model_hbm_gb_per_s": gpts * bpp,
         "s_per_iteration": seconds / steps if steps else 0.0,
         "time": time.time(),
     }

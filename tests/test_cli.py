@@ -69,6 +69,9 @@ def test_cli_flags_and_json(cli, tmp_path):
     import json
     r = json.loads((tmp_path / "r.json").read_text())
     assert r["n"] == 48 and r["steps"] == 9 and r["dtype"] == "fp32" and r["backend"] == "cpu"
+    # the cycles the timed loop launched, per depth: they add up to the steps run
+    assert sum(int(k) * c for k, c in r["cycles"].items()) == 9 and max(map(int, r["cycles"])) <= 4
+    assert "passes=" in out
 
 
 def test_cli_time_it_every_step_keeps_deep_cycles(cli, tmp_path):
