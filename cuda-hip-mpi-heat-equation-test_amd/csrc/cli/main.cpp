@@ -62,6 +62,8 @@ struct Args {
   std::string checkpoint;       // --checkpoint DIR (utils/checkpoint.py format)
   int64_t checkpoint_every = 0;
   std::string restart;          // --restart DIR (any writer rank count)
+  std::string transport = "rccl";  // GPU ranks: rccl | peer (device copies between the ranks' fields, no RCCL)
+  bool share_gpu = false;          // --share-gpu: every rank on device 0 (peer transport; tests / rehearsals)
 };
 
 void usage() {
@@ -70,7 +72,8 @@ void usage() {
       "              [--tb K] [--no-overlap] [--copy-swap] [--managed] [--graph] [--ic NAME]\n"
       "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
       "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith auto|exact|fma]\n"
-      "              [--checkpoint DIR [--checkpoint-every N]] [--restart DIR]\n");
+      "              [--checkpoint DIR [--checkpoint-every N]] [--restart DIR]\n"
+      "              [--transport rccl|peer] [--share-gpu]\n");
 }
 
 Args parse_args(int argc, char** argv) {
@@ -108,6 +111,8 @@ Args parse_args(int argc, char** argv) {
     else if (s == "--checkpoint") a.checkpoint = need("--checkpoint");
     else if (s == "--checkpoint-every") a.checkpoint_every = std::atoll(need("--checkpoint-every").c_str());
     else if (s == "--restart") a.restart = need("--restart");
+    else if (s == "--transport") a.transport = need("--transport");
+    else if (s == "--share-gpu") a.share_gpu = true;
     else if (!s.empty() && s[0] != '-') a.input = s;
     else { std::fprintf(stderr, "unknown flag %s\n", s.c_str()); usage(); std::exit(2); }
   }
@@ -126,6 +131,7 @@ struct Shared {
   std::string err;
   std::vector<std::shared_ptr<Transport>> trs;  // every rank's transport (fail-fast abort)
   std::vector<std::shared_ptr<Transport>> cpu_trs;  // --cpu with P > 1: the host-thread transports
+  std::vector<std::shared_ptr<Transport>> peer_trs;  // --transport peer with P > 1
   double final_stats[6] = {0};
   int tb_used = 1;  // largest temporal depth the solver may run (jit / copy-swap force 1)
   int64_t hist[kMaxTB + 1] = {0};  // cycles per depth of the timed loop (rank 0)
@@ -179,13 +185,15 @@ void run_rank(Shared& sh, int rank) {
   const bool root = rank == 0;
   try {
     std::shared_ptr<Transport> tr;
+    const int device = a.share_gpu ? 0 : rank;
     if (!a.cpu) {
-      if (hipSetDevice(rank) != hipSuccess) fail(__FILE__, __LINE__, "hipSetDevice failed");
-      if (!a.quiet && (root || P > 1)) std::printf(" MPI rank %12d using GPU %12d\n", rank, rank);
+      if (hipSetDevice(device) != hipSuccess) fail(__FILE__, __LINE__, "hipSetDevice failed");
+      if (!a.quiet && (root || P > 1)) std::printf(" MPI rank %12d using GPU %12d\n", rank, device);
     }
     if (P == 1) tr = make_self_transport();
     else if (a.cpu) tr = sh.cpu_trs[(size_t)rank];  // host threads (the reference's `make mpi`)
-    else tr = make_rccl_transport(sh.uid, rank, P, rank);
+    else if (a.transport == "peer") tr = sh.peer_trs[(size_t)rank];
+    else tr = make_rccl_transport(sh.uid, rank, P, device);
     {
       std::lock_guard<std::mutex> g(sh.mu);
       sh.trs[(size_t)rank] = tr;
@@ -202,7 +210,7 @@ void run_rank(Shared& sh, int rank) {
     cfg.overlap = a.overlap ? 1 : 0;
     cfg.copy_swap = a.copy_swap ? 1 : 0;
     cfg.managed = a.managed ? 1 : 0;
-    cfg.device = a.cpu ? -1 : rank;
+    cfg.device = a.cpu ? -1 : device;
     cfg.use_graph = a.graph ? 1 : 0;
     cfg.autotune = -1;  // split schedule on big slabs: pick the fastest launch plan on the first cycle
     if (a.engine != "tb" && a.engine != "jit") fail(__FILE__, __LINE__, "--engine must be tb or jit");
@@ -384,8 +392,12 @@ int main(int argc, char** argv) {
       a.cpu = true;
     }
     sh.nranks = a.cpu ? std::max(1, a.gpus) : (a.gpus > 0 ? a.gpus : 1);
-    if (!a.cpu && sh.nranks > ndev) fail(__FILE__, __LINE__, "more GPUs requested than present");
+    if (a.transport != "rccl" && a.transport != "peer") fail(__FILE__, __LINE__, "--transport must be rccl or peer");
+    if (a.share_gpu && a.transport != "peer")
+      fail(__FILE__, __LINE__, "--share-gpu needs --transport peer (RCCL refuses two ranks on one GPU)");
+    if (!a.cpu && !a.share_gpu && sh.nranks > ndev) fail(__FILE__, __LINE__, "more GPUs requested than present");
     if (a.cpu && sh.nranks > 1) sh.cpu_trs = make_thread_transports(sh.nranks);
+    else if (sh.nranks > 1 && a.transport == "peer") sh.peer_trs = make_peer_transports(sh.nranks);
     else if (sh.nranks > 1) rccl_unique_id(sh.uid);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "heat2d: %s\n", e.what());

@@ -122,6 +122,10 @@ std::vector<std::shared_ptr<Transport>> make_loopback_transports(int nranks);
 // barrier-synchronised zero-copy row exchange, fixed-order all-reduce;
 // barriers time out (HEAT2D_COMM_TIMEOUT) and abort() wakes every waiter.
 std::vector<std::shared_ptr<Transport>> make_thread_transports(int nranks);
+// P ranks as threads of one process with device fields, no RCCL: halos pulled
+// by device-to-device copies out of the neighbours' fields (peer access between
+// GPUs), ordered by events + host-side waits (transport.cpp PeerTransport).
+std::vector<std::shared_ptr<Transport>> make_peer_transports(int nranks);
 // RCCL over xGMI. `uid` = 128-byte ncclUniqueId produced by rccl_unique_id()
 // on rank 0 and broadcast out of band (torch.distributed store, file, or a
 // shared variable for thread-per-GPU).

@@ -571,9 +571,178 @@ class ThreadTransport final : public Transport {
   int rank_;
 };
 
+// ------------------------------------------------------------------ peer
+// P ranks as host threads of one process, each on its own GPU (or sharing one:
+// the native CLI's --share-gpu), device fields, NO RCCL: every halo is pulled
+// by the receiving rank on its exchange stream with a device-to-device
+// hipMemcpyAsync straight out of the neighbour's field (peer access over xGMI
+// between GPUs: a copy, not a send/recv kernel competing for wave slots with
+// the persistent interior, profiles/thin_slab.md §7-§8). The ordering is the
+// loopback transport's event protocol (a pull of cycle c waits for the peer's
+// band event of cycle c and for the peer's own pulls of cycle c-1); threads add
+// host-side waits so that those events are RECORDED before anyone waits on
+// them: a pull of cycle c starts once the peer has posted cycle c and enqueued
+// its pulls of cycle c-1. A peer runs at most one cycle ahead (its pull of
+// c+1 needs this rank's post of c+1), so its posted fields are kept per cycle
+// parity; waiting on a newer record of its band / done events is only
+// conservative. Barrier / all-reduce / abort / timeout: ThreadHub.
+struct PeerHub : ThreadHub {
+  struct Slot {
+    void* field[2] = {nullptr, nullptr};  // posted field of cycle c at [c & 1]
+    SlabLayout L{};
+    hipEvent_t ready = nullptr;  // the poster's band event (not owned)
+    hipEvent_t done[2] = {nullptr, nullptr};  // owned: pulls of cycle parity p done
+    int device = -1;
+    int64_t posted = 0, pulled = 0;
+  };
+  explicit PeerHub(int n) : ThreadHub(n), slot((size_t)n) {}
+  ~PeerHub() {
+    for (auto& sl : slot)
+      for (auto& e : sl.done)
+        if (e) (void)hipEventDestroy(e);
+  }
+  std::vector<Slot> slot;
+  std::mutex peer_mu;  // device pairs with peer access enabled
+  std::vector<std::pair<int, int>> peer_on;
+};
+
+class PeerTransport final : public Transport {
+ public:
+  PeerTransport(std::shared_ptr<PeerHub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int size() const override { return hub_->n; }
+  std::string name() const override { return "peer"; }
+  void abort(const std::string& reason) override { hub_->abort(reason); }
+  bool aborted() const override {
+    std::lock_guard<std::mutex> g(hub_->mu);
+    return hub_->aborted;
+  }
+  void check() override {
+    std::unique_lock<std::mutex> lk(hub_->mu);
+    if (hub_->aborted) hub_->throw_aborted(rank_);
+  }
+
+  void post(void* field, const SlabLayout& L, hipEvent_t ready) override {
+    int dev = 0;
+    H2D_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(hub_->mu);
+    auto& me = hub_->slot[(size_t)rank_];
+    HEAT2D_REQUIRE(me.posted == me.pulled, "peer: a cycle was posted twice without an exchange");
+    me.field[me.posted & 1] = field;
+    me.L = L;
+    me.ready = ready;
+    me.device = dev;
+    ++me.posted;
+    hub_->cv.notify_all();
+  }
+
+  void exchange(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
+                bool on_device) override {
+    HEAT2D_REQUIRE(on_device, "the peer transport moves device fields");
+    if (size() == 1 || k <= 0) return;
+    auto& me = hub_->slot[(size_t)rank_];
+    int dev = 0;
+    H2D_HIP(hipGetDevice(&dev));
+    int64_t c;
+    {
+      std::lock_guard<std::mutex> g(hub_->mu);
+      HEAT2D_REQUIRE(me.posted == me.pulled + 1 && me.field[me.pulled & 1] == field,
+                     "peer: exchange of a field that was not posted this cycle");
+      c = me.pulled;
+    }
+    for (auto& e : me.done)
+      if (!e) H2D_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const size_t es = dtype_size(dt);
+    const size_t bytes = halo_msg_bytes(L, k, es);
+    HaloMsg msg[2];
+    const int nmsg = halo_msgs(rank_, size(), L, k, msg);
+    for (int i = 0; i < nmsg; ++i) {
+      const int p = msg[i].peer;
+      PeerHub::Slot peer;
+      {  // the peer's post of cycle c and its pulls of cycle c-1 are enqueued
+        std::unique_lock<std::mutex> lk(hub_->mu);
+        const auto& ps = hub_->slot[(size_t)p];
+        const auto pred = [&] { return (ps.posted >= c + 1 && ps.pulled >= c) || hub_->aborted; };
+        if (hub_->timeout > 0) {
+          if (!hub_->cv.wait_for(lk, std::chrono::duration<double>(hub_->timeout), pred)) {
+            hub_->aborted = true;
+            hub_->reason = "rank " + std::to_string(rank_) + " waited " + std::to_string(hub_->timeout) +
+                           " s for rank " + std::to_string(p) + "'s halo (HEAT2D_COMM_TIMEOUT)";
+            hub_->cv.notify_all();
+          }
+        } else {
+          hub_->cv.wait(lk, pred);
+        }
+        if (hub_->aborted) hub_->throw_aborted(rank_);
+        peer = ps;
+      }
+      HEAT2D_REQUIRE(peer.L.pitch == L.pitch, "peer: slabs of different pitch");
+      HaloMsg pm[2];
+      const int np = halo_msgs(p, size(), peer.L, k, pm);
+      int64_t send_row = -1;
+      for (int j = 0; j < np; ++j)
+        if (pm[j].peer == rank_) send_row = pm[j].send_row;
+      HEAT2D_REQUIRE(send_row >= 0, "peer: neighbour does not send to this rank");
+      if (peer.device != dev) enable_peer(dev, peer.device);
+      const char* src = static_cast<const char*>(peer.field[c & 1]) + halo_row_bytes(peer.L, send_row, es);
+      char* dst = static_cast<char*>(field) + halo_row_bytes(L, msg[i].recv_row, es);
+      H2D_HIP(hipStreamWaitEvent(stream, peer.ready, 0));
+      if (c > 0) H2D_HIP(hipStreamWaitEvent(stream, peer.done[(c - 1) & 1], 0));
+      H2D_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream));
+    }
+    H2D_HIP(hipEventRecord(me.done[c & 1], stream));
+    std::lock_guard<std::mutex> g(hub_->mu);
+    ++me.pulled;
+    hub_->cv.notify_all();
+  }
+
+  void allreduce(double* vals, int n, int op) override {
+    HEAT2D_REQUIRE(n <= 64, "allreduce too large");
+    if (size() == 1) return;
+    std::copy(vals, vals + n, hub_->vals.begin() + (ptrdiff_t)rank_ * 64);
+    hub_->barrier(rank_);
+    for (int j = 0; j < n; ++j) {  // same fixed order on every rank: identical results
+      double a = hub_->vals[(size_t)j];
+      for (int r = 1; r < size(); ++r) {
+        const double b = hub_->vals[(size_t)r * 64 + j];
+        a = op == 0 ? a + b : (op == 1 ? std::max(a, b) : std::min(a, b));
+      }
+      vals[j] = a;
+    }
+    hub_->barrier(rank_);
+  }
+  void barrier() override { hub_->barrier(rank_); }
+
+ private:
+  // direct peer reads over xGMI for the copies this device pulls from `peer`
+  void enable_peer(int dev, int peer) {
+    std::lock_guard<std::mutex> g(hub_->peer_mu);
+    for (const auto& pr : hub_->peer_on)
+      if (pr.first == dev && pr.second == peer) return;
+    int can = 0;
+    H2D_HIP(hipDeviceCanAccessPeer(&can, dev, peer));
+    if (can) {
+      const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+      if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+      else H2D_HIP(e);
+    }
+    hub_->peer_on.emplace_back(dev, peer);
+  }
+  std::shared_ptr<PeerHub> hub_;
+  int rank_;
+};
+
 }  // namespace
 
 std::shared_ptr<Transport> make_self_transport() { return std::make_shared<SelfTransport>(); }
+
+std::vector<std::shared_ptr<Transport>> make_peer_transports(int nranks) {
+  HEAT2D_REQUIRE(nranks >= 1, "nranks >= 1");
+  auto hub = std::make_shared<PeerHub>(nranks);
+  std::vector<std::shared_ptr<Transport>> v;
+  for (int i = 0; i < nranks; ++i) v.push_back(std::make_shared<PeerTransport>(hub, i));
+  return v;
+}
 
 std::vector<std::shared_ptr<Transport>> make_thread_transports(int nranks) {
   HEAT2D_REQUIRE(nranks >= 1, "nranks >= 1");

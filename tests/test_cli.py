@@ -151,6 +151,44 @@ def test_cli_gpu_serial_variant(cli, gpu, tmp_path, extra):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--no-overlap"], ["--tb", "5"], ["--check-every", "10"], ["--dtype", "fp32"]])
+def test_cli_peer_transport_bitwise(cli, gpu, tmp_path, extra):
+    """P ranks as threads of the native CLI with the peer transport (no RCCL:
+    halos pulled by device copies out of the neighbours' fields, ordered by
+    events and host-side waits), all on one GPU (--share-gpu): the rank slabs
+    put together are bitwise the golden — split schedule (1100^2 slabs are
+    split into interior + bands), serial schedule, other depths, fused
+    statistics, fp32."""
+    (tmp_path / "input.dat").write_text("1100 0.25 0.05 1.0 31 0\n")
+    out = run_cli(tmp_path, "--gpus", "3", "--transport", "peer", "--share-gpu", "--output", "npy", *extra)
+    assert out.count("using GPU            0") == 3
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    npdt = np.float32 if "fp32" in extra else np.float64
+    got = np.concatenate([np.load(tmp_path / f"soln{r:05d}.npy") for r in range(3)])
+    assert np.array_equal(got, R.owned(R.ftcs(prob, dtype=npdt)))
+
+
+@pytest.mark.gpu
+def test_cli_peer_transport_eight_ranks_autotuned(cli, gpu, tmp_path):
+    """8 rank threads on one GPU, a grid big enough for the autotuner and the
+    measured schedules (4200^2 > 2^24 points): many cycles of real host
+    concurrency through the peer transport's waits, bitwise the golden."""
+    (tmp_path / "input.dat").write_text("4200 0.25 0.05 1.0 75 0\n")
+    run_cli(tmp_path, "--gpus", "8", "--transport", "peer", "--share-gpu", "--output", "npy", "--quiet",
+            "--print-every", "25", "--check-every", "25")
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    got = np.concatenate([np.load(tmp_path / f"soln{r:05d}.npy") for r in range(8)])
+    assert np.array_equal(got, R.owned(R.ftcs(prob)))
+
+
+def test_cli_share_gpu_needs_peer(cli, tmp_path):
+    (tmp_path / "input.dat").write_text("64 0.25 0.05 1.0 5 0\n")
+    p = subprocess.run([N.CLI_PATH, "--gpus", "2", "--share-gpu"], cwd=tmp_path, capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode != 0 and "--share-gpu needs --transport peer" in p.stderr
+
+
+@pytest.mark.gpu
 def test_cli_gpu_checkpoint_restart(cli, gpu, tmp_path):
     """GPU run checkpointed mid-way (HIP fields -> rank .npy), resumed on the GPU
     and, separately, on the CPU twin: both finish bitwise equal to the golden."""
