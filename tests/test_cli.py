@@ -181,6 +181,24 @@ def test_cli_peer_transport_eight_ranks_autotuned(cli, gpu, tmp_path):
     assert np.array_equal(got, R.owned(R.ftcs(prob)))
 
 
+@pytest.mark.gpu
+def test_cli_peer_transport_fails_fast(cli, gpu, tmp_path):
+    """Peer transport: one rank fails mid-run (fault injection); the others,
+    blocked in the transport's host-side waits for its halo, are woken by the
+    abort and the process exits non-zero naming the failed rank, well inside
+    the comm timeout."""
+    import time
+    (tmp_path / "input.dat").write_text("600 0.25 0.05 1.0 400 0\n")
+    env = dict(os.environ, HEAT2D_FAIL_RANK="1", HEAT2D_FAIL_STEP="16", HEAT2D_COMM_TIMEOUT="60")
+    t0 = time.time()
+    p = subprocess.run([N.CLI_PATH, "--gpus", "3", "--transport", "peer", "--share-gpu", "--tb", "8",
+                        "--print-every", "8", "--output", "none"], cwd=tmp_path, capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert p.returncode != 0
+    assert "rank 1" in p.stderr and "injected failure" in p.stderr, p.stderr
+    assert time.time() - t0 < 40
+
+
 def test_cli_share_gpu_needs_peer(cli, tmp_path):
     (tmp_path / "input.dat").write_text("64 0.25 0.05 1.0 5 0\n")
     p = subprocess.run([N.CLI_PATH, "--gpus", "2", "--share-gpu"], cwd=tmp_path, capture_output=True, text=True,
