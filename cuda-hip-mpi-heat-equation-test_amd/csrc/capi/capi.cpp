@@ -396,6 +396,22 @@ int heat2d_cycle_schedule(int64_t n, int kmax, const double* t_ms, int32_t* out,
   });
 }
 
+int heat2d_cycle_schedule_near(int64_t n, int kmax, const double* t_ms, double tol, int m, int32_t* out, int64_t cap,
+                               int64_t* lens, int32_t* count) {
+  return guarded([&] {
+    const auto v = cycle_schedule_near(n, kmax, [&](int k) { return k >= 1 && k <= kmax ? t_ms[k] : -1.0; }, tol, m);
+    *count = (int32_t)v.size();
+    int64_t pos = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+      lens[i] = (int64_t)v[i].size();
+      for (int d : v[i]) {
+        HEAT2D_REQUIRE(pos < cap, "schedule output buffer too small");
+        out[pos++] = d;
+      }
+    }
+  });
+}
+
 int heat2d_transport_abort(void* t, const char* reason) {
   return guarded([&] { static_cast<TransportHandle*>(t)->t->abort(reason ? reason : "aborted by the caller"); });
 }

@@ -162,6 +162,9 @@ int heat2d_solver_cycle_hist(void* s, int64_t* out, int n, int reset);
 int heat2d_solver_schedule(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len);
 /* the schedule search itself on given cycle times t_ms[k] (k = 1..kmax; t_ms[0] unused): depths in out */
 int heat2d_cycle_schedule(int64_t n, int kmax, const double* t_ms, int32_t* out, int64_t cap, int64_t* len);
+// cycle_schedule_near: up to m schedules within tol of the best estimate, concatenated in out, lengths in lens
+int heat2d_cycle_schedule_near(int64_t n, int kmax, const double* t_ms, double tol, int m, int32_t* out, int64_t cap,
+                               int64_t* lens, int32_t* count);
 
 /* I/O (io.cpp). */
 int heat2d_write_xyz(const char* path, int dtype, const void* host, int64_t nrows, int64_t ncols,

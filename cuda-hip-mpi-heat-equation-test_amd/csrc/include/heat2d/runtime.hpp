@@ -168,6 +168,10 @@ int num_threads();
 // from ceil(n / kmax) until the base depth's per-step time is 25 % above the
 // best seen. Empty if t(k) < 0 for a depth it needs.
 std::vector<int> cycle_schedule(int64_t n, int kmax, const std::function<double(int)>& t);
+// The same scan's cycle counts whose estimated cost is within `tol` (relative)
+// of the best, best first, at most m of them, as schedules.
+std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std::function<double(int)>& t,
+                                                  double tol, int m);
 
 class Solver {
  public:
@@ -267,6 +271,7 @@ class Solver {
   void trial_cycle(const kern::SplitPlan& c);
   bool schedule_graphs() const;
   void capture_schedule(int64_t n);
+  float time_trial_schedule(const std::vector<int>& sc);  // ms of one graph replay of sc's trial cycles
   void run_schedule_graph(int64_t n);
   float depth_ms(int k);
   std::vector<int> choose_schedule(int64_t n);

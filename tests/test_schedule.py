@@ -59,3 +59,34 @@ def test_schedule_examples(native):
 def test_schedule_missing_depth(native):
     """A depth without a tuned time (t < 0, e.g. a slab too thin to split) aborts the search."""
     assert schedule(20, 24, lambda k: -1.0 if k == 20 else 1.0) == []
+
+
+def schedules_near(n, kmax, t, tol, m):
+    tm = (C.c_double * (kmax + 1))(*([0.0] + [t(k) for k in range(1, kmax + 1)]))
+    out = (C.c_int32 * (m * n))()
+    lens = (C.c_int64 * m)()
+    cnt = C.c_int32()
+    N.call("heat2d_cycle_schedule_near", n, kmax, tm, tol, m, out, m * n, lens, C.byref(cnt))
+    res, pos = [], 0
+    for i in range(cnt.value):
+        res.append([int(v) for v in out[pos:pos + lens[i]]])
+        pos += lens[i]
+    return res
+
+
+@pytest.mark.parametrize("curve", sorted(CURVES))
+@pytest.mark.parametrize("n,kmax", [(20, 24), (1000, 16), (1000, 24), (480, 24), (37, 5)])
+def test_schedule_near_candidates(native, curve, n, kmax):
+    """prepare()'s graph-timed choice among near-tied schedules starts from
+    cycle_schedule_near: the best estimate first (= cycle_schedule), then other
+    balanced cycle counts within tol of it, at most m."""
+    t = CURVES[curve]
+    cost = lambda s: sum(t(k) for k in s)
+    near = schedules_near(n, kmax, t, 0.03, 3)
+    assert 1 <= len(near) <= 3
+    assert near[0] == schedule(n, kmax, t)
+    for s in near:
+        assert sum(s) == n and max(s) <= kmax and max(s) - min(s) <= 1
+        assert cost(s) <= cost(near[0]) * 1.03 + 1e-12
+    assert len({len(s) for s in near}) == len(near)  # distinct cycle counts
+    assert schedules_near(n, kmax, t, 0.0, 3)[0] == near[0]
