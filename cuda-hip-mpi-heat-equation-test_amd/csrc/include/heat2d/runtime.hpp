@@ -169,7 +169,7 @@ int num_threads();
 // best seen. Empty if t(k) < 0 for a depth it needs.
 std::vector<int> cycle_schedule(int64_t n, int kmax, const std::function<double(int)>& t);
 // The same scan's cycle counts whose estimated cost is within `tol` (relative)
-// of the best, best first, at most m of them, as schedules.
+// of the best, best first, at most m of them and one per base depth, as schedules.
 std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std::function<double(int)>& t,
                                                   double tol, int m);
 

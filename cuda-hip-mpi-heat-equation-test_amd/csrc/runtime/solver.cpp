@@ -803,8 +803,12 @@ std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std
   }
   std::sort(cost.begin(), cost.end());
   std::vector<std::vector<int>> out;
+  std::vector<int> bases;  // one candidate per base depth: neighbouring cycle counts are near-duplicates
   for (const auto& e : cost) {
     if ((int)out.size() >= m || e.first > cost.front().first * (1.0 + tol)) break;
+    const int base = (int)(n / e.second);
+    if (std::find(bases.begin(), bases.end(), base) != bases.end()) continue;
+    bases.push_back(base);
     std::vector<int> sched;
     const int kb = (int)(n / e.second);
     const int64_t rem = n % e.second;

@@ -88,5 +88,5 @@ def test_schedule_near_candidates(native, curve, n, kmax):
     for s in near:
         assert sum(s) == n and max(s) <= kmax and max(s) - min(s) <= 1
         assert cost(s) <= cost(near[0]) * 1.03 + 1e-12
-    assert len({len(s) for s in near}) == len(near)  # distinct cycle counts
+    assert len({min(s) for s in near}) == len(near)  # one candidate per base depth
     assert schedules_near(n, kmax, t, 0.0, 3)[0] == near[0]

@@ -1,7 +1,7 @@
 #!/bin/bash
 # prepare(n) times near-tied schedules as captured graphs of trial cycles: GPU suite, small-grid benches, headline.
 set -o pipefail
-O=gpurun_out/sched_graph
+O=gpurun_out/${SG_OUT:-sched_graph}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputests.log 2>&1 || { tail -30 $O/gputests.log; exit 1; }
