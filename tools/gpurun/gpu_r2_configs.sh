@@ -1,7 +1,7 @@
 #!/bin/bash
 # Every BASELINE.json configuration with round-2 code (bench/configs.py), one JSON line each.
 set -o pipefail
-O=gpurun_out/configs
+O=gpurun_out/${CFG_OUT:-configs}
 mkdir -p $O
 timeout -k 10 900 python -u bench/configs.py > $O/configs.jsonl || { tail -5 $O/configs.jsonl; exit 1; }
 python -c "
