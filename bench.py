@@ -59,7 +59,7 @@ def _free_port():
         return so.getsockname()[1]
 
 
-def _launch_ranks(n, backend):
+def _launch_ranks(n, backend, share_gpu=False):
     """`python bench.py --gpus N` without torchrun: start N rank processes of
     this script (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
     rendezvous on 127.0.0.1) and return the exit status. Rank 0 prints the
@@ -69,7 +69,7 @@ def _launch_ranks(n, backend):
     exec'd over a GPU-initialised process."""
     import signal
     import subprocess
-    if backend == "hip":
+    if backend == "hip" and not share_gpu:
         import torch  # device_count() does not initialise the GPU on this image
         have = torch.cuda.device_count()
         if have < n:
@@ -145,12 +145,21 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"],
                     help="cpu: the same harness on the native CPU twin over gloo (CI rehearsal of the "
                          "multi-process path: tests/test_bench_contract.py); not a performance number")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "peer"],
+                    help="halo exchange between rank processes: rccl (RCCL send/recv over xGMI) or peer (no RCCL: "
+                         "the neighbours' fields mapped through hipIpc handles, halos pulled by device copies "
+                         "ordered by stream-side counters; host collectives over gloo; capturable into hipGraphs)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank on GPU 0 (--transport peer): the exact multi-process path on a 1-GPU box "
+                         "(a correctness / overhead rehearsal, not a node throughput)")
     ap.add_argument("--rehearse-comm", action="store_true",
                     help="1 GPU only: run the multi-GPU schedule (bands + RCCL self-exchange beside a CU-masked "
                          "interior) to measure its per-rank cost; not the headline (periodic halo)")
     args = ap.parse_args()
+    if args.share_gpu and args.transport != "peer":
+        ap.error("--share-gpu needs --transport peer (RCCL refuses two ranks on one GPU)")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(_launch_ranks(args.gpus, args.backend))
+        sys.exit(_launch_ranks(args.gpus, args.backend, args.share_gpu))
     out_fd = _claim_stdout()
 
     import torch
@@ -163,17 +172,21 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
     hip = args.backend == "hip"
+    device = 0 if args.share_gpu else local
+    peer = args.transport == "peer" and world > 1 and hip
     if hip:
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(device)
     if world > 1:
         # a dead peer fails the run instead of hanging it: torch's own collectives
         # time out, and the native RCCL transport's watchdog uses the same limit
         from datetime import timedelta
         to = timedelta(seconds=float(os.environ.get("HEAT2D_COMM_TIMEOUT", "600")))
-        if hip:
+        if hip and not peer:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=to)
-        else:
+        else:  # host collectives only (CPU twin, or the IPC transport's handle exchange / all-reduces)
             dist.init_process_group("gloo", timeout=to)
+    # device of the torch collectives below (RCCL: device tensors; gloo: host tensors)
+    cdev = "cuda" if (hip and world > 1 and not peer) else "cpu"
 
     def sync():
         if hip:
@@ -181,7 +194,8 @@ def main():
 
     import heat2d
     from heat2d.models.heat2d import HeatSolver
-    from heat2d.parallel.transport import RcclLoopTransport, RcclTransport, SelfTransport, TorchDistTransport
+    from heat2d.parallel.transport import (IpcTransport, RcclLoopTransport, RcclTransport, SelfTransport,
+                                           TorchDistTransport)
 
     n_glob = args.n
     if args.weak:
@@ -190,20 +204,21 @@ def main():
     inp = heat2d.InputDat(n=n_glob, sigma=0.25, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     if world > 1:
-        tr = RcclTransport(rank, world, local) if hip else TorchDistTransport()
+        tr = (IpcTransport(device) if peer else RcclTransport(rank, world, local)) if hip else TorchDistTransport()
     elif args.rehearse_comm and hip:
         tr = RcclLoopTransport(local)
     else:
         tr = SelfTransport()
     rows = args.rows if (args.rows and world == 1) else None
-    graph = hip and (args.graph == "on" or (args.graph == "auto" and world == 1 and not args.rehearse_comm))
+    # graphs: single-rank runs, and multi-rank runs whose exchange captures (the IPC transport; RCCL's does not)
+    graph = hip and (args.graph == "on" or (args.graph == "auto" and (world == 1 or peer) and not args.rehearse_comm))
     s = HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb, overlap=not args.no_overlap, graph=graph,
-                   tile_rows=args.tile_rows, transport=tr, device=local if hip else None, rows=rows,
+                   tile_rows=args.tile_rows, transport=tr, device=device if hip else None, rows=rows,
                    comm_cus=args.comm_cus, arith=args.arith)
 
     def barrier():
         if world > 1:
-            tr_vals = torch.zeros(1, device="cuda" if hip else "cpu")
+            tr_vals = torch.zeros(1, device=cdev)
             dist.all_reduce(tr_vals)
         sync()
 
@@ -216,6 +231,7 @@ def main():
     s.prepare(args.steps)
     prepare_s = time.perf_counter() - tp
     s.cycle_hist(reset=True)
+    s.halo_rows_exchanged(reset=True)
     if args.phase_timers:
         s.set_timing(True)
     barrier()
@@ -227,7 +243,7 @@ def main():
     barrier()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda" if hip else "cpu", dtype=torch.float64)
+        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -249,10 +265,14 @@ def main():
             plans[str(k)] = {kk: pl[kk] for kk in ("order", "ring", "main_bands", "main_waves", "edge_items",
                                                     "tuned_ms")}
         traffic += c * plan_hbm_bytes(pl, es, s.nrows, s.ncols)["total"]
+    # halo traffic of the timed region: each exchange moves the NEXT cycle's
+    # depth in whole padded rows, one message per neighbour
+    nmsg = (rank > 0) + (rank < world - 1)
+    halo_bytes = float(s.halo_rows_exchanged()) * s.layout.pitch * es * nmsg
     if world > 1:
-        tt = torch.tensor([traffic], device="cuda" if hip else "cpu", dtype=torch.float64)
+        tt = torch.tensor([traffic, halo_bytes], device=cdev, dtype=torch.float64)
         dist.all_reduce(tt)
-        traffic = float(tt.item())
+        traffic, halo_bytes = float(tt[0].item()), float(tt[1].item())
     stats = s.stats() if args.check else None
     phases = s.phase_times() if args.phase_timers else None
     if rank == 0:
@@ -276,7 +296,9 @@ def main():
                 "grid": [rows or prob.n_owned, prob.n_owned],
                 "global_batch": 1,
                 "seq_len": prob.n_owned,
-                "parallelism": f"slab{world}" + ("-rehearsal" if args.rehearse_comm and world == 1 else ""),
+                "parallelism": f"slab{world}" + ("-rehearsal" if args.rehearse_comm and world == 1 else "")
+                               + ("-shared-gpu" if args.share_gpu and world > 1 else ""),
+                "transport": tr.name,
                 "tb_max": tb,
                 "cycles": {str(k): c for k, c in sorted(hist.items())},
                 "schedule": "measured" if s.schedule(args.steps) else "balanced",
@@ -288,6 +310,9 @@ def main():
                 "backend": args.backend,
             },
             "hbm_gb_per_s_plan": round(traffic / elapsed / 1e9, 1),
+            # halo bytes moved by all ranks in the timed region, and per cycle (whole node)
+            "halo_bytes": halo_bytes,
+            "halo_bytes_per_cycle": round(halo_bytes / max(1, sum(hist.values())), 1),
             "baseline_basis": "BASELINE.md derived ceiling 50 Gpts/s per MI250X GCD x n_gpus",
         }
         if stats:

@@ -198,6 +198,14 @@ int heat2d_transport_callback(heat2d_exchange_fn ex, heat2d_allreduce_fn ar, hea
   });
 }
 
+int heat2d_transport_ipc(heat2d_allgather_fn ag, heat2d_allreduce_fn ar, heat2d_barrier_fn br, void* ctx, int rank,
+                         int size, int device, void** out) {
+  return guarded([&] {
+    IpcOps ops{ctx, ag, ar, br};
+    *out = new TransportHandle{make_ipc_transport(ops, rank, size, device)};
+  });
+}
+
 int heat2d_transport_free(void* t) {
   return guarded([&] { delete static_cast<TransportHandle*>(t); });
 }
@@ -431,6 +439,27 @@ int heat2d_solver_schedule(void* s, int64_t n, int32_t* out, int64_t cap, int64_
     if (v && out)
       for (int64_t i = 0; i < std::min<int64_t>(cap, (int64_t)v->size()); ++i) out[i] = (*v)[(size_t)i];
   });
+}
+
+int heat2d_solver_step_cycles(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len) {
+  return guarded([&] {
+    const std::vector<int> v = static_cast<Solver*>(s)->step_cycles(n);
+    *len = (int64_t)v.size();
+    if (out)
+      for (int64_t i = 0; i < std::min<int64_t>(cap, *len); ++i) out[i] = v[(size_t)i];
+  });
+}
+
+int heat2d_solver_halo_rows(void* s, int reset, int64_t* out) {
+  return guarded([&] { *out = static_cast<Solver*>(s)->halo_rows_exchanged(reset != 0); });
+}
+
+int heat2d_solver_ghost_rows(void* s, int32_t* out) {
+  return guarded([&] { *out = static_cast<Solver*>(s)->ghost_rows(); });
+}
+
+int heat2d_autotune_slabs(int64_t n_rows, int64_t n_cols, int nranks, int autotune, int32_t* out) {
+  return guarded([&] { *out = autotune_slabs(n_rows, n_cols, nranks, autotune) ? 1 : 0; });
 }
 
 int heat2d_group_download(void* g, void* host, int64_t ld) {

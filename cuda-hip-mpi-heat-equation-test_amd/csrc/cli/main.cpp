@@ -64,6 +64,7 @@ struct Args {
   std::string restart;          // --restart DIR (any writer rank count)
   std::string transport = "rccl";  // GPU ranks: rccl | peer (device copies between the ranks' fields, no RCCL)
   bool share_gpu = false;          // --share-gpu: every rank on device 0 (peer transport; tests / rehearsals)
+  int autotune = -1;               // --autotune auto|on|off (SolverConfig::autotune)
 };
 
 void usage() {
@@ -73,7 +74,7 @@ void usage() {
       "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
       "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith auto|exact|fma]\n"
       "              [--checkpoint DIR [--checkpoint-every N]] [--restart DIR]\n"
-      "              [--transport rccl|peer] [--share-gpu]\n");
+      "              [--transport rccl|peer] [--share-gpu] [--autotune auto|on|off]\n");
 }
 
 Args parse_args(int argc, char** argv) {
@@ -113,6 +114,14 @@ Args parse_args(int argc, char** argv) {
     else if (s == "--restart") a.restart = need("--restart");
     else if (s == "--transport") a.transport = need("--transport");
     else if (s == "--share-gpu") a.share_gpu = true;
+    else if (s == "--autotune") {
+      const std::string v = need("--autotune");
+      if (v != "auto" && v != "on" && v != "off") {
+        std::fprintf(stderr, "--autotune must be auto, on or off\n");
+        std::exit(2);
+      }
+      a.autotune = v == "on" ? 1 : (v == "off" ? 0 : -1);
+    }
     else if (!s.empty() && s[0] != '-') a.input = s;
     else { std::fprintf(stderr, "unknown flag %s\n", s.c_str()); usage(); std::exit(2); }
   }
@@ -135,13 +144,20 @@ struct Shared {
   double final_stats[6] = {0};
   int tb_used = 1;  // largest temporal depth the solver may run (jit / copy-swap force 1)
   int64_t hist[kMaxTB + 1] = {0};  // cycles per depth of the timed loop (rank 0)
+  std::vector<std::vector<int64_t>> rank_hist;  // the same, every rank (they must agree)
+  std::vector<int64_t> rank_halo_rows;          // halo rows exchanged per side by each rank's timed loop
+  bool measured = false;  // a chunk of the timed loop runs a measured cycle schedule (Solver::prepare)
   int64_t start_step = 0;  // > 0 after --restart
 };
 
 // Collective checkpoint (every rank its slab, then rank 0 publishes meta.json).
 void save_checkpoint(Shared& sh, Solver& s, Transport& tr, int rank, int64_t step) {
   const Args& a = sh.args;
-  ckpt::write_rank(a.checkpoint, rank, step, s);
+  IoPhase io(tr);  // ranks wait on each other's file writes: not a hung fabric
+  // every rank names the same fresh step directory before any rank creates it
+  const std::string name = ckpt::step_dir_name(a.checkpoint, step);
+  tr.barrier();
+  ckpt::write_rank(a.checkpoint, name, rank, s);
   tr.barrier();
   if (rank == 0) {
     ckpt::Meta m;
@@ -155,7 +171,7 @@ void save_checkpoint(Shared& sh, Solver& s, Transport& tr, int rank, int64_t ste
     m.nu = sh.in.nu;
     m.dom_len = sh.in.dom_len;
     m.r = sh.prob.r;
-    ckpt::write_meta(a.checkpoint, m);
+    ckpt::write_meta(a.checkpoint, name, m);
   }
   tr.barrier();
 }
@@ -212,7 +228,9 @@ void run_rank(Shared& sh, int rank) {
     cfg.managed = a.managed ? 1 : 0;
     cfg.device = a.cpu ? -1 : device;
     cfg.use_graph = a.graph ? 1 : 0;
-    cfg.autotune = -1;  // split schedule on big slabs: pick the fastest launch plan on the first cycle
+    // split schedule: the fastest launch plan per depth and a measured cycle schedule
+    // (auto: slabs of >= 2^24 points — decided from the thinnest slab, the same on every rank)
+    cfg.autotune = a.autotune;
     if (a.engine != "tb" && a.engine != "jit") fail(__FILE__, __LINE__, "--engine must be tb or jit");
     cfg.engine = a.engine == "jit" ? 1 : 0;  // jit: hipRTC kernel rendered for this slab (python/cuda/cuda.py)
     if (a.arith != "exact" && a.arith != "fma" && a.arith != "auto")
@@ -228,7 +246,11 @@ void run_rank(Shared& sh, int rank) {
       HEAT2D_REQUIRE(m.convention == (inclusive ? "inclusive" : "ghost"), "checkpoint grid convention differs");
       const SlabLayout& L = s.layout();
       std::vector<char> host((size_t)(L.nrows * L.ncols) * dtype_size(s.dtype()));
-      ckpt::read_rows(m, L.row0, L.nrows, L.ncols, (int)s.dtype(), host.data());
+      {
+        IoPhase io(*tr);
+        ckpt::read_rows(m, L.row0, L.nrows, L.ncols, (int)s.dtype(), host.data());
+        tr->barrier();  // every rank has read its rows: the upload's exchange waits on no file system
+      }
       s.upload(host.data(), L.ncols);  // + halo exchange
       start = std::min<int64_t>(m.step, sh.in.ntime);
       if (root) {
@@ -243,6 +265,7 @@ void run_rank(Shared& sh, int rank) {
       std::fflush(stdout);
     }
     if (inclusive && a.output == "ascii" && start == 0) {  // int.dat: the IC (fortran/serial/heat.f90:50-55)
+      IoPhase io(*tr);
       for (int turn = 0; turn < P; ++turn) {
         if (turn == rank) write_inclusive(s, sh.prob, "int.dat", rank == 0, rank == P - 1, rank > 0);
         tr->barrier();
@@ -272,6 +295,7 @@ void run_rank(Shared& sh, int rank) {
         if (std::find(seen.begin(), seen.end(), c) == seen.end()) {
           seen.push_back(c);
           s.prepare(c);
+          if (root && s.schedule(c)) sh.measured = true;
         }
         d += c;
       }
@@ -280,6 +304,7 @@ void run_rank(Shared& sh, int rank) {
     {
       int64_t h[kMaxTB + 1];
       s.cycle_hist(h, true);  // count the timed loop's cycles only
+      (void)s.halo_rows_exchanged(true);
     }
     tr->barrier();
     s.synchronize();
@@ -324,8 +349,9 @@ void run_rank(Shared& sh, int rank) {
 
     if (!a.checkpoint.empty()) save_checkpoint(sh, s, *tr, rank, done);  // final state (outside the timed region)
 
-    // outputs
+    // outputs (serial rank turns / per-rank files: ranks wait on each other's I/O)
     if (a.output != "none") {
+      IoPhase io(*tr);
       if (inclusive) {
         if (a.output == "ascii") {
           for (int turn = 0; turn < P; ++turn) {
@@ -349,6 +375,7 @@ void run_rank(Shared& sh, int rank) {
             fail(__FILE__, __LINE__, heat2d_last_error());
         }
       }
+      tr->barrier();  // the statistics' all-reduce below then waits on no file system
     }
     double st[6];
     s.stats(st, false);
@@ -356,6 +383,13 @@ void run_rank(Shared& sh, int rank) {
       std::memcpy(sh.final_stats, st, sizeof(st));
       sh.tb_used = s.config().tb;
       s.cycle_hist(sh.hist, false);
+    }
+    {
+      int64_t h[kMaxTB + 1];
+      s.cycle_hist(h, false);
+      std::lock_guard<std::mutex> g(sh.mu);
+      sh.rank_hist[(size_t)rank].assign(h, h + kMaxTB + 1);
+      sh.rank_halo_rows[(size_t)rank] = s.halo_rows_exchanged(false);
     }
   } catch (const std::exception& e) {
     // fail fast: the first error is reported; every rank's communicator is
@@ -405,6 +439,8 @@ int main(int argc, char** argv) {
   }
   sh.t_elapsed.assign((size_t)sh.nranks, 0.0);
   sh.trs.assign((size_t)sh.nranks, nullptr);
+  sh.rank_hist.assign((size_t)sh.nranks, std::vector<int64_t>(kMaxTB + 1, 0));
+  sh.rank_halo_rows.assign((size_t)sh.nranks, 0);
   std::vector<std::thread> th;
   for (int r = 1; r < sh.nranks; ++r) th.emplace_back(run_rank, std::ref(sh), r);
   run_rank(sh, 0);
@@ -443,16 +479,29 @@ int main(int argc, char** argv) {
                 (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, (long long)passes, (long long)ntime, tmax,
                 gpts, gpts * bpp, sh.final_stats[0]);
   if (!a.json.empty()) {
+    // per-rank cycles (identical on every rank by construction: Solver::prepare
+    // agrees on the sequence) and halo rows moved per side
+    std::string per_rank, halo;
+    for (int r = 0; r < sh.nranks; ++r) {
+      std::string d;
+      for (int k = 1; k <= kMaxTB; ++k)
+        if (sh.rank_hist[(size_t)r][(size_t)k])
+          d += (d.empty() ? "" : ", ") + std::string("\"") + std::to_string(k) + "\": " +
+               std::to_string(sh.rank_hist[(size_t)r][(size_t)k]);
+      per_rank += (r ? ", {" : "{") + d + "}";
+      halo += (r ? ", " : "") + std::to_string(sh.rank_halo_rows[(size_t)r]);
+    }
     FILE* f = std::fopen(a.json.c_str(), "w");
     if (f) {
       std::fprintf(f,
                    "{\"n\": %lld, \"nranks\": %d, \"dtype\": \"%s\", \"tb\": %d, \"cycles\": {%s}, \"steps\": %lld, \"wall_s\": %.9g, "
                    "\"gpts_per_s\": %.9g, \"model_gb_per_s\": %.9g, \"sum\": %.17g, \"min\": %.17g, \"max\": %.17g, "
-                   "\"backend\": \"%s\", \"variant\": \"%s\", \"arith\": \"%s\"}\n",
+                   "\"backend\": \"%s\", \"variant\": \"%s\", \"arith\": \"%s\", \"cycles_per_rank\": [%s], "
+                   "\"halo_rows_per_rank\": [%s], \"schedule\": \"%s\"}\n",
                    (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, depths.c_str(), (long long)ntime, tmax,
                    gpts, gpts * bpp,
                    sh.final_stats[0], sh.final_stats[2], sh.final_stats[3], a.cpu ? "cpu" : "hip", a.variant.c_str(),
-                   a.arith.c_str());
+                   a.arith.c_str(), per_rank.c_str(), halo.c_str(), sh.measured ? "measured" : "balanced");
       std::fclose(f);
     }
   }

@@ -104,6 +104,10 @@ int heat2d_transport_rccl(const void* uid128, int rank, int size, int device, vo
 int heat2d_transport_rccl_loop(int device, void** out);
 int heat2d_transport_callback(heat2d_exchange_fn ex, heat2d_allreduce_fn ar, heat2d_barrier_fn br,
                               void* ctx, int rank, int size, void** out);
+typedef int (*heat2d_allgather_fn)(void* ctx, const void* mine, void* all, int64_t bytes);
+// IPC transport (process per GPU, no RCCL): host collectives through the callbacks.
+int heat2d_transport_ipc(heat2d_allgather_fn ag, heat2d_allreduce_fn ar, heat2d_barrier_fn br, void* ctx, int rank,
+                         int size, int device, void** out);
 int heat2d_transport_free(void* t);
 /* fail fast: abort the transport's fabric (RCCL: ncclCommAbort); its solver's next synchronisation raises */
 int heat2d_transport_abort(void* t, const char* reason);
@@ -160,6 +164,14 @@ int heat2d_solver_cycle_hist(void* s, int64_t* out, int n, int reset);
 /* the measured cycle schedule prepare(n) chose for step(n): depths in out[0..min(cap, len)); len = -1 if none
    (step(n) then runs balanced cycles of the preferred depth) */
 int heat2d_solver_schedule(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len);
+// Cycle depths step(n) runs from the solver's current state (len = count; out may be null).
+int heat2d_solver_step_cycles(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len);
+// Halo rows exchanged per side since the last reset (sum over cycles).
+int heat2d_solver_halo_rows(void* s, int reset, int64_t* out);
+// Valid ghost rows of the current buffer (the last exchange's depth).
+int heat2d_solver_ghost_rows(void* s, int32_t* out);
+// Autotune / measured-schedule eligibility of a decomposition (the same on every rank).
+int heat2d_autotune_slabs(int64_t n_rows, int64_t n_cols, int nranks, int autotune, int32_t* out);
 /* the schedule search itself on given cycle times t_ms[k] (k = 1..kmax; t_ms[0] unused): depths in out */
 int heat2d_cycle_schedule(int64_t n, int kmax, const double* t_ms, int32_t* out, int64_t cap, int64_t* len);
 // cycle_schedule_near: up to m schedules within tol of the best estimate, concatenated in out, lengths in lens

@@ -140,5 +140,15 @@ void launch_pack_rows(DType dt, const void* field, const SlabLayout& L, int64_t 
 void launch_unpack_rows(DType dt, void* field, const SlabLayout& L, int64_t row, int64_t nrows,
                         const void* buf, hipStream_t stream);
 
+// IPC transport ordering (kernels/ipc_sync.hip): one 64-B slot per rank in
+// host-shared memory; `ctrl` = {abort word, timed-out rank + 1}.
+struct IpcSlot {
+  uint64_t ready, done;
+  uint64_t pad[6];
+};
+void launch_ipc_arrive(IpcSlot* slots, uint64_t* ctrl, int me, int p0, int p1, uint64_t timeout_ticks,
+                       hipStream_t stream);
+void launch_ipc_depart(IpcSlot* slots, int me, hipStream_t stream);
+
 }  // namespace kern
 }  // namespace heat2d

@@ -69,6 +69,9 @@ class Transport {
   virtual void barrier() = 0;
   virtual std::string name() const = 0;
   virtual bool capturable() const { return false; }  // safe inside hipGraph capture
+  // allreduce() / barrier() really meet the other ranks (false for the
+  // loopback, whose members share one host thread: its group agrees instead)
+  virtual bool collective() const { return true; }
   // a graph with this transport's exchanges captured in it was launched on `stream`
   // (failure detection tracks the replay as a whole)
   virtual void graph_launched(hipStream_t /*stream*/) {}
@@ -89,6 +92,24 @@ class Transport {
   // other rank failed. Thread-safe, idempotent.
   virtual void abort(const std::string& /*reason*/) {}
   virtual bool aborted() const { return false; }
+  // I/O phase (serial per-rank output turns, checkpoint writes, restart
+  // reads): barriers / all-reduces issued while it is on may wait on a peer's
+  // host I/O for long; failure detection does not treat them as a hung fabric
+  // (RCCL: not tracked by the watchdog; host hubs: no barrier timeout).
+  // Nested on/off pairs; every rank brackets the same phase.
+  virtual void io_phase(bool /*on*/) {}
+  // The solver's two field buffers (allocation bases, layout L): transports
+  // that map their peers' fields once (IPC) do it here. Collective.
+  virtual void attach(void* /*buf0*/, void* /*buf1*/, const SlabLayout& /*L*/, DType /*dt*/) {}
+};
+
+// RAII bracket of Transport::io_phase.
+struct IoPhase {
+  Transport& t;
+  explicit IoPhase(Transport& tr) : t(tr) { t.io_phase(true); }
+  ~IoPhase() { t.io_phase(false); }
+  IoPhase(const IoPhase&) = delete;
+  IoPhase& operator=(const IoPhase&) = delete;
 };
 
 // The messages of one halo exchange, shared by every transport (RCCL sends
@@ -146,6 +167,19 @@ struct CallbackOps {
   int (*barrier)(void* ctx);
 };
 std::shared_ptr<Transport> make_callback_transport(const CallbackOps& ops, int rank, int size);
+// Process-per-GPU (or processes sharing a GPU) without RCCL: neighbours'
+// fields mapped once via hipIpc handles, halos pulled by device copies,
+// ordered by stream-side counters in host-shared memory (ipc_transport.cpp);
+// capturable into hipGraphs. Host collectives through these callbacks
+// (Python: torch.distributed gloo). Collective construction-free: the handle
+// exchange happens in attach() (Solver constructor, every rank).
+struct IpcOps {
+  void* ctx;
+  int (*allgather)(void* ctx, const void* mine, void* all, int64_t bytes);
+  int (*allreduce)(void* ctx, double* vals, int32_t n, int32_t op);
+  int (*barrier)(void* ctx);
+};
+std::shared_ptr<Transport> make_ipc_transport(const IpcOps& ops, int rank, int size, int device);
 
 // ---------------------------------------------------------------- CPU twins
 
@@ -172,6 +206,20 @@ std::vector<int> cycle_schedule(int64_t n, int kmax, const std::function<double(
 // of the best, best first, at most m of them and one per base depth, as schedules.
 std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std::function<double(int)>& t,
                                                   double tol, int m);
+// Whether slabs of this decomposition get autotuned split plans and measured
+// cycle schedules (SolverConfig::autotune, -1 = auto). A function of the
+// GLOBAL problem only — the smallest slab (n_rows / P rows) decides — so every
+// rank takes the same branch of prepare()'s collectives (uneven slabs that
+// straddle the 2^24-point threshold, e.g. 5793^2 on 2 ranks, would otherwise
+// split into ranks that all-reduce and ranks that do not).
+bool autotune_slabs(int64_t n_rows, int64_t n_cols, int nranks, int autotune);
+// Exchange depth after cycle i of a cycle sequence: the depth of the cycle that
+// follows (the ghost rows it reads); after the last one, `next` (the depth
+// the caller expects next, e.g. the sequence's own first depth when step(n)
+// repeats).
+inline int exchange_depth(const std::vector<int>& seq, size_t i, int next) {
+  return i + 1 < seq.size() ? seq[i + 1] : next;
+}
 
 class Solver {
  public:
@@ -217,16 +265,32 @@ class Solver {
   // ghost/frame included) -> host.
   void download_region(int64_t r0, int64_t r1, int64_t c0, int64_t c1, void* host, int64_t ld);
 
-  // Phase API. One cycle of depth k = cycle_launch(k) (kernels, the event
+  // Phase API. One cycle of depth k = cycle_launch(k, x) (kernels, the event
   // that marks the bands written, Transport::post) then cycle_finish() (halo
-  // exchange of the new field, buffer swap). step() runs the two back to
-  // back; LoopbackGroup runs every member's launch before any member's finish.
-  void cycle_launch(int k);
+  // exchange of x rows of the new field, buffer swap). step() runs the two back
+  // to back; LoopbackGroup runs every member's launch before any member's finish.
+  // x = the depth of the NEXT cycle (the ghost rows it will read; 0: k): the
+  // exchange moves x rows, and the boundary bands are max(k, x) rows — not the
+  // largest depth the halo allows. The current buffer must hold >= k valid
+  // ghost rows (ghost_rows(); topup() first otherwise).
+  void cycle_launch(int k, int x = 0);
   void cycle_finish();
   void cycle_compute(int k);   // whole-slab compute cur -> nxt (no exchange)
   void cycle_swap();
   void exchange_post();        // Transport::post of the current buffer (two-phase transports)
-  void exchange_now();         // exchange halos of the current buffer on the compute stream
+  void exchange_now(int k = 0);  // exchange k (0: band) halo rows of the current buffer on the compute stream
+  // Rows of the current buffer's ghost bands that hold valid neighbour data
+  // (band() after init / upload; the last exchange's depth after a cycle).
+  int ghost_rows() const { return ghost_; }
+  // Make ghost_rows() >= k with one blocking exchange of k rows (collective:
+  // every rank tops up at the same point; a no-op where nothing is exchanged).
+  void topup(int k);
+  bool needs_topup(int k) const { return tr_->exchanges() && ghost_ < k; }
+  // The cycle depths step(n) will run from the current state (measured
+  // schedule, graph pairs, balanced cycles), in order.
+  std::vector<int> step_cycles(int64_t n) const;
+  // Halo rows each cycle exchanged since the last reset (sum over cycles).
+  int64_t halo_rows_exchanged(bool reset);
   void upload_owned(const void* host, int64_t ld);  // upload() without the halo exchange
   // Cycles launched by step() since the last reset, by depth: hist[k] for
   // k = 0..kMaxTB (graph replays count their two cycles each).
@@ -256,15 +320,28 @@ class Solver {
   void phase_times(double out[5]);
 
  private:
-  void launch_overlap(int k);
+  void launch_overlap(int k, int64_t B);
   void launch_serial(int k);
   void launch_stats_cycle(int k);
   void reduce_global(const double loc[6], double out[6]);
   const kern::SplitPlan& split_plan(int k);
+  // depth-k plan with boundary bands of B >= k rows: split_plan(k)'s choice
+  // (order, ring, interior bands) re-cut for the wider bands
+  const kern::SplitPlan& split_plan_banded(int k, int64_t B);
   void autotune_split(int k);
   void cycle_copy_swap();
   void launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k);
-  void exchange_on(void* field, hipStream_t s);
+  void exchange_on(void* field, int64_t k, hipStream_t s);
+  // every rank must hold the same value (cycle sequence, exchange depths):
+  // all-reduced and compared, a mismatch fails naming each rank's value
+  void agree(uint64_t h, const std::string& what);
+  uint64_t sequence_hash(int64_t n) const;
+  struct CycleRun {
+    int k;
+    int64_t pairs;  // > 0: `pairs` replays of the two-cycle depth-k graph
+  };
+  std::vector<CycleRun> step_runs(int64_t n, int par) const;
+  bool pair_graphs() const;
   void run_graph_cycles(int64_t npairs);
   void ensure_pair_graph();
   bool measured_schedules() const;
@@ -272,6 +349,7 @@ class Solver {
   bool schedule_graphs() const;
   void capture_schedule(int64_t n);
   float time_trial_schedule(const std::vector<int>& sc);  // ms of one graph replay of sc's trial cycles
+  void prepare_plans(int64_t n);  // prepare()'s planning / autotune / measured schedule (HIP split engine)
   void run_schedule_graph(int64_t n);
   float depth_ms(int k);
   std::vector<int> choose_schedule(int64_t n);
@@ -283,7 +361,12 @@ class Solver {
   void* buf_[2] = {nullptr, nullptr};
   int cur_ = 0;
   int64_t steps_ = 0;
-  int64_t band_ = 0;     // boundary band rows (= halo exchange depth = K)
+  int64_t band_ = 0;     // largest boundary band / halo exchange depth (= K)
+  int ghost_ = 0;        // valid ghost rows of buf_[cur_] (see ghost_rows)
+  int pend_x_ = 0;       // exchange depth of the pending cycle
+  int last_x_[2] = {0, 0};  // rows of buf_[b] its last exchange moved (peers may still be pulling them)
+  int64_t halo_rows_ = 0;  // rows exchanged per side, summed over cycles (metrics)
+  std::map<std::pair<int, int64_t>, kern::SplitPlan> banded_;  // split_plan_banded cache
   hipStream_t s_compute_ = nullptr, s_comm_ = nullptr;
   bool own_streams_ = false;
   hipEvent_t ev_bnd_ = nullptr, ev_comm_ = nullptr, ev_int_ = nullptr;

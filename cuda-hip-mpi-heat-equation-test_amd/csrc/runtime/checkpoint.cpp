@@ -15,6 +15,7 @@
 #include <cstring>
 #include <string>
 #include <dirent.h>
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <vector>
@@ -44,13 +45,29 @@ bool exists(const std::string& p) {
   return ::stat(p.c_str(), &st) == 0;
 }
 
+// data of `path` (a file or a directory: its entries) on stable storage
+void fsync_path(const std::string& path) {
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  HEAT2D_REQUIRE(fd >= 0, "cannot open " + path + " to fsync");
+  const int rc = ::fsync(fd);
+  ::close(fd);
+  HEAT2D_REQUIRE(rc == 0 || errno == EINVAL, "fsync failed on " + path);
+}
+
+std::string parent_dir(const std::string& path) {
+  const size_t p = path.find_last_of('/');
+  return p == std::string::npos ? "." : (p == 0 ? "/" : path.substr(0, p));
+}
+
 void write_atomic(const std::string& path, const std::string& text) {
   const std::string tmp = path + ".tmp";
   FILE* f = std::fopen(tmp.c_str(), "wb");
   HEAT2D_REQUIRE(f != nullptr, "cannot write " + tmp);
-  const bool ok = std::fwrite(text.data(), 1, text.size(), f) == text.size();
+  const bool ok = std::fwrite(text.data(), 1, text.size(), f) == text.size() && std::fflush(f) == 0 &&
+                  ::fsync(fileno(f)) == 0;
   HEAT2D_REQUIRE(std::fclose(f) == 0 && ok, "error writing " + tmp);
   HEAT2D_REQUIRE(std::rename(tmp.c_str(), path.c_str()) == 0, "cannot publish " + path);
+  fsync_path(parent_dir(path));  // the rename itself
 }
 
 std::string rank_file(const std::string& dir, int rank) {
@@ -145,19 +162,29 @@ NpyInfo npy_header(FILE* f, const std::string& path) {
 
 }  // namespace
 
-void write_rank(const std::string& dir, int rank, int64_t step, Solver& s) {
+std::string step_dir_name(const std::string& dir, int64_t step) {
+  const std::string base = step_name(step);
+  if (!exists(join(dir, base))) return base;
+  for (int g = 1;; ++g) {  // sorts after `base` and before the next step: pruning order holds
+    const std::string name = base + "-" + std::to_string(g);
+    if (!exists(join(dir, name))) return name;
+  }
+}
+
+void write_rank(const std::string& dir, const std::string& name, int rank, Solver& s) {
   ::mkdir(dir.c_str(), 0755);  // all ranks may race on it: EEXIST is fine
-  const std::string sd = join(dir, step_name(step));
+  const std::string sd = join(dir, name);
   ::mkdir(sd.c_str(), 0755);
   const SlabLayout& L = s.layout();
   std::vector<char> host((size_t)(L.nrows * L.ncols) * dtype_size(s.dtype()));
   s.download(host.data(), L.ncols);
-  if (heat2d_write_npy(rank_file(sd, rank).c_str(), (int)s.dtype(), host.data(), L.nrows, L.ncols, L.ncols))
+  const std::string path = rank_file(sd, rank);
+  if (heat2d_write_npy(path.c_str(), (int)s.dtype(), host.data(), L.nrows, L.ncols, L.ncols))
     fail(__FILE__, __LINE__, heat2d_last_error());
+  fsync_path(path);
 }
 
-void write_meta(const std::string& dir, const Meta& m) {
-  const std::string name = step_name(m.step);
+void write_meta(const std::string& dir, const std::string& name, const Meta& m) {
   char buf[1024];
   std::snprintf(buf, sizeof(buf),
                 "{\n \"format\": \"%s\",\n \"step\": %lld,\n \"nranks\": %d,\n \"dtype\": \"%s\",\n"
@@ -165,7 +192,7 @@ void write_meta(const std::string& dir, const Meta& m) {
                 " \"nu\": %.17g,\n \"dom_len\": %.17g,\n \"r\": %.17g,\n \"writer\": \"heat2d-cli\"\n}\n",
                 kFormat, (long long)m.step, m.nranks, m.dtype == 0 ? "fp32" : "fp64", (long long)m.n_owned,
                 (long long)m.n_input, m.convention.c_str(), m.sigma, m.nu, m.dom_len, m.r);
-  write_atomic(join(join(dir, name), "meta.json"), buf);
+  write_atomic(join(join(dir, name), "meta.json"), buf);  // + fsync of the step directory (rank files' entries)
   write_atomic(join(dir, "latest"), name + "\n");  // the commit point
   // prune: keep the two newest complete steps (names sort by step)
   std::vector<std::string> steps;

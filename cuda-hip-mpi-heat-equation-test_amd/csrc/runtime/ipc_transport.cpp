@@ -1,0 +1,318 @@
+// Process-per-GPU halo exchange WITHOUT RCCL: every rank pulls its ghost rows
+// straight out of its neighbours' fields, mapped into its own address space
+// once with hipIpcGetMemHandle / hipIpcOpenMemHandle, by hipMemcpyAsync on the
+// solver's exchange stream (xGMI between GPUs; a device copy when ranks share
+// one GPU). The reference moves each halo with a pack kernel, a device sync,
+// D2H copies, two blocking MPI_Sendrecv, H2D copies and unpack kernels
+// (fortran/hip/heat.F90:196-230); here one exchange is two one-thread kernels
+// and two copies on a stream, nothing on the host.
+//
+// Ordering across processes: the counters of kernels/ipc_sync.hip in a small
+// host-shared memory block (POSIX shm, hipHostRegister'ed by every rank) —
+// arrive (ready[me] = c + 1; wait for the neighbours' ready >= c + 1 and
+// done >= c), the pulls, depart (done[me] = c + 1) — the same protocol the
+// in-process peer transport builds from events and host waits, here with no
+// host wait per cycle. The counters live in memory, so the exchange can be
+// captured into a hipGraph and replayed (capturable() = true): multi-rank runs
+// replay whole measured schedules, which RCCL's captured send/recv cannot
+// (transport.cpp RcclTransport).
+//
+// Host collectives (handle exchange, all-reduce, barrier) go through callbacks
+// (Python: torch.distributed over gloo), so N processes can share ONE GPU
+// (bench.py --share-gpu): the exact multi-process path runs on a 1-GPU box.
+// Failure detection: a Watchdog tracks the exchanges' completion events; on a
+// hang or abort() the shared abort word makes every rank's arrive kernel
+// return, so no wave keeps spinning and every stream drains.
+#include <hip/hip_runtime.h>
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "heat2d/runtime.hpp"
+#include "heat2d/watchdog.hpp"
+
+namespace heat2d {
+
+#define H2D_HIP(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) fail(__FILE__, __LINE__, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+// What every rank publishes at attach() (all-gathered).
+struct IpcCard {
+  hipIpcMemHandle_t buf[2];
+  char shm[64];  // rank 0's shared-memory block name
+  int32_t device;
+  int32_t pad;
+  SlabLayout L;
+};
+
+class IpcTransport final : public Transport {
+ public:
+  IpcTransport(const IpcOps& ops, int rank, int size, int device) : ops_(ops), rank_(rank), size_(size) {
+    HEAT2D_REQUIRE(size >= 1 && rank >= 0 && rank < size, "bad rank / size");
+    HEAT2D_REQUIRE(ops.allgather && ops.allreduce && ops.barrier, "IPC transport needs host collectives");
+    if (device >= 0) H2D_HIP(hipSetDevice(device));
+    H2D_HIP(hipGetDevice(&device_));
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || khz <= 0) khz = 100000;
+    timeout_s_ = Watchdog::env_timeout(600.0);
+    // the arrive kernel's own limit: a little past the watchdog's, which normally fires first
+    const double kt = timeout_s_ > 0 ? timeout_s_ * 1.5 + 5.0 : 3600.0;
+    timeout_ticks_ = (uint64_t)(kt * 1e3 * (double)khz);
+  }
+  ~IpcTransport() override {
+    wd_.reset();
+    for (auto& p : pend_) (void)hipEventDestroy(p.ev);
+    for (auto e : pool_) (void)hipEventDestroy(e);
+    for (auto& pb : peer_buf_)
+      for (void* b : pb)
+        if (b) (void)hipIpcCloseMemHandle(b);
+    if (host_) {
+      (void)hipHostUnregister(host_);
+      ::munmap(host_, shm_bytes_);
+    }
+  }
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  std::string name() const override { return "ipc"; }
+  bool capturable() const override { return true; }
+  bool exchanges() const override { return size_ > 1; }
+  bool aborted() const override { return aborted_.load(); }
+  void io_phase(bool on) override { io_ += on ? 1 : -1; }
+  void graph_launched(hipStream_t stream) override { track(stream, "graph replay"); }
+
+  void attach(void* buf0, void* buf1, const SlabLayout& L, DType dt) override {
+    if (size_ == 1) return;
+    HEAT2D_REQUIRE(!attached_, "IPC transport: one solver per transport");
+    attached_ = true;
+    mine_[0] = buf0;
+    mine_[1] = buf1;
+    L_ = L;
+    es_ = dtype_size(dt);
+    IpcCard me{};
+    H2D_HIP(hipIpcGetMemHandle(&me.buf[0], buf0));
+    H2D_HIP(hipIpcGetMemHandle(&me.buf[1], buf1));
+    me.device = device_;
+    me.L = L;
+    if (rank_ == 0) {
+      std::random_device rd;
+      std::snprintf(me.shm, sizeof(me.shm), "/heat2d-ipc-%d-%08x%08x", (int)::getpid(), rd(), rd());
+      shm_bytes_ = shm_size();
+      const int fd = ::shm_open(me.shm, O_CREAT | O_EXCL | O_RDWR, 0600);
+      HEAT2D_REQUIRE(fd >= 0, std::string("shm_open failed for ") + me.shm);
+      const int rc = ::ftruncate(fd, (off_t)shm_bytes_);
+      ::close(fd);
+      if (rc != 0) {
+        ::shm_unlink(me.shm);
+        fail(__FILE__, __LINE__, "ftruncate of the IPC counter block failed");
+      }
+    }
+    std::vector<IpcCard> all((size_t)size_);
+    HEAT2D_REQUIRE(ops_.allgather(ops_.ctx, &me, all.data(), (int64_t)sizeof(IpcCard)) == 0,
+                   "IPC transport: allgather callback failed");
+    // every rank maps rank 0's counter block; rank 0 unlinks it once all have
+    // (the mappings stay: nothing is left in /dev/shm)
+    std::string err;
+    try {
+      map_shm(all[0].shm);
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    double ok = err.empty() ? 0.0 : 1.0;
+    HEAT2D_REQUIRE(ops_.allreduce(ops_.ctx, &ok, 1, 1) == 0, "IPC transport: allreduce callback failed");
+    if (rank_ == 0) ::shm_unlink(all[0].shm);
+    HEAT2D_REQUIRE(ok == 0.0, "IPC transport: a rank could not map the counter block" + (err.empty() ? "" : ": " + err));
+    // open the neighbours' fields
+    for (int p : {rank_ - 1, rank_ + 1}) {
+      if (p < 0 || p >= size_) continue;
+      HEAT2D_REQUIRE(all[(size_t)p].L.pitch == L.pitch, "IPC transport: slabs of different pitch");
+      peer_L_[p > rank_] = all[(size_t)p].L;
+      for (int b = 0; b < 2; ++b)
+        H2D_HIP(hipIpcOpenMemHandle(&peer_buf_[p > rank_][b], all[(size_t)p].buf[b], hipIpcMemLazyEnablePeerAccess));
+    }
+    barrier();
+    if (timeout_s_ > 0)
+      wd_.reset(new Watchdog(
+          timeout_s_, 0.05, [this](std::string* d) { return poll(d); }, [this](const std::string& r) { abort(r); }));
+  }
+
+  void exchange(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
+                bool on_device) override {
+    HEAT2D_REQUIRE(on_device, "the IPC transport moves device fields");
+    if (size_ == 1 || k <= 0) return;
+    HEAT2D_REQUIRE(attached_, "IPC transport: exchange before attach()");
+    HEAT2D_REQUIRE(!aborted_, "IPC transport aborted: " + reason());
+    const int b = field == mine_[0] ? 0 : (field == mine_[1] ? 1 : -1);
+    HEAT2D_REQUIRE(b >= 0, "IPC transport: exchange of a buffer that was not attached");
+    HEAT2D_REQUIRE(dtype_size(dt) == es_ && L.pitch == L_.pitch, "IPC transport: layout changed since attach()");
+    const int lo = rank_ > 0 ? rank_ - 1 : -1, hi = rank_ < size_ - 1 ? rank_ + 1 : -1;
+    kern::launch_ipc_arrive(slots_, ctrl_, rank_, lo, hi, timeout_ticks_, stream);
+    HaloMsg msg[2];
+    const int nmsg = halo_msgs(rank_, size_, L, k, msg);
+    const size_t bytes = halo_msg_bytes(L, k, es_);
+    for (int i = 0; i < nmsg; ++i) {
+      const int side = msg[i].peer > rank_;
+      const SlabLayout& PL = peer_L_[side];
+      // the neighbour's rows toward this rank: its first k (upper neighbour) or last k (lower)
+      const int64_t send_row = side ? 0 : PL.nrows - k;
+      const char* src = static_cast<const char*>(peer_buf_[side][b]) + halo_row_bytes(PL, send_row, es_);
+      char* dst = static_cast<char*>(field) + halo_row_bytes(L, msg[i].recv_row, es_);
+      H2D_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream));
+    }
+    kern::launch_ipc_depart(slots_, rank_, stream);
+    track(stream, "halo exchange");
+  }
+
+  void allreduce(double* vals, int n, int op) override {
+    if (size_ == 1) return;
+    HEAT2D_REQUIRE(ops_.allreduce(ops_.ctx, vals, n, op) == 0, "IPC transport: allreduce callback failed");
+  }
+  void barrier() override {
+    if (size_ == 1) return;
+    HEAT2D_REQUIRE(ops_.barrier(ops_.ctx) == 0, "IPC transport: barrier callback failed");
+  }
+
+  void check() override {
+    if (aborted_) fail(__FILE__, __LINE__, "IPC transport aborted (rank " + std::to_string(rank_) + " of " +
+                                               std::to_string(size_) + "): " + reason());
+    if (hctrl_) {
+      const uint64_t t = __atomic_load_n(&hctrl_[1], __ATOMIC_ACQUIRE);
+      if (t != 0)
+        fail(__FILE__, __LINE__, "IPC transport: rank " + std::to_string((long long)t - 1) +
+                                     " timed out waiting for a neighbour's halo (rank " + std::to_string(rank_) + ")");
+    }
+  }
+
+  void abort(const std::string& why) override {
+    bool expect = false;
+    if (!aborted_.compare_exchange_strong(expect, true)) return;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      reason_ = why;
+    }
+    // every rank's arrive kernels return: the streams drain instead of spinning
+    if (hctrl_) __atomic_store_n(&hctrl_[0], (uint64_t)rank_ + 1, __ATOMIC_RELEASE);
+  }
+
+ private:
+  size_t shm_size() const { return (size_t)(64 + 64 * size_ + 4095) / 4096 * 4096; }
+  void map_shm(const char* name) {
+    shm_bytes_ = shm_size();
+    const int fd = ::shm_open(name, O_RDWR, 0600);
+    HEAT2D_REQUIRE(fd >= 0, std::string("shm_open of ") + name);
+    void* p = ::mmap(nullptr, shm_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    HEAT2D_REQUIRE(p != MAP_FAILED, "mmap of the IPC counter block");
+    host_ = p;
+    H2D_HIP(hipHostRegister(host_, shm_bytes_, hipHostRegisterMapped));
+    void* d = nullptr;
+    H2D_HIP(hipHostGetDevicePointer(&d, host_, 0));
+    hctrl_ = static_cast<uint64_t*>(host_);
+    ctrl_ = static_cast<uint64_t*>(d);  // host-coherent: the host reads the same words through hctrl_
+    slots_ = reinterpret_cast<kern::IpcSlot*>(static_cast<char*>(d) + 64);
+  }
+  std::string reason() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return reason_;
+  }
+  void track(hipStream_t s, const char* what) {
+    if (!wd_ || io_.load() > 0) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    H2D_HIP(hipStreamIsCapturing(s, &cs));
+    if (cs != hipStreamCaptureStatusNone) return;  // inside a capture: the replay is tracked
+    std::lock_guard<std::mutex> g(mu_);
+    if (pend_.size() >= 4096) return;
+    hipEvent_t e = nullptr;
+    if (!pool_.empty()) {
+      e = pool_.back();
+      pool_.pop_back();
+    } else {
+      H2D_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    H2D_HIP(hipEventRecord(e, s));
+    pend_.push_back(Pend{e, ++nops_, what});
+  }
+  Watchdog::Status poll(std::string* detail) {
+    if (aborted_) return Watchdog::Idle;
+    static thread_local int dev_set = -1;
+    if (dev_set != device_) {
+      (void)hipSetDevice(device_);
+      dev_set = device_;
+    }
+    if (hctrl_ && __atomic_load_n(&hctrl_[0], __ATOMIC_ACQUIRE) != 0) {
+      *detail = "rank " + std::to_string((long long)__atomic_load_n(&hctrl_[0], __ATOMIC_ACQUIRE) - 1) + " aborted";
+      return Watchdog::Error;
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    int done = 0;
+    while (!pend_.empty()) {
+      const hipError_t q = hipEventQuery(pend_.front().ev);
+      if (q == hipErrorNotReady) break;
+      if (q != hipSuccess) {
+        *detail = std::string("hipEventQuery: ") + hipGetErrorString(q);
+        return Watchdog::Error;
+      }
+      pool_.push_back(pend_.front().ev);
+      pend_.pop_front();
+      ++done;
+    }
+    if (done) return Watchdog::Progress;
+    if (pend_.empty()) return Watchdog::Idle;
+    *detail = std::string(pend_.front().what) + " #" + std::to_string(pend_.front().seq) + " of rank " +
+              std::to_string(rank_) + " of " + std::to_string(size_) + " still pending";
+    return Watchdog::Pending;
+  }
+
+  struct Pend {
+    hipEvent_t ev;
+    int64_t seq;
+    const char* what;
+  };
+  IpcOps ops_;
+  int rank_, size_;
+  int device_ = 0;
+  bool attached_ = false;
+  void* mine_[2] = {nullptr, nullptr};
+  SlabLayout L_{};
+  size_t es_ = 8;
+  void* peer_buf_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [lower, upper neighbour][buffer]
+  SlabLayout peer_L_[2]{};
+  void* host_ = nullptr;
+  size_t shm_bytes_ = 0;
+  uint64_t* ctrl_ = nullptr;   // device view of {abort word, timed-out rank + 1}
+  uint64_t* hctrl_ = nullptr;  // host view
+  kern::IpcSlot* slots_ = nullptr;
+  double timeout_s_ = 600.0;
+  uint64_t timeout_ticks_ = 0;
+  std::atomic<bool> aborted_{false};
+  std::atomic<int> io_{0};
+  mutable std::mutex mu_;  // reason_, pend_, pool_
+  std::string reason_;
+  std::deque<Pend> pend_;
+  std::vector<hipEvent_t> pool_;
+  int64_t nops_ = 0;
+  std::unique_ptr<Watchdog> wd_;
+};
+
+}  // namespace
+
+std::shared_ptr<Transport> make_ipc_transport(const IpcOps& ops, int rank, int size, int device) {
+  return std::make_shared<IpcTransport>(ops, rank, size, device);
+}
+
+}  // namespace heat2d

@@ -161,6 +161,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     cfg_.overlap = 0;
     cfg_.use_graph = 0;
   }
+  tr_->attach(buf_[0], buf_[1], L_, dtype());
 }
 
 Solver::~Solver() {
@@ -206,6 +207,9 @@ void Solver::init(const kern::IcParams& ic, const double* xg, const double* yg) 
   // ghost rows are filled from the global IC directly: no exchange needed
   cur_ = 0;
   steps_ = 0;
+  ghost_ = (int)band_;
+  last_x_[0] = last_x_[1] = 0;
+  last_k_ = 0;
 }
 
 void Solver::launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k) {
@@ -216,9 +220,17 @@ void Solver::launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k
     cpu::tb(dtype(), src, dst, L_, rb, re, k, cfg_.r, cfg_.arith);
 }
 
-void Solver::exchange_on(void* field, hipStream_t s) {
+void Solver::exchange_on(void* field, int64_t k, hipStream_t s) {
   if (!tr_->exchanges()) return;
-  tr_->exchange(field, L_, dtype(), band_, s, hip_);
+  HEAT2D_REQUIRE(k >= 1 && k <= band_, "halo exchange depth outside [1, band]");
+  tr_->exchange(field, L_, dtype(), k, s, hip_);
+  halo_rows_ += k;
+}
+
+int64_t Solver::halo_rows_exchanged(bool reset) {
+  const int64_t v = halo_rows_;
+  if (reset) halo_rows_ = 0;
+  return v;
 }
 
 void Solver::cycle_compute(int k) {
@@ -239,16 +251,48 @@ void Solver::exchange_post() {
   tr_->post(buf_[cur_], L_, hip_ ? ev_bnd_ : nullptr);
 }
 
-void Solver::exchange_now() { exchange_on(buf_[cur_], s_compute_); }
+void Solver::exchange_now(int k) {
+  const int64_t d = k > 0 ? k : band_;
+  exchange_on(buf_[cur_], d, s_compute_);
+  ghost_ = (int)d;
+  last_x_[cur_] = std::max<int>(last_x_[cur_], (int)d);
+}
 
-void Solver::cycle_launch(int k) {
+// One blocking exchange of k rows of the current buffer, between cycles: the
+// previous cycle's kernels on both streams have finished (synchronize), so
+// every band row sent is final, and the next cycle starts after the copies
+// landed. Used where a cycle needs deeper ghost rows than the last exchange
+// moved (a step(n) whose first depth exceeds the previous call's last
+// exchange); prepare(n) does it outside timed regions.
+void Solver::topup(int k) {
+  if (!needs_topup(k)) return;
+  HEAT2D_REQUIRE(k <= band_, "top-up deeper than the halo band");
+  synchronize();
+  exchange_post();
+  exchange_now(k);
+  synchronize();
+}
+
+void Solver::cycle_launch(int k, int x) {
   HEAT2D_REQUIRE(pend_ == Pending::None, "cycle_launch: previous cycle not finished");
   HEAT2D_REQUIRE(k >= 1 && k <= cfg_.tb, "cycle depth outside [1, tb]");
+  if (x <= 0 || !tr_->exchanges()) x = k;
+  HEAT2D_REQUIRE(x <= band_, "exchange depth outside [1, band]");
+  HEAT2D_REQUIRE(!tr_->exchanges() || ghost_ >= k,
+                 "cycle of depth " + std::to_string(k) + " on " + std::to_string(ghost_) +
+                     " valid ghost rows (rank " + std::to_string(tr_->rank()) + "): topup() first");
   if (stats_next_ && hip_ && !jit_) launch_stats_cycle(k);
-  else if (cfg_.overlap && hip_) launch_overlap(k);
+  // Boundary bands: the rows the exchange sends (x) must be written by the
+  // band launch, and MAIN must not touch rows a receiver-driven transport
+  // (loopback, peer, IPC pulls) may still be reading: the previous exchange
+  // of this cycle's destination buffer moved last_x_ rows of it, and only the
+  // band launch is ordered after that exchange's pulls (the concurrent order's
+  // MAIN waits for the previous EDGE only).
+  else if (cfg_.overlap && hip_) launch_overlap(k, std::max({k, x, last_x_[cur_ ^ 1]}));
   else launch_serial(k);
   stats_next_ = false;
   pend_k_ = k;
+  pend_x_ = x;
 }
 
 // The fused-statistics cycle: one general launch over the whole slab on the
@@ -274,14 +318,14 @@ void Solver::cycle_finish() {
   void* dst = buf_[cur_ ^ 1];
   PhaseEvents* pe = pend_pe_ >= 0 ? &phase_ev_[(size_t)pend_pe_] : nullptr;
   if (pend_ == Pending::Serial) {
-    exchange_on(dst, s_compute_);
+    exchange_on(dst, pend_x_, s_compute_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
   } else {
     // both split orders: the exchange of the new bands runs on the comm
     // stream (concurrent: right behind the EDGE launch there; edge-first:
     // behind the bands, which ran first on the compute stream)
     if (pend_ == Pending::EdgeFirst) H2D_HIP(hipStreamWaitEvent(s_comm_, ev_bnd_, 0));
-    exchange_on(dst, s_comm_);
+    exchange_on(dst, pend_x_, s_comm_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[5], s_comm_));
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
   }
@@ -291,6 +335,8 @@ void Solver::cycle_finish() {
   steps_ += pend_k_;
   hist_[pend_k_] += 1;
   last_k_ = pend_k_;
+  ghost_ = pend_x_;
+  if (tr_->exchanges()) last_x_[cur_ ^ 1] = pend_x_;
   cycle_swap();
 }
 
@@ -365,11 +411,11 @@ const kern::SplitPlan& Solver::split_plan(int k) {
   if (p.k != k) {
     // room for RCCL's workgroups beside the two stencil launches when exchanging
     const int spare = spare_waves();
-    p = kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, 0, 0, cfg_.arith);
+    // bands of k rows (split_plan_banded widens them when a deeper exchange follows)
+    p = kern::plan_split(dtype(), L_, k, k, compute_cus_, spare, 0, 0, cfg_.arith);
     p.k = k;
     ++plans_made_;
-    const bool big = L_.nrows * L_.ncols >= (int64_t(1) << 24);
-    if (p.valid && (cfg_.autotune > 0 || (cfg_.autotune < 0 && big))) autotune_split(k);
+    if (p.valid && autotune_slabs(cfg_.n_rows, cfg_.n_cols, tr_->size(), cfg_.autotune)) autotune_split(k);
     // HEAT2D_SPLIT_ORDER=edge-first | concurrent overrides the split's ordering (tests, A/B);
     // HEAT2D_SPLIT_ORDER=single forces one general launch per cycle (no exchange only)
     if (const char* env = std::getenv("HEAT2D_SPLIT_ORDER")) {
@@ -391,13 +437,30 @@ const kern::SplitPlan& Solver::split_plan(int k) {
       if (nseg != 0 && p.valid) {
         const int valid = p.valid, ring = p.ring;
         p = valid == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, -nseg, cfg_.arith)
-                       : kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, -nseg, cfg_.arith);
+                       : kern::plan_split(dtype(), L_, k, k, compute_cus_, spare, ring, -nseg, cfg_.arith);
         if (p.valid) p.valid = valid;
         p.k = k;
       }
     }
   }
   return p;
+}
+
+const kern::SplitPlan& Solver::split_plan_banded(int k, int64_t B) {
+  const kern::SplitPlan& base = split_plan(k);
+  if (B <= k || !base.valid || base.valid == 2) return base;
+  auto it = banded_.find({k, B});
+  if (it != banded_.end()) return it->second;
+  // the same choice (order, ring, interior bands / segments) over the interior
+  // left between B-row bands; too thin for that: valid = 0 (serial cycle)
+  kern::SplitPlan d = kern::plan_split(dtype(), L_, k, B, compute_cus_, spare_waves(), base.ring, base.main.nb,
+                                       cfg_.arith);
+  if (d.valid) {
+    d.valid = base.valid;
+    d.main_waves = std::min<int64_t>(d.main_items, std::max<int64_t>(1, base.main_waves));
+  }
+  d.k = k;
+  return banded_.emplace(std::make_pair(k, B), d).first->second;
 }
 
 // Time candidate split plans (ring 4/6 x MAIN band counts) in the steady
@@ -436,6 +499,7 @@ constexpr float kEdgeFirstMinCycleMs = 0.4f;
 void Solver::trial_cycle(const kern::SplitPlan& c) {
   void* src = buf_[cur_];
   void* dst = buf_[cur_ ^ 1];
+  last_k_ = 0;  // the other buffer no longer holds T_{n-1}: stats(residual) reports NaN
   if (c.valid == 3) {  // edge-first: both parts in order on the compute stream
     H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
     kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_compute_, cfg_.arith);
@@ -502,7 +566,7 @@ void Solver::autotune_split(int k) {
         const int64_t nb = std::max<int64_t>(1, (int64_t)((mode == 2 ? nb1 : nb0) * f + 0.5));
         if (mode == 1 && ring == best.ring && nb == best.main.nb) continue;
         kern::SplitPlan c = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, nb, cfg_.arith)
-                                      : kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, nb,
+                                      : kern::plan_split(dtype(), L_, k, k, compute_cus_, spare, ring, nb,
                                                          cfg_.arith);
         if (!c.valid) continue;
         if (mode == 3) c.valid = 3;
@@ -522,7 +586,7 @@ void Solver::autotune_split(int k) {
       for (double f : {0.5, 1.0, 1.5, 2.0}) {
         const int64_t nseg = std::max<int64_t>(1, (int64_t)(w0 * f + 0.5));
         kern::SplitPlan c = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, -nseg, cfg_.arith)
-                                      : kern::plan_split(dtype(), L_, k, band_, compute_cus_, spare, ring, -nseg,
+                                      : kern::plan_split(dtype(), L_, k, k, compute_cus_, spare, ring, -nseg,
                                                          cfg_.arith);
         if (!c.valid) continue;
         if (mode == 3) c.valid = 3;
@@ -551,10 +615,10 @@ void Solver::autotune_split(int k) {
   synchronize();
 }
 
-void Solver::launch_overlap(int k) {
+void Solver::launch_overlap(int k, int64_t B) {
   void* src = buf_[cur_];
   void* dst = buf_[cur_ ^ 1];
-  const kern::SplitPlan& sp = split_plan(k);
+  const kern::SplitPlan& sp = split_plan_banded(k, B);
   HEAT2D_REQUIRE(sp.valid != 2 || !tr_->exchanges(), "single-launch plan with a halo exchange");
   roctxRangePushA("heat2d.cycle.split");
   PhaseEvents* pe = timing_ ? phase_begin(0) : nullptr;
@@ -606,7 +670,10 @@ void Solver::cycle_copy_swap() {
   if (hip_) kern::launch_copy(old, cur, (int64_t)bytes, s_compute_);
   else std::memcpy(old, cur, bytes);
   launch_tb(old, cur, 0, L_.nrows, 1);
-  exchange_on(cur, s_compute_);
+  exchange_on(cur, 1, s_compute_);
+  ghost_ = 1;
+  if (tr_->exchanges()) last_x_[0] = last_x_[1] = 1;
+  last_k_ = 1;
 }
 
 void Solver::run_graph_cycles(int64_t npairs) {
@@ -621,7 +688,14 @@ void Solver::run_graph_cycles(int64_t npairs) {
   for (int64_t i = 0; i < npairs; ++i) H2D_HIP(hipGraphLaunch(graph_exec_, s_compute_));
   if (npairs > 0 && tr_->exchanges()) tr_->graph_launched(s_compute_);
   hist_[K] += 2 * npairs;
-  if (npairs > 0) last_k_ = K;
+  if (npairs > 0) {
+    last_k_ = K;
+    ghost_ = K;  // both captured cycles exchange K rows
+    if (tr_->exchanges()) {
+      last_x_[0] = last_x_[1] = K;
+      halo_rows_ += 2 * npairs * K;
+    }
+  }
   if (ovl) {  // eager cycles after the graph order against its end
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
@@ -640,8 +714,11 @@ void Solver::ensure_pair_graph() {
   if (!graph_exec_ || graph_k_ != K) {
     if (graph_exec_) H2D_HIP(hipGraphExecDestroy(graph_exec_));
     hipGraph_t g = nullptr;
-    const int saved = cur_;
-    const int64_t saved_steps = steps_, saved_hist = hist_[K];
+    const int saved = cur_, saved_ghost = ghost_, saved_last = last_k_;
+    const int64_t saved_steps = steps_, saved_hist = hist_[K], saved_halo = halo_rows_;
+    ghost_ = (int)band_;  // replays start after step()'s top-up
+    const int saved_lx0 = last_x_[0], saved_lx1 = last_x_[1];
+    if (tr_->exchanges()) last_x_[0] = last_x_[1] = (int)band_;  // whatever a replay follows
     if (!ovl) {
       H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
       for (int c = 0; c < 2; ++c) {
@@ -679,6 +756,11 @@ void Solver::ensure_pair_graph() {
     cur_ = saved;
     steps_ = saved_steps;
     hist_[K] = saved_hist;
+    ghost_ = saved_ghost;
+    last_k_ = saved_last;
+    halo_rows_ = saved_halo;
+    last_x_[0] = saved_lx0;
+    last_x_[1] = saved_lx1;
     if (!g) H2D_HIP(hipStreamEndCapture(s_compute_, &g));
     H2D_HIP(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
     H2D_HIP(hipGraphDestroy(g));
@@ -691,6 +773,48 @@ void Solver::ensure_pair_graph() {
   }
 }
 
+bool Solver::pair_graphs() const {
+  return cfg_.use_graph && hip_ && (!tr_->exchanges() || tr_->capturable());
+}
+
+// step(n)'s cycles from buffer parity `par`: the measured schedule if prepare()
+// chose one, else graph pairs of depth pref_depth (parity 0 only, the parity
+// the pair graph was captured for) and balanced cycles: ceil(left / K) cycles
+// of depth base or base + 1 rather than full-depth cycles plus one short
+// remainder cycle (a K = 4 cycle runs ~3x slower per step than K = 12: 100
+// steps = 8 x 11 + 12, not 8 x 12 + 4).
+std::vector<Solver::CycleRun> Solver::step_runs(int64_t n, int par) const {
+  std::vector<CycleRun> runs;
+  if (n <= 0) return runs;
+  if (const std::vector<int>* sc = schedule(n)) {
+    for (int k : *sc) runs.push_back({k, 0});
+    return runs;
+  }
+  const int K = k_pref_;
+  int64_t left = n;
+  while (left > 0) {
+    if (pair_graphs() && left >= 2 * K && par == 0) {
+      const int64_t pairs = left / (2 * K);
+      runs.push_back({K, pairs});
+      left -= pairs * 2 * K;
+      continue;
+    }
+    const int64_t ncyc = (left + K - 1) / K;
+    const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
+    runs.push_back({k, 0});
+    left -= k;
+    par ^= 1;
+  }
+  return runs;
+}
+
+std::vector<int> Solver::step_cycles(int64_t n) const {
+  if (cfg_.copy_swap) return std::vector<int>((size_t)std::max<int64_t>(0, n), 1);
+  std::vector<int> seq;
+  for (const CycleRun& r : step_runs(n, cur_)) seq.insert(seq.end(), (size_t)(r.pairs > 0 ? 2 * r.pairs : 1), r.k);
+  return seq;
+}
+
 void Solver::step(int64_t n) {
   if (n <= 0) return;
   if (hip_) H2D_HIP(hipSetDevice(cfg_.device));
@@ -699,44 +823,85 @@ void Solver::step(int64_t n) {
     steps_ += n;
     return;
   }
-  if (auto it = sched_.find(n); it != sched_.end()) {
-    if (schedule_graphs()) {
-      run_schedule_graph(n);
-      return;
-    }
-    for (int k : it->second) {
-      cycle_launch(k);
-      cycle_finish();
-    }
+  const std::vector<CycleRun> runs = step_runs(n, cur_);
+  // each cycle's exchange moves the rows the NEXT cycle reads; the last one
+  // those of this call's first cycle (a repeated step(n) — bench, the CLI's
+  // chunks — then never tops up)
+  const int first = runs.front().k;
+  topup(first);
+  if (schedule(n) && schedule_graphs()) {
+    run_schedule_graph(n);
     return;
   }
-  const int K = k_pref_;
-  const bool multi = tr_->exchanges();
-  int64_t left = n;
-  while (left > 0) {
-    if (cfg_.use_graph && hip_ && (!multi || tr_->capturable()) && left >= 2 * K && cur_ == 0) {
-      const int64_t pairs = left / (2 * K);
-      run_graph_cycles(pairs);
-      left -= pairs * 2 * K;
-      steps_ += pairs * 2 * K;
+  for (size_t i = 0; i < runs.size(); ++i) {
+    if (runs[i].pairs > 0) {
+      run_graph_cycles(runs[i].pairs);
+      steps_ += runs[i].pairs * 2 * runs[i].k;
       continue;
     }
-    // balanced depths: ceil(left / K) cycles of depth base or base + 1 rather
-    // than full-depth cycles plus one short remainder cycle (a K = 4 cycle runs
-    // ~3x slower per step than K = 12: 100 steps = 8 x 11 + 12, not 8 x 12 + 4)
-    const int64_t ncyc = (left + K - 1) / K;
-    const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
-    cycle_launch(k);
+    cycle_launch(runs[i].k, i + 1 < runs.size() ? runs[i + 1].k : first);
     cycle_finish();
-    left -= k;
   }
 }
 
+// Same decision on every rank (autotune_slabs: the global problem decides).
 bool Solver::measured_schedules() const {
   if (!hip_ || !cfg_.overlap || cfg_.copy_swap || jit_) return false;
   if (cfg_.use_graph && tr_->exchanges() && !tr_->capturable()) return false;  // graphs of the pair kind
-  const bool big = L_.nrows * L_.ncols >= (int64_t(1) << 24);
-  return cfg_.autotune > 0 || (cfg_.autotune < 0 && big);
+  return autotune_slabs(cfg_.n_rows, cfg_.n_cols, tr_->size(), cfg_.autotune);
+}
+
+bool autotune_slabs(int64_t n_rows, int64_t n_cols, int nranks, int autotune) {
+  if (autotune >= 0) return autotune > 0;
+  const int64_t min_rows = n_rows / std::max(1, nranks);  // the thinnest slab of decompose()
+  return min_rows * n_cols >= (int64_t(1) << 24);
+}
+
+// FNV-1a over the cycles step(n) runs from the current parity and the
+// exchange depth after each: what RCCL pairs by order across ranks.
+uint64_t Solver::sequence_hash(int64_t n) const {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](int64_t v) {
+    for (int b = 0; b < 8; ++b) {
+      h ^= (uint64_t)((v >> (8 * b)) & 0xff);
+      h *= 1099511628211ull;
+    }
+  };
+  mix(n);
+  mix(band_);
+  mix(cfg_.copy_swap);
+  const std::vector<int> seq = step_cycles(n);
+  for (size_t i = 0; i < seq.size(); ++i) {
+    mix(seq[i]);
+    mix(exchange_depth(seq, i, seq.front()));
+  }
+  return h;
+}
+
+void Solver::agree(uint64_t h, const std::string& what) {
+  if (!tr_->exchanges() || !tr_->collective() || tr_->size() <= 1) return;
+  const int P = tr_->size(), me = tr_->rank();
+  const double hv = (double)(h >> 12);  // 52 bits: exact in a double, exact under a sum with zeros
+  if (P <= 64) {
+    std::vector<double> v((size_t)P, 0.0);
+    v[(size_t)me] = hv;
+    tr_->allreduce(v.data(), P, 0);
+    bool same = true;
+    for (int r = 1; r < P; ++r) same = same && v[(size_t)r] == v[0];
+    if (same) return;
+    std::string msg = "ranks disagree on " + what + " (a collective would mismatch): ";
+    char b[64];
+    for (int r = 0; r < P; ++r) {
+      std::snprintf(b, sizeof(b), "%srank %d: %013llx", r ? ", " : "", r, (unsigned long long)v[(size_t)r]);
+      msg += b;
+    }
+    fail(__FILE__, __LINE__, msg + " (this is rank " + std::to_string(me) + ")");
+  }
+  double mm[2] = {hv, -hv};
+  tr_->allreduce(mm, 2, 1);
+  if (mm[0] != -mm[1])
+    fail(__FILE__, __LINE__, "ranks disagree on " + what + " (rank " + std::to_string(me) + " of " +
+                                 std::to_string(P) + ")");
 }
 
 // Autotuned steady-state cycle time of depth k, max over ranks (0: no tuned
@@ -870,10 +1035,14 @@ bool Solver::schedule_graphs() const {
 // cross-stream launches are a quarter of a 4096^2 fp32 cycle).
 void Solver::capture_schedule(int64_t n) {
   const std::vector<int>& sc = sched_.at(n);
-  for (int k : sc) (void)split_plan(k);  // plan / autotune (synchronising) before the capture
+  for (size_t i = 0; i < sc.size(); ++i)  // plan / autotune (synchronising) before the capture
+    (void)split_plan_banded(sc[i], std::max(sc[i], exchange_depth(sc, i, sc[0])));
   synchronize();
-  const int saved = cur_;
-  const int64_t saved_steps = steps_;
+  const int saved = cur_, saved_ghost = ghost_, saved_last = last_k_;
+  const int64_t saved_steps = steps_, saved_halo = halo_rows_;
+  ghost_ = (int)band_;  // replays start after step()'s top-up
+  const int saved_lx0 = last_x_[0], saved_lx1 = last_x_[1];
+  if (tr_->exchanges()) last_x_[0] = last_x_[1] = (int)band_;  // whatever a replay follows
   int64_t saved_hist[kMaxTB + 1];
   std::copy(hist_, hist_ + kMaxTB + 1, saved_hist);
   hipEvent_t fork = nullptr, join = nullptr;
@@ -888,8 +1057,8 @@ void Solver::capture_schedule(int64_t n) {
   H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
   const bool timing = timing_;
   timing_ = false;
-  for (int k : sc) {
-    cycle_launch(k);
+  for (size_t i = 0; i < sc.size(); ++i) {
+    cycle_launch(sc[i], exchange_depth(sc, i, sc[0]));
     cycle_finish();
   }
   timing_ = timing;
@@ -900,6 +1069,11 @@ void Solver::capture_schedule(int64_t n) {
   H2D_HIP(hipEventDestroy(join));
   cur_ = saved;
   steps_ = saved_steps;
+  ghost_ = saved_ghost;
+  last_k_ = saved_last;
+  halo_rows_ = saved_halo;
+  last_x_[0] = saved_lx0;
+  last_x_[1] = saved_lx1;
   std::copy(saved_hist, saved_hist + kMaxTB + 1, hist_);
   hipGraphExec_t ge = nullptr;
   H2D_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
@@ -928,11 +1102,15 @@ void Solver::run_schedule_graph(int64_t n) {
   H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
   H2D_HIP(hipEventRecord(ev_comm_, s_compute_));
   H2D_HIP(hipStreamWaitEvent(s_comm_, ev_comm_, 0));
-  for (int k : sc) {
-    hist_[k] += 1;
-    steps_ += k;
+  for (size_t i = 0; i < sc.size(); ++i) {
+    hist_[sc[i]] += 1;
+    steps_ += sc[i];
+    if (tr_->exchanges()) halo_rows_ += exchange_depth(sc, i, sc[0]);
   }
   last_k_ = sc.back();
+  ghost_ = sc.front();  // the last captured cycle's exchange depth
+  if (tr_->exchanges())  // conservative: the deepest exchange of the replay, on both buffers
+    last_x_[0] = last_x_[1] = *std::max_element(sc.begin(), sc.end());
   if (sc.size() % 2) cycle_swap();
 }
 
@@ -942,7 +1120,18 @@ const std::vector<int>* Solver::schedule(int64_t n) const {
 }
 
 void Solver::prepare(int64_t n) {
-  if (!hip_ || !cfg_.overlap || cfg_.copy_swap || n <= 0) return;
+  if (n <= 0) return;
+  if (hip_ && cfg_.overlap && !cfg_.copy_swap) prepare_plans(n);
+  // every rank runs the same cycles with the same exchange depths (RCCL pairs
+  // the sends / receives by order: a mismatch is a hang or wrong ghost rows)
+  agree(sequence_hash(n), "step(" + std::to_string(n) + ")'s cycle sequence / exchange depths");
+  // step(n)'s first cycle reads deeper ghost rows than the last exchange moved
+  // (e.g. a shallow warmup before it): top up here, outside the timed step
+  const std::vector<int> seq = step_cycles(n);
+  if (!seq.empty()) topup(seq.front());
+}
+
+void Solver::prepare_plans(int64_t n) {
   if (measured_schedules() && !sched_.count(n)) {
     std::vector<int> s = choose_schedule(n);
     // Short graph-replayed runs: the per-depth estimates of near-tied
@@ -994,6 +1183,8 @@ void Solver::prepare(int64_t n) {
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
     synchronize();
+    for (size_t i = 0; i < s->size(); ++i)
+      (void)split_plan_banded((*s)[i], std::max((*s)[i], exchange_depth(*s, i, (*s)[0])));
     return;
   }
   // walk step(n)'s loop (graph pairs of depth K, then balanced eager cycles)
@@ -1002,22 +1193,15 @@ void Solver::prepare(int64_t n) {
   // both, since a warmup between prepare() and step(n) may flip it (4096^2
   // fp32 graph, K = 6 / 14: an unplanned remainder depth autotuned inside the
   // timed run cost 10 ms of 16).
-  const int K = k_pref_;
-  const bool multi = tr_->exchanges();
   for (int start = 0; start < 2; ++start) {
-    int par = start;
-    int64_t left = n;
-    while (left > 0) {
-      if (cfg_.use_graph && (!multi || tr_->capturable()) && left >= 2 * K && par == 0) {
+    const std::vector<CycleRun> runs = step_runs(n, start);
+    for (size_t i = 0; i < runs.size(); ++i) {
+      if (runs[i].pairs > 0) {
         ensure_pair_graph();
-        left -= left / (2 * K) * 2 * K;
         continue;
       }
-      const int64_t ncyc = (left + K - 1) / K;
-      const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
-      (void)split_plan(k);
-      left -= k;
-      par ^= 1;
+      const int x = tr_->exchanges() ? (i + 1 < runs.size() ? runs[i + 1].k : runs[0].k) : runs[i].k;
+      (void)split_plan_banded(runs[i].k, std::max(runs[i].k, x));
     }
   }
 }
@@ -1067,9 +1251,10 @@ void Solver::step_stats(int64_t n, double out[6]) {
       left -= k;
     }
   }
+  topup(seq.front());
   for (size_t i = 0; i < seq.size(); ++i) {
     stats_next_ = i + 1 == seq.size();
-    cycle_launch(seq[i]);
+    cycle_launch(seq[i], exchange_depth(seq, i, seq.front()));
     cycle_finish();
   }
   double loc[6];
@@ -1176,14 +1361,27 @@ void LoopbackGroup::init(const kern::IcParams& ic, const double* xg, const doubl
 // members: all launches (each posts its new field and band event), then all
 // exchanges — the order a multi-process run gets from RCCL's rendezvous.
 void LoopbackGroup::step(int64_t n) {
+  if (n <= 0) return;
   const int K = members_[0]->pref_depth();
-  int64_t left = n;
-  while (left > 0) {
+  std::vector<int> seq;
+  for (int64_t left = n; left > 0;) {
     const int64_t ncyc = (left + K - 1) / K;
     const int k = (int)(left / ncyc + (left % ncyc ? 1 : 0));
-    for (auto& m : members_) m->cycle_launch(k);
-    for (auto& m : members_) m->cycle_finish();
+    seq.push_back(k);
     left -= k;
+  }
+  // deeper first cycle than the last exchange moved: every member posts its
+  // current field, then every member pulls (Solver::topup's two phases)
+  if (members_[0]->needs_topup(seq[0])) {
+    for (auto& m : members_) m->synchronize();
+    for (auto& m : members_) m->exchange_post();
+    for (auto& m : members_) m->exchange_now(seq[0]);
+    synchronize();
+  }
+  for (size_t i = 0; i < seq.size(); ++i) {
+    const int x = exchange_depth(seq, i, seq[0]);
+    for (auto& m : members_) m->cycle_launch(seq[i], x);
+    for (auto& m : members_) m->cycle_finish();
   }
 }
 

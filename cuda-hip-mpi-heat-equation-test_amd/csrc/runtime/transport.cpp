@@ -99,10 +99,14 @@ class RcclTransport final : public Transport {
   void graph_launched(hipStream_t stream) override { track(stream, "graph replay"); }
   bool exchanges() const override { return size_ > 1 || loop_; }
   bool aborted() const override { return aborted_.load(); }
+  // collectives of an I/O phase wait on peers' host I/O: not tracked (a slow
+  // output turn is not a hung fabric); exchanges are never issued inside one
+  void io_phase(bool on) override { io_ += on ? 1 : -1; }
 
   void check() override {
     if (aborted_) fail_aborted();
     std::unique_lock<std::timed_mutex> lk(cmu_);
+    live();  // an abort between the test above and the lock: report it, not a null communicator
     ncclResult_t st = ncclSuccess;
     H2D_NCCL(ncclCommGetAsyncError(comm_, &st));
     if (st != ncclSuccess && st != ncclInProgress)
@@ -199,7 +203,7 @@ class RcclTransport final : public Transport {
   }
   // record a completion event of the operation just enqueued on `s` (watchdog)
   void track(hipStream_t s, const char* what) {
-    if (!wd_) return;
+    if (!wd_ || io_.load() > 0) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     H2D_HIP(hipStreamIsCapturing(s, &cs));
     if (cs != hipStreamCaptureStatusNone) return;  // inside a capture: the replay is tracked
@@ -270,6 +274,7 @@ class RcclTransport final : public Transport {
   std::vector<hipEvent_t> pool_;
   int64_t nops_ = 0;
   std::atomic<bool> aborted_{false};
+  std::atomic<int> io_{0};
   std::string abort_reason_;
   std::unique_ptr<Watchdog> wd_;
 };
@@ -395,6 +400,7 @@ class LoopbackTransport final : public Transport {
   int size() const override { return (int)hub_->slot.size(); }
   std::string name() const override { return "loopback"; }
   // the members share one host thread: collectives over them are the group's job
+  bool collective() const override { return false; }
   void allreduce(double*, int, int) override {}
   void barrier() override {}
 
@@ -465,7 +471,9 @@ struct ThreadHub {
   explicit ThreadHub(int n) : n(n), field((size_t)n), layout((size_t)n), vals((size_t)n * 64) {
     timeout = Watchdog::env_timeout(600.0);
   }
-  void barrier(int rank) {
+  // io: an I/O-phase barrier (Transport::io_phase) — a peer may be writing
+  // its output for long, so no timeout (abort() still wakes it)
+  void barrier(int rank, bool io = false) {
     std::unique_lock<std::mutex> lk(mu);
     if (aborted) throw_aborted(rank);
     const int64_t g = gen;
@@ -476,7 +484,7 @@ struct ThreadHub {
       return;
     }
     const auto pred = [&] { return gen != g || aborted; };
-    if (timeout > 0) {
+    if (timeout > 0 && !io) {
       if (!cv.wait_for(lk, std::chrono::duration<double>(timeout), pred)) {
         aborted = true;
         reason = "rank " + std::to_string(rank) + " waited " + std::to_string(timeout) +
@@ -517,6 +525,7 @@ class ThreadTransport final : public Transport {
   int rank() const override { return rank_; }
   int size() const override { return hub_->n; }
   std::string name() const override { return "host-threads"; }
+  void io_phase(bool on) override { io_ += on ? 1 : -1; }
   void abort(const std::string& reason) override { hub_->abort(reason); }
   bool aborted() const override {
     std::lock_guard<std::mutex> g(hub_->mu);
@@ -553,7 +562,7 @@ class ThreadTransport final : public Transport {
     HEAT2D_REQUIRE(n <= 64, "allreduce too large");
     if (size() == 1) return;
     std::copy(vals, vals + n, hub_->vals.begin() + (ptrdiff_t)rank_ * 64);
-    hub_->barrier(rank_);
+    hub_->barrier(rank_, io_ > 0);
     for (int j = 0; j < n; ++j) {  // same fixed order on every rank: identical results
       double a = hub_->vals[(size_t)j];
       for (int r = 1; r < size(); ++r) {
@@ -562,13 +571,14 @@ class ThreadTransport final : public Transport {
       }
       vals[j] = a;
     }
-    hub_->barrier(rank_);
+    hub_->barrier(rank_, io_ > 0);
   }
-  void barrier() override { hub_->barrier(rank_); }
+  void barrier() override { hub_->barrier(rank_, io_ > 0); }
 
  private:
   std::shared_ptr<ThreadHub> hub_;
   int rank_;
+  int io_ = 0;
 };
 
 // ------------------------------------------------------------------ peer
@@ -612,6 +622,7 @@ class PeerTransport final : public Transport {
   int rank() const override { return rank_; }
   int size() const override { return hub_->n; }
   std::string name() const override { return "peer"; }
+  void io_phase(bool on) override { io_ += on ? 1 : -1; }
   void abort(const std::string& reason) override { hub_->abort(reason); }
   bool aborted() const override {
     std::lock_guard<std::mutex> g(hub_->mu);
@@ -700,7 +711,7 @@ class PeerTransport final : public Transport {
     HEAT2D_REQUIRE(n <= 64, "allreduce too large");
     if (size() == 1) return;
     std::copy(vals, vals + n, hub_->vals.begin() + (ptrdiff_t)rank_ * 64);
-    hub_->barrier(rank_);
+    hub_->barrier(rank_, io_ > 0);
     for (int j = 0; j < n; ++j) {  // same fixed order on every rank: identical results
       double a = hub_->vals[(size_t)j];
       for (int r = 1; r < size(); ++r) {
@@ -709,11 +720,12 @@ class PeerTransport final : public Transport {
       }
       vals[j] = a;
     }
-    hub_->barrier(rank_);
+    hub_->barrier(rank_, io_ > 0);
   }
-  void barrier() override { hub_->barrier(rank_); }
+  void barrier() override { hub_->barrier(rank_, io_ > 0); }
 
  private:
+  int io_ = 0;
   // direct peer reads over xGMI for the copies this device pulls from `peer`
   void enable_peer(int dev, int peer) {
     std::lock_guard<std::mutex> g(hub_->peer_mu);

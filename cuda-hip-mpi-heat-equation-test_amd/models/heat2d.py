@@ -207,6 +207,28 @@ class HeatSolver:
         """{depth: cycles} that step() launched since the last reset (graph replays count 2 each)."""
         return _cycle_hist(self._h, reset)
 
+    def step_cycles(self, n: int) -> list:
+        """The cycle depths step(n) will run from the current state, in order."""
+        ln = C.c_int64()
+        N.call("heat2d_solver_step_cycles", self._h, int(n), None, 0, C.byref(ln))
+        out = (C.c_int32 * max(1, ln.value))()
+        N.call("heat2d_solver_step_cycles", self._h, int(n), out, ln.value, C.byref(ln))
+        return [int(v) for v in out[:ln.value]]
+
+    def halo_rows_exchanged(self, reset: bool = False) -> int:
+        """Halo rows this rank exchanged per side since the last reset (each
+        cycle moves the rows the NEXT cycle reads: its depth, not the maximum)."""
+        v = C.c_int64()
+        N.call("heat2d_solver_halo_rows", self._h, int(bool(reset)), C.byref(v))
+        return v.value
+
+    @property
+    def ghost_rows(self) -> int:
+        """Valid ghost rows of the current field (the last exchange's depth)."""
+        v = C.c_int32()
+        N.call("heat2d_solver_ghost_rows", self._h, C.byref(v))
+        return v.value
+
     @property
     def plans_made(self) -> int:
         """Split plans made so far (each the first use of a depth; autotuned on

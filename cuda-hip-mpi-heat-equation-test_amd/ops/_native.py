@@ -105,6 +105,7 @@ EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_
                           C.c_int64, C.c_int32)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int32, C.c_int32)
 BARRIER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
 
 _P = C.c_void_p
 _I64 = C.c_int64
@@ -147,6 +148,8 @@ _SIGS = {
     "heat2d_transport_callback": (C.c_int, [EXCHANGE_FN, ALLREDUCE_FN, BARRIER_FN, _P, C.c_int, C.c_int,
                                             C.POINTER(_P)]),
     "heat2d_transport_free": (C.c_int, [_P]),
+    "heat2d_transport_ipc": (C.c_int, [ALLGATHER_FN, ALLREDUCE_FN, BARRIER_FN, _P, C.c_int, C.c_int, C.c_int,
+                                       C.POINTER(_P)]),
     "heat2d_solver_create": (C.c_int, [C.POINTER(Config), _P, C.POINTER(_P)]),
     "heat2d_solver_free": (C.c_int, [_P]),
     "heat2d_solver_init": (C.c_int, [_P, C.POINTER(IcParams), _P, _P]),
@@ -178,6 +181,10 @@ _SIGS = {
     "heat2d_solver_schedule": (C.c_int, [_P, _I64, C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64)]),
     "heat2d_write_xyz": (C.c_int, [C.c_char_p, C.c_int, _P, _I64, _I64, _I64, _P, _P, C.c_int]),
     "heat2d_write_npy": (C.c_int, [C.c_char_p, C.c_int, _P, _I64, _I64, _I64]),
+    "heat2d_solver_step_cycles": (C.c_int, [_P, _I64, C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64)]),
+    "heat2d_solver_halo_rows": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int64)]),
+    "heat2d_solver_ghost_rows": (C.c_int, [_P, C.POINTER(C.c_int32)]),
+    "heat2d_autotune_slabs": (C.c_int, [_I64, _I64, C.c_int, C.c_int, C.POINTER(C.c_int32)]),
 }
 
 _lib = None
@@ -267,6 +274,14 @@ def plan_split(dtype: int, layout: Layout, k: int, band: int) -> SplitPlan:
     out = SplitPlan()
     call("heat2d_plan_split", dtype, C.byref(layout), k, band, C.byref(out))
     return out
+
+
+def autotune_slabs(n_rows: int, n_cols: int, nranks: int, autotune: int = -1) -> bool:
+    """Whether a decomposition's slabs are autotuned and run measured schedules
+    (decided from the global problem: identical on every rank)."""
+    out = C.c_int32()
+    call("heat2d_autotune_slabs", n_rows, n_cols, nranks, autotune, C.byref(out))
+    return bool(out.value)
 
 
 def max_tb() -> int:

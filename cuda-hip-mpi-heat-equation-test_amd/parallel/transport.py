@@ -14,6 +14,12 @@ Here a transport is a native object the solver calls once per cycle:
 * :class:`TorchDistTransport` — host callbacks over ``torch.distributed`` point-to-point
   (gloo on CPU): runs the *same native schedule* in CPU-only multi-process CI.
 * :class:`CallbackTransport` — any Python callables (tests, custom fabrics).
+* :class:`IpcTransport` — process per GPU WITHOUT RCCL: the neighbours' fields are
+  mapped once through hipIpc handles and halos are pulled by device copies on the
+  solver's exchange stream, ordered by stream-side counters in host-shared memory
+  (csrc/runtime/ipc_transport.cpp, kernels/ipc_sync.hip); capturable into hipGraphs.
+  Host collectives over ``torch.distributed`` (gloo), so several processes may
+  share one GPU (``bench.py --transport peer --share-gpu``).
 """
 from __future__ import annotations
 
@@ -197,6 +203,66 @@ class TorchDistTransport(CallbackTransport):
             dist.barrier(group=group)
 
         super().__init__(rank, size, exchange, allreduce, barrier, name="torch-dist")
+
+
+def _dist_ops(group):
+    """allgather(bytes) / allreduce(doubles) / barrier over torch.distributed as
+    native callbacks (CPU tensors on gloo, device tensors on nccl)."""
+    import torch
+    import torch.distributed as dist
+    size = dist.get_world_size(group)
+    dev = (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl"
+           else torch.device("cpu"))
+
+    def ag(ctx, mine, out, nbytes):
+        try:
+            t = torch.frombuffer(bytearray(C.string_at(mine, nbytes)), dtype=torch.uint8).to(dev)
+            outs = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(size)]
+            dist.all_gather(outs, t, group=group)
+            buf = b"".join(bytes(o.cpu().numpy().tobytes()) for o in outs)
+            C.memmove(out, buf, len(buf))
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    def ar(ctx, vals, n, op):
+        try:
+            t = torch.from_numpy(np.ctypeslib.as_array(vals, shape=(n,)).copy()).to(dev)
+            rop = {0: dist.ReduceOp.SUM, 1: dist.ReduceOp.MAX, 2: dist.ReduceOp.MIN}[int(op)]
+            dist.all_reduce(t, op=rop, group=group)
+            np.ctypeslib.as_array(vals, shape=(n,))[:] = t.cpu().numpy()
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    def br(ctx):
+        try:
+            dist.barrier(group=group)
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    return N.ALLGATHER_FN(ag), N.ALLREDUCE_FN(ar), N.BARRIER_FN(br)
+
+
+class IpcTransport(Transport):
+    """Process per GPU (or processes sharing one GPU) without RCCL: halos pulled
+    out of the neighbours' fields through hipIpc mappings, ordered on the
+    stream by counters in host-shared memory (no host wait per cycle), and
+    capturable into hipGraphs. The fields are mapped when the solver is built
+    (Transport.attach, collective). Host collectives: ``torch.distributed``."""
+
+    def __init__(self, device: int, group=None):
+        import torch.distributed as dist
+        rank, size = dist.get_rank(group), dist.get_world_size(group)
+        self._cbs = _dist_ops(group)  # keep the CFUNCTYPE objects alive
+        h = C.c_void_p()
+        N.call("heat2d_transport_ipc", self._cbs[0], self._cbs[1], self._cbs[2], None, rank, size, device,
+               C.byref(h))
+        super().__init__(h, rank, size, "ipc")
 
 
 def default_transport(backend: str, device: Optional[int] = None) -> Transport:

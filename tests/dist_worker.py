@@ -43,7 +43,8 @@ def main():
     if backend == "hip":
         torch.cuda.set_device(0)
     tr = TorchDistTransport()
-    s = HeatSolver(prob, dtype=args.get("dtype", "fp64"), backend=backend, tb=args.get("tb", 8),
+    tb = args.get("tb_rank", {}).get(str(rank), args.get("tb", 8))  # per-rank override: a deliberate mismatch
+    s = HeatSolver(prob, dtype=args.get("dtype", "fp64"), backend=backend, tb=tb,
                    overlap=args.get("overlap", True), transport=tr, device=0 if backend == "hip" else None)
     if args.get("random"):  # non-trivial data everywhere: a stale halo cannot hide
         from heat2d.models import reference as R
@@ -52,18 +53,38 @@ def main():
         s.upload(R.owned(T0)[lay.row0:lay.row0 + lay.nrows])
     # split the stepping to exercise restarts of the cycle schedule
     first = args["steps"] // 3
+    if args.get("prepare"):  # collective: the ranks agree on step(first)'s cycles / exchange depths
+        try:
+            s.prepare(first)
+        except Exception as e:  # noqa: BLE001 - the test inspects the message
+            with open(os.path.join(outdir, f"err{rank}.txt"), "w") as f:
+                f.write(str(e))
+            s.close()
+            dist.barrier()
+            dist.destroy_process_group()
+            return
+    s.halo_rows_exchanged(reset=True)
+    seqs = [s.step_cycles(first)]
     s.step(first)
     if args.get("die_rank") == rank:  # failure injection: this rank dies mid-run (tests/test_watchdog.py)
         s.step(args.get("die_after", 0))
         sys.stdout.flush()
         os._exit(3)
     # the rest with the global statistics + one-step residual of the final field
-    st = s.step_stats(args["steps"] - first)
+    seqs.append(s.step_cycles(args["steps"] - first))
+    ghost_before = s.ghost_rows
+    if args.get("plain_step"):  # step() itself (step_stats on the CPU twin runs n-1 + 1 steps)
+        s.step(args["steps"] - first)
+        st = s.stats()
+    else:
+        st = s.step_stats(args["steps"] - first)
+    halo = s.halo_rows_exchanged()
     full = s.gather()
     if rank == 0:
         np.save(os.path.join(outdir, "result.npy"), full)
         with open(os.path.join(outdir, "stats.json"), "w") as f:
-            json.dump({"stats": st, "info": {k: v for k, v in s.info().items() if k != "layout"}}, f)
+            json.dump({"stats": st, "info": {k: v for k, v in s.info().items() if k != "layout"}, "seqs": seqs,
+                       "halo_rows": halo, "ghost_before": ghost_before, "ghost_after": s.ghost_rows}, f)
     s.close()
     dist.barrier()
     dist.destroy_process_group()

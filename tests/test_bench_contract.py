@@ -78,3 +78,51 @@ def test_bench_refuses_missing_gpus():
                        capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode != 0 and p.stdout.strip() == ""
     assert "GPU(s) visible" in p.stderr
+
+
+def run_plain(*args, timeout=600):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_share_gpu_needs_peer():
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode != 0 and "--share-gpu needs --transport peer" in p.stderr
+
+
+def test_bench_reports_halo_traffic_cpu():
+    """Halo bytes of the timed region: each exchange moves the next cycle's depth (whole padded rows)."""
+    d = run_plain("--backend", "cpu", "--gpus", "2", "--grid", "100", "--steps", "16", "--warmup", "4", "--tb", "4")
+    cyc = sum(d["config"]["cycles"].values())
+    assert d["halo_bytes"] > 0 and d["halo_bytes_per_cycle"] == pytest.approx(d["halo_bytes"] / cyc, rel=1e-3)
+    # 4 cycles of depth 4, two messages (one per rank), 4 rows of a 192-element (pitch) fp64 row each
+    assert d["halo_bytes"] == 4 * 2 * 4 * 192 * 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,steps", [("fp64", 40), ("fp32", 37)])
+def test_bench_ipc_transport_share_gpu_matches_one_rank(dtype, steps):
+    """`bench.py --gpus 4 --share-gpu --transport peer`: four rank PROCESSES on the
+    one GPU, fields mapped through hipIpc handles, halos pulled by device copies
+    ordered by stream-side counters (no RCCL), cycles replayed from hipGraphs —
+    the exact multi-process bench path on a 1-GPU box. The field statistics
+    equal the 1-rank run's exactly (sum, min, max; the sum is all-reduced, so
+    compared to 1e-12)."""
+    common = ["--grid", "8192", "--steps", str(steps), "--warmup", "5", "--check", "--dtype", dtype]
+    one = run_plain("--gpus", "1", *common)
+    four = run_plain("--gpus", "4", "--share-gpu", "--transport", "peer", *common)
+    assert four["config"]["transport"] == "ipc" and four["config"]["graph"] is True
+    assert four["config"]["parallelism"] == "slab4-shared-gpu"
+    a, b = one["field_stats"], four["field_stats"]
+    assert a["min"] == b["min"] and a["max"] == b["max"]
+    assert b["sum"] == pytest.approx(a["sum"], rel=1e-12, abs=0)
+    assert four["halo_bytes"] > 0

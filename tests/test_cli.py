@@ -169,10 +169,11 @@ def test_cli_peer_transport_bitwise(cli, gpu, tmp_path, extra):
 
 
 @pytest.mark.gpu
-def test_cli_peer_transport_eight_ranks_autotuned(cli, gpu, tmp_path):
-    """8 rank threads on one GPU, a grid big enough for the autotuner and the
-    measured schedules (4200^2 > 2^24 points): many cycles of real host
-    concurrency through the peer transport's waits, bitwise the golden."""
+def test_cli_peer_transport_eight_ranks(cli, gpu, tmp_path):
+    """8 rank threads on one GPU (525-row slabs: below the 2^24-point autotune
+    threshold, so balanced cycles; the forced-autotune run with prepare()'s
+    collective measured schedule is tests/test_collective.py): many cycles of
+    real host concurrency through the peer transport's waits, bitwise the golden."""
     (tmp_path / "input.dat").write_text("4200 0.25 0.05 1.0 75 0\n")
     run_cli(tmp_path, "--gpus", "8", "--transport", "peer", "--share-gpu", "--output", "npy", "--quiet",
             "--print-every", "25", "--check-every", "25")
