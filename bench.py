@@ -259,6 +259,7 @@ def main():
     assert sum(k * c for k, c in hist.items()) == args.steps, hist
     plans, traffic = {}, 0.0
     from heat2d.utils.metrics import plan_hbm_bytes
+    from heat2d.ops import _native as N
     for k, c in sorted(hist.items()):
         pl = s.plan(k) if hip else {"k": k, "valid": 0}
         if hip:
@@ -303,6 +304,7 @@ def main():
                 "cycles": {str(k): c for k, c in sorted(hist.items())},
                 "schedule": "measured" if s.schedule(args.steps) else "balanced",
                 "prepare_s": round(prepare_s, 2),
+                "plan_cache": {"hits": s.plan_cache_hits, "path": N.plan_cache_path()} if hip else None,
                 "arith": ("fma" if N_arith(prob.r, args.arith) else "exact") + (" (auto)" if args.arith == "auto" else ""),
                 "overlap": not args.no_overlap,
                 "graph": bool(graph),

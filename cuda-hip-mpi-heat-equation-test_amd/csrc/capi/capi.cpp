@@ -13,6 +13,7 @@
 #include <string>
 
 #include "heat2d/config.hpp"
+#include "heat2d/plan_cache.hpp"
 #include "heat2d/runtime.hpp"
 #include "heat2d/watchdog.hpp"
 
@@ -456,6 +457,21 @@ int heat2d_solver_halo_rows(void* s, int reset, int64_t* out) {
 
 int heat2d_solver_ghost_rows(void* s, int32_t* out) {
   return guarded([&] { *out = static_cast<Solver*>(s)->ghost_rows(); });
+}
+
+int heat2d_solver_plan_cache_hits(void* s, int64_t* out) {
+  return guarded([&] { *out = static_cast<Solver*>(s)->plan_cache_hits(); });
+}
+
+int heat2d_plan_cache_path(char* buf, int64_t cap) {
+  return guarded([&] {
+    const std::string p = plancache::enabled() ? plancache::path() : std::string();
+    const size_t n = std::min<size_t>((size_t)std::max<int64_t>(cap - 1, 0), p.size());
+    if (cap > 0) {
+      std::memcpy(buf, p.data(), n);
+      buf[n] = 0;
+    }
+  });
 }
 
 int heat2d_autotune_slabs(int64_t n_rows, int64_t n_cols, int nranks, int autotune, int32_t* out) {

@@ -170,6 +170,9 @@ int heat2d_solver_step_cycles(void* s, int64_t n, int32_t* out, int64_t cap, int
 int heat2d_solver_halo_rows(void* s, int reset, int64_t* out);
 // Valid ghost rows of the current buffer (the last exchange's depth).
 int heat2d_solver_ghost_rows(void* s, int32_t* out);
+// Plans / schedules the solver took from the persistent plan cache; the cache file path.
+int heat2d_solver_plan_cache_hits(void* s, int64_t* out);
+int heat2d_plan_cache_path(char* buf, int64_t cap);
 // Autotune / measured-schedule eligibility of a decomposition (the same on every rank).
 int heat2d_autotune_slabs(int64_t n_rows, int64_t n_cols, int nranks, int autotune, int32_t* out);
 /* the schedule search itself on given cycle times t_ms[k] (k = 1..kmax; t_ms[0] unused): depths in out */

@@ -312,6 +312,8 @@ class Solver {
   float tuned_ms(int k) const { return k >= 0 && k <= kMaxTB ? tuned_ms_[k] : 0.f; }
   // split plans planned so far (each a first use of a depth; autotuned on big slabs)
   int64_t plans_made() const { return plans_made_; }
+  // plans and schedules taken from the persistent plan cache (plan_cache.hpp)
+  int64_t plan_cache_hits() const { return plan_cache_hits_; }
   int spare_waves() const;
   // Phase timers (hipEvents on the GPU timeline) for every cycle while
   // enabled: [main ms, edge ms, exchange ms, whole-cycle ms (serial schedule),
@@ -350,6 +352,11 @@ class Solver {
   void capture_schedule(int64_t n);
   float time_trial_schedule(const std::vector<int>& sc);  // ms of one graph replay of sc's trial cycles
   void prepare_plans(int64_t n);  // prepare()'s planning / autotune / measured schedule (HIP split engine)
+  float time_plan(const kern::SplitPlan& c, int kTimed);  // steady-state ms per trial cycle
+  std::string cache_ctx() const;   // plan-cache key of this slab (plan_cache.hpp)
+  std::string sched_ctx() const;   // ... of the decomposition's schedules
+  bool cached_split(int k);        // plan of depth k from the cache, re-validated
+  bool cached_schedule(int64_t n); // measured schedule of n steps from the cache (collective)
   void run_schedule_graph(int64_t n);
   float depth_ms(int k);
   std::vector<int> choose_schedule(int64_t n);
@@ -399,6 +406,8 @@ class Solver {
   kern::SplitPlan split_[kMaxTB + 1] = {};  // per temporal depth (k == 0: not planned yet)
   float tuned_ms_[kMaxTB + 1] = {};           // autotuned cycle time (ms), 0 if not tuned
   int64_t plans_made_ = 0;
+  int64_t plan_cache_hits_ = 0;
+  hipEvent_t ev_t0_ = nullptr, ev_t1_ = nullptr;  // time_plan
   hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K
   int graph_k_ = 0;
   std::vector<char> host_stage_;  // CPU-backend / callback staging

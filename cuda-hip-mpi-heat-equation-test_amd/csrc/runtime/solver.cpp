@@ -36,6 +36,7 @@
 #include <cstring>
 #include <vector>
 
+#include "heat2d/plan_cache.hpp"
 #include "heat2d/runtime.hpp"
 
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -178,6 +179,8 @@ Solver::~Solver() {
     if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
     if (ev_int_) (void)hipEventDestroy(ev_int_);
+    if (ev_t0_) (void)hipEventDestroy(ev_t0_);
+    if (ev_t1_) (void)hipEventDestroy(ev_t1_);
     for (auto* v : {&phase_ev_, &phase_pool_})
       for (auto& pe : *v)
         for (auto& e : pe.ev) (void)hipEventDestroy(e);
@@ -415,7 +418,8 @@ const kern::SplitPlan& Solver::split_plan(int k) {
     p = kern::plan_split(dtype(), L_, k, k, compute_cus_, spare, 0, 0, cfg_.arith);
     p.k = k;
     ++plans_made_;
-    if (p.valid && autotune_slabs(cfg_.n_rows, cfg_.n_cols, tr_->size(), cfg_.autotune)) autotune_split(k);
+    if (p.valid && autotune_slabs(cfg_.n_rows, cfg_.n_cols, tr_->size(), cfg_.autotune) && !cached_split(k))
+      autotune_split(k);
     // HEAT2D_SPLIT_ORDER=edge-first | concurrent overrides the split's ordering (tests, A/B);
     // HEAT2D_SPLIT_ORDER=single forces one general launch per cycle (no exchange only)
     if (const char* env = std::getenv("HEAT2D_SPLIT_ORDER")) {
@@ -516,28 +520,75 @@ void Solver::trial_cycle(const kern::SplitPlan& c) {
   H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
 }
 
+// Steady-state ms per cycle of plan c: one warm-up trial cycle, then
+// kTimed back-to-back trial cycles between two events (both streams, the real
+// event protocol, no exchange; the solution is untouched).
+float Solver::time_plan(const kern::SplitPlan& c, int kTimed) {
+  constexpr int kWarm = 1;
+  if (!ev_t0_) {
+    H2D_HIP(hipEventCreate(&ev_t0_));
+    H2D_HIP(hipEventCreate(&ev_t1_));
+  }
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+  for (int i = 0; i < kWarm; ++i) trial_cycle(c);
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+  H2D_HIP(hipEventRecord(ev_t0_, s_compute_));
+  for (int i = 0; i < kTimed; ++i) trial_cycle(c);
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+  H2D_HIP(hipEventRecord(ev_t1_, s_compute_));
+  H2D_HIP(hipEventSynchronize(ev_t1_));
+  float ms = 0.f;
+  H2D_HIP(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));
+  return ms / kTimed;
+}
+
+// Plan-cache context of this slab: what a tuned plan's timing depends on
+// besides the depth (plan_cache.hpp).
+std::string Solver::cache_ctx() const {
+  hipDeviceProp_t prop{};
+  std::string arch = "unknown";
+  int ncu = 0;
+  if (hipGetDeviceProperties(&prop, cfg_.device) == hipSuccess) {
+    arch = prop.gcnArchName;
+    ncu = prop.multiProcessorCount;
+  }
+  const int pos = (L_.row0 == 0 ? 1 : 0) | (L_.row0 + L_.nrows == L_.nrows_global ? 2 : 0);
+  char b[512];
+  std::snprintf(b, sizeof(b), "%s|cu%d|%s|ar%d|%lldx%lld|p%lld|h%lld|pos%d|ccu%d|sp%d|x%d", arch.c_str(), ncu,
+                dtype_name(dtype()), cfg_.arith, (long long)L_.nrows, (long long)L_.ncols, (long long)L_.pitch,
+                (long long)L_.halo, pos, compute_cus_, spare_waves(), tr_->exchanges() ? 1 : 0);
+  return b;
+}
+
+// The cached autotuned plan of depth k for this slab, re-validated by one
+// short re-time (5 trial cycles): kept if within 10 % of the cached time.
+bool Solver::cached_split(int k) {
+  if (!hip_ || !plancache::enabled()) return false;
+  kern::SplitPlan c{};
+  float ms = 0.f;
+  if (!plancache::get_plan(cache_ctx(), k, k, &c, &ms) || ms <= 0.f) return false;
+  // geometry must match this slab (defensive: the key already pins it)
+  const kern::SplitPlan fresh = kern::plan_split(dtype(), L_, k, k, compute_cus_, spare_waves(), c.ring,
+                                                 c.main.nb, cfg_.arith);
+  if (!c.valid || (c.valid != 2 && !fresh.valid) || c.main.r1 > L_.nrows || c.nedge > 4) return false;
+  synchronize();
+  const float t = time_plan(c, 4);
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+  synchronize();
+  if (std::fabs(t - ms) > 0.10f * ms) return false;
+  c.k = k;
+  split_[k] = c;
+  tuned_ms_[k] = t;
+  ++plan_cache_hits_;
+  return true;
+}
+
 void Solver::autotune_split(int k) {
   const int spare = spare_waves();
   synchronize();
-  hipEvent_t e0, e1;
-  H2D_HIP(hipEventCreate(&e0));
-  H2D_HIP(hipEventCreate(&e1));
-  auto run_cycle = [&](const kern::SplitPlan& c) { trial_cycle(c); };
-  auto time_plan = [&](const kern::SplitPlan& c, int kTimed) {
-    constexpr int kWarm = 1;
-    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
-    for (int i = 0; i < kWarm; ++i) run_cycle(c);
-    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
-    H2D_HIP(hipEventRecord(e0, s_compute_));
-    for (int i = 0; i < kTimed; ++i) run_cycle(c);
-    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
-    H2D_HIP(hipEventRecord(e1, s_compute_));
-    H2D_HIP(hipEventSynchronize(e1));
-    float ms = 0.f;
-    H2D_HIP(hipEventElapsedTime(&ms, e0, e1));
-    return ms / kTimed;
-  };
+  auto time_plan = [&](const kern::SplitPlan& c, int kTimed) { return this->time_plan(c, kTimed); };
   // pass 1: every candidate over 4 steady-state cycles; pass 2: the 4 fastest
   // re-timed over 12 cycles each (the spread between the leaders is ~1-2 %,
   // about the noise of a 4-cycle sample)
@@ -604,11 +655,10 @@ void Solver::autotune_split(int k) {
     }
   }
   synchronize();
-  H2D_HIP(hipEventDestroy(e0));
-  H2D_HIP(hipEventDestroy(e1));
   best.k = k;
   split_[k] = best;
   tuned_ms_[k] = best_ms;
+  if (plancache::enabled()) plancache::put_plan(cache_ctx(), k, k, best, best_ms);
   // restore the event protocol: both streams idle, events recorded
   H2D_HIP(hipEventRecord(ev_int_, s_compute_));
   H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
@@ -849,6 +899,34 @@ bool Solver::measured_schedules() const {
   if (!hip_ || !cfg_.overlap || cfg_.copy_swap || jit_) return false;
   if (cfg_.use_graph && tr_->exchanges() && !tr_->capturable()) return false;  // graphs of the pair kind
   return autotune_slabs(cfg_.n_rows, cfg_.n_cols, tr_->size(), cfg_.autotune);
+}
+
+std::string Solver::sched_ctx() const {
+  // the schedule is the ranks' common choice: the whole decomposition is its key
+  return cache_ctx() + "|P" + std::to_string(tr_->size()) + "|N" + std::to_string(cfg_.n_rows) + "|kmax" +
+         std::to_string(cfg_.tb) + "|g" + std::to_string(schedule_graphs() ? 1 : 0);
+}
+
+// A cached measured schedule for step(n), used only if EVERY rank has the
+// same one (min/max of its hash all-reduced): a hit on some ranks only must
+// not let them skip the collectives of the schedule search the others run.
+bool Solver::cached_schedule(int64_t n) {
+  if (!hip_ || !plancache::enabled()) return false;
+  std::vector<int> s;
+  const bool hit = plancache::get_schedule(sched_ctx(), n, &s);
+  uint64_t h = 1469598103934665603ull;
+  for (int d : s) h = (h ^ (uint64_t)d) * 1099511628211ull;
+  const double hv = (double)(h >> 12);
+  if (tr_->exchanges() && tr_->collective()) {
+    double v[3] = {hit ? 1.0 : 0.0, hv, -hv};
+    tr_->allreduce(v, 3, 2);  // min
+    if (v[0] != 1.0 || v[1] != -v[2]) return false;
+  } else if (!hit) {
+    return false;
+  }
+  sched_[n] = std::move(s);
+  ++plan_cache_hits_;
+  return true;
 }
 
 bool autotune_slabs(int64_t n_rows, int64_t n_cols, int nranks, int autotune) {
@@ -1132,6 +1210,10 @@ void Solver::prepare(int64_t n) {
 }
 
 void Solver::prepare_plans(int64_t n) {
+  if (measured_schedules() && !sched_.count(n) && cached_schedule(n)) {
+    // plans of the cached schedule's depths (cached too: re-validated, else re-tuned)
+    for (int k : sched_.at(n)) (void)split_plan(k);
+  }
   if (measured_schedules() && !sched_.count(n)) {
     std::vector<int> s = choose_schedule(n);
     // Short graph-replayed runs: the per-depth estimates of near-tied
@@ -1155,7 +1237,10 @@ void Solver::prepare_plans(int64_t n) {
         }
       }
     }
-    if (!s.empty()) sched_[n] = std::move(s);
+    if (!s.empty()) {
+      if (plancache::enabled()) plancache::put_schedule(sched_ctx(), n, s);
+      sched_[n] = std::move(s);
+    }
   }
   if (schedule(n) && schedule_graphs()) {
     // both buffer parities (a warmup between prepare and step(n) may flip it);

@@ -223,6 +223,13 @@ class HeatSolver:
         return v.value
 
     @property
+    def plan_cache_hits(self) -> int:
+        """Plans / schedules taken from the persistent plan cache (re-validated by one re-time)."""
+        v = C.c_int64()
+        N.call("heat2d_solver_plan_cache_hits", self._h, C.byref(v))
+        return v.value
+
+    @property
     def ghost_rows(self) -> int:
         """Valid ghost rows of the current field (the last exchange's depth)."""
         v = C.c_int32()

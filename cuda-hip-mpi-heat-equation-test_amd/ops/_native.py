@@ -185,6 +185,8 @@ _SIGS = {
     "heat2d_solver_halo_rows": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int64)]),
     "heat2d_solver_ghost_rows": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "heat2d_autotune_slabs": (C.c_int, [_I64, _I64, C.c_int, C.c_int, C.POINTER(C.c_int32)]),
+    "heat2d_solver_plan_cache_hits": (C.c_int, [_P, C.POINTER(C.c_int64)]),
+    "heat2d_plan_cache_path": (C.c_int, [C.c_char_p, _I64]),
 }
 
 _lib = None
@@ -282,6 +284,13 @@ def autotune_slabs(n_rows: int, n_cols: int, nranks: int, autotune: int = -1) ->
     out = C.c_int32()
     call("heat2d_autotune_slabs", n_rows, n_cols, nranks, autotune, C.byref(out))
     return bool(out.value)
+
+
+def plan_cache_path() -> str:
+    """The persistent plan cache file ("" when disabled: HEAT2D_PLAN_CACHE=off)."""
+    buf = C.create_string_buffer(4096)
+    call("heat2d_plan_cache_path", buf, 4096)
+    return buf.value.decode()
 
 
 def max_tb() -> int:

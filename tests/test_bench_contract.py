@@ -126,3 +126,23 @@ def test_bench_ipc_transport_share_gpu_matches_one_rank(dtype, steps):
     assert a["min"] == b["min"] and a["max"] == b["max"]
     assert b["sum"] == pytest.approx(a["sum"], rel=1e-12, abs=0)
     assert four["halo_bytes"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_plan_cache_second_run(tmp_path):
+    """Persistent plan cache: the second identical bench run takes its split
+    plans and measured schedule from the cache (each re-validated by one short
+    re-time) — prepare() under a second, the same throughput."""
+    env_cache = str(tmp_path / "plans.txt")
+    os.environ["HEAT2D_PLAN_CACHE"] = env_cache
+    try:
+        args = ["--gpus", "1", "--grid", "8192", "--steps", "20", "--warmup", "5"]
+        first = run_plain(*args)
+        second = run_plain(*args)
+    finally:
+        os.environ.pop("HEAT2D_PLAN_CACHE", None)
+    assert first["config"]["plan_cache"]["path"] == env_cache and os.path.getsize(env_cache) > 0
+    assert first["config"]["plan_cache"]["hits"] == 0 and second["config"]["plan_cache"]["hits"] >= 2
+    assert second["config"]["prepare_s"] < 1.0, second["config"]
+    assert second["config"]["cycles"] == first["config"]["cycles"]
+    assert second["value"] == pytest.approx(first["value"], rel=0.05)
