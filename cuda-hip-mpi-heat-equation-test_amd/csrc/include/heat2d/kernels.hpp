@@ -83,6 +83,24 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int rin
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith = 0);
 
+// Persistent multi-cycle launch (tb_impl.hpp tb_persist_kernel): `ncycles`
+// cycles of depth plan.k over the whole slab in ONE cooperative dispatch, one
+// co-resident wave per item of a single-launch plan (plan_single), items
+// synchronised by per-item completion counters instead of kernel boundaries.
+// alternate = 1: cycle c reads buffer c & 1 and writes the other (the real
+// loop: the result lands in buf0 / buf1 by the parity of ncycles); 0: every
+// cycle buf0 -> buf1 (timing trials; buf0 untouched).
+struct PersistCtl {
+  uint32_t* done;          // device, >= nitems_cap counters
+  int64_t nitems_cap;
+  uint32_t base;           // the counters' value at launch (advance by ncycles after each launch)
+  uint64_t timeout_ticks;  // a dependency wait longer than this fails the launch (*err = 1)
+  unsigned int* err;       // host-visible
+};
+int64_t persist_capacity(DType dt, int ring, int k, int arith);  // co-resident waves of the persistent kernel
+void launch_tb_persist(DType dt, void* buf0, void* buf1, const SlabLayout& L, const SplitPlan& plan, double r,
+                       const PersistCtl& ctl, int ncycles, int alternate, hipStream_t stream, int arith = 0);
+
 // Initial / boundary condition kinds (covers every IC of the reference
 // variants, see models/presets.py for the mapping).
 enum class IcKind : int32_t {

@@ -314,6 +314,11 @@ class Solver {
   int64_t plans_made() const { return plans_made_; }
   // plans and schedules taken from the persistent plan cache (plan_cache.hpp)
   int64_t plan_cache_hits() const { return plan_cache_hits_; }
+  // step(n) runs as persistent multi-cycle launches (prepare() decided)
+  bool persistent(int64_t n) const {
+    auto it = persist_.find(n);
+    return it != persist_.end() && it->second;
+  }
   int spare_waves() const;
   // Phase timers (hipEvents on the GPU timeline) for every cycle while
   // enabled: [main ms, edge ms, exchange ms, whole-cycle ms (serial schedule),
@@ -357,6 +362,15 @@ class Solver {
   std::string sched_ctx() const;   // ... of the decomposition's schedules
   bool cached_split(int k);        // plan of depth k from the cache, re-validated
   bool cached_schedule(int64_t n); // measured schedule of n steps from the cache (collective)
+  // Persistent multi-cycle launches (kern::launch_tb_persist): single-rank
+  // runs of many short cycles (small grids), one dispatch per run of equal
+  // depths instead of a launch (or graph node) per cycle. HEAT2D_PERSIST:
+  // 0 off, 1 on where possible, unset = auto (prepare() times both).
+  bool persist_eligible() const;
+  const kern::SplitPlan* persist_plan(int k);  // nullptr: too many items to be co-resident
+  void ensure_persist_ctl();
+  void run_persist(const std::vector<int>& seq, bool trial);
+  float time_persist(const std::vector<int>& seq);  // ms of one trial run (solution untouched)
   void run_schedule_graph(int64_t n);
   float depth_ms(int k);
   std::vector<int> choose_schedule(int64_t n);
@@ -407,6 +421,14 @@ class Solver {
   float tuned_ms_[kMaxTB + 1] = {};           // autotuned cycle time (ms), 0 if not tuned
   int64_t plans_made_ = 0;
   int64_t plan_cache_hits_ = 0;
+  int persist_mode_ = -1;                 // HEAT2D_PERSIST (-1 auto, 0 off, 1 on)
+  std::map<int64_t, bool> persist_;       // step(n) runs persistent launches (decided in prepare)
+  kern::SplitPlan persist_plans_[kMaxTB + 1] = {};
+  uint32_t* d_done_ = nullptr;            // persistent launches: per-item counters
+  int64_t done_cap_ = 0;
+  uint32_t done_base_ = 0;
+  unsigned int* h_err_ = nullptr;         // pinned, host-visible error word of the persistent kernel
+  uint64_t persist_timeout_ticks_ = 0;
   hipEvent_t ev_t0_ = nullptr, ev_t1_ = nullptr;  // time_plan
   hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K
   int graph_k_ = 0;

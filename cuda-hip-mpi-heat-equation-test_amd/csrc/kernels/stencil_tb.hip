@@ -359,6 +359,73 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   return p;
 }
 
+int64_t persist_capacity(DType dt, int ring, int k, int arith) {
+  HEAT2D_REQUIRE(ring == 4 || ring == 6, "ring must be 4 or 6");
+  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 or 1");
+  int bpc;
+  if (dt == DType::F32)
+    bpc = ring == 4 ? (arith ? occupancy_persist<float, 4, 1>(k) : occupancy_persist<float, 4, 0>(k))
+                    : (arith ? occupancy_persist<float, 6, 1>(k) : occupancy_persist<float, 6, 0>(k));
+  else
+    bpc = ring == 4 ? (arith ? occupancy_persist<double, 4, 1>(k) : occupancy_persist<double, 4, 0>(k))
+                    : (arith ? occupancy_persist<double, 6, 1>(k) : occupancy_persist<double, 6, 0>(k));
+  return (int64_t)cu_count() * bpc * 4;
+}
+
+void launch_tb_persist(DType dt, void* buf0, void* buf1, const SlabLayout& L, const SplitPlan& plan, double r,
+                       const PersistCtl& ctl, int ncycles, int alternate, hipStream_t stream, int arith) {
+  const int k = plan.k;
+  check_layout(dt, L, k);
+  HEAT2D_REQUIRE(plan.valid == 2, "the persistent launch runs a single-launch plan (plan_single)");
+  HEAT2D_REQUIRE(ncycles >= 1, "ncycles >= 1");
+  const TbRect& R = plan.main;
+  HEAT2D_REQUIRE(R.r0 == 0 && R.r1 == L.nrows && R.nb != 0 && R.s1 > R.s0, "persistent plan must cover the slab");
+  TbArgs a{};
+  a.pitch = L.pitch;
+  a.ncols = L.ncols;
+  a.col_lo = -L.cpad;
+  a.col_hi = L.col_hi();
+  a.fixed_lo = -L.row0;
+  a.fixed_hi = L.nrows_global - L.row0;
+  a.nrect = 1;
+  a.rect[0] = TbRectArg{R.r0, R.r1, R.s0, R.s1, R.nb, 0};
+  const int64_t rows = R.r1 - R.r0, ns = R.s1 - R.s0;
+  HEAT2D_REQUIRE(R.nb > 0 || -R.nb <= rows * ns, "more segments than strip rows");
+  HEAT2D_REQUIRE(rows * ns < (int64_t(1) << 31), "rect exceeds 2^31 strip rows");
+  a.nitems = R.nb > 0 ? R.nb * ns : -R.nb;
+  a.nwaves = a.nitems;
+  // every item's wave must be resident at once (they wait on each other)
+  HEAT2D_REQUIRE(a.nitems <= persist_capacity(dt, plan.ring, k, arith) && a.nitems <= ctl.nitems_cap,
+                 "persistent launch: more items than co-resident waves / counters");
+  PersistArgs p{};
+  p.done = ctl.done;
+  p.base = ctl.base;
+  p.ncycles = ncycles;
+  p.alternate = alternate;
+  p.timeout_ticks = ctl.timeout_ticks;
+  p.err = ctl.err;
+  const unsigned nblocks = (unsigned)((a.nitems + 3) / 4);
+  const int64_t o = L.origin();
+  hipError_t e;
+  if (dt == DType::F32) {
+    float* f0 = static_cast<float*>(buf0) + o;
+    float* f1 = static_cast<float*>(buf1) + o;
+    const float rf = (float)r;
+    if (plan.ring == 4) e = arith ? dispatch_persist<float, 4, 1>(k, nblocks, f0, f1, a, rf, p, stream)
+                                  : dispatch_persist<float, 4, 0>(k, nblocks, f0, f1, a, rf, p, stream);
+    else e = arith ? dispatch_persist<float, 6, 1>(k, nblocks, f0, f1, a, rf, p, stream)
+                   : dispatch_persist<float, 6, 0>(k, nblocks, f0, f1, a, rf, p, stream);
+  } else {
+    double* d0 = static_cast<double*>(buf0) + o;
+    double* d1 = static_cast<double*>(buf1) + o;
+    if (plan.ring == 4) e = arith ? dispatch_persist<double, 4, 1>(k, nblocks, d0, d1, a, r, p, stream)
+                                  : dispatch_persist<double, 4, 0>(k, nblocks, d0, d1, a, r, p, stream);
+    else e = arith ? dispatch_persist<double, 6, 1>(k, nblocks, d0, d1, a, r, p, stream)
+                   : dispatch_persist<double, 6, 0>(k, nblocks, d0, d1, a, r, p, stream);
+  }
+  if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("persistent launch: ") + hipGetErrorString(e));
+}
+
 int64_t max_stats_waves() { return (int64_t)cu_count() * 32; }  // 8 x 256-thread blocks per CU
 
 void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, int k, double r, double* partials,

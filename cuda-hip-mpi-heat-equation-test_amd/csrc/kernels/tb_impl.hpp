@@ -894,6 +894,185 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
   }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent multi-cycle launch (small grids / short cycles).
+//
+// One dispatch runs `ncycles` cycles of depth K over the whole slab: exactly
+// one wave per work item, all co-resident (cooperative launch), each wave
+// marching ITS item in every cycle. Between cycles there is no kernel
+// boundary: an item of cycle c waits only for the items of cycle c - 1 whose
+// output its own cycle reads (the K rows above and below it in its strip and
+// the two neighbour strips: read-after-write on the source) — which are also
+// the only items that read the rows its cycle overwrites (write-after-read on
+// the destination). Per item a completion counter (`done`, epoch-based: it
+// holds base + cycles completed) is published with an agent-scope release
+// after the item's stores, and read with an agent-scope acquire. This removes
+// the per-cycle dispatch ramp / drain and the inter-launch gap (~11 + 8-10 us
+// of a ~61 us 4096^2 fp32 cycle, profiles/small_grid/README.md): a wave starts
+// cycle c + 1 as soon as its neighbourhood is done, a wavefront through the
+// grid instead of a grid-wide barrier. A wait that exceeds timeout_ticks of
+// the wall clock (a wave that never ran: not co-resident) sets *err and the
+// wave returns — the launch fails loudly instead of hanging the GPU.
+struct PersistArgs {
+  uint32_t* done;          // per item
+  uint32_t base;           // value every item's counter holds at launch
+  int32_t ncycles;
+  int32_t alternate;       // 1: cycle c reads buf[c & 1], writes buf[(c + 1) & 1]; 0: buf0 -> buf1 each cycle (trials)
+  int32_t pad;
+  uint64_t timeout_ticks;  // wall_clock64 ticks
+  unsigned int* err;       // host-visible error word (1: a dependency wait timed out)
+};
+
+// Item of rect R holding strip-local row `row` of strip-local strip `sl`.
+__device__ __forceinline__ int64_t item_of(const TbRectArg& R, int64_t sl, int64_t row) {
+  const int64_t rows = R.r1 - R.r0, ns = R.s1 - R.s0;
+  if (R.nb > 0) return R.item0 + ((row + 1) * R.nb - 1) / rows * ns + sl;  // band-major (tb_span)
+  const int64_t total = ns * rows, nseg = -R.nb, lin = sl * rows + row;
+  return R.item0 + ((lin + 1) * nseg - 1) / total;
+}
+
+__device__ __forceinline__ bool wait_item(const PersistArgs& p, int64_t j, uint32_t target, uint64_t t_start) {
+  while ((int32_t)(__hip_atomic_load(&p.done[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+    if (wall_clock64() - t_start > p.timeout_ticks) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+// Wait until every item whose cycle-(c-1) output the piece (strip, rows
+// [t0, t1)) reads — rows [t0 - K, t1 + K) of strips strip - 1 .. strip + 1 —
+// has counter >= target. Single-rect launches (plan_single).
+template <int K>
+__device__ bool wait_piece(const TbArgs& a, const PersistArgs& p, int64_t self, int64_t strip, int64_t t0, int64_t t1,
+                           uint32_t target, uint64_t t_start) {
+  const TbRectArg R = a.rect[0];
+  const int64_t rows = R.r1 - R.r0;
+  const int64_t lo = max(t0 - K, R.r0) - R.r0, hi = min(t1 + K, R.r1) - R.r0;  // strip-local rows [lo, hi)
+  for (int64_t s = max(strip - 1, R.s0); s <= min(strip + 1, R.s1 - 1); ++s) {
+    const int64_t sl = s - R.s0;
+    if (R.nb > 0) {
+      const int64_t ns = R.s1 - R.s0;
+      const int64_t b0 = ((lo + 1) * R.nb - 1) / rows, b1 = (hi * R.nb - 1) / rows;
+      for (int64_t b = b0; b <= b1; ++b) {
+        const int64_t j = R.item0 + b * ns + sl;
+        if (j != self && !wait_item(p, j, target, t_start)) return false;
+      }
+    } else {
+      for (int64_t j = item_of(R, sl, lo); j <= item_of(R, sl, hi - 1); ++j)
+        if (j != self && !wait_item(p, j, target, t_start)) return false;
+    }
+  }
+  return true;
+}
+
+template <typename T, int NV, int K, int RING, int AR>
+__global__ __launch_bounds__(256) void tb_persist_kernel(T* __restrict__ b0, T* __restrict__ b1, TbArgs a, T r,
+                                                         PersistArgs p) {
+  using S = TbShape<T, NV, K>;
+  const int lane = threadIdx.x & 63;
+  const int64_t it = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (it >= a.nitems) return;  // one item per wave, for every cycle
+  for (int32_t c = 0; c < p.ncycles; ++c) {
+    const bool odd = p.alternate && (c & 1);
+    const T* src = odd ? b1 : b0;
+    T* dst = odd ? b0 : b1;
+    int64_t strip, t0, t1;
+    if (c > 0) {
+      const uint32_t target = p.base + (uint32_t)c;
+      const uint64_t t_start = wall_clock64();  // this cycle's waits
+      int32_t lin = tb_span(a, it).lin;
+      bool ok = true;
+      while (ok && tb_piece(a, it, lin, strip, t0, t1)) {
+        lin += (int32_t)(t1 - t0);
+        ok = wait_piece<K>(a, p, it, strip, t0, t1, target, t_start);
+      }
+      if (!ok) {
+        if (lane == 0) __hip_atomic_store(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the neighbours' stores, not stale cache lines
+    }
+    int32_t lin = tb_span(a, it).lin;
+    while (tb_piece(a, it, lin, strip, t0, t1)) {
+      lin += (int32_t)(t1 - t0);
+      const int64_t c0 = strip * S::U - S::KA;
+      const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
+                     (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
+      switch (ek) {
+        case 0: march<T, NV, K, 0, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
+        case 1: march<T, NV, K, 1, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
+        case 2: march<T, NV, K, 2, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
+        default: march<T, NV, K, 3, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this item's rows out of the XCD's L2 first
+    if (lane == 0) __hip_atomic_store(&p.done[it], p.base + (uint32_t)c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <typename T, int K, int RING, int AR>
+int persist_blocks_per_cu() {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&tb_persist_kernel<T, 1, K, RING, AR>),
+                                                   256, 0) != hipSuccess || nb <= 0)
+    nb = 1;
+  cache[dev] = nb;
+  return nb;
+}
+
+template <typename T, int K, int RING, int AR>
+hipError_t persist_launch(unsigned nblocks, T* b0, T* b1, const TbArgs& a, T r, const PersistArgs& p, hipStream_t s) {
+  TbArgs aa = a;
+  T rr = r;
+  PersistArgs pp = p;
+  void* args[] = {&b0, &b1, &aa, &rr, &pp};
+  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tb_persist_kernel<T, 1, K, RING, AR>), dim3(nblocks),
+                                    dim3(256), args, 0, s);
+}
+
+// Per-(T, RING, AR) entry points, instantiated in tb_<dtype>_r<RING>_persist[_fma].hip.
+template <typename T, int RING, int AR>
+hipError_t dispatch_persist(int k, unsigned nblocks, T* b0, T* b1, const TbArgs& a, T r, const PersistArgs& p,
+                            hipStream_t s);
+template <typename T, int RING, int AR>
+int occupancy_persist(int k);
+#define H2D_PS_CASE(T, RING, MAIN, AR, KK) \
+  case KK:                                 \
+    return persist_launch<T, KK, RING, AR>(nblocks, b0, b1, a, r, p, s);
+#define H2D_PS_OCC_CASE(T, RING, MAIN, AR, KK) \
+  case KK:                                     \
+    return persist_blocks_per_cu<T, KK, RING, AR>();
+#define H2D_PS_UNIT(T, RING, AR, DEEP)                                                                              \
+  template <>                                                                                                        \
+  hipError_t dispatch_persist<T, RING, AR>(int k, unsigned nblocks, T* b0, T* b1, const TbArgs& a, T r,              \
+                                           const PersistArgs& p, hipStream_t s) {                                    \
+    switch (k) {                                                                                                     \
+      H2D_TB_CASES(H2D_PS_CASE, T, RING, false, AR)                                                                  \
+      DEEP(H2D_PS_CASE, T, RING, false, AR)                                                                          \
+      default:                                                                                                       \
+        break;                                                                                                       \
+    }                                                                                                                \
+    HEAT2D_REQUIRE(false, "temporal depth not instantiated for the persistent kernel");                              \
+    return hipErrorInvalidValue;                                                                                     \
+  }                                                                                                                  \
+  template <>                                                                                                        \
+  int occupancy_persist<T, RING, AR>(int k) {                                                                        \
+    switch (k) {                                                                                                     \
+      H2D_TB_CASES(H2D_PS_OCC_CASE, T, RING, false, AR)                                                              \
+      DEEP(H2D_PS_OCC_CASE, T, RING, false, AR)                                                                      \
+      default:                                                                                                       \
+        break;                                                                                                       \
+    }                                                                                                                \
+    return 1;                                                                                                        \
+  }
+
 template <typename T, int NV, int K, int RING, bool MAIN, int AR, int VAR = kVarPlain>
 constexpr auto kernel_ptr() {
   return &tb_kernel<T, NV, K, RING, MAIN, AR, VAR>;

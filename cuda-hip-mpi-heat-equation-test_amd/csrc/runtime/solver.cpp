@@ -163,6 +163,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     cfg_.use_graph = 0;
   }
   tr_->attach(buf_[0], buf_[1], L_, dtype());
+  if (const char* e = std::getenv("HEAT2D_PERSIST")) persist_mode_ = std::atoi(e) != 0 ? 1 : 0;
 }
 
 Solver::~Solver() {
@@ -176,6 +177,8 @@ Solver::~Solver() {
       if (b) (void)hipFree(b);
     if (d_work_) (void)hipFree(d_work_);
     if (d_part_) (void)hipFree(d_part_);
+    if (d_done_) (void)hipFree(d_done_);
+    if (h_err_) (void)hipHostFree(h_err_);
     if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
     if (ev_int_) (void)hipEventDestroy(ev_int_);
@@ -873,6 +876,10 @@ void Solver::step(int64_t n) {
     steps_ += n;
     return;
   }
+  if (persistent(n)) {
+    run_persist(step_cycles(n), false);
+    return;
+  }
   const std::vector<CycleRun> runs = step_runs(n, cur_);
   // each cycle's exchange moves the rows the NEXT cycle reads; the last one
   // those of this call's first cycle (a repeated step(n) — bench, the CLI's
@@ -1207,6 +1214,25 @@ void Solver::prepare(int64_t n) {
   // (e.g. a shallow warmup before it): top up here, outside the timed step
   const std::vector<int> seq = step_cycles(n);
   if (!seq.empty()) topup(seq.front());
+  if (const std::vector<int>* s = schedule(n); s && hip_ && cfg_.overlap && !cfg_.copy_swap) {
+    // Leave the GPU in the schedule's steady state, last (after the
+    // agreement and the top-up): the search ends on its shallowest
+    // (HBM-bound) depths, and a VALU-bound cycle that follows HBM-bound work
+    // or an idle gap runs at lower clocks (32768^2 fp64, one depth-20 pass:
+    // 6.4 ms after a compute-bound cycle, 6.8 ms after a depth-5 one, 7.5 ms
+    // after 0.5 s idle; profiles/depth_schedule.md). Trial cycles of its first
+    // depths (>= 3 cycles and ~20 ms), state untouched.
+    synchronize();
+    float ms = 0.f;
+    for (size_t i = 0; i < 64 && (i < 3 || ms < 20.f); ++i) {
+      const int k = (*s)[i % s->size()];
+      trial_cycle(split_plan(k));
+      ms += tuned_ms_[k] > 0.f ? tuned_ms_[k] : 1.f;  // local estimate: no collective here
+    }
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+    synchronize();
+  }
 }
 
 void Solver::prepare_plans(int64_t n) {
@@ -1251,23 +1277,29 @@ void Solver::prepare_plans(int64_t n) {
       cur_ ^= p;
     }
   }
-  if (const std::vector<int>* s = schedule(n)) {
-    // Leave the GPU in the schedule's steady state: the search ends on its
-    // shallowest (HBM-bound) depths, and a VALU-bound cycle that follows
-    // HBM-bound work or an idle gap runs at lower clocks (32768^2 fp64, one
-    // depth-20 pass: 6.4 ms after a compute-bound cycle, 6.8 ms after a
-    // depth-5 one, 7.5 ms after 0.5 s idle; profiles/depth_schedule.md).
-    // Trial cycles of its first depths (>= 3 cycles and ~20 ms), state untouched.
-    synchronize();
-    float ms = 0.f;
-    for (size_t i = 0; i < 64 && (i < 3 || ms < 20.f); ++i) {
-      const int k = (*s)[i % s->size()];
-      trial_cycle(split_plan(k));
-      ms += depth_ms(k);
+  if (persist_eligible() && !persist_.count(n)) {
+    // persistent launches vs the schedule's graph replay (or eager cycles):
+    // both timed as trial runs of the same cycles, the faster one kept
+    const std::vector<int> seq = step_cycles(n);
+    bool ok = !seq.empty();
+    for (int k : seq) ok = ok && persist_plan(k) != nullptr;
+    bool use = false;
+    if (ok && persist_mode_ == 1) {
+      use = true;
+    } else if (ok && schedule(n)) {
+      const float tp = time_persist(seq);
+      float tg;
+      if (schedule_graphs()) {
+        tg = time_trial_schedule(seq);
+      } else {
+        tg = 0.f;
+        for (int k : seq) tg += depth_ms(k);
+      }
+      use = tp < tg;
     }
-    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
-    synchronize();
+    persist_[n] = use;
+  }
+  if (const std::vector<int>* s = schedule(n)) {
     for (size_t i = 0; i < s->size(); ++i)
       (void)split_plan_banded((*s)[i], std::max((*s)[i], exchange_depth(*s, i, (*s)[0])));
     return;
@@ -1291,12 +1323,101 @@ void Solver::prepare_plans(int64_t n) {
   }
 }
 
+bool Solver::persist_eligible() const {
+  return hip_ && !jit_ && !cfg_.copy_swap && !tr_->exchanges() && persist_mode_ != 0;
+}
+
+// Single-launch plan of depth k for the persistent kernel: the autotuned one
+// when the autotuner chose a single launch, else plan_single's default, cut
+// to at most the co-resident waves.
+const kern::SplitPlan* Solver::persist_plan(int k) {
+  kern::SplitPlan& p = persist_plans_[k];
+  if (p.k != k) {
+    const kern::SplitPlan& t = split_plan(k);
+    kern::SplitPlan c = t.valid == 2 ? t : kern::plan_single(dtype(), L_, k, 0, 0, 0, cfg_.arith);
+    const int64_t cap = kern::persist_capacity(dtype(), c.ring, k, cfg_.arith);
+    if (c.main_items > cap) c = kern::plan_single(dtype(), L_, k, 0, c.ring, -cap, cfg_.arith);
+    if (!c.valid || c.main_items > cap || c.main_items < 1) c.valid = 0;
+    c.k = k;
+    p = c;
+  }
+  return p.valid == 2 ? &p : nullptr;
+}
+
+void Solver::ensure_persist_ctl() {
+  if (d_done_) return;
+  int ncu = 0;
+  H2D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg_.device));
+  done_cap_ = (int64_t)ncu * 32;  // 8 workgroups of 4 waves per CU
+  H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_done_), (size_t)done_cap_ * sizeof(uint32_t)));
+  H2D_HIP(hipMemsetAsync(d_done_, 0, (size_t)done_cap_ * sizeof(uint32_t), s_compute_));
+  H2D_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_err_), sizeof(unsigned int), hipHostMallocCoherent));
+  *h_err_ = 0;
+  done_base_ = 0;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg_.device) != hipSuccess || khz <= 0) khz = 100000;
+  persist_timeout_ticks_ = (uint64_t)khz * 2000;  // 2 s: a healthy wait lasts about one cycle (< 1 ms here)
+}
+
+// seq's cycles as one persistent launch per run of equal depths. trial: every
+// cycle reads the current buffer and writes the other (timing; the solution
+// and the step / histogram counters are untouched).
+void Solver::run_persist(const std::vector<int>& seq, bool trial) {
+  ensure_persist_ctl();
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
+  for (size_t i = 0; i < seq.size();) {
+    size_t j = i;
+    while (j < seq.size() && seq[j] == seq[i]) ++j;
+    const int k = seq[i];
+    const int nc = (int)(j - i);
+    const kern::SplitPlan* p = persist_plan(k);
+    HEAT2D_REQUIRE(p != nullptr, "persistent launch: no co-resident plan for this depth");
+    kern::PersistCtl ctl{d_done_, done_cap_, done_base_, persist_timeout_ticks_, h_err_};
+    kern::launch_tb_persist(dtype(), buf_[cur_], buf_[cur_ ^ 1], L_, *p, cfg_.r, ctl, nc, trial ? 0 : 1, s_compute_,
+                            cfg_.arith);
+    done_base_ += (uint32_t)nc;
+    if (trial) {
+      last_k_ = 0;  // the other buffer was overwritten
+    } else {
+      if (nc & 1) cur_ ^= 1;
+      steps_ += (int64_t)k * nc;
+      hist_[k] += nc;
+      last_k_ = k;
+    }
+    i = j;
+  }
+  // later eager cycles order against the launches' end
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_comm_, s_compute_));
+  H2D_HIP(hipStreamWaitEvent(s_comm_, ev_comm_, 0));
+}
+
+float Solver::time_persist(const std::vector<int>& seq) {
+  synchronize();
+  run_persist(seq, true);  // warm (clocks, code objects)
+  if (!ev_t0_) {
+    H2D_HIP(hipEventCreate(&ev_t0_));
+    H2D_HIP(hipEventCreate(&ev_t1_));
+  }
+  H2D_HIP(hipEventRecord(ev_t0_, s_compute_));
+  run_persist(seq, true);
+  H2D_HIP(hipEventRecord(ev_t1_, s_compute_));
+  synchronize();
+  float ms = 0.f;
+  H2D_HIP(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));
+  return ms;
+}
+
 void Solver::synchronize() {
   if (!hip_) return;
   H2D_HIP(hipSetDevice(cfg_.device));
   if (!tr_->exchanges()) {
     H2D_HIP(hipStreamSynchronize(s_compute_));
     if (s_comm_ != s_compute_) H2D_HIP(hipStreamSynchronize(s_comm_));
+    if (h_err_ && __atomic_load_n(h_err_, __ATOMIC_ACQUIRE) != 0)
+      fail(__FILE__, __LINE__, "persistent launch: a wave timed out waiting for its neighbours (not co-resident?)");
     tr_->check();
     return;
   }

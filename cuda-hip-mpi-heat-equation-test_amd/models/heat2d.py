@@ -222,6 +222,14 @@ class HeatSolver:
         N.call("heat2d_solver_halo_rows", self._h, int(bool(reset)), C.byref(v))
         return v.value
 
+    def persistent(self, n: int) -> bool:
+        """True if prepare(n) chose persistent multi-cycle launches for step(n)
+        (one cooperative dispatch per run of equal depths, items synchronised by
+        neighbour completion counters: kern::launch_tb_persist)."""
+        v = C.c_int32()
+        N.call("heat2d_solver_persistent", self._h, int(n), C.byref(v))
+        return bool(v.value)
+
     @property
     def plan_cache_hits(self) -> int:
         """Plans / schedules taken from the persistent plan cache (re-validated by one re-time)."""

@@ -187,6 +187,7 @@ _SIGS = {
     "heat2d_autotune_slabs": (C.c_int, [_I64, _I64, C.c_int, C.c_int, C.POINTER(C.c_int32)]),
     "heat2d_solver_plan_cache_hits": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "heat2d_plan_cache_path": (C.c_int, [C.c_char_p, _I64]),
+    "heat2d_solver_persistent": (C.c_int, [_P, _I64, C.POINTER(C.c_int32)]),
 }
 
 _lib = None
