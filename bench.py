@@ -194,8 +194,8 @@ def main():
 
     import heat2d
     from heat2d.models.heat2d import HeatSolver
-    from heat2d.parallel.transport import (IpcTransport, RcclLoopTransport, RcclTransport, SelfTransport,
-                                           TorchDistTransport)
+    from heat2d.parallel.transport import (IpcLoopTransport, IpcTransport, RcclLoopTransport, RcclTransport,
+                                           SelfTransport, TorchDistTransport)
 
     n_glob = args.n
     if args.weak:
@@ -205,13 +205,14 @@ def main():
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     if world > 1:
         tr = (IpcTransport(device) if peer else RcclTransport(rank, world, local)) if hip else TorchDistTransport()
-    elif args.rehearse_comm and hip:
-        tr = RcclLoopTransport(local)
+    elif args.rehearse_comm and hip:  # one rank's exchange with itself: RCCL kernels or IPC pulls
+        tr = IpcLoopTransport(device) if args.transport == "peer" else RcclLoopTransport(local)
     else:
         tr = SelfTransport()
     rows = args.rows if (args.rows and world == 1) else None
     # graphs: single-rank runs, and multi-rank runs whose exchange captures (the IPC transport; RCCL's does not)
-    graph = hip and (args.graph == "on" or (args.graph == "auto" and (world == 1 or peer) and not args.rehearse_comm))
+    ipc = peer or (args.rehearse_comm and args.transport == "peer")
+    graph = hip and (args.graph == "on" or (args.graph == "auto" and ((world == 1 and not args.rehearse_comm) or ipc)))
     s = HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb, overlap=not args.no_overlap, graph=graph,
                    tile_rows=args.tile_rows, transport=tr, device=device if hip else None, rows=rows,
                    comm_cus=args.comm_cus, arith=args.arith)
@@ -268,7 +269,7 @@ def main():
         traffic += c * plan_hbm_bytes(pl, es, s.nrows, s.ncols)["total"]
     # halo traffic of the timed region: each exchange moves the NEXT cycle's
     # depth in whole padded rows, one message per neighbour
-    nmsg = (rank > 0) + (rank < world - 1)
+    nmsg = 2 if (args.rehearse_comm and world == 1) else (rank > 0) + (rank < world - 1)
     halo_bytes = float(s.halo_rows_exchanged()) * s.layout.pitch * es * nmsg
     if world > 1:
         tt = torch.tensor([traffic, halo_bytes], device=cdev, dtype=torch.float64)

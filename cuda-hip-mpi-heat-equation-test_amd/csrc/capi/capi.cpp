@@ -78,6 +78,21 @@ int heat2d_device_count(int* n) {
   });
 }
 
+int heat2d_device_limits(int device, int64_t* out10) {
+  return guarded([&] {
+    const hipDeviceAttribute_t attrs[10] = {
+        hipDeviceAttributeMaxBlockDimX,  hipDeviceAttributeMaxBlockDimY,   hipDeviceAttributeMaxBlockDimZ,
+        hipDeviceAttributeMaxGridDimX,   hipDeviceAttributeMaxGridDimY,    hipDeviceAttributeMaxGridDimZ,
+        hipDeviceAttributeTotalConstantMemory, hipDeviceAttributeMaxThreadsPerBlock, hipDeviceAttributeWarpSize,
+        hipDeviceAttributeMultiprocessorCount};
+    for (int i = 0; i < 10; ++i) {
+      int v = 0;
+      if (hipDeviceGetAttribute(&v, attrs[i], device) != hipSuccess) fail(__FILE__, __LINE__, "hipDeviceGetAttribute failed");
+      out10[i] = v;
+    }
+  });
+}
+
 int heat2d_make_layout(int64_t nrows, int64_t ncols, int64_t halo, int64_t row0, int64_t nrows_global,
                        heat2d_layout* out) {
   return guarded([&] {
@@ -205,6 +220,10 @@ int heat2d_transport_ipc(heat2d_allgather_fn ag, heat2d_allreduce_fn ar, heat2d_
     IpcOps ops{ctx, ag, ar, br};
     *out = new TransportHandle{make_ipc_transport(ops, rank, size, device)};
   });
+}
+
+int heat2d_transport_ipc_loop(int device, void** out) {
+  return guarded([&] { *out = new TransportHandle{make_ipc_loop_transport(device)}; });
 }
 
 int heat2d_transport_free(void* t) {

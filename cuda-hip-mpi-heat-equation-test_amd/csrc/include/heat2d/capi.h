@@ -61,6 +61,10 @@ const char* heat2d_last_error(void);
 int heat2d_version(void);
 int heat2d_max_tb(void);
 int heat2d_device_count(int* n);
+// Device limits the reference's PyCUDA program queries (python/cuda/cuda.py:16-27):
+// out = [max_block_dim_x, _y, _z, max_grid_dim_x, _y, _z, total_constant_memory,
+//        max_threads_per_block, warp_size, multiprocessor_count]
+int heat2d_device_limits(int device, int64_t* out10);
 
 int heat2d_make_layout(int64_t nrows, int64_t ncols, int64_t halo, int64_t row0,
                        int64_t nrows_global, heat2d_layout* out);
@@ -108,6 +112,7 @@ typedef int (*heat2d_allgather_fn)(void* ctx, const void* mine, void* all, int64
 // IPC transport (process per GPU, no RCCL): host collectives through the callbacks.
 int heat2d_transport_ipc(heat2d_allgather_fn ag, heat2d_allreduce_fn ar, heat2d_barrier_fn br, void* ctx, int rank,
                          int size, int device, void** out);
+int heat2d_transport_ipc_loop(int device, void** out);
 int heat2d_transport_free(void* t);
 /* fail fast: abort the transport's fabric (RCCL: ncclCommAbort); its solver's next synchronisation raises */
 int heat2d_transport_abort(void* t, const char* reason);

@@ -180,6 +180,10 @@ struct IpcOps {
   int (*barrier)(void* ctx);
 };
 std::shared_ptr<Transport> make_ipc_transport(const IpcOps& ops, int rank, int size, int device);
+// 1-rank IPC transport exchanging the slab's boundary rows with itself
+// (periodic wrap, like make_rccl_loop_transport): a rehearsal of one rank's
+// IPC cycle on one GPU. Not physics (it overwrites the frame rows).
+std::shared_ptr<Transport> make_ipc_loop_transport(int device);
 
 // ---------------------------------------------------------------- CPU twins
 

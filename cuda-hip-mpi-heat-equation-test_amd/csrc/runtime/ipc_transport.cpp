@@ -63,9 +63,13 @@ struct IpcCard {
 
 class IpcTransport final : public Transport {
  public:
-  IpcTransport(const IpcOps& ops, int rank, int size, int device) : ops_(ops), rank_(rank), size_(size) {
+  // loop: a 1-rank periodic self-exchange (rows [0, k) land above the top, the
+  // top k rows below row 0) — a rehearsal of one rank's multi-GPU cycle (the
+  // counters' kernels, the two pulls, graph capture) on one GPU; not physics.
+  IpcTransport(const IpcOps& ops, int rank, int size, int device, bool loop = false)
+      : ops_(ops), rank_(rank), size_(size), loop_(loop && size == 1) {
     HEAT2D_REQUIRE(size >= 1 && rank >= 0 && rank < size, "bad rank / size");
-    HEAT2D_REQUIRE(ops.allgather && ops.allreduce && ops.barrier, "IPC transport needs host collectives");
+    HEAT2D_REQUIRE(loop_ || (ops.allgather && ops.allreduce && ops.barrier), "IPC transport needs host collectives");
     if (device >= 0) H2D_HIP(hipSetDevice(device));
     H2D_HIP(hipGetDevice(&device_));
     int khz = 0;
@@ -82,28 +86,45 @@ class IpcTransport final : public Transport {
     for (auto& pb : peer_buf_)
       for (void* b : pb)
         if (b) (void)hipIpcCloseMemHandle(b);
-    if (host_) {
+    if (host_ && loop_) {
+      (void)hipHostFree(host_);
+    } else if (host_) {
       (void)hipHostUnregister(host_);
       ::munmap(host_, shm_bytes_);
     }
   }
   int rank() const override { return rank_; }
   int size() const override { return size_; }
-  std::string name() const override { return "ipc"; }
+  std::string name() const override { return loop_ ? "ipc-loop" : "ipc"; }
   bool capturable() const override { return true; }
-  bool exchanges() const override { return size_ > 1; }
+  bool exchanges() const override { return size_ > 1 || loop_; }
   bool aborted() const override { return aborted_.load(); }
   void io_phase(bool on) override { io_ += on ? 1 : -1; }
   void graph_launched(hipStream_t stream) override { track(stream, "graph replay"); }
 
   void attach(void* buf0, void* buf1, const SlabLayout& L, DType dt) override {
-    if (size_ == 1) return;
+    if (size_ == 1 && !loop_) return;
     HEAT2D_REQUIRE(!attached_, "IPC transport: one solver per transport");
     attached_ = true;
     mine_[0] = buf0;
     mine_[1] = buf1;
     L_ = L;
     es_ = dtype_size(dt);
+    if (loop_) {  // the counters in this process's pinned memory; the "neighbours" are this slab
+      shm_bytes_ = shm_size();
+      H2D_HIP(hipHostMalloc(&host_, shm_bytes_, hipHostMallocCoherent | hipHostMallocMapped));
+      std::memset(host_, 0, shm_bytes_);
+      void* d = nullptr;
+      H2D_HIP(hipHostGetDevicePointer(&d, host_, 0));
+      hctrl_ = static_cast<uint64_t*>(host_);
+      ctrl_ = static_cast<uint64_t*>(d);
+      slots_ = reinterpret_cast<kern::IpcSlot*>(static_cast<char*>(d) + 64);
+      for (int side = 0; side < 2; ++side) {
+        peer_L_[side] = L;
+        for (int b = 0; b < 2; ++b) peer_buf_[side][b] = mine_[b];
+      }
+      return;
+    }
     IpcCard me{};
     H2D_HIP(hipIpcGetMemHandle(&me.buf[0], buf0));
     H2D_HIP(hipIpcGetMemHandle(&me.buf[1], buf1));
@@ -154,16 +175,23 @@ class IpcTransport final : public Transport {
   void exchange(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
                 bool on_device) override {
     HEAT2D_REQUIRE(on_device, "the IPC transport moves device fields");
-    if (size_ == 1 || k <= 0) return;
+    if ((size_ == 1 && !loop_) || k <= 0) return;
     HEAT2D_REQUIRE(attached_, "IPC transport: exchange before attach()");
     HEAT2D_REQUIRE(!aborted_, "IPC transport aborted: " + reason());
     const int b = field == mine_[0] ? 0 : (field == mine_[1] ? 1 : -1);
     HEAT2D_REQUIRE(b >= 0, "IPC transport: exchange of a buffer that was not attached");
     HEAT2D_REQUIRE(dtype_size(dt) == es_ && L.pitch == L_.pitch, "IPC transport: layout changed since attach()");
-    const int lo = rank_ > 0 ? rank_ - 1 : -1, hi = rank_ < size_ - 1 ? rank_ + 1 : -1;
+    const int lo = loop_ ? 0 : (rank_ > 0 ? rank_ - 1 : -1), hi = loop_ ? 0 : (rank_ < size_ - 1 ? rank_ + 1 : -1);
     kern::launch_ipc_arrive(slots_, ctrl_, rank_, lo, hi, timeout_ticks_, stream);
     HaloMsg msg[2];
-    const int nmsg = halo_msgs(rank_, size_, L, k, msg);
+    int nmsg;
+    if (loop_) {  // an interior rank's two messages, both from this slab (periodic wrap)
+      nmsg = 2;
+      msg[0] = HaloMsg{-1, 0, -k};
+      msg[1] = HaloMsg{1, 0, L.nrows};
+    } else {
+      nmsg = halo_msgs(rank_, size_, L, k, msg);
+    }
     const size_t bytes = halo_msg_bytes(L, k, es_);
     for (int i = 0; i < nmsg; ++i) {
       const int side = msg[i].peer > rank_;
@@ -285,6 +313,7 @@ class IpcTransport final : public Transport {
   };
   IpcOps ops_;
   int rank_, size_;
+  bool loop_ = false;
   int device_ = 0;
   bool attached_ = false;
   void* mine_[2] = {nullptr, nullptr};
@@ -313,6 +342,10 @@ class IpcTransport final : public Transport {
 
 std::shared_ptr<Transport> make_ipc_transport(const IpcOps& ops, int rank, int size, int device) {
   return std::make_shared<IpcTransport>(ops, rank, size, device);
+}
+
+std::shared_ptr<Transport> make_ipc_loop_transport(int device) {
+  return std::make_shared<IpcTransport>(IpcOps{}, 0, 1, device, true);
 }
 
 }  // namespace heat2d

@@ -115,6 +115,7 @@ _SIGS = {
     "heat2d_version": (C.c_int, []),
     "heat2d_max_tb": (C.c_int, []),
     "heat2d_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "heat2d_device_limits": (C.c_int, [C.c_int, C.POINTER(C.c_int64)]),
     "heat2d_make_layout": (C.c_int, [_I64, _I64, _I64, _I64, _I64, _LP]),
     "heat2d_parse_input": (C.c_int, [C.c_char_p, C.POINTER(C.c_double)]),
     "heat2d_decompose": (C.c_int, [_I64, C.c_int, C.c_int, C.POINTER(_I64), C.POINTER(_I64)]),
@@ -148,6 +149,7 @@ _SIGS = {
     "heat2d_transport_callback": (C.c_int, [EXCHANGE_FN, ALLREDUCE_FN, BARRIER_FN, _P, C.c_int, C.c_int,
                                             C.POINTER(_P)]),
     "heat2d_transport_free": (C.c_int, [_P]),
+    "heat2d_transport_ipc_loop": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "heat2d_transport_ipc": (C.c_int, [ALLGATHER_FN, ALLREDUCE_FN, BARRIER_FN, _P, C.c_int, C.c_int, C.c_int,
                                        C.POINTER(_P)]),
     "heat2d_solver_create": (C.c_int, [C.POINTER(Config), _P, C.POINTER(_P)]),
@@ -302,6 +304,17 @@ def device_count() -> int:
     n = C.c_int(0)
     call("heat2d_device_count", C.byref(n))
     return n.value
+
+
+LIMIT_NAMES = ("MAX_BLOCK_DIM_X", "MAX_BLOCK_DIM_Y", "MAX_BLOCK_DIM_Z", "MAX_GRID_DIM_X", "MAX_GRID_DIM_Y",
+               "MAX_GRID_DIM_Z", "TOTAL_CONSTANT_MEMORY", "MAX_THREADS_PER_BLOCK", "WARP_SIZE", "MULTIPROCESSOR_COUNT")
+
+
+def device_limits(device: int = 0) -> dict:
+    """The device attributes python/cuda/cuda.py:16-27 queries (plus wave size and CU count)."""
+    out = (C.c_int64 * 10)()
+    call("heat2d_device_limits", int(device), out)
+    return dict(zip(LIMIT_NAMES, (int(v) for v in out)))
 
 
 def rccl_unique_id() -> bytes:

@@ -96,6 +96,13 @@ def run(argv=None) -> int:
 
     if backend == "hip" and not a.quiet:
         print(f" MPI rank {rank:12d} using GPU {local:12d}", flush=True)
+    if var.name == "pycuda" and backend == "hip" and root and not a.quiet:
+        # the reference's PyCUDA program queries the device limits and prints
+        # MAX_THREADS_PER_BLOCK (python/cuda/cuda.py:16-27)
+        from heat2d.ops import _native as N
+        lim = N.device_limits(local)
+        print(lim["MAX_THREADS_PER_BLOCK"])
+        print(" device limits: " + " ".join(f"{k}={v}" for k, v in lim.items()), flush=True)
     if world > 1:
         tr = T.RcclTransport(rank, world, local) if backend == "hip" else T.TorchDistTransport()
     else:

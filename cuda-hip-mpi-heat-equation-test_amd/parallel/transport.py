@@ -265,6 +265,18 @@ class IpcTransport(Transport):
         super().__init__(h, rank, size, "ipc")
 
 
+class IpcLoopTransport(Transport):
+    """1-rank IPC transport exchanging the slab's boundary rows with itself
+    (periodic wrap): one rank's IPC cycle — counter kernels, two pulls, graph
+    capture — rehearsed on one GPU (like :class:`RcclLoopTransport`).
+    Performance only: it overwrites the Dirichlet frame rows."""
+
+    def __init__(self, device: int):
+        h = C.c_void_p()
+        N.call("heat2d_transport_ipc_loop", device, C.byref(h))
+        super().__init__(h, 0, 1, "ipc-loop")
+
+
 def default_transport(backend: str, device: Optional[int] = None) -> Transport:
     """Pick the transport for the current process: self if not distributed, RCCL for
     device fields, torch.distributed host callbacks for CPU fields."""

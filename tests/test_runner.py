@@ -198,3 +198,17 @@ def test_checkpoint_python_load_checks(native, tmp_path):
     s2 = HeatSolver(p, dtype="fp64", backend="cpu", tb=2)
     assert checkpoint.load(s2, str(v1))["step"] == 7
     assert np.array_equal(s2.download(), R.owned(R.ftcs(p)))
+
+
+@pytest.mark.gpu
+def test_pycuda_variant_prints_device_limits(native, gpu, tmp_path):
+    """--variant pycuda (python/cuda/cuda.py): the device limits the reference
+    queries (:16-27) are printed, MAX_THREADS_PER_BLOCK on its own line, and the
+    run goes through the hipRTC-specialised kernel (the reference's JIT)."""
+    (tmp_path / "input.dat").write_text("64 0.25 0.05 2.0 10\n")
+    out = py(tmp_path, "--backend", "hip", "--variant", "pycuda", "--output", "none")
+    lim = N.device_limits(0)
+    lines = [l.strip() for l in out.splitlines()]
+    assert str(lim["MAX_THREADS_PER_BLOCK"]) in lines
+    assert lim["MAX_THREADS_PER_BLOCK"] >= 256 and lim["WARP_SIZE"] == 64 and lim["MAX_BLOCK_DIM_X"] >= 256
+    assert any(l.startswith("device limits:") and "MAX_GRID_DIM_X=" in l for l in lines)
