@@ -6,10 +6,13 @@ Layout (v2, shared with the native CLI, csrc/runtime/checkpoint.cpp):
     DIR/step-NNNNNNNNNNNN/meta.json          problem + solver parameters + completed step count
     DIR/latest                               the newest COMPLETE step directory (atomic commit point)
 
-Every step is written into its own directory; only after all rank files and
-meta.json are there does rank 0 republish ``latest`` (temp file + rename) and
+Every save writes into a FRESH directory (``step-N``, or ``step-N-G`` when step N
+was saved before — a restart at its final step, a re-run into the same
+directory — so files ``latest`` may point at are never overwritten in place);
+rank files and meta.json are fsynced, and only after all of them are there does
+rank 0 republish ``latest`` (temp file + fsync + rename + directory fsync) and
 prune all but the two newest steps. A crash at any point leaves ``latest`` on a
-complete checkpoint — rank files of two different steps are never mixed.
+complete checkpoint — rank files of two different saves are never mixed.
 Readers also accept a step directory itself and the v1 flat layout.
 
 Restart re-decomposes: a run on P ranks can resume a checkpoint written by Q
@@ -34,6 +37,26 @@ def step_dir(directory: str, step: int) -> str:
     return os.path.join(directory, f"step-{int(step):012d}")
 
 
+def fresh_step_dir(directory: str, step: int) -> str:
+    """A step directory name no earlier save used (sorts after the older
+    generations of the same step and before the next step)."""
+    base = step_dir(directory, step)
+    if not os.path.exists(base):
+        return base
+    g = 1
+    while os.path.exists(f"{base}-{g}"):
+        g += 1
+    return f"{base}-{g}"
+
+
+def _fsync_dir(path: str) -> None:
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
 def _write_atomic(path: str, text: str) -> None:
     tmp = path + ".tmp"
     with open(tmp, "w") as f:
@@ -41,16 +64,22 @@ def _write_atomic(path: str, text: str) -> None:
         f.flush()
         os.fsync(f.fileno())
     os.replace(tmp, path)
+    _fsync_dir(os.path.dirname(os.path.abspath(path)))
 
 
 def save(solver, directory: str, step: Optional[int] = None, extra: Optional[dict] = None) -> None:
     """Collective: every rank writes its slab into the step's directory; rank 0
     then writes meta.json there and atomically republishes ``latest``."""
     step = int(solver.steps_done if step is None else step)
-    sd = step_dir(directory, step)
+    # every rank names the same fresh directory: rank 0 picks it, the others receive it
+    sd = fresh_step_dir(directory, step) if solver.rank == 0 else None
+    sd = _broadcast_str(solver, sd)
     os.makedirs(sd, exist_ok=True)
     local = solver.download()
-    np.save(os.path.join(sd, f"rank{solver.rank:05d}.npy"), local, allow_pickle=False)
+    with open(os.path.join(sd, f"rank{solver.rank:05d}.npy"), "wb") as f:
+        np.save(f, local, allow_pickle=False)
+        f.flush()
+        os.fsync(f.fileno())
     _barrier(solver)
     if solver.rank == 0:
         p = solver.problem
@@ -67,7 +96,7 @@ def save(solver, directory: str, step: Optional[int] = None, extra: Optional[dic
         meta.update(extra or {})
         _write_atomic(os.path.join(sd, "meta.json"), json.dumps(meta, indent=1))
         _write_atomic(os.path.join(directory, "latest"), os.path.basename(sd) + "\n")  # the commit point
-        steps = sorted(d for d in os.listdir(directory) if d.startswith("step-"))
+        steps = sorted(d for d in os.listdir(directory) if d.startswith("step-") and not d.endswith(".tmp"))
         for d in steps[:max(0, steps.index(os.path.basename(sd)) - 1)]:  # keep the two newest
             shutil.rmtree(os.path.join(directory, d), ignore_errors=True)
     _barrier(solver)
@@ -124,3 +153,12 @@ def _barrier(solver) -> None:
     if solver.size > 1:
         import torch.distributed as dist
         dist.barrier()
+
+
+def _broadcast_str(solver, s):
+    if solver.size == 1:
+        return s
+    import torch.distributed as dist
+    box = [s]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]

@@ -212,3 +212,31 @@ def test_pycuda_variant_prints_device_limits(native, gpu, tmp_path):
     assert str(lim["MAX_THREADS_PER_BLOCK"]) in lines
     assert lim["MAX_THREADS_PER_BLOCK"] >= 256 and lim["WARP_SIZE"] == 64 and lim["MAX_BLOCK_DIM_X"] >= 256
     assert any(l.startswith("device limits:") and "MAX_GRID_DIM_X=" in l for l in lines)
+
+
+@pytest.mark.parametrize("writer", ["native", "python"])
+def test_checkpoint_resave_same_step_never_overwrites(native, tmp_path, writer):
+    """A step saved again (a restart at its final step, a re-run into the same
+    directory) goes to a fresh generation directory: the files `latest` points
+    at are never rewritten in place, and the new save resumes bitwise."""
+    from heat2d.models.heat2d import HeatSolver
+    from heat2d.utils import checkpoint
+    (tmp_path / "input.dat").write_text("44 0.25 0.05 1.0 9 1\n")
+    ck = tmp_path / "ck"
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    for _ in range(2):
+        if writer == "native":
+            subprocess.run([N.CLI_PATH, "--cpu", "--quiet", "--tb", "3", "--checkpoint", "ck", "--output", "none"],
+                           cwd=tmp_path, check=True, capture_output=True)
+        else:
+            s = HeatSolver(prob, dtype="fp64", backend="cpu", tb=3)
+            s.step(9)
+            checkpoint.save(s, str(ck))
+            s.close()
+    names = sorted(d.name for d in ck.iterdir() if d.name.startswith("step-"))
+    assert names == ["step-000000000009", "step-000000000009-1"]
+    assert (ck / "latest").read_text().strip() == "step-000000000009-1"
+    assert checkpoint.load_meta(str(ck))["step"] == 9
+    s = HeatSolver(prob, dtype="fp64", backend="cpu", tb=3)
+    checkpoint.load(s, str(ck))
+    assert np.array_equal(s.download(), R.owned(R.ftcs(prob)))
