@@ -86,12 +86,13 @@ void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, con
 // Persistent multi-cycle launch (tb_impl.hpp tb_persist_kernel): `ncycles`
 // cycles of depth plan.k over the whole slab in ONE cooperative dispatch, one
 // co-resident wave per item of a single-launch plan (plan_single), items
-// synchronised by per-item completion counters instead of kernel boundaries.
+// synchronised by per-item completion counters (a wavefront, no grid barrier)
+// instead of kernel boundaries.
 // alternate = 1: cycle c reads buffer c & 1 and writes the other (the real
 // loop: the result lands in buf0 / buf1 by the parity of ncycles); 0: every
 // cycle buf0 -> buf1 (timing trials; buf0 untouched).
 struct PersistCtl {
-  uint32_t* done;          // device, >= nitems_cap counters
+  uint32_t* done;          // device, >= nitems_cap per-item completion counters
   int64_t nitems_cap;
   uint32_t base;           // the counters' value at launch (advance by ncycles after each launch)
   uint64_t timeout_ticks;  // a dependency wait longer than this fails the launch (*err = 1)

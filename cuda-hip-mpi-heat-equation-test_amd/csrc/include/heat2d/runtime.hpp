@@ -428,9 +428,9 @@ class Solver {
   int persist_mode_ = -1;                 // HEAT2D_PERSIST (-1 auto, 0 off, 1 on)
   std::map<int64_t, bool> persist_;       // step(n) runs persistent launches (decided in prepare)
   kern::SplitPlan persist_plans_[kMaxTB + 1] = {};
-  uint32_t* d_done_ = nullptr;            // persistent launches: per-item counters
+  uint32_t* d_done_ = nullptr;            // persistent launches: per-item completion counters
   int64_t done_cap_ = 0;
-  uint32_t done_base_ = 0;
+  uint32_t done_base_ = 0;                // their value at the next launch
   unsigned int* h_err_ = nullptr;         // pinned, host-visible error word of the persistent kernel
   uint64_t persist_timeout_ticks_ = 0;
   hipEvent_t ev_t0_ = nullptr, ev_t1_ = nullptr;  // time_plan

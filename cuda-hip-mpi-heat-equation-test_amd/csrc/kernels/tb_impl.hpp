@@ -258,7 +258,16 @@ constexpr int chain_len() {
 #define HEAT2D_STORE_AUX 2
 #endif
 
-template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, int CL = K>
+// CP (cache policy of the field loads / stores): 0 = default (stores nt); 1 =
+// device-coherent (sc1 loads, nt sc1 stores): the values go to / come from the
+// memory side, coherent across the 8 XCDs' L2s without cache maintenance —
+// the persistent kernel's cross-wave hand-off (tb_persist_kernel).
+template <int CP>
+constexpr int kLoadAux = CP ? 16 : 0;
+template <int CP>
+constexpr int kStoreAux = CP ? (16 | 2) : HEAT2D_STORE_AUX;
+
+template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, int CL = K, int CP = 0>
 struct March {
   using S = TbShape<T, NV, K>;
   static constexpr int V = S::V;
@@ -292,7 +301,7 @@ struct March {
     const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + (int64_t)m * pitch_b, nrec);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      U4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off + v * 16, 0, 0);
+      U4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off + v * 16, 0, kLoadAux<CP>);
       out[v] = __builtin_bit_cast(VT, b);
     }
   }
@@ -305,7 +314,7 @@ struct March {
       VT w;
 #pragma unroll
       for (int e = 0; e < VM; ++e) w[e] = out[v * VM + e];
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off + v * 16, 0, HEAT2D_STORE_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off + v * 16, 0, kStoreAux<CP>);
     }
   }
 
@@ -480,7 +489,7 @@ struct March {
 // ~2x the registers: 209 VGPRs at K = 10). Same operation order and rounding
 // per element as March (bitwise identical); the loads / stores / ring /
 // descriptors / edge kinds are March's.
-template <int K, int EK, int RING, int AR, bool ST = false, int CL = K>
+template <int K, int EK, int RING, int AR, bool ST = false, int CL = K, int CP = 0>
 struct MarchF32 {
   using F2 = float __attribute__((ext_vector_type(2)));
   using VT = float __attribute__((ext_vector_type(4)));
@@ -517,12 +526,12 @@ struct MarchF32 {
 
   __device__ __forceinline__ void load_row(int32_t m, Row& out) const {
     const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + (int64_t)m * pitch_b, nrec);
-    const VT v = __builtin_bit_cast(VT, __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off, 0, 0));
+    const VT v = __builtin_bit_cast(VT, __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off, 0, kLoadAux<CP>));
     out = Row{F2{v.x, v.y}, F2{v.z, v.w}};
   }
   __device__ __forceinline__ void store_row(int32_t row, bool live, const VT& w) const {
     const __amdgpu_buffer_rsrc_t rs = row_rsrc(drow + (int64_t)row * pitch_b, live ? nrec : 0u);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off, 0, HEAT2D_STORE_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off, 0, kStoreAux<CP>);
   }
   static __device__ __forceinline__ Row split(const Row& v) { return Row{F2{v.a.x, v.b.x}, F2{v.a.y, v.b.y}}; }
 
@@ -670,7 +679,8 @@ template <typename T, int NV>
 constexpr bool kPackedF32 = false;
 #endif
 
-template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, bool PS = false, int CLX = 0>
+template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, bool PS = false, int CLX = 0,
+          int CP = 0>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
                                       int64_t t1, int lane, StatAcc* acc = nullptr) {
   using S = TbShape<T, NV, K>;
@@ -684,8 +694,8 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   // the chains' extra rows spill at fp64 K >= 21
   // (CLX > 0: an explicit chain length — the boundary-band kernel)
   constexpr int CL = CLX > 0 ? (CLX < K ? CLX : K) : (ST ? K : chain_len<T, K>());
-  using W = typename std::conditional<kPackedF32<T, NV>, MarchF32<K, EK, RING, AR, ST, CL>,
-                                      March<T, NV, K, EK, RING, AR, ST, CL>>::type;
+  using W = typename std::conditional<kPackedF32<T, NV>, MarchF32<K, EK, RING, AR, ST, CL, CP>,
+                                      March<T, NV, K, EK, RING, AR, ST, CL, CP>>::type;
   W w;
   // row base = column col_lo (= -cpad) of row 0; offsets are relative to it
   w.srow = reinterpret_cast<const char*>(src + a.col_lo);
@@ -898,21 +908,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
 // Persistent multi-cycle launch (small grids / short cycles).
 //
 // One dispatch runs `ncycles` cycles of depth K over the whole slab: exactly
-// one wave per work item, all co-resident (cooperative launch), each wave
-// marching ITS item in every cycle. Between cycles there is no kernel
-// boundary: an item of cycle c waits only for the items of cycle c - 1 whose
-// output its own cycle reads (the K rows above and below it in its strip and
-// the two neighbour strips: read-after-write on the source) — which are also
-// the only items that read the rows its cycle overwrites (write-after-read on
-// the destination). Per item a completion counter (`done`, epoch-based: it
-// holds base + cycles completed) is published with an agent-scope release
-// after the item's stores, and read with an agent-scope acquire. This removes
-// the per-cycle dispatch ramp / drain and the inter-launch gap (~11 + 8-10 us
-// of a ~61 us 4096^2 fp32 cycle, profiles/small_grid/README.md): a wave starts
-// cycle c + 1 as soon as its neighbourhood is done, a wavefront through the
-// grid instead of a grid-wide barrier. A wait that exceeds timeout_ticks of
-// the wall clock (a wave that never ran: not co-resident) sets *err and the
-// wave returns — the launch fails loudly instead of hanging the GPU.
+// one wave per work item (all resident: the grid is sized to the occupancy),
+// each wave marching ITS item in every cycle. Between cycles there is no
+// kernel boundary — no dispatch ramp, no drain into an empty queue, no
+// inter-launch gap (~11 + 8-10 us of a ~61 us 4096^2 fp32 cycle,
+// profiles/small_grid/) — and no grid barrier either: an item of cycle c waits
+// only for the items whose cycle-(c-1) output it reads (the K rows above and
+// below it in its strip and the two neighbour strips: read-after-write on the
+// source), which are also the only items that read the rows its cycle
+// overwrites (write-after-read on the destination). A wavefront through the
+// grid, synchronised by one completion counter per item (epoch-based: it holds
+// base + cycles completed).
+//
+// Coherence across the 8 XCDs (separate, mutually non-coherent L2s) without
+// cache maintenance: the field loads / stores of this kernel carry device
+// scope (march CP = 1: sc1 loads, nt sc1 stores), so a row a wave stored is at
+// the memory side once its vmcnt drains, and a row a wave loads comes from
+// there. Whole-L2 maintenance (buffer_wbl2 / buffer_inv per wave or per XCD,
+// the usual release / acquire) measured 3x slower (profiles/r3/persist_v1/).
+// A wait longer than timeout_ticks of the wall clock (a wave that never became
+// resident) sets *err and the wave returns: the launch fails loudly instead of
+// hanging the GPU.
 struct PersistArgs {
   uint32_t* done;          // per item
   uint32_t base;           // value every item's counter holds at launch
@@ -990,7 +1006,7 @@ __global__ __launch_bounds__(256) void tb_persist_kernel(T* __restrict__ b0, T* 
         if (lane == 0) __hip_atomic_store(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the neighbours' stores, not stale cache lines
+      asm volatile("buffer_inv sc0" ::: "memory");  // nothing of this CU's L1 survives into the next reads
     }
     int32_t lin = tb_span(a, it).lin;
     while (tb_piece(a, it, lin, strip, t0, t1)) {
@@ -999,13 +1015,14 @@ __global__ __launch_bounds__(256) void tb_persist_kernel(T* __restrict__ b0, T* 
       const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
                      (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
       switch (ek) {
-        case 0: march<T, NV, K, 0, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
-        case 1: march<T, NV, K, 1, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
-        case 2: march<T, NV, K, 2, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
-        default: march<T, NV, K, 3, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
+        case 0: march<T, NV, K, 0, RING, AR, false, false, 0, 1>(src, dst, a, r, strip, t0, t1, lane); break;
+        case 1: march<T, NV, K, 1, RING, AR, false, false, 0, 1>(src, dst, a, r, strip, t0, t1, lane); break;
+        case 2: march<T, NV, K, 2, RING, AR, false, false, 0, 1>(src, dst, a, r, strip, t0, t1, lane); break;
+        default: march<T, NV, K, 3, RING, AR, false, false, 0, 1>(src, dst, a, r, strip, t0, t1, lane); break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this item's rows out of the XCD's L2 first
+    // this item's rows are at the device-coherent level once the stores drain
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(&p.done[it], p.base + (uint32_t)c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -1027,14 +1044,15 @@ int persist_blocks_per_cu() {
   return nb;
 }
 
+// A plain launch on the caller's stream: a cooperative launch guarantees
+// co-residency too, but went through a separate hardware queue with ~1 ms of
+// launch latency per dispatch (rocprofv3 trace, profiles/r3/persist_v2/); the
+// host sizes the grid to the occupancy instead, and the kernel's wait timeout
+// turns a non-resident wave into an error, not a hang.
 template <typename T, int K, int RING, int AR>
 hipError_t persist_launch(unsigned nblocks, T* b0, T* b1, const TbArgs& a, T r, const PersistArgs& p, hipStream_t s) {
-  TbArgs aa = a;
-  T rr = r;
-  PersistArgs pp = p;
-  void* args[] = {&b0, &b1, &aa, &rr, &pp};
-  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tb_persist_kernel<T, 1, K, RING, AR>), dim3(nblocks),
-                                    dim3(256), args, 0, s);
+  hipLaunchKernelGGL((tb_persist_kernel<T, 1, K, RING, AR>), dim3(nblocks), dim3(256), 0, s, b0, b1, a, r, p);
+  return hipGetLastError();
 }
 
 // Per-(T, RING, AR) entry points, instantiated in tb_<dtype>_r<RING>_persist[_fma].hip.

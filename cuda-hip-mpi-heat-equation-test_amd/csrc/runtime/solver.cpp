@@ -1348,15 +1348,15 @@ void Solver::ensure_persist_ctl() {
   if (d_done_) return;
   int ncu = 0;
   H2D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg_.device));
-  done_cap_ = (int64_t)ncu * 32;  // 8 workgroups of 4 waves per CU
+  done_cap_ = (int64_t)ncu * 32;  // per-item counters: 8 workgroups of 4 waves per CU at most
   H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_done_), (size_t)done_cap_ * sizeof(uint32_t)));
   H2D_HIP(hipMemsetAsync(d_done_, 0, (size_t)done_cap_ * sizeof(uint32_t), s_compute_));
+  done_base_ = 0;
   H2D_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_err_), sizeof(unsigned int), hipHostMallocCoherent));
   *h_err_ = 0;
-  done_base_ = 0;
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg_.device) != hipSuccess || khz <= 0) khz = 100000;
-  persist_timeout_ticks_ = (uint64_t)khz * 2000;  // 2 s: a healthy wait lasts about one cycle (< 1 ms here)
+  persist_timeout_ticks_ = (uint64_t)khz * 2000;  // 2 s: a healthy wait lasts about one cycle
 }
 
 // seq's cycles as one persistent launch per run of equal depths. trial: every
