@@ -1295,7 +1295,9 @@ void Solver::prepare_plans(int64_t n) {
         tg = 0.f;
         for (int k : seq) tg += depth_ms(k);
       }
-      use = tp < tg;
+      // a clear win only: on MI355X the persistent kernel's cross-XCD hand-off
+      // costs about what a launch boundary does (profiles/r3/persist_v3/)
+      use = tp < 0.97f * tg;
     }
     persist_[n] = use;
   }
