@@ -210,12 +210,15 @@ def main():
     else:
         tr = SelfTransport()
     rows = args.rows if (args.rows and world == 1) else None
+    # a rehearsal of one rank's slab is a MIDDLE slab of the grid (interior
+    # boundary bands, as on rank 3 of 8); --rows alone is a standalone rows x n grid
+    slab_row0 = (prob.n_owned - rows) // 2 if (rows and args.rehearse_comm) else None
     # graphs: single-rank runs, and multi-rank runs whose exchange captures (the IPC transport; RCCL's does not)
     ipc = peer or (args.rehearse_comm and args.transport == "peer")
     graph = hip and (args.graph == "on" or (args.graph == "auto" and ((world == 1 and not args.rehearse_comm) or ipc)))
     s = HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb, overlap=not args.no_overlap, graph=graph,
                    tile_rows=args.tile_rows, transport=tr, device=device if hip else None, rows=rows,
-                   comm_cus=args.comm_cus, arith=args.arith)
+                   comm_cus=args.comm_cus, arith=args.arith, slab_row0=slab_row0)
 
     def barrier():
         if world > 1:

@@ -33,6 +33,8 @@ typedef struct heat2d_config {
   int64_t tile_rows, halo;
   int32_t comm_cus, autotune;
   int32_t engine, arith; /* arith: 0 reference rounding, 1 contracted fma */
+  int32_t pad0;
+  int64_t slab_row0, slab_rows_global; /* 1-rank rehearsal of a middle slab (0: the slab is the grid) */
 } heat2d_config;
 
 typedef struct heat2d_tb_plan {
@@ -50,6 +52,9 @@ typedef struct heat2d_split_plan {
   heat2d_rect main;
   heat2d_rect edge[4];
   int64_t main_waves, edge_waves, main_items, edge_items;
+  int32_t nfused, pad;
+  heat2d_rect fused[4];
+  int64_t sig_items;
 } heat2d_split_plan;
 
 typedef int (*heat2d_exchange_fn)(void* ctx, void* send_lo, void* send_hi, void* recv_lo,

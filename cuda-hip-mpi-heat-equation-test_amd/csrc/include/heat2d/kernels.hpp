@@ -70,6 +70,12 @@ struct SplitPlan {
   TbRect main;
   TbRect edge[4];
   int64_t main_waves, edge_waves, main_items, edge_items;
+  // valid = 4 (fused, plan_fused): the MAIN launch's rects in item order —
+  // the exchanged bands first (sig_items items that signal their completion),
+  // then the interior — and `edge` holds only bands on the Dirichlet frame
+  int32_t nfused, pad;
+  TbRect fused[4];
+  int64_t sig_items;
 };
 // ring_override: 4 | 6 (0: default); main_bands: MAIN row bands (0: persistent default;
 // < 0: -main_bands segments, TbRect)
@@ -80,6 +86,27 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
 // where the second launch costs more than it saves.
 SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int ring_override = 0, int64_t bands = 0,
                       int arith = 0);
+// Fused cycle (valid = 4) for slabs whose halo exchange can be gated on a
+// device counter (Transport::gates()): ONE interior-kernel launch whose first
+// items are the boundary bands the exchange sends (top if send_top, bottom if
+// send_bottom; their rows stored at device scope, each item counted in a
+// device counter when its stores drain), the interior cut so that the waves
+// that took a band item get correspondingly less interior (every wave ends
+// together); bands on the Dirichlet frame (a first / last rank) go to a small
+// general launch beside it. The exchange starts as soon as the band count is
+// reached instead of after a separate band launch (the edge-first order's
+// serial phase: 77 of 879 us on the 8-rank fp64 slab, profiles/r3/thin/).
+// valid = 0 if the slab is too thin or has more band items than waves.
+SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool send_top, bool send_bottom, int cus = 0,
+                     int spare_waves = 0, int ring_override = 0, int arith = 0);
+// Launch the MAIN part of a fused plan, counting band items into *sig.
+void launch_fused_main(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, uint32_t* sig,
+                       double r, hipStream_t stream, int arith = 0);
+// A one-wave kernel on `stream` that waits until *counter >= target (an
+// exchange gated on a fused cycle's band count); a wait longer than
+// timeout_ticks sets *err and returns.
+void launch_wait_counter(const uint32_t* counter, uint32_t target, uint64_t timeout_ticks, unsigned int* err,
+                         hipStream_t stream);
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith = 0);
 

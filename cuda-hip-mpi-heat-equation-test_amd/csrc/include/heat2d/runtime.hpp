@@ -48,6 +48,12 @@ struct SolverConfig {
   int32_t engine;      // 0: temporal-blocked kernels; 1: run-time specialised hipRTC kernel (K = 1, jit.hpp)
   int32_t arith;       // 0: reference arithmetic, every op rounded (bitwise == NumPy golden);
                        // 1: contracted fma(r, sum - 4c, c) (one op fewer per point, kernels.hpp)
+  int32_t pad0;
+  // 1-rank rehearsal of a MIDDLE slab (slab_rows_global > 0): this solver owns
+  // rows [slab_row0, slab_row0 + n_rows) of a grid of slab_rows_global rows,
+  // so its bands are interior bands, as on rank 3 of 8 (0: the slab is the grid)
+  int64_t slab_row0;
+  int64_t slab_rows_global;
 };
 
 // ---------------------------------------------------------------- transports
@@ -101,6 +107,18 @@ class Transport {
   // The solver's two field buffers (allocation bases, layout L): transports
   // that map their peers' fields once (IPC) do it here. Collective.
   virtual void attach(void* /*buf0*/, void* /*buf1*/, const SlabLayout& /*L*/, DType /*dt*/) {}
+  // Exchanges that can wait on a device-side gate (a kernel on the stream
+  // spinning on a counter): the fused cycle (kern::plan_fused), whose band
+  // rows are produced by the first items of the still-running interior launch.
+  struct Gate {
+    uint32_t* counter;       // device: band items done (the gate consumes it)
+    uint32_t target;
+    uint64_t timeout_ticks;
+    unsigned int* err;       // host-visible: the wait timed out
+  };
+  virtual bool gates() const { return false; }
+  virtual void exchange_gated(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
+                              const Gate& g);
 };
 
 // RAII bracket of Transport::io_phase.
@@ -371,6 +389,12 @@ class Solver {
   // depths instead of a launch (or graph node) per cycle. HEAT2D_PERSIST:
   // 0 off, 1 on where possible, unset = auto (prepare() times both).
   bool persist_eligible() const;
+  // fused cycles (kern::plan_fused): the exchange gated on the interior
+  // launch's band items (HEAT2D_FUSED=0 disables)
+  bool fused_ok() const;
+  void sent_sides(bool* top, bool* bottom) const;
+  void ensure_err();
+  void ensure_sig();
   const kern::SplitPlan* persist_plan(int k);  // nullptr: too many items to be co-resident
   void ensure_persist_ctl();
   void run_persist(const std::vector<int>& seq, bool trial);
@@ -406,7 +430,7 @@ class Solver {
   double phase_acc_[5] = {};
   PhaseEvents* phase_begin(int kind);
   // the launched, not yet finished cycle (cycle_launch -> cycle_finish)
-  enum class Pending { None, Serial, Concurrent, EdgeFirst };
+  enum class Pending { None, Serial, Concurrent, EdgeFirst, Fused };
   Pending pend_ = Pending::None;
   int pend_k_ = 0;
   int64_t pend_pe_ = -1;  // index into phase_ev_ (timing) or -1
@@ -431,7 +455,10 @@ class Solver {
   uint32_t* d_done_ = nullptr;            // persistent launches: per-item completion counters
   int64_t done_cap_ = 0;
   uint32_t done_base_ = 0;                // their value at the next launch
-  unsigned int* h_err_ = nullptr;         // pinned, host-visible error word of the persistent kernel
+  unsigned int* h_err_ = nullptr;         // pinned, host-visible error word (persistent kernel, exchange gates)
+  uint32_t* d_sig_ = nullptr;             // [0]: band items of the running fused cycle; [1]: trial scratch
+  int64_t pend_sig_ = 0;                  // band items the pending fused cycle signals
+  uint64_t gate_timeout_ticks_ = 0;
   uint64_t persist_timeout_ticks_ = 0;
   hipEvent_t ev_t0_ = nullptr, ev_t1_ = nullptr;  // time_plan
   hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K

@@ -177,7 +177,7 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t simds, int k, int64_t pri
 // partials != nullptr: the fused-statistics kernel (general, ring 4). Returns the waves launched.
 int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
                      const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith,
-                     double* partials = nullptr) {
+                     double* partials = nullptr, int64_t sig_items = 0, uint32_t* sig = nullptr) {
   HEAT2D_REQUIRE(nrect >= 1 && nrect <= kMaxRects, "bad rect count");
   TbArgs a{};
   a.pitch = L.pitch;
@@ -205,6 +205,9 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   a.nitems = items;
   a.nwaves = std::max<int64_t>(1, std::min<int64_t>(nwaves, items));
   a.partials = partials;
+  HEAT2D_REQUIRE(sig_items == 0 || (main && sig != nullptr && sig_items <= items), "bad band-signal items");
+  a.sig_items = sig_items;
+  a.sig = sig;
   const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
   const int64_t o = L.origin();
   if (partials) {
@@ -217,6 +220,22 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
     } else {
       if (arith) dispatch_stats<double, 1>(k, nblocks, s64, static_cast<double*>(dst) + o, a, r, stream);
       else dispatch_stats<double, 0>(k, nblocks, s64, static_cast<double*>(dst) + o, a, r, stream);
+    }
+  } else if (sig) {  // the fused cycle's interior kernel
+    const float* s32 = static_cast<const float*>(src) + o;
+    const double* s64 = static_cast<const double*>(src) + o;
+    float* d32 = static_cast<float*>(dst) + o;
+    double* d64 = static_cast<double*>(dst) + o;
+    if (dt == DType::F32) {
+      if (ring == 4) arith ? dispatch_fused<float, 4, 1>(k, nblocks, s32, d32, a, (float)r, stream)
+                           : dispatch_fused<float, 4, 0>(k, nblocks, s32, d32, a, (float)r, stream);
+      else arith ? dispatch_fused<float, 6, 1>(k, nblocks, s32, d32, a, (float)r, stream)
+                 : dispatch_fused<float, 6, 0>(k, nblocks, s32, d32, a, (float)r, stream);
+    } else {
+      if (ring == 4) arith ? dispatch_fused<double, 4, 1>(k, nblocks, s64, d64, a, r, stream)
+                           : dispatch_fused<double, 4, 0>(k, nblocks, s64, d64, a, r, stream);
+      else arith ? dispatch_fused<double, 6, 1>(k, nblocks, s64, d64, a, r, stream)
+                 : dispatch_fused<double, 6, 0>(k, nblocks, s64, d64, a, r, stream);
     }
   } else if (dt == DType::F32) {
     dispatch_t<float>(ring, main, arith, k, nblocks, static_cast<const float*>(src) + o, static_cast<float*>(dst) + o, a,
@@ -339,6 +358,79 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   return p;
 }
 
+SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool send_top, bool send_bottom, int cus,
+                     int spare_waves, int ring_override, int arith) {
+  check_layout(dt, L, k);
+  SplitPlan p{};
+  p.k = k;
+  p.ring = (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k);
+  const int64_t n = L.nrows, B = std::max<int64_t>(band, k);
+  const int64_t U = useful_width(dt, k);
+  const int64_t ns = (L.ncols + U - 1) / U;
+  const int64_t rows_m = n - 2 * B;
+  if (rows_m < 4 * k) return p;
+  // a band whose march reaches the Dirichlet frame needs the general kernel
+  const bool frame_top = L.row0 < k, frame_bottom = L.row0 + n + k > L.nrows_global;
+  if ((send_top && frame_top) || (send_bottom && frame_bottom)) return p;
+  const int nsig = (send_top ? 1 : 0) + (send_bottom ? 1 : 0);
+  if (nsig == 0) return p;
+  int bpc;
+  if (dt == DType::F32)
+    bpc = p.ring == 4 ? (arith ? occupancy_fused<float, 4, 1>(k) : occupancy_fused<float, 4, 0>(k))
+                      : (arith ? occupancy_fused<float, 6, 1>(k) : occupancy_fused<float, 6, 0>(k));
+  else
+    bpc = p.ring == 4 ? (arith ? occupancy_fused<double, 4, 1>(k) : occupancy_fused<double, 4, 0>(k))
+                      : (arith ? occupancy_fused<double, 6, 1>(k) : occupancy_fused<double, 6, 0>(k));
+  const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
+  const int64_t W = std::max<int64_t>(4, slots - std::max(0, spare_waves));
+  const int64_t Nb = nsig * ns;
+  if (Nb >= W) return p;
+  // per-wave march rows: a band item B + prime, an interior segment of s rows
+  // s + prime; waves w < Nb take one band item and an interior segment of
+  // sA rows, the others one segment of sB rows: sA = sB - (B + prime) ends
+  // every wave together (the fp32 interior kernel skips ~k - 1 priming rows)
+  const double prime = dt == DType::F32 ? std::max(1, k - 1) : 2.0 * k;
+  const double cb = (double)B + prime;
+  const double S_int = (double)rows_m * (double)ns;
+  double sB = (S_int + (double)Nb * cb) / (double)W;
+  double sA = sB - cb;
+  int64_t hA = 0;
+  if (sA > 2.0 * k) hA = std::min<int64_t>(rows_m - 4 * k, (int64_t)((double)Nb * sA / (double)ns + 0.5));
+  if (hA * ns < Nb) hA = 0;  // too few strip rows for one segment per band wave
+  int nf = 0;
+  if (send_top) p.fused[nf++] = TbRect{0, B, 0, ns, 1};
+  if (send_bottom) p.fused[nf++] = TbRect{n - B, n, 0, ns, 1};
+  // item order = wave order of the grid stride (nwaves = W): band items
+  // [0, Nb) on waves 0 .. Nb-1; rect B (rows [B + hA, n - B)), one segment per
+  // wave Nb .. W-1; rect A (rows [B, B + hA)), items W .. W+Nb-1: the second
+  // item of waves 0 .. Nb-1
+  p.fused[nf++] = TbRect{B + hA, n - B, 0, ns, -std::min<int64_t>(W - Nb, (rows_m - hA) * ns)};
+  if (hA > 0) p.fused[nf++] = TbRect{B, B + hA, 0, ns, -Nb};
+  p.nfused = nf;
+  p.sig_items = Nb;
+  p.main = p.fused[nsig];
+  p.main_items = 0;
+  for (int i = 0; i < nf; ++i) p.main_items += p.fused[i].nb > 0 ? p.fused[i].nb * ns : -p.fused[i].nb;
+  p.main_waves = W;
+  // bands on the frame (first / last rank): general kernel, beside the main launch
+  int ne = 0;
+  if (!send_top) p.edge[ne++] = TbRect{0, B, 0, ns, 1};
+  if (!send_bottom) p.edge[ne++] = TbRect{n - B, n, 0, ns, 1};
+  p.nedge = ne;
+  p.edge_items = ne * ns;
+  const int bpc_e = occupancy(dt, p.ring, false, k, arith);
+  p.edge_waves = std::min<int64_t>(std::max<int64_t>(p.edge_items, 1), (int64_t)cu_count() * bpc_e * 4);
+  p.valid = 4;
+  return p;
+}
+
+void launch_fused_main(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, uint32_t* sig,
+                       double r, hipStream_t stream, int arith) {
+  HEAT2D_REQUIRE(p.valid == 4 && p.nfused >= 2 && p.nfused <= 4, "not a fused plan");
+  launch_rects(dt, src, dst, L, p.k, p.ring, true, p.fused, p.nfused, p.main_waves, r, stream, arith, nullptr,
+               p.sig_items, sig);
+}
+
 SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_override, int64_t bands, int arith) {
   check_layout(dt, L, k);
   SplitPlan p{};
@@ -445,6 +537,8 @@ void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, 
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith) {
   HEAT2D_REQUIRE(p.valid, "invalid split plan");
+  HEAT2D_REQUIRE(p.valid != 4 || !main_part, "a fused plan's main part needs its band counter (launch_fused_main)");
+  if (p.valid == 4 && p.nedge == 0) return;  // no band on the frame
   if (p.valid == 2) {  // single general launch over the whole slab (no edge part)
     if (main_part) launch_rects(dt, src, dst, L, p.k, p.ring, false, &p.main, 1, p.main_waves, r, stream, arith);
     return;

@@ -101,6 +101,12 @@ struct TbArgs {
   int32_t xcd_remap;  // 1: XCD-aware block -> wave-id mapping (tb_kernel)
   TbRectArg rect[kMaxRects];
   double* partials;   // ST kernels: per-wave statistics, partials[j * nwaves + wave] (kNStatFused = 6 values)
+  // Fused cycles (MAIN kernel): items [0, sig_items) are the boundary bands a
+  // halo exchange sends. Their rows are stored at device scope and each one
+  // counts itself done in *sig once its stores have drained, so the exchange
+  // (gated on the count) starts while the rest of the launch runs.
+  int64_t sig_items;
+  uint32_t* sig;
 };
 
 // Fused statistics of the stored (last) level (ST kernels): sum T, sum T^2,
@@ -261,9 +267,11 @@ constexpr int chain_len() {
 // CP (cache policy of the field loads / stores): 0 = default (stores nt); 1 =
 // device-coherent (sc1 loads, nt sc1 stores): the values go to / come from the
 // memory side, coherent across the 8 XCDs' L2s without cache maintenance —
-// the persistent kernel's cross-wave hand-off (tb_persist_kernel).
+// the persistent kernel's cross-wave hand-off (tb_persist_kernel); 2 =
+// device-coherent stores only (the band items of a fused cycle, read by the
+// exchange while the launch still runs).
 template <int CP>
-constexpr int kLoadAux = CP ? 16 : 0;
+constexpr int kLoadAux = CP == 1 ? 16 : 0;
 template <int CP>
 constexpr int kStoreAux = CP ? (16 | 2) : HEAT2D_STORE_AUX;
 
@@ -828,12 +836,15 @@ __device__ __forceinline__ double wave_max(double v) {
 // (A third, latency-oriented variant for the boundary-band launch — priming
 // skip + dependency chains — measured slower everywhere and was removed:
 // profiles/edge_kernel.md.)
-constexpr int kVarPlain = 0, kVarStats = 1;
+// 2: the interior kernel of a fused cycle (kern::plan_fused): device-scope
+// row stores, band items counted into TbArgs::sig.
+constexpr int kVarPlain = 0, kVarStats = 1, kVarFused = 2;
 
 template <typename T, int NV, int K, int RING, bool MAIN, int AR, int VAR = kVarPlain>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T, NV, K, RING, MAIN, AR>))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
   constexpr bool ST = VAR == kVarStats;
-  static_assert(VAR == kVarPlain || !MAIN, "the statistics variant uses the general kernel");
+  static_assert(VAR != kVarStats || !MAIN, "the statistics variant uses the general kernel");
+  static_assert(VAR != kVarFused || MAIN, "the fused variant is an interior kernel");
   using S = TbShape<T, NV, K>;
   const int lane = threadIdx.x & 63;
   // readfirstlane: make the wave id (and everything derived from it: strip, rows,
@@ -862,6 +873,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
   while (it < a.nitems) {
     int64_t strip, t0, t1;
     if (!tb_piece(a, it, lin, strip, t0, t1)) {
+      if constexpr (VAR == kVarFused) {
+        if (it < a.sig_items) {  // a band item of a fused cycle is complete: count it
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_fetch_add(a.sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
       it += a.nwaves;
       if (it < a.nitems) lin = tb_span(a, it).lin;
       continue;
@@ -879,10 +896,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
       }
     } else if constexpr (MAIN) {
       constexpr bool PS = std::is_same<T, float>::value;  // priming skip: fp32 interior kernel only
+      // fused variant: every row stored at device scope (one code path, the
+      // plain kernel's registers; a second march instance for the band items
+      // alone cost the fp64 K = 20 interior a wave per SIMD)
+      constexpr int CPX = VAR == kVarFused ? 2 : 0;
       if ((c0 < 0) || (c0 + S::W > a.ncols))
-        march<T, NV, K, 2, RING, AR, false, PS>(src, dst, a, r, strip, t0, t1, lane);
+        march<T, NV, K, 2, RING, AR, false, PS, 0, CPX>(src, dst, a, r, strip, t0, t1, lane);
       else
-        march<T, NV, K, 0, RING, AR, false, PS>(src, dst, a, r, strip, t0, t1, lane);
+        march<T, NV, K, 0, RING, AR, false, PS, 0, CPX>(src, dst, a, r, strip, t0, t1, lane);
     } else {
       const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
                      (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
@@ -1121,6 +1142,11 @@ template <typename T, int RING, bool MAIN, int AR>
 void dispatch(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
 template <typename T, int RING, bool MAIN, int AR>
 int occupancy_blocks(int k);
+// fused-cycle interior kernels (VAR = kVarFused), instantiated beside the MAIN ones
+template <typename T, int RING, int AR>
+void dispatch_fused(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
+template <typename T, int RING, int AR>
+int occupancy_fused(int k);
 // fused-statistics kernels: general kernel, ring 4 (tb_<dtype>_stats.hip)
 template <typename T, int AR>
 void dispatch_stats(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
@@ -1166,6 +1192,36 @@ int occupancy_blocks_stats(int k);
         break;                                                                                          \
     }                                                                                                   \
     return 1;                                                                                           \
+  }
+#define H2D_FU_CASE(T, RING, MAIN, AR, KK)                                                                          \
+  case KK:                                                                                                          \
+    hipLaunchKernelGGL((tb_kernel<T, 1, KK, RING, true, AR, kVarFused>), dim3(nblocks), dim3(256), 0, s, src, dst, a, \
+                       r);                                                                                          \
+    return;
+#define H2D_FU_OCC_CASE(T, RING, MAIN, AR, KK) \
+  case KK:                                     \
+    return blocks_per_cu<T, 1, KK, RING, true, AR, kVarFused>();
+#define H2D_FU_UNIT(T, RING, AR, DEEP)                                                                     \
+  template <>                                                                                              \
+  void dispatch_fused<T, RING, AR>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r,    \
+                                   hipStream_t s) {                                                        \
+    switch (k) {                                                                                           \
+      H2D_TB_CASES(H2D_FU_CASE, T, RING, true, AR)                                                         \
+      DEEP(H2D_FU_CASE, T, RING, true, AR)                                                                 \
+      default:                                                                                             \
+        break;                                                                                             \
+    }                                                                                                      \
+    HEAT2D_REQUIRE(false, "temporal depth not instantiated for the fused interior kernel");                \
+  }                                                                                                        \
+  template <>                                                                                              \
+  int occupancy_fused<T, RING, AR>(int k) {                                                                \
+    switch (k) {                                                                                           \
+      H2D_TB_CASES(H2D_FU_OCC_CASE, T, RING, true, AR)                                                     \
+      DEEP(H2D_FU_OCC_CASE, T, RING, true, AR)                                                             \
+      default:                                                                                             \
+        break;                                                                                             \
+    }                                                                                                      \
+    return 1;                                                                                              \
   }
 #define H2D_TB_UNIT(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_NO_CASES)
 #define H2D_TB_UNIT_F64(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_DEEP)

@@ -129,7 +129,16 @@ bool get_plan(const std::string& ctx, int k, int64_t band, kern::SplitPlan* p, f
   q.edge_items = w[3];
   float t = 0.f;
   in >> t;
-  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4) return false;
+  long long nf = 0, sig = 0;
+  in >> nf;
+  for (auto& e : q.fused) {
+    for (auto& x : r) in >> x;
+    e = kern::TbRect{r[0], r[1], r[2], r[3], r[4]};
+  }
+  in >> sig;
+  q.nfused = (int32_t)nf;
+  q.sig_items = sig;
+  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > 4) return false;
   *p = q;
   *ms = t;
   return true;
@@ -142,6 +151,9 @@ void put_plan(const std::string& ctx, int k, int64_t band, const kern::SplitPlan
   rect(p.main);
   for (const auto& e : p.edge) rect(e);
   o << ' ' << p.main_waves << ' ' << p.edge_waves << ' ' << p.main_items << ' ' << p.edge_items << ' ' << ms;
+  o << ' ' << p.nfused;
+  for (const auto& e : p.fused) rect(e);
+  o << ' ' << p.sig_items;
   store(plan_key(ctx, k, band), o.str());
 }
 

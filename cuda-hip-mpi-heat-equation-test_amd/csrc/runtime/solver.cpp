@@ -38,6 +38,7 @@
 
 #include "heat2d/plan_cache.hpp"
 #include "heat2d/runtime.hpp"
+#include "heat2d/watchdog.hpp"
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
@@ -101,7 +102,14 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
   const int64_t halo = cfg_.halo > 0 ? cfg_.halo : kDefaultHalo;
   HEAT2D_REQUIRE(halo >= K, "halo must be >= temporal depth");
   const SlabRange sr = decompose(cfg_.n_rows, P, rank);
-  L_ = make_layout(sr.nrows, cfg_.n_cols, halo, sr.row0, cfg_.n_rows);
+  if (cfg_.slab_rows_global > 0) {  // 1-rank rehearsal of a middle slab of a bigger grid
+    HEAT2D_REQUIRE(P == 1, "slab_rows_global: single-rank rehearsal only");
+    HEAT2D_REQUIRE(cfg_.slab_row0 >= 0 && cfg_.slab_row0 + cfg_.n_rows <= cfg_.slab_rows_global,
+                   "slab outside the grid");
+    L_ = make_layout(cfg_.n_rows, cfg_.n_cols, halo, cfg_.slab_row0, cfg_.slab_rows_global);
+  } else {
+    L_ = make_layout(sr.nrows, cfg_.n_cols, halo, sr.row0, cfg_.n_rows);
+  }
 
   const size_t bytes = (size_t)L_.elems() * dtype_size(dtype());
   if (hip_) {
@@ -178,6 +186,7 @@ Solver::~Solver() {
     if (d_work_) (void)hipFree(d_work_);
     if (d_part_) (void)hipFree(d_part_);
     if (d_done_) (void)hipFree(d_done_);
+    if (d_sig_) (void)hipFree(d_sig_);
     if (h_err_) (void)hipHostFree(h_err_);
     if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
@@ -197,7 +206,8 @@ Solver::~Solver() {
 }
 
 void Solver::init(const kern::IcParams& ic, const double* xg, const double* yg) {
-  const size_t nx = (size_t)(cfg_.n_rows + 2), ny = (size_t)(cfg_.n_cols + 2);
+  // xg covers the whole grid's rows (frame-inclusive)
+  const size_t nx = (size_t)(std::max(cfg_.n_rows, cfg_.slab_rows_global) + 2), ny = (size_t)(cfg_.n_cols + 2);
   if (hip_) {
     H2D_HIP(hipSetDevice(cfg_.device));
     double* d = nullptr;
@@ -326,6 +336,15 @@ void Solver::cycle_finish() {
   if (pend_ == Pending::Serial) {
     exchange_on(dst, pend_x_, s_compute_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
+  } else if (pend_ == Pending::Fused) {
+    if (tr_->exchanges()) {
+      HEAT2D_REQUIRE(pend_x_ >= 1 && pend_x_ <= band_, "halo exchange depth outside [1, band]");
+      tr_->exchange_gated(dst, L_, dtype(), pend_x_, s_comm_,
+                          Transport::Gate{d_sig_, (uint32_t)pend_sig_, gate_timeout_ticks_, h_err_});
+      halo_rows_ += pend_x_;
+    }
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[5], s_comm_));
+    H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
   } else {
     // both split orders: the exchange of the new bands runs on the comm
     // stream (concurrent: right behind the EDGE launch there; edge-first:
@@ -429,6 +448,13 @@ const kern::SplitPlan& Solver::split_plan(int k) {
       const std::string o = env;
       if (o == "edge-first" && p.valid == 1) p.valid = 3;
       if (o == "concurrent" && p.valid == 3) p.valid = 1;
+      if (o == "fused" && fused_ok()) {
+        bool top, bot;
+        sent_sides(&top, &bot);
+        const kern::SplitPlan f = kern::plan_fused(dtype(), L_, k, k, top, bot, compute_cus_, spare, 0, cfg_.arith);
+        if (f.valid) p = f;
+        p.k = k;
+      }
       if (o == "single" && !tr_->exchanges()) {
         p = kern::plan_single(dtype(), L_, k, compute_cus_, 0, 0, cfg_.arith);
         p.k = k;
@@ -458,6 +484,13 @@ const kern::SplitPlan& Solver::split_plan_banded(int k, int64_t B) {
   if (B <= k || !base.valid || base.valid == 2) return base;
   auto it = banded_.find({k, B});
   if (it != banded_.end()) return it->second;
+  if (base.valid == 4) {  // fused: the same ring, the bands and the interior balance re-cut for B
+    bool top, bot;
+    sent_sides(&top, &bot);
+    kern::SplitPlan d = kern::plan_fused(dtype(), L_, k, B, top, bot, compute_cus_, spare_waves(), base.ring, cfg_.arith);
+    d.k = k;
+    return banded_.emplace(std::make_pair(k, B), d).first->second;
+  }
   // the same choice (order, ring, interior bands / segments) over the interior
   // left between B-row bands; too thin for that: valid = 0 (serial cycle)
   kern::SplitPlan d = kern::plan_split(dtype(), L_, k, B, compute_cus_, spare_waves(), base.ring, base.main.nb,
@@ -507,6 +540,16 @@ void Solver::trial_cycle(const kern::SplitPlan& c) {
   void* src = buf_[cur_];
   void* dst = buf_[cur_ ^ 1];
   last_k_ = 0;  // the other buffer no longer holds T_{n-1}: stats(residual) reports NaN
+  if (c.valid == 4) {  // fused: interior launch (its band items counted into the scratch counter) + frame bands
+    ensure_sig();
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
+    kern::launch_fused_main(dtype(), src, dst, L_, c, d_sig_ + 1, cfg_.r, s_compute_, cfg_.arith);
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_, cfg_.arith);
+    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+    return;
+  }
   if (c.valid == 3) {  // edge-first: both parts in order on the compute stream
     H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
     kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_compute_, cfg_.arith);
@@ -607,8 +650,20 @@ void Solver::autotune_split(int k) {
   // (no exchange): one general launch; mode 3 (exchange): edge-first split —
   // the short band launch first on the whole chip, then the interior, with the
   // exchange of the bands running beside the interior (valid = 3)
-  for (int mode : {1, 2, 3}) {
+  bool top = false, bot = false;
+  sent_sides(&top, &bot);
+  for (int mode : {1, 2, 3, 4}) {
     if (mode == 2 && !single_ok) continue;
+    if (mode == 4) {
+      // fused (exchange gated on the interior launch's band items): like the
+      // edge-first order it needs an interior long enough to hide the exchange
+      if (!fused_ok() || best.valid != 1 || timed.front().first < kEdgeFirstMinCycleMs) continue;
+      for (int ring : {4, 6}) {
+        kern::SplitPlan c = kern::plan_fused(dtype(), L_, k, k, top, bot, compute_cus_, spare, ring, cfg_.arith);
+        if (c.valid) timed.emplace_back(time_plan(c, 4), c);
+      }
+      continue;
+    }
     // the trials run without the exchange, which the edge-first order puts
     // beside the WHOLE interior: only where the interior is long enough to
     // hide it (measured on the 1-rank RCCL rehearsal, profiles/multi_gpu_rehearsal_v4.md:
@@ -676,6 +731,27 @@ void Solver::launch_overlap(int k, int64_t B) {
   roctxRangePushA("heat2d.cycle.split");
   PhaseEvents* pe = timing_ ? phase_begin(0) : nullptr;
   pend_pe_ = pe ? (int64_t)phase_ev_.size() - 1 : -1;
+  if (sp.valid == 4) {
+    // fused: compute stream = [exchange c-1 landed, frame bands c-1 done]
+    // interior launch c, its first items the bands the exchange sends;
+    // comm stream = [interior c-1 done] frame bands c, then (cycle_finish)
+    // the exchange, gated on the band items' count, beside the interior.
+    ensure_sig();
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
+    kern::launch_fused_main(dtype(), src, dst, L_, sp, d_sig_, cfg_.r, s_compute_, cfg_.arith);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
+    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_, cfg_.arith);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[3], s_comm_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+    pend_sig_ = sp.sig_items;
+    pend_ = Pending::Fused;
+    return;
+  }
   if (sp.valid == 3) {
     // edge-first: compute stream = [exchange c-1 landed] bands(c) -> interior(c);
     // comm stream (cycle_finish) = [bands(c) done] exchange(c), beside the interior.
@@ -1325,6 +1401,43 @@ void Solver::prepare_plans(int64_t n) {
   }
 }
 
+bool Solver::fused_ok() const {
+  static const bool env_off = [] {
+    const char* e = std::getenv("HEAT2D_FUSED");
+    return e && std::atoi(e) == 0;
+  }();
+  return hip_ && cfg_.overlap && !cfg_.copy_swap && !jit_ && tr_->exchanges() && tr_->gates() && !env_off &&
+         s_comm_ != s_compute_;
+}
+
+// the bands this rank's exchange sends: toward rank - 1 (top) / rank + 1
+// (bottom); a 1-rank periodic rehearsal sends both
+void Solver::sent_sides(bool* top, bool* bottom) const {
+  const int P = tr_->size(), r = tr_->rank();
+  const bool loop = P == 1 && tr_->exchanges();
+  *top = loop || r > 0;
+  *bottom = loop || r < P - 1;
+}
+
+void Solver::ensure_err() {
+  if (h_err_) return;
+  H2D_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_err_), sizeof(unsigned int), hipHostMallocCoherent));
+  *h_err_ = 0;
+}
+
+void Solver::ensure_sig() {
+  if (d_sig_) return;
+  ensure_err();
+  H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_sig_), 2 * sizeof(uint32_t)));
+  H2D_HIP(hipMemsetAsync(d_sig_, 0, 2 * sizeof(uint32_t), s_compute_));
+  H2D_HIP(hipStreamSynchronize(s_compute_));
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg_.device) != hipSuccess || khz <= 0) khz = 100000;
+  // the watchdog (HEAT2D_COMM_TIMEOUT) normally fires first; this bounds the wave
+  const double to = Watchdog::env_timeout(600.0);
+  gate_timeout_ticks_ = (uint64_t)((to > 0 ? to * 1.5 + 5.0 : 3600.0) * 1e3 * (double)khz);
+}
+
 bool Solver::persist_eligible() const {
   return hip_ && !jit_ && !cfg_.copy_swap && !tr_->exchanges() && persist_mode_ != 0;
 }
@@ -1354,8 +1467,7 @@ void Solver::ensure_persist_ctl() {
   H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_done_), (size_t)done_cap_ * sizeof(uint32_t)));
   H2D_HIP(hipMemsetAsync(d_done_, 0, (size_t)done_cap_ * sizeof(uint32_t), s_compute_));
   done_base_ = 0;
-  H2D_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_err_), sizeof(unsigned int), hipHostMallocCoherent));
-  *h_err_ = 0;
+  ensure_err();
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg_.device) != hipSuccess || khz <= 0) khz = 100000;
   persist_timeout_ticks_ = (uint64_t)khz * 2000;  // 2 s: a healthy wait lasts about one cycle
@@ -1434,6 +1546,9 @@ void Solver::synchronize() {
     }
     H2D_HIP(q);
   }
+  if (h_err_ && __atomic_load_n(h_err_, __ATOMIC_ACQUIRE) != 0)
+    fail(__FILE__, __LINE__, "rank " + std::to_string(tr_->rank()) +
+                                 ": an exchange gate timed out waiting for the interior launch's band items");
   tr_->check();
 }
 

@@ -44,7 +44,7 @@ def _plan(h, k: int) -> dict:
     p, ms = N.SplitPlan(), C.c_float()
     N.call("heat2d_solver_plan", h, int(k), C.byref(p), C.byref(ms))
     return {"k": p.k, "ring": p.ring, "valid": p.valid,
-            "order": {1: "concurrent", 2: "single", 3: "edge-first"}.get(p.valid, "serial"),
+            "order": {1: "concurrent", 2: "single", 3: "edge-first", 4: "fused"}.get(p.valid, "serial"),
             "main_bands": p.main.nb, "main_items": p.main_items, "main_waves": p.main_waves,
             "edge_items": p.edge_items, "edge_waves": p.edge_waves, "tuned_ms": ms.value,
             "main_rect": [p.main.r0, p.main.r1, p.main.s0, p.main.s1, p.main.nb],
@@ -86,6 +86,9 @@ class HeatSolver:
             (-1: only for slabs of >= 2**24 points, 0: off, 1: on).
         rows: solve only the first ``rows`` x-rows of the grid (a rectangular
             rows x n domain, e.g. one rank's slab shape for a 1-GPU rehearsal).
+        slab_row0: with ``rows``: own rows [slab_row0, slab_row0 + rows) of the
+            WHOLE grid instead — a middle rank's slab (its boundary bands are
+            interior bands, as on rank 3 of 8) for 1-GPU rehearsals.
         arith: "exact" — every operation of the reference update rounded as
             written (-ffp-contract=off; bitwise equal to the NumPy golden);
             "fma" — the update contracted to fma(r, sum - 4c, c), what hipcc's
@@ -98,7 +101,8 @@ class HeatSolver:
                  overlap: bool = True, copy_swap: bool = False, managed: bool = False, graph: bool = False,
                  tile_rows: int = 0, halo: int = 0, transport: Optional[T.Transport] = None,
                  device: Optional[int] = None, init: bool = True, rows: Optional[int] = None,
-                 comm_cus: int = 0, autotune: int = -1, engine: str = "tb", arith: str = "auto"):
+                 comm_cus: int = 0, autotune: int = -1, engine: str = "tb", arith: str = "auto",
+                 slab_row0: Optional[int] = None):
         self.problem = problem
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]
@@ -112,6 +116,11 @@ class HeatSolver:
         if rows is not None and not 1 <= rows <= problem.n_owned:
             raise ValueError(f"rows must be in [1, {problem.n_owned}]")
         cfg.n_rows = problem.n_owned if rows is None else int(rows)  # rows < n: the first rows x n of the grid
+        if slab_row0 is not None:  # 1-rank rehearsal of the middle slab rows [slab_row0, slab_row0 + rows)
+            if rows is None or not 0 <= slab_row0 <= problem.n_owned - rows:
+                raise ValueError("slab_row0 needs rows and must keep the slab inside the grid")
+            cfg.slab_row0 = int(slab_row0)
+            cfg.slab_rows_global = problem.n_owned
         cfg.n_cols = problem.n_owned
         cfg.dtype = self.dtype
         cfg.backend = N.BACKEND_HIP if self.backend == "hip" else N.BACKEND_CPU

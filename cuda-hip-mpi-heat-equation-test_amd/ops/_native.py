@@ -77,6 +77,7 @@ class Config(C.Structure):
         ("tile_rows", C.c_int64), ("halo", C.c_int64),
         ("comm_cus", C.c_int32), ("autotune", C.c_int32),
         ("engine", C.c_int32), ("arith", C.c_int32),
+        ("pad0", C.c_int32), ("slab_row0", C.c_int64), ("slab_rows_global", C.c_int64),
     ]
 
 
@@ -89,6 +90,7 @@ class SplitPlan(C.Structure):
         ("k", C.c_int32), ("ring", C.c_int32), ("valid", C.c_int32), ("nedge", C.c_int32),
         ("main", Rect), ("edge", Rect * 4),
         ("main_waves", C.c_int64), ("edge_waves", C.c_int64), ("main_items", C.c_int64), ("edge_items", C.c_int64),
+        ("nfused", C.c_int32), ("pad", C.c_int32), ("fused", Rect * 4), ("sig_items", C.c_int64),
     ]
 
 

@@ -31,7 +31,7 @@ def main():
 
     import heat2d
     from heat2d.models.heat2d import HeatSolver
-    from heat2d.parallel.transport import TorchDistTransport
+    from heat2d.parallel.transport import IpcTransport, TorchDistTransport
 
     from datetime import timedelta
     timeout = float(os.environ.get("HEAT2D_COMM_TIMEOUT", "600"))
@@ -42,10 +42,12 @@ def main():
     backend = args.get("backend", "cpu")
     if backend == "hip":
         torch.cuda.set_device(0)
-    tr = TorchDistTransport()
+    # ipc: process-per-GPU transport (all ranks on GPU 0), host collectives over this gloo group
+    tr = IpcTransport(0) if args.get("transport") == "ipc" else TorchDistTransport()
     tb = args.get("tb_rank", {}).get(str(rank), args.get("tb", 8))  # per-rank override: a deliberate mismatch
     s = HeatSolver(prob, dtype=args.get("dtype", "fp64"), backend=backend, tb=tb,
-                   overlap=args.get("overlap", True), transport=tr, device=0 if backend == "hip" else None)
+                   overlap=args.get("overlap", True), transport=tr, device=0 if backend == "hip" else None,
+                   graph=args.get("graph", False))
     if args.get("random"):  # non-trivial data everywhere: a stale halo cannot hide
         from heat2d.models import reference as R
         T0 = random_field(prob, args.get("dtype", "fp64"))
