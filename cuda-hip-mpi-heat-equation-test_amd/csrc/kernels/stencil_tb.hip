@@ -363,7 +363,9 @@ SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool se
   check_layout(dt, L, k);
   SplitPlan p{};
   p.k = k;
-  p.ring = (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k);
+  // default ring: the fused fp64 K >= 17 interior keeps 2 waves/SIMD only at ring 6
+  p.ring = (ring_override == 4 || ring_override == 6) ? ring_override
+                                                      : (dt == DType::F64 && k >= 17 ? 6 : default_ring(dt, k));
   const int64_t n = L.nrows, B = std::max<int64_t>(band, k);
   const int64_t U = useful_width(dt, k);
   const int64_t ns = (L.ncols + U - 1) / U;

@@ -814,6 +814,38 @@ __device__ __forceinline__ bool tb_piece(const TbArgs& a, int64_t it, int32_t li
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
 constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K >= 11 && K <= 12) ? 4 : 1;
 
+// Rows [t0, t1) of `strip` that this wave just stored: re-read (sc0: past the
+// CU's L1, from the XCD's L2 that holds them) and store again at device scope
+// (nt sc1: written through past the non-coherent L2), 8 rows in flight.
+template <typename T, int NV, int K>
+__device__ __forceinline__ void republish(T* dst, const TbArgs& a, int64_t strip, int64_t t0, int64_t t1, int lane) {
+  using S = TbShape<T, NV, K>;
+  using U4 = unsigned int __attribute__((ext_vector_type(4)));
+  static_assert(NV == 1, "16 B per lane");
+  constexpr int ES = (int)sizeof(T);
+  const int64_t u0 = strip * S::U;
+  const int64_t mycol = u0 - S::KA + (int64_t)lane * S::V;
+  const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
+  const bool ok = mycol >= u0 && mycol < ustop && mycol >= a.col_lo && mycol + S::V <= a.col_hi;
+  const int32_t off = ok ? (int32_t)((mycol - a.col_lo) * ES) : kOob;
+  const char* base = reinterpret_cast<const char*>(dst + a.col_lo);
+  const int64_t pitch_b = a.pitch * ES;
+  constexpr int kChunk = 8;
+  for (int64_t r0 = t0; r0 < t1; r0 += kChunk) {
+    U4 v[kChunk];
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) {
+      const __amdgpu_buffer_rsrc_t rs = row_rsrc(base + (r0 + i) * pitch_b, r0 + i < t1 ? (uint32_t)pitch_b : 0u);
+      v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 1);
+    }
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) {
+      const __amdgpu_buffer_rsrc_t rs = row_rsrc(base + (r0 + i) * pitch_b, r0 + i < t1 ? (uint32_t)pitch_b : 0u);
+      __builtin_amdgcn_raw_buffer_store_b128(v[i], rs, off, 0, 16 | 2);
+    }
+  }
+}
+
 // wave-wide sum / min / max (fixed xor butterfly: every lane ends with the
 // same bits, lane 0's are written)
 __device__ __forceinline__ double wave_sum(double v) {
@@ -840,6 +872,9 @@ __device__ __forceinline__ double wave_max(double v) {
 // row stores, band items counted into TbArgs::sig.
 constexpr int kVarPlain = 0, kVarStats = 1, kVarFused = 2;
 
+// (The fused interior variant's band-item code costs the fp64 K = 20 ring-4
+// kernel 2 VGPRs over 256 — 1 wave/SIMD; a 2-wave floor spilled 28 B to
+// scratch. Its ring-6 twin keeps 2 waves at 245: the autotuner weighs both.)
 template <typename T, int NV, int K, int RING, bool MAIN, int AR, int VAR = kVarPlain>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T, NV, K, RING, MAIN, AR>))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
   constexpr bool ST = VAR == kVarStats;
@@ -896,14 +931,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T
       }
     } else if constexpr (MAIN) {
       constexpr bool PS = std::is_same<T, float>::value;  // priming skip: fp32 interior kernel only
-      // fused variant: every row stored at device scope (one code path, the
-      // plain kernel's registers; a second march instance for the band items
-      // alone cost the fp64 K = 20 interior a wave per SIMD)
-      constexpr int CPX = VAR == kVarFused ? 2 : 0;
       if ((c0 < 0) || (c0 + S::W > a.ncols))
-        march<T, NV, K, 2, RING, AR, false, PS, 0, CPX>(src, dst, a, r, strip, t0, t1, lane);
+        march<T, NV, K, 2, RING, AR, false, PS>(src, dst, a, r, strip, t0, t1, lane);
       else
-        march<T, NV, K, 0, RING, AR, false, PS, 0, CPX>(src, dst, a, r, strip, t0, t1, lane);
+        march<T, NV, K, 0, RING, AR, false, PS>(src, dst, a, r, strip, t0, t1, lane);
+      if constexpr (VAR == kVarFused) {
+        // a band item (single piece): its rows again, written through to the
+        // device-coherent level, for the exchange that reads them while this
+        // launch still runs (storing every row at device scope cost the
+        // interior ~25 %, and a second march instance a wave per SIMD)
+        if (it < a.sig_items) republish<T, NV, K>(dst, a, strip, t0, t1, lane);
+      }
     } else {
       const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
                      (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);

@@ -631,6 +631,18 @@ bool Solver::cached_split(int k) {
   return true;
 }
 
+// Fused plans among the autotuner's candidates: opt-in (HEAT2D_FUSED=1). The
+// trials cannot see the exchange, and end to end the fused cycle measured
+// level with or behind the edge-first order on the rehearsed slabs
+// (profiles/r3/fused_v2/README.md); HEAT2D_SPLIT_ORDER=fused forces it.
+static bool fused_candidates() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_FUSED");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 void Solver::autotune_split(int k) {
   const int spare = spare_waves();
   synchronize();
@@ -657,7 +669,8 @@ void Solver::autotune_split(int k) {
     if (mode == 4) {
       // fused (exchange gated on the interior launch's band items): like the
       // edge-first order it needs an interior long enough to hide the exchange
-      if (!fused_ok() || best.valid != 1 || timed.front().first < kEdgeFirstMinCycleMs) continue;
+      if (!fused_candidates() || !fused_ok() || best.valid != 1 || timed.front().first < kEdgeFirstMinCycleMs)
+        continue;
       for (int ring : {4, 6}) {
         kern::SplitPlan c = kern::plan_fused(dtype(), L_, k, k, top, bot, compute_cus_, spare, ring, cfg_.arith);
         if (c.valid) timed.emplace_back(time_plan(c, 4), c);
@@ -1402,13 +1415,9 @@ void Solver::prepare_plans(int64_t n) {
 }
 
 bool Solver::fused_ok() const {
-  static const bool env_off = [] {
-    const char* e = std::getenv("HEAT2D_FUSED");
-    return e && std::atoi(e) == 0;
-  }();
-  return hip_ && cfg_.overlap && !cfg_.copy_swap && !jit_ && tr_->exchanges() && tr_->gates() && !env_off &&
-         s_comm_ != s_compute_;
+  return hip_ && cfg_.overlap && !cfg_.copy_swap && !jit_ && tr_->exchanges() && tr_->gates() && s_comm_ != s_compute_;
 }
+
 
 // the bands this rank's exchange sends: toward rank - 1 (top) / rank + 1
 // (bottom); a 1-rank periodic rehearsal sends both
