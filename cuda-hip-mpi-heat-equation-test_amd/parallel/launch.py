@@ -10,6 +10,8 @@ native engine. One process per GPU:
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m heat2d input.dat   # 8 GPUs, RCCL
     torchrun --nproc-per-node 4 -m heat2d input.dat --backend cpu              # 4 CPU ranks, gloo
 
+    torchrun --nproc-per-node 2 -m heat2d input.dat --transport peer --share-gpu  # 2 ranks, 1 GPU, hipIpc
+
 Extras: --tb K, --dtype, --check-every N (global sum / residual, NaN abort),
 --checkpoint DIR --checkpoint-every N, --restart DIR, --json FILE, --output npy.
 """
@@ -50,21 +52,27 @@ def build_parser():
     ap.add_argument("--checkpoint-every", type=int, default=0)
     ap.add_argument("--restart", default=None)
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "peer"],
+                    help="halo exchange between GPU rank processes: rccl (RCCL send/recv) or peer (hipIpc "
+                         "mappings of the neighbours' fields, stream-ordered by host-shared counters; host "
+                         "collectives over gloo)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank on GPU 0 (needs --transport peer): the multi-process path on one GPU")
     return ap
 
 
-def _dist_setup(backend: str):
+def _dist_setup(backend: str, peer: bool = False, share_gpu: bool = False):
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if backend == "hip":
         torch.cuda.set_device(local)
     if world > 1 and not dist.is_initialized():
         from datetime import timedelta
         to = timedelta(seconds=float(os.environ.get("HEAT2D_COMM_TIMEOUT", "600")))  # dead peer -> error, not hang
-        if backend == "hip":
+        if backend == "hip" and not peer:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=to)
         else:
             dist.init_process_group("gloo", timeout=to)
@@ -81,7 +89,10 @@ def run(argv=None) -> int:
     from heat2d.utils.config import make_problem, read_input
 
     backend = resolve_backend(a.backend)
-    rank, world, local = _dist_setup(backend)
+    if a.share_gpu and a.transport != "peer":
+        raise SystemExit("--share-gpu needs --transport peer (RCCL refuses two ranks on one GPU)")
+    peer = a.transport == "peer" and backend == "hip"
+    rank, world, local = _dist_setup(backend, peer, a.share_gpu)
     root = rank == 0
     inp = read_input(a.input)
     if a.n:
@@ -104,7 +115,10 @@ def run(argv=None) -> int:
         print(lim["MAX_THREADS_PER_BLOCK"])
         print(" device limits: " + " ".join(f"{k}={v}" for k, v in lim.items()), flush=True)
     if world > 1:
-        tr = T.RcclTransport(rank, world, local) if backend == "hip" else T.TorchDistTransport()
+        if backend != "hip":
+            tr = T.TorchDistTransport()
+        else:
+            tr = T.IpcTransport(local) if peer else T.RcclTransport(rank, world, local)
     else:
         tr = T.SelfTransport()
     engine = a.engine or ("jit" if var.name == "pycuda" and backend == "hip" else "tb")
@@ -169,7 +183,7 @@ def run(argv=None) -> int:
     s.synchronize()
     _barrier(world)
     elapsed = time.perf_counter() - t0
-    elapsed = _max_over_ranks(elapsed, world, backend)
+    elapsed = _max_over_ranks(elapsed, world, "hip" if backend == "hip" and not peer else "cpu")
     ran = nsteps - start_step
     cycles = s.cycle_hist()
 

@@ -240,3 +240,27 @@ def test_checkpoint_resave_same_step_never_overwrites(native, tmp_path, writer):
     s = HeatSolver(prob, dtype="fp64", backend="cpu", tb=3)
     checkpoint.load(s, str(ck))
     assert np.array_equal(s.download(), R.owned(R.ftcs(prob)))
+
+
+def test_share_gpu_needs_peer_transport(native, tmp_path):
+    (tmp_path / "input.dat").write_text("20 0.25 0.05 1.0 3 0\n")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, "-m", "heat2d", "--backend", "cpu", "--share-gpu"], cwd=tmp_path, env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "--share-gpu needs --transport peer" in out.stderr
+
+
+@pytest.mark.gpu
+def test_torchrun_peer_transport_share_gpu_checkpoint(native, gpu, tmp_path):
+    """`python -m heat2d --transport peer --share-gpu` under torchrun: rank
+    processes on one GPU, halos over hipIpc mappings; a 3-rank run checkpoints
+    at step 12 and a 2-rank run resumes it — bitwise == the NumPy golden."""
+    (tmp_path / "input.dat").write_text("200 0.25 0.05 1.0 37 1\n")
+    flags = ("--backend", "hip", "--transport", "peer", "--share-gpu", "--arith", "exact")
+    py(tmp_path, *flags, "--ntime", "12", "--checkpoint", "ck", "--output", "none", nproc=3)
+    assert ck_meta(tmp_path / "ck")["nranks"] == 3
+    out = py(tmp_path, *flags, "--restart", "ck", nproc=2)
+    assert "Automatic MPI decomposition:            2  x 1" in out
+    T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
