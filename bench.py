@@ -44,12 +44,12 @@ sys.path.insert(0, _ROOT)
 REF_GPTS_PER_RANK = 50.0  # BASELINE.md derived ceiling, 1 MI250X GCD, fp64
 
 
-def N_arith(r, arith):
-    """1 if the run uses the contracted update (see --arith)."""
+def arith_name(r, arith):
+    """The update form the run uses (see --arith)."""
     import math
     if arith == "auto":
-        return r > 0 and math.frexp(r)[0] == 0.5
-    return arith == "fma"
+        return "fma" if r > 0 and math.frexp(r)[0] == 0.5 else "exact"
+    return arith
 
 
 def _free_port():
@@ -128,9 +128,10 @@ def main():
                     help="largest time-step depth fused per HBM pass (0: every depth the kernels have, fp64 24 / "
                          "fp32 16; prepare() picks the cycle schedule of the timed steps by measurement)")
     ap.add_argument("--tile-rows", type=int, default=0)
-    ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma"],
+    ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma", "jacobi"],
                     help="fma: contracted update (one op fewer per point); exact: every op rounded; auto: fma when "
-                         "bitwise identical to exact (r a power of two, as here), else exact")
+                         "bitwise identical to exact (r a power of two, as here), else exact; jacobi: r == 1/4 "
+                         "only, r * (S + E + N + W) (3 adds per point; bitwise == exact on this benchmark's IC)")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="replay the timed schedule from one hipGraph captured in prepare() (auto: single-rank runs, "
@@ -309,7 +310,7 @@ def main():
                 "schedule": "measured" if s.schedule(args.steps) else "balanced",
                 "prepare_s": round(prepare_s, 2),
                 "plan_cache": {"hits": s.plan_cache_hits, "path": N.plan_cache_path()} if hip else None,
-                "arith": ("fma" if N_arith(prob.r, args.arith) else "exact") + (" (auto)" if args.arith == "auto" else ""),
+                "arith": arith_name(prob.r, args.arith) + (" (auto)" if args.arith == "auto" else ""),
                 "overlap": not args.no_overlap,
                 "graph": bool(graph),
                 "launch_plans": plans or None,

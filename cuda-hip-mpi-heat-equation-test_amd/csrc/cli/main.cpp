@@ -58,7 +58,7 @@ struct Args {
   bool quiet = false;
   bool timers = false;
   std::string engine = "tb";
-  std::string arith = "auto";  // auto | exact | fma (SolverConfig::arith; auto: fma iff bitwise-identical)
+  std::string arith = "auto";  // auto | exact | fma | jacobi (SolverConfig::arith; auto: fma iff bitwise-identical)
   std::string checkpoint;       // --checkpoint DIR (utils/checkpoint.py format)
   int64_t checkpoint_every = 0;
   std::string restart;          // --restart DIR (any writer rank count)
@@ -72,7 +72,7 @@ void usage() {
       "usage: heat2d [input.dat] [--variant mpi|serial|cuda] [--gpus N | --cpu] [--dtype fp64|fp32]\n"
       "              [--tb K] [--no-overlap] [--copy-swap] [--managed] [--graph] [--ic NAME]\n"
       "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
-      "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith auto|exact|fma]\n"
+      "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith auto|exact|fma|jacobi]\n"
       "              [--checkpoint DIR [--checkpoint-every N]] [--restart DIR]\n"
       "              [--transport rccl|peer] [--share-gpu] [--autotune auto|on|off]\n");
 }
@@ -233,9 +233,9 @@ void run_rank(Shared& sh, int rank) {
     cfg.autotune = a.autotune;
     if (a.engine != "tb" && a.engine != "jit") fail(__FILE__, __LINE__, "--engine must be tb or jit");
     cfg.engine = a.engine == "jit" ? 1 : 0;  // jit: hipRTC kernel rendered for this slab (python/cuda/cuda.py)
-    if (a.arith != "exact" && a.arith != "fma" && a.arith != "auto")
-      fail(__FILE__, __LINE__, "--arith must be auto, exact or fma");
-    cfg.arith = a.arith == "fma" ? 1 : (a.arith == "exact" ? 0 : -1);
+    if (a.arith != "exact" && a.arith != "fma" && a.arith != "jacobi" && a.arith != "auto")
+      fail(__FILE__, __LINE__, "--arith must be auto, exact, fma or jacobi");
+    cfg.arith = a.arith == "jacobi" ? 2 : a.arith == "fma" ? 1 : (a.arith == "exact" ? 0 : -1);
     Solver s(cfg, tr);
     s.init(sh.prob.ic, sh.prob.x.data(), sh.prob.x.data());
     const bool inclusive = sh.prob.conv == Convention::Inclusive;

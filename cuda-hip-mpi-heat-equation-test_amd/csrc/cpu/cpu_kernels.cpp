@@ -68,6 +68,11 @@ void row_fma_sw(const T* up, const T* mid, const T* dn, T* out, int64_t n, T r) 
     out[j] = std::fma(r, sum - T(4) * mid[j], mid[j]);
   }
 }
+// arith 2 (r == 1/4): the centre weight 1 - 4r is zero, r * sum (r*x exact)
+template <typename T>
+void row_jacobi(const T* up, const T* mid, const T* dn, T* out, int64_t n, T r) {
+  for (int64_t j = 0; j < n; ++j) out[j] = r * (((dn[j] + mid[j + 1]) + up[j]) + mid[j - 1]);
+}
 bool host_has_fma() {
   static const bool v = __builtin_cpu_supports("fma");
   return v;
@@ -84,7 +89,9 @@ void tb_impl(const T* src, T* dst, const SlabLayout& L, int64_t rb, int64_t re, 
   const int64_t c = L.cpad;
   T* a = A.data();
   T* b = B.data();
-  auto* row_update = arith == 1 ? (host_has_fma() ? &row_fma_hw<T> : &row_fma_sw<T>) : &row_exact<T>;
+  auto* row_update = arith == 2   ? &row_jacobi<T>
+                     : arith == 1 ? (host_has_fma() ? &row_fma_hw<T> : &row_fma_sw<T>)
+                                  : &row_exact<T>;
   for (int s = 1; s <= k; ++s) {
     parallel_rows(s, R - s, [&](int64_t lb, int64_t le) {
       for (int64_t li = lb; li < le; ++li) {
@@ -184,7 +191,8 @@ int num_threads() {
 void tb(DType dt, const void* src, void* dst, const SlabLayout& L, int64_t row_begin, int64_t row_end,
         int k, double r, int arith) {
   HEAT2D_REQUIRE(k >= 1 && k <= L.halo, "k out of range");
-  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 or 1");
+  HEAT2D_REQUIRE(arith >= 0 && arith <= 2, "arith must be 0, 1 or 2");
+  HEAT2D_REQUIRE(arith != 2 || r == 0.25, "arith 2 (jacobi) needs r == 1/4 exactly");
   if (row_end <= row_begin) return;
   if (dt == DType::F32)
     tb_impl<float>(static_cast<const float*>(src), static_cast<float*>(dst), L, row_begin, row_end, k, (float)r, arith);

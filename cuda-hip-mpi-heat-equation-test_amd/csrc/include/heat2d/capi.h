@@ -32,7 +32,7 @@ typedef struct heat2d_config {
   int32_t tb, overlap, copy_swap, managed, device, use_graph;
   int64_t tile_rows, halo;
   int32_t comm_cus, autotune;
-  int32_t engine, arith; /* arith: 0 reference rounding, 1 contracted fma */
+  int32_t engine, arith; /* arith: 0 reference rounding, 1 contracted fma, 2 jacobi (r = 1/4) */
   int32_t pad0;
   int64_t slab_row0, slab_rows_global; /* 1-rank rehearsal of a middle slab (0: the slab is the grid) */
 } heat2d_config;

@@ -31,8 +31,9 @@ struct TbPlan {
 // tile_rows == 0 selects the occupancy-driven row bands, > 0 bands of that many
 // rows, < 0 -tile_rows segments (TbRect nb < 0; ntiles = -segments); cus > 0 plans for a
 // stream restricted to that many CUs (comm-reserving CU mask).
-// arith: 0 = reference arithmetic (every op rounded), 1 = contracted fma form
-// (tb_impl.hpp, March); every launcher below takes it last.
+// arith: 0 = reference arithmetic (every op rounded), 1 = contracted fma form,
+// 2 = r == 1/4: (S + E + N + W) / 4 (tb_impl.hpp, March); every launcher below
+// takes it last.
 TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end, int k,
                int64_t tile_rows = 0, int cus = 0, int arith = 0);
 

@@ -47,7 +47,8 @@ struct SolverConfig {
                        // (-1 auto: on for slabs >= 2^24 points, 0 off, 1 on)
   int32_t engine;      // 0: temporal-blocked kernels; 1: run-time specialised hipRTC kernel (K = 1, jit.hpp)
   int32_t arith;       // 0: reference arithmetic, every op rounded (bitwise == NumPy golden);
-                       // 1: contracted fma(r, sum - 4c, c) (one op fewer per point, kernels.hpp)
+                       // 1: contracted fma(r, sum - 4c, c) (one op fewer per point, kernels.hpp);
+                       // 2: r == 1/4 only: r * sum (zero centre weight: 3 adds per point, tb_impl.hpp)
   int32_t pad0;
   // 1-rank rehearsal of a MIDDLE slab (slab_rows_global > 0): this solver owns
   // rows [slab_row0, slab_row0 + n_rows) of a grid of slab_rows_global rows,

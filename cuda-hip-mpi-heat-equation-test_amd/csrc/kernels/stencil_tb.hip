@@ -32,7 +32,12 @@
 //     reference and to an unblocked K=1 run, in fp64 and in fp32. arith = 1
 //     selects the contracted form fma(r, sum - 4c, c) (one op fewer per point;
 //     bitwise equal to its CPU twin; equal to arith 0 when r is a power of two).
+//     arith = 2 (r == 1/4 only): ((((S + E) + N) + W)) / 4, the update with its
+//     zero centre weight folded away — 3 adds + 2 DPP moves per interior point
+//     and level (levels carried scaled by 4^level, tb_impl.hpp); bitwise equal
+//     to its CPU twin, and to arith 0 on data where sum - 4c is exact.
 #include <cmath>
+#include <type_traits>
 
 #include "tb_impl.hpp"
 
@@ -88,6 +93,17 @@ int default_ring(DType dt, int k) {
   return (k == 10 || k == 11) ? 6 : 4;
 }
 
+// arith code -> the kernels' AR template argument (0 reference rounding,
+// 1 contracted fma, 2 r = 1/4: tb_impl.hpp); f is called with
+// std::integral_constant<int, AR>.
+template <class F>
+decltype(auto) with_ar(int arith, F&& f) {
+  HEAT2D_REQUIRE(arith >= 0 && arith <= 2, "arith must be 0 (exact), 1 (fma) or 2 (r = 1/4)");
+  if (arith == 2) return f(std::integral_constant<int, 2>{});
+  if (arith == 1) return f(std::integral_constant<int, 1>{});
+  return f(std::integral_constant<int, 0>{});
+}
+
 template <typename T, int AR>
 int occupancy_t(int ring, bool main, int k) {
   if (ring == 4) return main ? occupancy_blocks<T, 4, true, AR>(k) : occupancy_blocks<T, 4, false, AR>(k);
@@ -95,15 +111,17 @@ int occupancy_t(int ring, bool main, int k) {
 }
 
 int occupancy_stats(DType dt, int k, int arith) {
-  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 (exact) or 1 (fma)");
-  if (dt == DType::F32) return arith ? occupancy_blocks_stats<float, 1>(k) : occupancy_blocks_stats<float, 0>(k);
-  return arith ? occupancy_blocks_stats<double, 1>(k) : occupancy_blocks_stats<double, 0>(k);
+  return with_ar(arith, [&](auto ar) {
+    constexpr int AR = decltype(ar)::value;
+    return dt == DType::F32 ? occupancy_blocks_stats<float, AR>(k) : occupancy_blocks_stats<double, AR>(k);
+  });
 }
 
 int occupancy(DType dt, int ring, bool main, int k, int arith) {
-  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 (exact) or 1 (fma)");
-  if (dt == DType::F32) return arith ? occupancy_t<float, 1>(ring, main, k) : occupancy_t<float, 0>(ring, main, k);
-  return arith ? occupancy_t<double, 1>(ring, main, k) : occupancy_t<double, 0>(ring, main, k);
+  return with_ar(arith, [&](auto ar) {
+    constexpr int AR = decltype(ar)::value;
+    return dt == DType::F32 ? occupancy_t<float, AR>(ring, main, k) : occupancy_t<double, AR>(ring, main, k);
+  });
 }
 
 template <typename T, int AR>
@@ -121,9 +139,7 @@ void dispatch_ar(int ring, bool main, int k, unsigned nblocks, const T* s, T* d,
 template <typename T>
 void dispatch_t(int ring, bool main, int arith, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
                 hipStream_t st) {
-  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 (exact) or 1 (fma)");
-  if (arith) dispatch_ar<T, 1>(ring, main, k, nblocks, s, d, a, r, st);
-  else dispatch_ar<T, 0>(ring, main, k, nblocks, s, d, a, r, st);
+  with_ar(arith, [&](auto ar) { dispatch_ar<T, decltype(ar)::value>(ring, main, k, nblocks, s, d, a, r, st); });
 }
 
 void check_layout(DType dt, const SlabLayout& L, int k) {
@@ -214,29 +230,26 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
     HEAT2D_REQUIRE(a.nwaves <= max_stats_waves(), "statistics partials buffer too small");
     const float* s32 = static_cast<const float*>(src) + o;
     const double* s64 = static_cast<const double*>(src) + o;
-    if (dt == DType::F32) {
-      if (arith) dispatch_stats<float, 1>(k, nblocks, s32, static_cast<float*>(dst) + o, a, (float)r, stream);
-      else dispatch_stats<float, 0>(k, nblocks, s32, static_cast<float*>(dst) + o, a, (float)r, stream);
-    } else {
-      if (arith) dispatch_stats<double, 1>(k, nblocks, s64, static_cast<double*>(dst) + o, a, r, stream);
-      else dispatch_stats<double, 0>(k, nblocks, s64, static_cast<double*>(dst) + o, a, r, stream);
-    }
+    with_ar(arith, [&](auto ar) {
+      constexpr int AR = decltype(ar)::value;
+      if (dt == DType::F32) dispatch_stats<float, AR>(k, nblocks, s32, static_cast<float*>(dst) + o, a, (float)r, stream);
+      else dispatch_stats<double, AR>(k, nblocks, s64, static_cast<double*>(dst) + o, a, r, stream);
+    });
   } else if (sig) {  // the fused cycle's interior kernel
     const float* s32 = static_cast<const float*>(src) + o;
     const double* s64 = static_cast<const double*>(src) + o;
     float* d32 = static_cast<float*>(dst) + o;
     double* d64 = static_cast<double*>(dst) + o;
-    if (dt == DType::F32) {
-      if (ring == 4) arith ? dispatch_fused<float, 4, 1>(k, nblocks, s32, d32, a, (float)r, stream)
-                           : dispatch_fused<float, 4, 0>(k, nblocks, s32, d32, a, (float)r, stream);
-      else arith ? dispatch_fused<float, 6, 1>(k, nblocks, s32, d32, a, (float)r, stream)
-                 : dispatch_fused<float, 6, 0>(k, nblocks, s32, d32, a, (float)r, stream);
-    } else {
-      if (ring == 4) arith ? dispatch_fused<double, 4, 1>(k, nblocks, s64, d64, a, r, stream)
-                           : dispatch_fused<double, 4, 0>(k, nblocks, s64, d64, a, r, stream);
-      else arith ? dispatch_fused<double, 6, 1>(k, nblocks, s64, d64, a, r, stream)
-                 : dispatch_fused<double, 6, 0>(k, nblocks, s64, d64, a, r, stream);
-    }
+    with_ar(arith, [&](auto ar) {
+      constexpr int AR = decltype(ar)::value;
+      if (dt == DType::F32) {
+        if (ring == 4) dispatch_fused<float, 4, AR>(k, nblocks, s32, d32, a, (float)r, stream);
+        else dispatch_fused<float, 6, AR>(k, nblocks, s32, d32, a, (float)r, stream);
+      } else {
+        if (ring == 4) dispatch_fused<double, 4, AR>(k, nblocks, s64, d64, a, r, stream);
+        else dispatch_fused<double, 6, AR>(k, nblocks, s64, d64, a, r, stream);
+      }
+    });
   } else if (dt == DType::F32) {
     dispatch_t<float>(ring, main, arith, k, nblocks, static_cast<const float*>(src) + o, static_cast<float*>(dst) + o, a,
                       (float)r, stream);
@@ -376,13 +389,11 @@ SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool se
   if ((send_top && frame_top) || (send_bottom && frame_bottom)) return p;
   const int nsig = (send_top ? 1 : 0) + (send_bottom ? 1 : 0);
   if (nsig == 0) return p;
-  int bpc;
-  if (dt == DType::F32)
-    bpc = p.ring == 4 ? (arith ? occupancy_fused<float, 4, 1>(k) : occupancy_fused<float, 4, 0>(k))
-                      : (arith ? occupancy_fused<float, 6, 1>(k) : occupancy_fused<float, 6, 0>(k));
-  else
-    bpc = p.ring == 4 ? (arith ? occupancy_fused<double, 4, 1>(k) : occupancy_fused<double, 4, 0>(k))
-                      : (arith ? occupancy_fused<double, 6, 1>(k) : occupancy_fused<double, 6, 0>(k));
+  const int bpc = with_ar(arith, [&](auto ar) {
+    constexpr int AR = decltype(ar)::value;
+    if (dt == DType::F32) return p.ring == 4 ? occupancy_fused<float, 4, AR>(k) : occupancy_fused<float, 6, AR>(k);
+    return p.ring == 4 ? occupancy_fused<double, 4, AR>(k) : occupancy_fused<double, 6, AR>(k);
+  });
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
   const int64_t W = std::max<int64_t>(4, slots - std::max(0, spare_waves));
   const int64_t Nb = nsig * ns;
@@ -455,14 +466,11 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
 
 int64_t persist_capacity(DType dt, int ring, int k, int arith) {
   HEAT2D_REQUIRE(ring == 4 || ring == 6, "ring must be 4 or 6");
-  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 or 1");
-  int bpc;
-  if (dt == DType::F32)
-    bpc = ring == 4 ? (arith ? occupancy_persist<float, 4, 1>(k) : occupancy_persist<float, 4, 0>(k))
-                    : (arith ? occupancy_persist<float, 6, 1>(k) : occupancy_persist<float, 6, 0>(k));
-  else
-    bpc = ring == 4 ? (arith ? occupancy_persist<double, 4, 1>(k) : occupancy_persist<double, 4, 0>(k))
-                    : (arith ? occupancy_persist<double, 6, 1>(k) : occupancy_persist<double, 6, 0>(k));
+  const int bpc = with_ar(arith, [&](auto ar) {
+    constexpr int AR = decltype(ar)::value;
+    if (dt == DType::F32) return ring == 4 ? occupancy_persist<float, 4, AR>(k) : occupancy_persist<float, 6, AR>(k);
+    return ring == 4 ? occupancy_persist<double, 4, AR>(k) : occupancy_persist<double, 6, AR>(k);
+  });
   return (int64_t)cu_count() * bpc * 4;
 }
 
@@ -500,23 +508,20 @@ void launch_tb_persist(DType dt, void* buf0, void* buf1, const SlabLayout& L, co
   p.err = ctl.err;
   const unsigned nblocks = (unsigned)((a.nitems + 3) / 4);
   const int64_t o = L.origin();
-  hipError_t e;
-  if (dt == DType::F32) {
-    float* f0 = static_cast<float*>(buf0) + o;
-    float* f1 = static_cast<float*>(buf1) + o;
-    const float rf = (float)r;
-    if (plan.ring == 4) e = arith ? dispatch_persist<float, 4, 1>(k, nblocks, f0, f1, a, rf, p, stream)
-                                  : dispatch_persist<float, 4, 0>(k, nblocks, f0, f1, a, rf, p, stream);
-    else e = arith ? dispatch_persist<float, 6, 1>(k, nblocks, f0, f1, a, rf, p, stream)
-                   : dispatch_persist<float, 6, 0>(k, nblocks, f0, f1, a, rf, p, stream);
-  } else {
+  const hipError_t e = with_ar(arith, [&](auto ar) {
+    constexpr int AR = decltype(ar)::value;
+    if (dt == DType::F32) {
+      float* f0 = static_cast<float*>(buf0) + o;
+      float* f1 = static_cast<float*>(buf1) + o;
+      const float rf = (float)r;
+      return plan.ring == 4 ? dispatch_persist<float, 4, AR>(k, nblocks, f0, f1, a, rf, p, stream)
+                            : dispatch_persist<float, 6, AR>(k, nblocks, f0, f1, a, rf, p, stream);
+    }
     double* d0 = static_cast<double*>(buf0) + o;
     double* d1 = static_cast<double*>(buf1) + o;
-    if (plan.ring == 4) e = arith ? dispatch_persist<double, 4, 1>(k, nblocks, d0, d1, a, r, p, stream)
-                                  : dispatch_persist<double, 4, 0>(k, nblocks, d0, d1, a, r, p, stream);
-    else e = arith ? dispatch_persist<double, 6, 1>(k, nblocks, d0, d1, a, r, p, stream)
-                   : dispatch_persist<double, 6, 0>(k, nblocks, d0, d1, a, r, p, stream);
-  }
+    return plan.ring == 4 ? dispatch_persist<double, 4, AR>(k, nblocks, d0, d1, a, r, p, stream)
+                          : dispatch_persist<double, 6, AR>(k, nblocks, d0, d1, a, r, p, stream);
+  });
   if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("persistent launch: ") + hipGetErrorString(e));
 }
 

@@ -1,0 +1,12 @@
+// Instantiation unit: interior kernel of the fused cycle (float, ring 4, arithmetic
+// AR = 2; device-scope row stores, band items counted for the gated exchange —
+// tb_impl.hpp kVarFused, stencil_tb.hip plan_fused).
+#include "tb_impl.hpp"
+
+namespace heat2d {
+namespace kern {
+namespace tbimpl {
+H2D_FU_UNIT(float, 4, 2, H2D_NO_CASES)
+}  // namespace tbimpl
+}  // namespace kern
+}  // namespace heat2d

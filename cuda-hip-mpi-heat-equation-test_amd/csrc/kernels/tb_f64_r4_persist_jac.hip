@@ -1,0 +1,12 @@
+// Instantiation unit: persistent multi-cycle temporal-blocked stencil (double, ring 4,
+// arithmetic AR = 2; one co-resident wave per item, neighbour-counter sync between
+// cycles — see tb_impl.hpp tb_persist_kernel).
+#include "tb_impl.hpp"
+
+namespace heat2d {
+namespace kern {
+namespace tbimpl {
+H2D_PS_UNIT(double, 4, 2, H2D_TB_CASES_DEEP)
+}  // namespace tbimpl
+}  // namespace kern
+}  // namespace heat2d

@@ -190,6 +190,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uin
 // fewer per point (5 fp64 ops + 2 DPP moves instead of 6 + 2) for a kernel that
 // is VALU-co-bound. When r is a power of two (sigma = 0.25 in every shipped
 // input) r*x is exact and both forms round identically (normal range).
+// 2 = r == 1/4 exactly (sigma = 0.25: the reference configuration): the centre
+// weight 1 - 4r is zero and the update is T' = (((S + E) + N) + W) / 4, the
+// reference's own sum with one exact multiply. Kind-0 items (no pinned point:
+// the bulk of every launch) carry level s scaled by 4^s, so a level is the
+// plain sum — 3 adds + 2 DPP moves per point instead of 5 + 2 — and multiply by
+// 4^-K once, at the store (powers of two: exact, so the stored bits equal the
+// per-level /4 form for |T| < 2^(emax - 2K)). Pinned kinds (re = 0 where
+// pinned) compute re * sum + (C - 4 re C): the second term is exactly 0 at
+// updated points and C at pinned ones — the same bits. Where every (sum, 4C)
+// pair lies within a factor of two (smooth positive data, e.g. the reference IC
+// with values in [1, 2]), sum - 4C is exact (Sterbenz) and the reference
+// rounding gives the same bits too.
+template <typename T>
+constexpr T inv_pow4(int l) {
+  T s = T(1);
+  for (int i = 0; i < l; ++i) s *= T(0.25);
+  return s;
+}
 // Dependency chains of the march (CL levels per chain). Level s computes
 // row m + off(s) while the march is at level-0 row m. Inside a chain (delta 1)
 // level s reads level s-1's row of THIS iteration — a serial dependency, K
@@ -297,6 +315,7 @@ struct March {
   int32_t ld_off;    // per-lane load byte offset (kOob outside the allocation)
   int32_t st_off;    // per-lane vector store offset (kOob unless the lane holds output columns)
   T rl[(EK & 2) ? V : 1];  // EK & 2: r per element, 0 in Dirichlet / pad columns
+  static constexpr bool kScaled = AR == 2 && EK == 0;  // levels carried x 4^level (AR 2)
 
   using Ch = ChainShape<K, CL>;
   static constexpr int L = Ch::unroll(RING);  // march rows per loop body
@@ -359,8 +378,17 @@ struct March {
       else if constexpr (EK == 1) re = rs;
       else if constexpr (EK == 2) re = rl[e];
       else re = frame_row ? T(0) : rl[e];
-      if constexpr (AR == 1) out[e] = fma_t(re, fma_t(T(-4), C[e], sum), C[e]);
-      else out[e] = C[e] + re * fma_t(T(-4), C[e], sum);
+      if constexpr (AR == 2) {
+        // scaled kind 0: the plain sum (4^s T); pinned kinds (re = 0 where
+        // pinned): re * sum + (C - 4 re C), whose second term is exactly 0 at
+        // updated points (re = 1/4) and C at pinned ones
+        if constexpr (EK == 0) out[e] = sum;
+        else out[e] = fma_t(re, sum, fma_t(re, T(-4) * C[e], C[e]));
+      } else if constexpr (AR == 1) {
+        out[e] = fma_t(re, fma_t(T(-4), C[e], sum), C[e]);
+      } else {
+        out[e] = C[e] + re * fma_t(T(-4), C[e], sum);
+      }
     }
   }
 
@@ -415,11 +443,16 @@ struct March {
       } else {
         const int32_t row = m + Ch::off(K);
         const bool live = row < t1 && row >= t0;  // wave-uniform
+        if constexpr (kScaled) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) out[e] *= inv_pow4<T>(K);
+        }
         store_row(row, live, out);
         if constexpr (ST) {
           if (live) {
+            constexpr T cu = kScaled ? inv_pow4<T>(K - 1) : T(1);  // level K-1 scale
 #pragma unroll
-            for (int e = 0; e < V; ++e) acc.add((colmask >> e) & 1u, (double)out[e], (double)C[e]);
+            for (int e = 0; e < V; ++e) acc.add((colmask >> e) & 1u, (double)out[e], (double)(C[e] * cu));
           }
         }
       }
@@ -520,6 +553,7 @@ struct MarchF32 {
   int32_t ld_off;
   int32_t st_off;
   Row rl;  // EK & 2: r per element (0 in Dirichlet / pad columns)
+  static constexpr bool kScaled = AR == 2 && EK == 0;  // levels carried x 4^level (see March)
 
   using Ch = ChainShape<K, CL>;
   static constexpr int L = Ch::unroll(RING);
@@ -547,11 +581,23 @@ struct MarchF32 {
   static __device__ __forceinline__ Row partial(const Row& S, const Row& C) {
     return Row{S.a + C.b, F2{sadd(S.b.x, C.a.y), sadd_from_upper(S.b.y, C.a.x)}};
   }
+  // ((part + N) + W): the reference's sum
+  static __device__ __forceinline__ Row sum4(const Row& part, const Row& C, const Row& N) {
+    const F2 ta = part.a + N.a;
+    return Row{F2{sadd_from_lower(ta.x, C.b.y), sadd(ta.y, C.b.x)}, (part.b + N.b) + C.a};
+  }
+  // AR 2, pinned kinds: re * sum + (C - 4 re C) (see March::update)
+  static __device__ __forceinline__ F2 pin2(F2 re, F2 sum, F2 c) {
+    const F2 m4 = {-4.f, -4.f};
+    return __builtin_elementwise_fma(re, sum, __builtin_elementwise_fma(re, m4 * c, c));
+  }
+  static __device__ __forceinline__ float pin1(float re, float sum, float c) {
+    return __builtin_fmaf(re, sum, __builtin_fmaf(re, -4.f * c, c));
+  }
   // sum - 4C (in) and the per-element r (re) of the update C + r*(sum - 4C)
   __device__ __forceinline__ void terms(const Row& part, const Row& C, const Row& N, int32_t row, Row& in,
                                         Row& re) const {
-    const F2 ta = part.a + N.a;
-    const Row sum = {F2{sadd_from_lower(ta.x, C.b.y), sadd(ta.y, C.b.x)}, (part.b + N.b) + C.a};
+    const Row sum = sum4(part, C, N);
     const F2 m4 = {-4.f, -4.f};
     in = Row{__builtin_elementwise_fma(m4, C.a, sum.a), __builtin_elementwise_fma(m4, C.b, sum.b)};
     const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
@@ -568,6 +614,13 @@ struct MarchF32 {
     }
   }
   __device__ __forceinline__ Row update(const Row& part, const Row& C, const Row& N, int32_t row) const {
+    if constexpr (AR == 2) {
+      const Row sum = sum4(part, C, N);
+      if constexpr (EK == 0) return sum;  // scaled: 4^s T
+      Row in, re;
+      terms(part, C, N, row, in, re);  // (in unused: dead code)
+      return Row{pin2(re.a, sum.a, C.a), pin2(re.b, sum.b, C.b)};
+    }
     Row in, re;
     terms(part, C, N, row, in, re);
     if constexpr (AR == 1)
@@ -583,6 +636,17 @@ struct MarchF32 {
   // store vector in memory order (c0, c1, c2, c3) — a packed op would produce
   // the even/odd pairs and need a transpose before the 16-B store.
   __device__ __forceinline__ VT update_last(const Row& part, const Row& C, const Row& N, int32_t row) const {
+    if constexpr (AR == 2) {
+      const Row sum = sum4(part, C, N);
+      if constexpr (EK == 0) {  // unscale 4^K T once, at the store (exact)
+        constexpr float u = inv_pow4<float>(K);
+        return VT{sum.a.x * u, sum.b.x * u, sum.a.y * u, sum.b.y * u};
+      }
+      Row in, re;
+      terms(part, C, N, row, in, re);  // (in unused: dead code)
+      return VT{pin1(re.a.x, sum.a.x, C.a.x), pin1(re.b.x, sum.b.x, C.b.x), pin1(re.a.y, sum.a.y, C.a.y),
+                pin1(re.b.y, sum.b.y, C.b.y)};
+    }
     Row in, re;
     terms(part, C, N, row, in, re);
     return VT{fin(re.a.x, in.a.x, C.a.x), fin(re.b.x, in.b.x, C.b.x), fin(re.a.y, in.a.y, C.a.y),
@@ -622,10 +686,11 @@ struct MarchF32 {
         store_row(row, live, w);
         if constexpr (ST) {
           if (live) {  // C in even/odd form: a = (c0, c2), b = (c1, c3)
-            acc.add(colmask & 1u, (double)w.x, (double)C.a.x);
-            acc.add((colmask >> 1) & 1u, (double)w.y, (double)C.b.x);
-            acc.add((colmask >> 2) & 1u, (double)w.z, (double)C.a.y);
-            acc.add((colmask >> 3) & 1u, (double)w.w, (double)C.b.y);
+            constexpr float cu = kScaled ? inv_pow4<float>(K - 1) : 1.f;  // level K-1 scale
+            acc.add(colmask & 1u, (double)w.x, (double)(C.a.x * cu));
+            acc.add((colmask >> 1) & 1u, (double)w.y, (double)(C.b.x * cu));
+            acc.add((colmask >> 2) & 1u, (double)w.z, (double)(C.a.y * cu));
+            acc.add((colmask >> 3) & 1u, (double)w.w, (double)(C.b.y * cu));
           }
         }
       }
@@ -809,10 +874,15 @@ __device__ __forceinline__ bool tb_piece(const TbArgs& a, int64_t it, int32_t li
 // kernel at K = 11..12 lands at 129 VGPRs and fits 128 (4 waves/SIMD instead
 // of 3) without spilling; its exact-arithmetic twin would spill. (The packed
 // fp32 march with the single across-lane adds spills under a 3-wave floor from
-// K = 12 on, so it has none.) Checked per build: ScratchSize = 0 in the ISA
-// (tools/isa_report.py, tests/test_isa.py).
+// K = 12 on, so it has none.) The r = 1/4 (AR 2) fp64 interior kernel keeps 2
+// waves/SIMD at K = 18..19 under a floor; at K = 20 ring 4 a floor spills (its
+// ring-6 twin fits 241 VGPRs, which the autotuner weighs). The fused-cycle
+// variant (more state) takes no floor. Checked per build:
+// ScratchSize = 0 in the ISA (tools/isa_report.py, tests/test_isa.py).
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
-constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K >= 11 && K <= 12) ? 4 : 1;
+constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K >= 11 && K <= 12) ? 4
+                          : (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 2 && K >= 18 && K <= 19) ? 2
+                                                                                                                  : 1;
 
 // Rows [t0, t1) of `strip` that this wave just stored: re-read (sc0: past the
 // CU's L1, from the XCD's L2 that holds them) and store again at device scope
@@ -876,7 +946,7 @@ constexpr int kVarPlain = 0, kVarStats = 1, kVarFused = 2;
 // kernel 2 VGPRs over 256 — 1 wave/SIMD; a 2-wave floor spilled 28 B to
 // scratch. Its ring-6 twin keeps 2 waves at 245: the autotuner weighs both.)
 template <typename T, int NV, int K, int RING, bool MAIN, int AR, int VAR = kVarPlain>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves<T, NV, K, RING, MAIN, AR>))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVarPlain ? kMinWaves<T, NV, K, RING, MAIN, AR> : 1))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
   constexpr bool ST = VAR == kVarStats;
   static_assert(VAR != kVarStats || !MAIN, "the statistics variant uses the general kernel");
   static_assert(VAR != kVarFused || MAIN, "the fused variant is an interior kernel");

@@ -69,8 +69,10 @@ std::string jit_render(DType dt, const SlabLayout& L, double r, int arith) {
   s += "#define FOUR ((real)4)\n";
   // arith 1: the contracted form hipcc's default -ffp-contract=fast gives the
   // reference line; spelled out, since the module is compiled with contraction off
-  s += arith == 1 ? "#define UPDATE(c, sum) fma(R, (sum) - FOUR * (c), (c))\n"
-                  : "#define UPDATE(c, sum) ((c) + R * ((sum) - FOUR * (c)))\n";
+  // arith 2 (r == 1/4): the centre weight 1 - 4r is zero — R * sum
+  s += arith == 2   ? "#define UPDATE(c, sum) (R * (sum))\n"
+       : arith == 1 ? "#define UPDATE(c, sum) fma(R, (sum) - FOUR * (c), (c))\n"
+                    : "#define UPDATE(c, sum) ((c) + R * ((sum) - FOUR * (c)))\n";
   s += R"(
 extern "C" __global__ void __launch_bounds__(256) heat2d_jit_ftcs(const real* __restrict__ src,
                                                                   real* __restrict__ dst) {
@@ -94,7 +96,8 @@ JitStencil::JitStencil(DType dt, const SlabLayout& L, double r, int device, int 
   HEAT2D_REQUIRE(L.nrows >= 1 && L.ncols >= 1 && L.halo >= 1 && L.cpad >= 1, "layout needs a ghost frame");
   if (device >= 0) H2D_HIP(hipSetDevice(device));
   H2D_HIP(hipGetDevice(&device_));
-  HEAT2D_REQUIRE(arith == 0 || arith == 1, "arith must be 0 or 1");
+  HEAT2D_REQUIRE(arith >= 0 && arith <= 2, "arith must be 0, 1 or 2");
+  HEAT2D_REQUIRE(arith != 2 || r == 0.25, "arith 2 (jacobi) needs r == 1/4 exactly");
   src_ = jit_render(dt, L, r, arith);
   std::lock_guard<std::mutex> g(g_mu);
   auto key = std::make_pair(device_, src_);

@@ -88,7 +88,9 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     int e = 0;
     cfg_.arith = (cfg_.r > 0 && std::frexp(cfg_.r, &e) == 0.5) ? 1 : 0;
   }
-  HEAT2D_REQUIRE(cfg_.arith == 0 || cfg_.arith == 1, "arith must be 0 (reference rounding), 1 (fma) or -1 (auto)");
+  HEAT2D_REQUIRE(cfg_.arith >= 0 && cfg_.arith <= 2,
+                 "arith must be 0 (reference rounding), 1 (fma), 2 (jacobi, r = 1/4) or -1 (auto)");
+  HEAT2D_REQUIRE(cfg_.arith != 2 || cfg_.r == 0.25, "arith 2 (jacobi) needs r == 1/4 exactly (sigma = 0.25)");
   if (cfg_.engine == 1) {
     HEAT2D_REQUIRE(hip_, "the jit engine runs on the HIP backend");
     HEAT2D_REQUIRE(!cfg_.copy_swap, "the jit engine has no copy-swap mode");

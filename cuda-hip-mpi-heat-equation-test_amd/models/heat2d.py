@@ -94,7 +94,12 @@ class HeatSolver:
             "fma" — the update contracted to fma(r, sum - 4c, c), what hipcc's
             default contraction makes of fortran/hip/heat_kernel.cpp:43: one op
             fewer per point; identical to "exact" when r is a power of two
-            (sigma = 0.25), bitwise equal to the CPU twin for any r.
+            (sigma = 0.25), bitwise equal to the CPU twin for any r;
+            "jacobi" — r == 1/4 only: the centre weight 1 - 4r is zero and the
+            update is r * (((S + E) + N) + W) (3 adds per interior point and
+            level in the kernels instead of 5); bitwise equal to the CPU twin
+            and to models.reference.ftcs(arith="jacobi"), and to "exact"
+            wherever sum - 4c is exact (e.g. the reference IC, values in [1, 2]).
     """
 
     def __init__(self, problem: Problem, *, dtype: str = "fp64", backend: str = "auto", tb: int = 0,

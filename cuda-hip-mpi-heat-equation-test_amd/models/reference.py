@@ -46,8 +46,10 @@ def initial_field(problem: Problem, dtype=np.float64) -> np.ndarray:
     return np.ascontiguousarray(T, dtype=np.float64).astype(dtype)
 
 
-def ftcs_step(T: np.ndarray, r) -> np.ndarray:
-    """One FTCS step of a frame-inclusive field (frame kept fixed)."""
+def ftcs_step(T: np.ndarray, r, arith: str = "exact") -> np.ndarray:
+    """One FTCS step of a frame-inclusive field (frame kept fixed).
+    arith "jacobi" (r == 1/4 only): r * sum, the zero centre weight folded
+    away — the engine's arith 2."""
     r = T.dtype.type(r)
     four = T.dtype.type(4)
     c = T[1:-1, 1:-1]
@@ -56,16 +58,22 @@ def ftcs_step(T: np.ndarray, r) -> np.ndarray:
     north = T[:-2, 1:-1]  # x-1
     west = T[1:-1, :-2]   # y-1
     out = T.copy()
-    out[1:-1, 1:-1] = c + r * ((((south + east) + north) + west) - four * c)
+    if arith == "jacobi":
+        if r != 0.25:
+            raise ValueError("arith 'jacobi' needs r == 1/4")
+        out[1:-1, 1:-1] = r * (((south + east) + north) + west)
+    else:
+        out[1:-1, 1:-1] = c + r * ((((south + east) + north) + west) - four * c)
     return out
 
 
-def ftcs(problem: Problem, nsteps: int | None = None, dtype=np.float64, T0: np.ndarray | None = None) -> np.ndarray:
+def ftcs(problem: Problem, nsteps: int | None = None, dtype=np.float64, T0: np.ndarray | None = None,
+         arith: str = "exact") -> np.ndarray:
     """Run FTCS; returns the frame-inclusive field."""
     T = initial_field(problem, dtype) if T0 is None else T0.astype(dtype)
     n = problem.ntime if nsteps is None else nsteps
     for _ in range(n):
-        T = ftcs_step(T, problem.r)
+        T = ftcs_step(T, problem.r, arith)
     return T
 
 

@@ -26,8 +26,9 @@ LIB_PATH = os.environ.get("HEAT2D_LIB") or os.path.join(NATIVE_DIR, "libheat2d.s
 CLI_PATH = os.path.join(NATIVE_DIR, "heat2d")
 
 F32, F64 = 0, 1
-# SolverConfig::arith: reference rounding (bitwise == NumPy golden) | contracted fma(r, sum - 4c, c)
-ARITH = {"exact": 0, "fma": 1, "auto": -1}
+# SolverConfig::arith: reference rounding (bitwise == NumPy golden) | contracted fma(r, sum - 4c, c) |
+# jacobi: r == 1/4 only, r * sum (the zero centre weight folded away)
+ARITH = {"exact": 0, "fma": 1, "jacobi": 2, "auto": -1}
 
 
 def arith_code(arith: str, r: float) -> int:
@@ -36,6 +37,8 @@ def arith_code(arith: str, r: float) -> int:
     import math
     if arith == "auto":
         return 1 if r > 0 and math.frexp(r)[0] == 0.5 else 0
+    if arith == "jacobi" and r != 0.25:
+        raise ValueError("arith 'jacobi' needs r == 1/4 exactly (sigma = 0.25)")
     return ARITH[arith]
 BACKEND_HIP, BACKEND_CPU = 0, 1
 

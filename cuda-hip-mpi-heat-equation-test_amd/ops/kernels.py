@@ -88,7 +88,8 @@ def tb_step(src: torch.Tensor, dst: torch.Tensor, layout: N.Layout, k: int, r: f
             rows: Optional[tuple[int, int]] = None, tile_rows: int = 0, arith: str = "exact") -> None:
     """dst[rows] = k FTCS steps of src (temporal-blocked kernel). The k ghost rows
     around ``rows`` must be valid in ``src``; Dirichlet rows/cols are kept.
-    ``arith``: "exact" (reference rounding) or "fma" (contracted update)."""
+    ``arith``: "exact" (reference rounding), "fma" (contracted update) or
+    "jacobi" (r == 1/4: r * sum)."""
     _check_field(src, layout)
     _check_field(dst, layout)
     if src.dtype != dst.dtype or src.device != dst.device:

@@ -40,8 +40,9 @@ def build_parser():
     ap.add_argument("--engine", default=None, choices=["tb", "jit"],
                     help="tb: temporal-blocked kernels; jit: hipRTC kernel rendered at run time "
                          "(default: jit for --variant pycuda on a GPU, else tb)")
-    ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma"],
-                    help="exact: reference rounding (bitwise == NumPy golden); fma: contracted update, one op fewer")
+    ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma", "jacobi"],
+                    help="exact: reference rounding (bitwise == NumPy golden); fma: contracted update, one op fewer; "
+                         "jacobi: r == 1/4 only, r * (S + E + N + W), 3 adds per point")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--ntime", type=int, default=None)
     ap.add_argument("--print-every", type=int, default=0)

@@ -28,10 +28,10 @@ def tb():
         p = isa_report.tb_params(k["name"])
         if p:
             ks[p] = k
-    # 2 rings x main/gen x 2 arith x (fp32 K 1..16 + fp64 K 1..24), plus the
-    # fused-statistics variants (general, ring 4, 2 arith)
-    assert sum(len(p) == 6 for p in ks) == 8 * (16 + 24), len(ks)
-    assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 2 * (16 + 24), len(ks)
+    # 2 rings x main/gen x 3 arith x (fp32 K 1..16 + fp64 K 1..24), plus the
+    # fused-statistics variants (general, ring 4, 3 arith)
+    assert sum(len(p) == 6 for p in ks) == 12 * (16 + 24), len(ks)
+    assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 3 * (16 + 24), len(ks)
     return ks
 
 
@@ -44,16 +44,18 @@ def test_occupancy_floors(tb):
     for k in (11, 12):
         assert tb[("fp64", 1, k, 4, True, 1)]["waves_per_simd"] >= 4, k
     for k in range(1, 12):  # the packed fp32 interior kernel keeps >= 3 waves/SIMD up to K = 11
-        for ar in (0, 1):
+        for ar in (0, 1, 2):
             assert tb[("fp32", 1, k, 4, True, ar)]["waves_per_simd"] >= 3, k
 
 
 def test_deep_fp64_interior_two_waves(tb):
     """fp64 K = 17..24 exist for one-pass short runs: the interior (MAIN) kernel
-    must keep 2 waves/SIMD with ring 4 there (the general one may drop to 1)."""
+    must keep 2 waves/SIMD with ring 4 there (the general one may drop to 1;
+    the r = 1/4 K = 20 kernel with ring 6)."""
     for k in range(17, 25):
-        for ar in (0, 1):
-            assert tb[("fp64", 1, k, 4, True, ar)]["waves_per_simd"] >= 2, k
+        for ar in (0, 1, 2):
+            ring = 6 if (ar, k) == (2, 20) else 4  # r = 1/4, K = 20: ring 4 needs 258 VGPRs, ring 6 fits
+            assert tb[("fp64", 1, k, ring, True, ar)]["waves_per_simd"] >= 2, (k, ar)
     assert not any(p[0] == "fp32" and p[2] > 16 for p in tb)
 
 

@@ -72,8 +72,8 @@ def tb_params(mangled):
         return None
     p = ("fp64" if m.group(1) == "d" else "fp32", int(m.group(2)), int(m.group(3)), int(m.group(4)),
          m.group(5) == "1", int(m.group(6)))
-    var = m.group(7) or "0"  # kernel variant (tb_impl.hpp): 1 fused statistics
-    return p + ("stats",) if var == "1" else p
+    var = m.group(7) or "0"  # kernel variant (tb_impl.hpp): 1 fused statistics, 2 fused-cycle interior
+    return p + ({"1": "stats", "2": "fused"}[var],) if var in ("1", "2") else p
 
 
 def main():
@@ -89,7 +89,7 @@ def main():
             continue
         p = tb_params(k["name"])
         tag = (f"tb_kernel<{p[0]}, NV={p[1]}, K={p[2]:2d}, RING={p[3]}, {'main' if p[4] else 'gen '}, "
-               f"{'fma' if p[5] else 'exact'}>") if p else k["name"][:60]
+               f"{('exact', 'fma', 'jacobi')[p[5]]}>") if p else k["name"][:60]
         print(f"{tag:55s} vgpr {k['vgpr']:3d} agpr {k['agpr']:3d} scratch {k['scratch']:4d} "
               f"waves/SIMD {k['waves_per_simd']}")
 
