@@ -73,7 +73,9 @@ struct SplitPlan {
   int64_t main_waves, edge_waves, main_items, edge_items;
   // valid = 4 (fused, plan_fused): the MAIN launch's rects in item order —
   // the exchanged bands first (sig_items items that signal their completion),
-  // then the interior — and `edge` holds only bands on the Dirichlet frame
+  // then the interior — and `edge` holds only bands on the Dirichlet frame.
+  // valid = 1..3 with nfused > 0 (arith 2): `main` cut into frame-strip-
+  // weighted rects, launched instead of `main` (stencil_tb.hip weight_main).
   int32_t nfused, pad;
   TbRect fused[4];
   int64_t sig_items;

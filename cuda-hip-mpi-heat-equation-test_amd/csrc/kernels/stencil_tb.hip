@@ -334,6 +334,51 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
   launch_rects(dt, src, dst, L, k, p.prefetch, false, rects, nr, slots, r, stream, arith);
 }
 
+// r = 1/4 kernels (arith 2): an interior item costs 3 adds + 2 DPP moves per
+// point and level, a frame-column strip's item (edge kinds 2 / 3: the unscaled
+// 2-3 op update) ~1.6x that. Launched as equals, the two frame-column strips'
+// items end last — with one item per wave, the launch lasts as long as its
+// slowest wave (4096^2 fp32: +5 % per cycle over arith 1 before weighting).
+// Weighted: the first and last strip get rects of their own whose items are
+// shorter by that factor (plan.fused[], plan.nfused; plan.main keeps the
+// unweighted rect that describes the plan).
+constexpr double kFrameStripCost = 1.6;
+
+int weighted_main(const TbRect& R, TbRect out[3]) {
+  const int64_t ns = R.s1 - R.s0, rows = R.r1 - R.r0;
+  if (ns < 3 || rows < 2) return 0;
+  const double w = kFrameStripCost;
+  int64_t ne, ni;
+  if (R.nb < 0) {  // segments: interior length Li, frame-strip length Li / w
+    const int64_t S = -R.nb;
+    const double Li = ((double)rows * (double)(ns - 2) + 2.0 * w * (double)rows) / (double)S;
+    ne = std::min<int64_t>(rows, std::max<int64_t>(1, std::llround(w * (double)rows / Li)));
+    ni = std::min<int64_t>(rows * (ns - 2), std::max<int64_t>(1, S - 2 * ne));
+    ne = -ne;
+    ni = -ni;
+  } else {  // bands: more (shorter) bands on the frame strips
+    ni = R.nb;
+    ne = std::min<int64_t>(rows, std::max<int64_t>(R.nb, std::llround((double)R.nb * w)));
+  }
+  out[0] = TbRect{R.r0, R.r1, R.s0, R.s0 + 1, ne};
+  out[1] = TbRect{R.r0, R.r1, R.s0 + 1, R.s1 - 1, ni};
+  out[2] = TbRect{R.r0, R.r1, R.s1 - 1, R.s1, ne};
+  return 3;
+}
+
+int64_t rect_items(const TbRect& R) { return R.nb > 0 ? R.nb * (R.s1 - R.s0) : -R.nb; }
+
+// arith 2: put the weighted rects of p.main into p.fused (see weighted_main)
+void weight_main(SplitPlan& p, int arith, int64_t slots) {
+  if (arith != 2) return;
+  const int n = weighted_main(p.main, p.fused);
+  if (n == 0) return;
+  p.nfused = n;
+  p.main_items = 0;
+  for (int i = 0; i < n; ++i) p.main_items += rect_items(p.fused[i]);
+  p.main_waves = std::min<int64_t>(p.main_items, slots);
+}
+
 SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus, int spare_waves,
                      int ring_override, int64_t main_bands, int arith) {
   check_layout(dt, L, k);
@@ -357,6 +402,7 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   p.main = TbRect{B, n - B, 0, ns, nb_m};
   p.main_items = nb_m > 0 ? nb_m * ns : -nb_m;
   p.main_waves = std::min<int64_t>(p.main_items, mw);  // > one item per wave if main_bands asks for it
+  weight_main(p, arith, mw);
   // EDGE: the two boundary bands (one band each), general kernel. Short
   // (B + 2k march rows per item): beside MAIN where wave slots allow, else
   // right after it — either way the halo exchange that follows overlaps the
@@ -459,6 +505,7 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   p.main = TbRect{0, L.nrows, 0, ns, nb};
   p.main_items = nb > 0 ? nb * ns : -nb;
   p.main_waves = std::min<int64_t>(p.main_items, slots);
+  weight_main(p, arith, slots);
   p.nedge = 0;
   p.valid = 2;
   return p;
@@ -546,12 +593,15 @@ void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, con
   HEAT2D_REQUIRE(p.valid, "invalid split plan");
   HEAT2D_REQUIRE(p.valid != 4 || !main_part, "a fused plan's main part needs its band counter (launch_fused_main)");
   if (p.valid == 4 && p.nedge == 0) return;  // no band on the frame
+  // the main part: p.main, or its frame-strip-weighted rects (weight_main)
+  const TbRect* mr = p.nfused > 0 ? p.fused : &p.main;
+  const int nm = p.nfused > 0 ? p.nfused : 1;
   if (p.valid == 2) {  // single general launch over the whole slab (no edge part)
-    if (main_part) launch_rects(dt, src, dst, L, p.k, p.ring, false, &p.main, 1, p.main_waves, r, stream, arith);
+    if (main_part) launch_rects(dt, src, dst, L, p.k, p.ring, false, mr, nm, p.main_waves, r, stream, arith);
     return;
   }
   if (main_part)
-    launch_rects(dt, src, dst, L, p.k, p.ring, true, &p.main, 1, p.main_waves, r, stream, arith);
+    launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith);
   else
     launch_rects(dt, src, dst, L, p.k, p.ring, false, p.edge, p.nedge, p.edge_waves, r, stream, arith);
 }

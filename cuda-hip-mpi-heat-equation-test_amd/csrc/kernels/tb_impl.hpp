@@ -197,8 +197,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uin
 // plain sum — 3 adds + 2 DPP moves per point instead of 5 + 2 — and multiply by
 // 4^-K once, at the store (powers of two: exact, so the stored bits equal the
 // per-level /4 form for |T| < 2^(emax - 2K)). Pinned kinds (re = 0 where
-// pinned) compute re * sum + (C - 4 re C): the second term is exactly 0 at
-// updated points and C at pinned ones — the same bits. Where every (sum, 4C)
+// pinned) compute unscaled: kind 1 fma(ke, C, re * sum) with scalar ke = 1 -
+// 4 re (2 ops, as arith 1), kinds 2 / 3 re * sum + (C - 4 re C) (3 ops); the
+// added term is exactly 0 at updated points and C at pinned ones — the same
+// bits. Where every (sum, 4C)
 // pair lies within a factor of two (smooth positive data, e.g. the reference IC
 // with values in [1, 2]), sum - 4C is exact (Sterbenz) and the reference
 // rounding gives the same bits too.
@@ -379,10 +381,13 @@ struct March {
       else if constexpr (EK == 2) re = rl[e];
       else re = frame_row ? T(0) : rl[e];
       if constexpr (AR == 2) {
-        // scaled kind 0: the plain sum (4^s T); pinned kinds (re = 0 where
-        // pinned): re * sum + (C - 4 re C), whose second term is exactly 0 at
-        // updated points (re = 1/4) and C at pinned ones
+        // scaled kind 0: the plain sum (4^s T). Pinned kinds (re = 0 where
+        // pinned), unscaled: kind 1 (frame rows: wave-uniform) fma(ke, C, re *
+        // sum) with scalar ke = 1 - 4 re; kinds 2 / 3 (per-element re)
+        // re * sum + (C - 4 re C). The added term is exactly 0 at updated
+        // points (re = 1/4) and C at pinned ones.
         if constexpr (EK == 0) out[e] = sum;
+        else if constexpr (EK == 1) out[e] = fma_t(frame_row ? T(1) : T(0), C[e], re * sum);
         else out[e] = fma_t(re, sum, fma_t(re, T(-4) * C[e], C[e]));
       } else if constexpr (AR == 1) {
         out[e] = fma_t(re, fma_t(T(-4), C[e], sum), C[e]);
@@ -617,8 +622,13 @@ struct MarchF32 {
     if constexpr (AR == 2) {
       const Row sum = sum4(part, C, N);
       if constexpr (EK == 0) return sum;  // scaled: 4^s T
-      Row in, re;
-      terms(part, C, N, row, in, re);  // (in unused: dead code)
+      const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
+      if constexpr (EK == 1) {  // fma(ke, C, re * sum), scalar (re, ke) (see March::update)
+        const F2 re = {frame_row ? 0.f : r, frame_row ? 0.f : r}, ke = {frame_row ? 1.f : 0.f, frame_row ? 1.f : 0.f};
+        return Row{__builtin_elementwise_fma(ke, C.a, re * sum.a), __builtin_elementwise_fma(ke, C.b, re * sum.b)};
+      }
+      const F2 z = {0.f, 0.f};
+      const Row re = (EK == 3 && frame_row) ? Row{z, z} : rl;
       return Row{pin2(re.a, sum.a, C.a), pin2(re.b, sum.b, C.b)};
     }
     Row in, re;
@@ -642,8 +652,14 @@ struct MarchF32 {
         constexpr float u = inv_pow4<float>(K);
         return VT{sum.a.x * u, sum.b.x * u, sum.a.y * u, sum.b.y * u};
       }
-      Row in, re;
-      terms(part, C, N, row, in, re);  // (in unused: dead code)
+      const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
+      if constexpr (EK == 1) {
+        const float re = frame_row ? 0.f : r, ke = frame_row ? 1.f : 0.f;
+        return VT{__builtin_fmaf(ke, C.a.x, re * sum.a.x), __builtin_fmaf(ke, C.b.x, re * sum.b.x),
+                  __builtin_fmaf(ke, C.a.y, re * sum.a.y), __builtin_fmaf(ke, C.b.y, re * sum.b.y)};
+      }
+      const F2 z = {0.f, 0.f};
+      const Row re = (EK == 3 && frame_row) ? Row{z, z} : rl;
       return VT{pin1(re.a.x, sum.a.x, C.a.x), pin1(re.b.x, sum.b.x, C.b.x), pin1(re.a.y, sum.a.y, C.a.y),
                 pin1(re.b.y, sum.b.y, C.b.y)};
     }

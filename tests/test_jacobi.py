@@ -174,6 +174,7 @@ def test_hip_jacobi_jit_and_ranks(gpu, native):
     assert np.array_equal(a, b) and np.array_equal(b, golden(p, np.float64, T0))
     p = prob(700, 41)
     g = LoopbackGroup(p, 3, dtype="fp64", backend="hip", tb=13, arith="jacobi")
+    g.upload(R.owned(R.initial_field(p)))  # the host IC (device sin() may differ in the last bit)
     g.step(p.ntime)
     assert np.array_equal(g.download(), golden(p, np.float64))
     g.close()

@@ -9,7 +9,8 @@ Env: CP_ROWS=R solves the first R rows only (one rank's slab shape); CP_LOOP=1
 exchanges the slab's band rows with itself over a 1-rank RCCL communicator
 (the multi-GPU schedule rehearsal of bench.py --rehearse-comm); CP_AUTOTUNE=1
 autotunes the plan first (its trial cycles appear in a profile before the
-timed ones); CP_TIMERS=1 prints the hipEvent phase times of the timed cycles.
+timed ones); CP_TIMERS=1 prints the hipEvent phase times of the timed cycles;
+CP_ARITH=exact|fma|jacobi picks the update form (default auto).
 """
 import json
 import os
@@ -35,7 +36,7 @@ if os.environ.get("CP_LOOP") == "1":
     from heat2d.parallel.transport import RcclLoopTransport
     tr = RcclLoopTransport(0)
 s = HeatSolver(prob, dtype=dtype, backend="hip", tb=k, device=0, autotune=int(os.environ.get("CP_AUTOTUNE", "0")),
-               overlap=overlap, graph=graph, rows=rows, transport=tr)
+               overlap=overlap, graph=graph, rows=rows, transport=tr, arith=os.environ.get("CP_ARITH", "auto"))
 s.prepare(k * cycles)
 s.step(k)  # warm
 s.synchronize()
