@@ -21,12 +21,17 @@ plans move per second (utils/metrics.plan_hbm_bytes: strip halos and priming
 rows counted, no cache reuse assumed — an upper bound; rocprof cross-check in
 profiles/hbm_model_check.md).
 
-Arithmetic (--arith, default auto = fma here): the update is the reference expression
-c + r*(sum - 4c) (fortran/hip/heat_kernel.cpp:43) in fp64, contracted to
-fma(r, sum - 4c, c) — what hipcc's default -ffp-contract=fast makes of that
-line. With this config's r = 0.25 (a power of two) every rounding is the same
-as the uncontracted form, so the field is bitwise identical to --arith exact
-(checked on the GPU: tests/test_gpu_solver.py::test_hip_fma_equals_exact_pow2).
+Arithmetic (--arith, default "bench": jacobi when r == 1/4, as here, else the
+library's auto). The reference update is c + r*(sum - 4c)
+(fortran/hip/heat_kernel.cpp:43). At r = 1/4 its centre weight 1 - 4r is zero
+and the step is r * (((S + E) + N) + W) — the same sum, one exact multiply:
+the kernels then carry the interior levels scaled by 4^level and spend 3 adds
++ 2 DPP moves per point and level instead of 5 + 2 (tb_impl.hpp, AR 2). On
+this benchmark's IC (T = 2 inside, 1 on the frame) every value stays in
+[1, 2], so sum - 4c is exact (Sterbenz) and the field is bitwise identical to
+--arith exact (GPU-checked: tests/test_jacobi.py::
+test_hip_jacobi_equals_exact_on_reference_ic). --arith auto (fma, also bitwise
+identical here) and exact remain available.
 
 vs_baseline: the reference publishes no numbers. We divide by the
 derived reference ceiling of BASELINE.md — 50 Gpts/s per MI250X GCD for its
@@ -128,10 +133,11 @@ def main():
                     help="largest time-step depth fused per HBM pass (0: every depth the kernels have, fp64 24 / "
                          "fp32 16; prepare() picks the cycle schedule of the timed steps by measurement)")
     ap.add_argument("--tile-rows", type=int, default=0)
-    ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma", "jacobi"],
+    ap.add_argument("--arith", default="bench", choices=["bench", "auto", "exact", "fma", "jacobi"],
                     help="fma: contracted update (one op fewer per point); exact: every op rounded; auto: fma when "
                          "bitwise identical to exact (r a power of two, as here), else exact; jacobi: r == 1/4 "
-                         "only, r * (S + E + N + W) (3 adds per point; bitwise == exact on this benchmark's IC)")
+                         "only, r * (S + E + N + W) (3 adds per point; bitwise == exact on this benchmark's IC); "
+                         "bench (default): jacobi when r == 1/4, else auto")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="replay the timed schedule from one hipGraph captured in prepare() (auto: single-rank runs, "
@@ -204,6 +210,7 @@ def main():
         n_glob = int(round(args.n * math.sqrt(world)))
     inp = heat2d.InputDat(n=n_glob, sigma=0.25, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
+    arith = args.arith if args.arith != "bench" else ("jacobi" if prob.r == 0.25 else "auto")
     if world > 1:
         tr = (IpcTransport(device) if peer else RcclTransport(rank, world, local)) if hip else TorchDistTransport()
     elif args.rehearse_comm and hip:  # one rank's exchange with itself: RCCL kernels or IPC pulls
@@ -219,7 +226,7 @@ def main():
     graph = hip and (args.graph == "on" or (args.graph == "auto" and ((world == 1 and not args.rehearse_comm) or ipc)))
     s = HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb, overlap=not args.no_overlap, graph=graph,
                    tile_rows=args.tile_rows, transport=tr, device=device if hip else None, rows=rows,
-                   comm_cus=args.comm_cus, arith=args.arith, slab_row0=slab_row0)
+                   comm_cus=args.comm_cus, arith=arith, slab_row0=slab_row0)
 
     def barrier():
         if world > 1:
@@ -310,7 +317,7 @@ def main():
                 "schedule": "measured" if s.schedule(args.steps) else "balanced",
                 "prepare_s": round(prepare_s, 2),
                 "plan_cache": {"hits": s.plan_cache_hits, "path": N.plan_cache_path()} if hip else None,
-                "arith": arith_name(prob.r, args.arith) + (" (auto)" if args.arith == "auto" else ""),
+                "arith": arith_name(prob.r, arith) + {"auto": " (auto)", "bench": " (r = 1/4)"}.get(args.arith, ""),
                 "overlap": not args.no_overlap,
                 "graph": bool(graph),
                 "launch_plans": plans or None,

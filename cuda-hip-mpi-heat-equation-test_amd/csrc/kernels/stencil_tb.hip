@@ -335,30 +335,43 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 }
 
 // r = 1/4 kernels (arith 2): an interior item costs 3 adds + 2 DPP moves per
-// point and level, a frame-column strip's item (edge kinds 2 / 3: the unscaled
-// 2-3 op update) ~1.6x that. Launched as equals, the two frame-column strips'
-// items end last — with one item per wave, the launch lasts as long as its
-// slowest wave (4096^2 fp32: +5 % per cycle over arith 1 before weighting).
-// Weighted: the first and last strip get rects of their own whose items are
-// shorter by that factor (plan.fused[], plan.nfused; plan.main keeps the
-// unweighted rect that describes the plan).
-constexpr double kFrameStripCost = 1.6;
-
-int weighted_main(const TbRect& R, TbRect out[3]) {
+// point and level (fp32: 8 VALU ops per 4 points, fp64: 10 per 2), a
+// frame-column strip's item (edge kinds 2 / 3: the unscaled 3-op update) w =
+// 1.75x (fp32: 14) / 1.6x (fp64: 16) that. Launched as equals, the two
+// frame-column strips' items end last — with one item per wave the launch
+// lasts as long as its slowest wave (4096^2 fp32 K = 15: 69 us per cycle
+// against 66 for arith 1, whose kinds all cost ~12). Weighted: the first and
+// last strip get rects of their own whose items cost what an interior one
+// does, priming rows (2k per item) included: (Le + 2k) w = Li + 2k. A plan
+// whose segments tile every strip exactly keeps doing so (a segment crossing
+// a strip end pays a second priming), with as many interior segments per
+// strip as fit the original item count. plan.fused[] / plan.nfused hold the
+// rects; plan.main keeps the unweighted rect that describes the plan.
+int weighted_main(DType dt, int k, const TbRect& R, TbRect out[3]) {
   const int64_t ns = R.s1 - R.s0, rows = R.r1 - R.r0;
   if (ns < 3 || rows < 2) return 0;
-  const double w = kFrameStripCost;
+  const double w = dt == DType::F32 ? 1.75 : 1.6, prime = 2.0 * k;
+  auto edge_items = [&](double li) {  // items of one frame strip for interior items of li rows
+    const double le = std::max(8.0, (li + prime) / w - prime);
+    return std::min<int64_t>(rows, (int64_t)std::ceil((double)rows / le));
+  };
   int64_t ne, ni;
-  if (R.nb < 0) {  // segments: interior length Li, frame-strip length Li / w
+  if (R.nb < 0) {
     const int64_t S = -R.nb;
-    const double Li = ((double)rows * (double)(ns - 2) + 2.0 * w * (double)rows) / (double)S;
-    ne = std::min<int64_t>(rows, std::max<int64_t>(1, std::llround(w * (double)rows / Li)));
-    ni = std::min<int64_t>(rows * (ns - 2), std::max<int64_t>(1, S - 2 * ne));
+    if (S % ns == 0) {  // strip-aligned segments: q per interior strip, as many as fit S items
+      int64_t q = S / ns, qe = edge_items((double)rows / q);
+      while (q > 1 && (ns - 2) * q + 2 * qe > S) qe = edge_items((double)rows / --q);
+      ni = (ns - 2) * q;
+      ne = qe;
+    } else {  // segments already cross strip ends: carve the frame strips out
+      ne = edge_items((double)rows * (double)ns / (double)S);
+      ni = std::max<int64_t>(1, S - 2 * ne);
+    }
+    ni = -std::min<int64_t>(ni, rows * (ns - 2));
     ne = -ne;
-    ni = -ni;
   } else {  // bands: more (shorter) bands on the frame strips
     ni = R.nb;
-    ne = std::min<int64_t>(rows, std::max<int64_t>(R.nb, std::llround((double)R.nb * w)));
+    ne = std::max<int64_t>(R.nb, edge_items((double)rows / R.nb));
   }
   out[0] = TbRect{R.r0, R.r1, R.s0, R.s0 + 1, ne};
   out[1] = TbRect{R.r0, R.r1, R.s0 + 1, R.s1 - 1, ni};
@@ -369,9 +382,9 @@ int weighted_main(const TbRect& R, TbRect out[3]) {
 int64_t rect_items(const TbRect& R) { return R.nb > 0 ? R.nb * (R.s1 - R.s0) : -R.nb; }
 
 // arith 2: put the weighted rects of p.main into p.fused (see weighted_main)
-void weight_main(SplitPlan& p, int arith, int64_t slots) {
+void weight_main(DType dt, SplitPlan& p, int arith, int64_t slots) {
   if (arith != 2) return;
-  const int n = weighted_main(p.main, p.fused);
+  const int n = weighted_main(dt, p.k, p.main, p.fused);
   if (n == 0) return;
   p.nfused = n;
   p.main_items = 0;
@@ -402,7 +415,7 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   p.main = TbRect{B, n - B, 0, ns, nb_m};
   p.main_items = nb_m > 0 ? nb_m * ns : -nb_m;
   p.main_waves = std::min<int64_t>(p.main_items, mw);  // > one item per wave if main_bands asks for it
-  weight_main(p, arith, mw);
+  weight_main(dt, p, arith, mw);
   // EDGE: the two boundary bands (one band each), general kernel. Short
   // (B + 2k march rows per item): beside MAIN where wave slots allow, else
   // right after it — either way the halo exchange that follows overlaps the
@@ -505,7 +518,7 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   p.main = TbRect{0, L.nrows, 0, ns, nb};
   p.main_items = nb > 0 ? nb * ns : -nb;
   p.main_waves = std::min<int64_t>(p.main_items, slots);
-  weight_main(p, arith, slots);
+  weight_main(dt, p, arith, slots);
   p.nedge = 0;
   p.valid = 2;
   return p;
