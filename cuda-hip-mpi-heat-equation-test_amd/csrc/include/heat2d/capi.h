@@ -53,7 +53,7 @@ typedef struct heat2d_split_plan {
   heat2d_rect edge[4];
   int64_t main_waves, edge_waves, main_items, edge_items;
   int32_t nfused, pad;
-  heat2d_rect fused[4];
+  heat2d_rect fused[6];
   int64_t sig_items;
 } heat2d_split_plan;
 

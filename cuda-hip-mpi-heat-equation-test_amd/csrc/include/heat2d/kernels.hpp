@@ -66,6 +66,8 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 struct TbRect {
   int64_t r0, r1, s0, s1, nb;
 };
+// rects of one launch (SplitPlan::fused, the kernel's TbArgs::rect)
+constexpr int kMaxFused = 6;
 struct SplitPlan {
   int32_t k, ring, valid, nedge;
   TbRect main;
@@ -77,7 +79,7 @@ struct SplitPlan {
   // valid = 1..3 with nfused > 0 (arith 2): `main` cut into frame-strip-
   // weighted rects, launched instead of `main` (stencil_tb.hip weight_main).
   int32_t nfused, pad;
-  TbRect fused[4];
+  TbRect fused[kMaxFused];
   int64_t sig_items;
 };
 // ring_override: 4 | 6 (0: default); main_bands: MAIN row bands (0: persistent default;

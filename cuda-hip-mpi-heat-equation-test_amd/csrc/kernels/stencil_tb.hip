@@ -194,7 +194,7 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t simds, int k, int64_t pri
 int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
                      const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith,
                      double* partials = nullptr, int64_t sig_items = 0, uint32_t* sig = nullptr) {
-  HEAT2D_REQUIRE(nrect >= 1 && nrect <= kMaxRects, "bad rect count");
+  HEAT2D_REQUIRE(nrect >= 1 && nrect <= (main ? kMainRects : kMaxRects), "bad rect count");
   TbArgs a{};
   a.pitch = L.pitch;
   a.ncols = L.ncols;
@@ -347,44 +347,98 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 // a strip end pays a second priming), with as many interior segments per
 // strip as fit the original item count. plan.fused[] / plan.nfused hold the
 // rects; plan.main keeps the unweighted rect that describes the plan.
-int weighted_main(DType dt, int k, const TbRect& R, TbRect out[3]) {
+//
+// Frame ROWS likewise: an item whose march reaches the global top / bottom row
+// (edge kind 1: the unscaled 2-op form, fp32 12 VALU ops per 4 points against
+// 8, fp64 14 per 2 against 10) runs ~1.4-1.5x an interior item per march row.
+// In a single-launch plan (plan_single: the small grid's, where every wave
+// holds one item and the launch lasts as long as its slowest wave) those are
+// the first and last item of every strip. When the rect's marches reach a
+// frame row, the interior strips get a top / bottom rect of one short band
+// each, (h + 2k) w1 = Li + 2k, and the segments / bands in between: 5 rects.
+// Weights: HEAT2D_W_ROW / HEAT2D_W_COL override (A/B).
+double pinned_weight(DType dt, bool row) {
+  const char* env = std::getenv(row ? "HEAT2D_W_ROW" : "HEAT2D_W_COL");
+  if (env && std::atof(env) >= 1.0) return std::atof(env);
+  if (row) return dt == DType::F32 ? 1.5 : 1.4;
+  return dt == DType::F32 ? 1.75 : 1.6;
+}
+
+int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect out[kMaxFused]) {
   const int64_t ns = R.s1 - R.s0, rows = R.r1 - R.r0;
   if (ns < 3 || rows < 2) return 0;
-  const double w = dt == DType::F32 ? 1.75 : 1.6, prime = 2.0 * k;
+  const double w = pinned_weight(dt, false), w1 = pinned_weight(dt, true), prime = 2.0 * k;
   auto edge_items = [&](double li) {  // items of one frame strip for interior items of li rows
     const double le = std::max(8.0, (li + prime) / w - prime);
     return std::min<int64_t>(rows, (int64_t)std::ceil((double)rows / le));
   };
+  // frame rows within the marches of the rect's first / last rows (the
+  // kernel's edge-kind test: t0 - k < fixed_lo, t1 + k > fixed_hi)
+  const bool ftop = L.row0 + R.r0 < k, fbot = L.row0 + R.r1 + k > L.nrows_global;
+  // rows of the top / bottom band for interior items of li rows: as costly as
+  // one of those, and at least k (so the next item is kind 0)
+  auto frame_rows = [&](double li) {
+    return std::max<int64_t>(k, (int64_t)std::floor((li + prime) / w1 - prime));
+  };
+  int64_t hT = 0, hB = 0;  // rows carved out at the top / bottom of the interior strips
   int64_t ne, ni;
   if (R.nb < 0) {
     const int64_t S = -R.nb;
     if (S % ns == 0) {  // strip-aligned segments: q per interior strip, as many as fit S items
-      int64_t q = S / ns, qe = edge_items((double)rows / q);
-      while (q > 1 && (ns - 2) * q + 2 * qe > S) qe = edge_items((double)rows / --q);
+      const int nf = (ftop ? 1 : 0) + (fbot ? 1 : 0);
+      auto fit = [&](int64_t q, int64_t* qe, int64_t* ht, int64_t* hb) {
+        // frame bands of the interior strips, sized for the segments between them
+        *ht = *hb = 0;
+        if (nf > 0) {
+          const int64_t h = frame_rows((double)rows / (q + nf));
+          if (rows - nf * h >= std::max<int64_t>(q * 2 * (int64_t)k, 1)) {
+            const int64_t h2 = frame_rows((double)(rows - nf * h) / q);
+            *ht = ftop ? h2 : 0;
+            *hb = fbot ? h2 : 0;
+            if (rows - *ht - *hb < std::max<int64_t>(q * 2 * (int64_t)k, 1)) *ht = *hb = 0;
+          }
+        }
+        *qe = edge_items((double)(rows - *ht - *hb) / q);
+        return (ns - 2) * (q + (*ht > 0) + (*hb > 0)) + 2 * *qe;
+      };
+      int64_t q = S / ns, qe = 0;
+      while (q > 1 && fit(q, &qe, &hT, &hB) > S) --q;
+      fit(q, &qe, &hT, &hB);
       ni = (ns - 2) * q;
       ne = qe;
     } else {  // segments already cross strip ends: carve the frame strips out
       ne = edge_items((double)rows * (double)ns / (double)S);
       ni = std::max<int64_t>(1, S - 2 * ne);
     }
-    ni = -std::min<int64_t>(ni, rows * (ns - 2));
+    ni = -std::min<int64_t>(ni, (rows - hT - hB) * (ns - 2));
     ne = -ne;
-  } else {  // bands: more (shorter) bands on the frame strips
+  } else {  // bands: more (shorter) bands on the frame strips, one short band per frame side
     ni = R.nb;
-    ne = std::max<int64_t>(R.nb, edge_items((double)rows / R.nb));
+    const double li = (double)rows / R.nb;
+    if (R.nb >= 2) {
+      const int64_t h = frame_rows(li);
+      if (rows - (ftop + fbot) * h >= R.nb * 2 * (int64_t)k) {
+        hT = ftop ? h : 0;
+        hB = fbot ? h : 0;
+      }
+    }
+    ne = std::max<int64_t>(R.nb, edge_items(li));
   }
-  out[0] = TbRect{R.r0, R.r1, R.s0, R.s0 + 1, ne};
-  out[1] = TbRect{R.r0, R.r1, R.s0 + 1, R.s1 - 1, ni};
-  out[2] = TbRect{R.r0, R.r1, R.s1 - 1, R.s1, ne};
-  return 3;
+  int n = 0;
+  out[n++] = TbRect{R.r0, R.r1, R.s0, R.s0 + 1, ne};
+  if (hT > 0) out[n++] = TbRect{R.r0, R.r0 + hT, R.s0 + 1, R.s1 - 1, 1};
+  out[n++] = TbRect{R.r0 + hT, R.r1 - hB, R.s0 + 1, R.s1 - 1, ni};
+  if (hB > 0) out[n++] = TbRect{R.r1 - hB, R.r1, R.s0 + 1, R.s1 - 1, 1};
+  out[n++] = TbRect{R.r0, R.r1, R.s1 - 1, R.s1, ne};
+  return n;
 }
 
 int64_t rect_items(const TbRect& R) { return R.nb > 0 ? R.nb * (R.s1 - R.s0) : -R.nb; }
 
 // arith 2: put the weighted rects of p.main into p.fused (see weighted_main)
-void weight_main(DType dt, SplitPlan& p, int arith, int64_t slots) {
+void weight_main(DType dt, const SlabLayout& L, SplitPlan& p, int arith, int64_t slots) {
   if (arith != 2) return;
-  const int n = weighted_main(dt, p.k, p.main, p.fused);
+  const int n = weighted_main(dt, p.k, p.main, L, p.fused);
   if (n == 0) return;
   p.nfused = n;
   p.main_items = 0;
@@ -415,7 +469,7 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   p.main = TbRect{B, n - B, 0, ns, nb_m};
   p.main_items = nb_m > 0 ? nb_m * ns : -nb_m;
   p.main_waves = std::min<int64_t>(p.main_items, mw);  // > one item per wave if main_bands asks for it
-  weight_main(dt, p, arith, mw);
+  weight_main(dt, L, p, arith, mw);
   // EDGE: the two boundary bands (one band each), general kernel. Short
   // (B + 2k march rows per item): beside MAIN where wave slots allow, else
   // right after it — either way the halo exchange that follows overlaps the
@@ -498,7 +552,7 @@ SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool se
 
 void launch_fused_main(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, uint32_t* sig,
                        double r, hipStream_t stream, int arith) {
-  HEAT2D_REQUIRE(p.valid == 4 && p.nfused >= 2 && p.nfused <= 4, "not a fused plan");
+  HEAT2D_REQUIRE(p.valid == 4 && p.nfused >= 2 && p.nfused <= kMaxFused, "not a fused plan");
   launch_rects(dt, src, dst, L, p.k, p.ring, true, p.fused, p.nfused, p.main_waves, r, stream, arith, nullptr,
                p.sig_items, sig);
 }
@@ -518,7 +572,7 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   p.main = TbRect{0, L.nrows, 0, ns, nb};
   p.main_items = nb > 0 ? nb * ns : -nb;
   p.main_waves = std::min<int64_t>(p.main_items, slots);
-  weight_main(dt, p, arith, slots);
+  weight_main(dt, L, p, arith, slots);
   p.nedge = 0;
   p.valid = 2;
   return p;

@@ -82,7 +82,8 @@ __device__ __forceinline__ float sadd_from_lower(float a, float x) { return fenc
 // Kernel arguments: the work is up to kMaxRects rectangles (output rows x
 // strips), each cut into `nb` row bands; a work item is one (band, strip) of
 // one rectangle. item0 = index of the rectangle's first item.
-constexpr int kMaxRects = 4;
+constexpr int kMaxRects = kMaxFused;
+constexpr int kMainRects = 4;  // interior (MAIN) kernels: frame-strip rects or a fused plan's
 struct TbRectArg {
   int64_t r0, r1;  // output rows [r0, r1)
   int64_t s0, s1;  // strips [s0, s1)
@@ -846,12 +847,15 @@ struct TbSpan {
   int32_t lin, lin_end, rows;
   int64_t r0, s0;
 };
+// NR: rects the kernel instance can be handed (the interior kernels take at
+// most 4: a larger scan costs the deep fp64 ones SGPRs that spill to scratch).
+template <int NR = kMaxRects>
 __device__ __forceinline__ TbSpan tb_span(const TbArgs& a, int64_t it) {
   // select the rect with constant indices only (a dynamic index into the
   // by-value kernarg struct would be lowered to a private-memory copy)
   TbRectArg R = a.rect[0];
 #pragma unroll
-  for (int i = 1; i < kMaxRects; ++i)
+  for (int i = 1; i < NR; ++i)
     if (i < a.nrect && it >= a.rect[i].item0) R = a.rect[i];
   const int64_t local = it - R.item0;
   const int64_t ns = R.s1 - R.s0;
@@ -870,9 +874,10 @@ __device__ __forceinline__ TbSpan tb_span(const TbArgs& a, int64_t it) {
 }
 // The piece of item `it` starting at lin -> (strip, output rows [t0, t1));
 // false when lin is past the item. Advance with lin += t1 - t0.
+template <int NR = kMaxRects>
 __device__ __forceinline__ bool tb_piece(const TbArgs& a, int64_t it, int32_t lin, int64_t& strip, int64_t& t0,
                                          int64_t& t1) {
-  const TbSpan g = tb_span(a, it);
+  const TbSpan g = tb_span<NR>(a, it);
   if (lin >= g.lin_end) return false;
   const int32_t sl = lin / g.rows, row = lin - sl * g.rows;
   strip = g.s0 + sl;
@@ -989,11 +994,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
   StatAcc acc;
   // one flat loop over the pieces of items wid, wid + nwaves, ... (a nested
   // piece loop around the march costs the deep fp64 kernels registers)
+  constexpr int NR = MAIN ? kMainRects : kMaxRects;
   int64_t it = wid;
-  int32_t lin = tb_span(a, it).lin;
+  int32_t lin = tb_span<NR>(a, it).lin;
   while (it < a.nitems) {
     int64_t strip, t0, t1;
-    if (!tb_piece(a, it, lin, strip, t0, t1)) {
+    if (!tb_piece<NR>(a, it, lin, strip, t0, t1)) {
       if constexpr (VAR == kVarFused) {
         if (it < a.sig_items) {  // a band item of a fused cycle is complete: count it
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1001,7 +1007,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
         }
       }
       it += a.nwaves;
-      if (it < a.nitems) lin = tb_span(a, it).lin;
+      if (it < a.nitems) lin = tb_span<NR>(a, it).lin;
       continue;
     }
     lin += (int32_t)(t1 - t0);

@@ -33,7 +33,7 @@ std::string default_path() {
   if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) base = x;
   else if (const char* h = std::getenv("HOME"); h && *h) base = std::string(h) + "/.cache";
   else return "";
-  return base + "/heat2d/plans-v1.txt";
+  return base + "/heat2d/plans-v2.txt";
 }
 
 void mkdirs(const std::string& file) {
@@ -138,7 +138,7 @@ bool get_plan(const std::string& ctx, int k, int64_t band, kern::SplitPlan* p, f
   in >> sig;
   q.nfused = (int32_t)nf;
   q.sig_items = sig;
-  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > 4) return false;
+  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > kern::kMaxFused) return false;
   *p = q;
   *ms = t;
   return true;

@@ -524,6 +524,12 @@ int Solver::spare_waves() const {
   return 8;
 }
 
+static int device_cus_of(int device) {
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
+  return ncu;
+}
+
 static bool tune_segments() {
   static const bool on = [] {
     const char* e = std::getenv("HEAT2D_TUNE_SEGMENTS");
@@ -707,8 +713,22 @@ void Solver::autotune_split(int k) {
       if (!tune_segments() || (dtype() == DType::F32 && mode != 2)) continue;
       const int64_t w0 = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, 0, cfg_.arith).main_waves
                                    : best.main_waves;
-      for (double f : {0.5, 1.0, 1.5, 2.0}) {
-        const int64_t nseg = std::max<int64_t>(1, (int64_t)(w0 * f + 0.5));
+      std::vector<int64_t> segs;
+      for (double f : {0.5, 1.0, 1.5, 2.0}) segs.push_back(std::max<int64_t>(1, (int64_t)(w0 * f + 0.5)));
+      if (mode == 2 && cfg_.arith == 2) {
+        // r = 1/4 single launches: strip-aligned segment counts too (a whole
+        // number per strip), whose frame-row items the plan can weight
+        // (stencil_tb.hip weighted_main) — one per SIMD and one per wave
+        const int64_t ns = kern::plan_single(dtype(), L_, k, compute_cus_, ring, 0, cfg_.arith).main.s1;
+        const int64_t simds = (int64_t)(compute_cus_ > 0 ? compute_cus_ : device_cus_of(cfg_.device)) * 4;
+        for (int64_t target : {simds, w0, 2 * simds}) {
+          const int64_t q = target / std::max<int64_t>(ns, 1);
+          if (q >= 2) segs.push_back(q * ns);
+        }
+      }
+      std::sort(segs.begin(), segs.end());
+      segs.erase(std::unique(segs.begin(), segs.end()), segs.end());
+      for (int64_t nseg : segs) {
         kern::SplitPlan c = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, -nseg, cfg_.arith)
                                       : kern::plan_split(dtype(), L_, k, k, compute_cus_, spare, ring, -nseg,
                                                          cfg_.arith);

@@ -48,7 +48,9 @@ def _plan(h, k: int) -> dict:
             "main_bands": p.main.nb, "main_items": p.main_items, "main_waves": p.main_waves,
             "edge_items": p.edge_items, "edge_waves": p.edge_waves, "tuned_ms": ms.value,
             "main_rect": [p.main.r0, p.main.r1, p.main.s0, p.main.s1, p.main.nb],
-            "edge_rects": [[e.r0, e.r1, e.s0, e.s1, e.nb] for e in list(p.edge)[:p.nedge]]}
+            "edge_rects": [[e.r0, e.r1, e.s0, e.s1, e.nb] for e in list(p.edge)[:p.nedge]],
+            # the rects launched instead of main_rect: frame-weighted (arith 2) or a fused cycle's
+            "main_rects": [[e.r0, e.r1, e.s0, e.s1, e.nb] for e in list(p.fused)[:p.nfused]]}
 
 
 def _cycle_hist(h, reset: bool) -> dict:

@@ -178,3 +178,32 @@ def test_hip_jacobi_jit_and_ranks(gpu, native):
     g.step(p.ntime)
     assert np.array_equal(g.download(), golden(p, np.float64))
     g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,tb,env", [("fp32", 16, {"HEAT2D_SEGMENTS": "30"}),
+                                          ("fp64", 12, {"HEAT2D_SEGMENTS": "44"}),
+                                          ("fp32", 15, {"HEAT2D_BANDS": "4"}),
+                                          ("fp64", 20, {"HEAT2D_BANDS": "3"})])
+def test_hip_jacobi_single_launch_frame_rects(gpu, native, monkeypatch, dtype, tb, env):
+    """Single-launch plan (the small grid's) with frame-weighted rects: the two
+    frame-column strips and a short top / bottom band on every interior strip
+    (edge kind 1 costs ~1.5x an interior row: stencil_tb.hip weighted_main),
+    strip-aligned segments or bands in between — 5 rects, rough data, bitwise."""
+    monkeypatch.setenv("HEAT2D_SPLIT_ORDER", "single")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    p = prob(1100, 2 * tb + 3)
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    T0 = rough(p, npdt)
+    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0, arith="jacobi")
+    s.upload(T0)
+    s.step(p.ntime)
+    got = s.download()
+    pl = s.plan(tb)
+    s.close()
+    assert pl["order"] == "single" and len(pl["main_rects"]) == 5, pl
+    top, bot = pl["main_rects"][1], pl["main_rects"][3]
+    assert top[0] == 0 and top[4] == 1 and bot[1] == p.n_owned and bot[4] == 1, pl
+    assert top[1] - top[0] >= tb and bot[1] - bot[0] >= tb
+    assert np.array_equal(got, golden(p, npdt, T0))
