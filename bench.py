@@ -320,6 +320,7 @@ def main():
                 "arith": arith_name(prob.r, arith) + {"auto": " (auto)", "bench": " (r = 1/4)"}.get(args.arith, ""),
                 "overlap": not args.no_overlap,
                 "graph": bool(graph),
+                "persistent": bool(s.persistent(args.steps)) if hip else False,
                 "launch_plans": plans or None,
                 "backend": args.backend,
             },

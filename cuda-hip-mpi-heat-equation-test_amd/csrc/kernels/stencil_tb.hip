@@ -603,12 +603,26 @@ void launch_tb_persist(DType dt, void* buf0, void* buf1, const SlabLayout& L, co
   a.col_hi = L.col_hi();
   a.fixed_lo = -L.row0;
   a.fixed_hi = L.nrows_global - L.row0;
-  a.nrect = 1;
-  a.rect[0] = TbRectArg{R.r0, R.r1, R.s0, R.s1, R.nb, 0};
-  const int64_t rows = R.r1 - R.r0, ns = R.s1 - R.s0;
-  HEAT2D_REQUIRE(R.nb > 0 || -R.nb <= rows * ns, "more segments than strip rows");
-  HEAT2D_REQUIRE(rows * ns < (int64_t(1) << 31), "rect exceeds 2^31 strip rows");
-  a.nitems = R.nb > 0 ? R.nb * ns : -R.nb;
+  // the plan's rects (frame-weighted, weight_main) or its one main rect; they
+  // tile the slab, which the kernel's neighbour waits rely on
+  const TbRect* rects = plan.nfused > 0 ? plan.fused : &plan.main;
+  const int nr = plan.nfused > 0 ? plan.nfused : 1;
+  HEAT2D_REQUIRE(nr <= kMaxRects, "bad rect count");
+  int64_t items = 0, covered = 0;
+  for (int i = 0; i < nr; ++i) {
+    const TbRect& Q = rects[i];
+    const int64_t rows = Q.r1 - Q.r0, ns = Q.s1 - Q.s0;
+    HEAT2D_REQUIRE(rows > 0 && ns > 0 && Q.nb != 0 && Q.r0 >= 0 && Q.r1 <= L.nrows && Q.s0 >= R.s0 && Q.s1 <= R.s1,
+                   "persistent rect outside the slab");
+    HEAT2D_REQUIRE(Q.nb > 0 || -Q.nb <= rows * ns, "more segments than strip rows");
+    HEAT2D_REQUIRE(rows * ns < (int64_t(1) << 31), "rect exceeds 2^31 strip rows");
+    a.rect[i] = TbRectArg{Q.r0, Q.r1, Q.s0, Q.s1, Q.nb, items};
+    items += Q.nb > 0 ? Q.nb * ns : -Q.nb;
+    covered += rows * ns;
+  }
+  HEAT2D_REQUIRE(covered == (R.r1 - R.r0) * (R.s1 - R.s0), "persistent rects must tile the slab");
+  a.nrect = nr;
+  a.nitems = items;
   a.nwaves = a.nitems;
   // every item's wave must be resident at once (they wait on each other)
   HEAT2D_REQUIRE(a.nitems <= persist_capacity(dt, plan.ring, k, arith) && a.nitems <= ctl.nitems_cap,

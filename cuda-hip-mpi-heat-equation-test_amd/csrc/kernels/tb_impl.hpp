@@ -1108,25 +1108,32 @@ __device__ __forceinline__ bool wait_item(const PersistArgs& p, int64_t j, uint3
 
 // Wait until every item whose cycle-(c-1) output the piece (strip, rows
 // [t0, t1)) reads — rows [t0 - K, t1 + K) of strips strip - 1 .. strip + 1 —
-// has counter >= target. Single-rect launches (plan_single).
+// has counter >= target. The rects of a launch tile the slab without overlap
+// (a single-launch plan, or its frame-weighted rects: stencil_tb.hip
+// weighted_main), so those items are found rect by rect.
 template <int K>
 __device__ bool wait_piece(const TbArgs& a, const PersistArgs& p, int64_t self, int64_t strip, int64_t t0, int64_t t1,
                            uint32_t target, uint64_t t_start) {
-  const TbRectArg R = a.rect[0];
-  const int64_t rows = R.r1 - R.r0;
-  const int64_t lo = max(t0 - K, R.r0) - R.r0, hi = min(t1 + K, R.r1) - R.r0;  // strip-local rows [lo, hi)
-  for (int64_t s = max(strip - 1, R.s0); s <= min(strip + 1, R.s1 - 1); ++s) {
-    const int64_t sl = s - R.s0;
-    if (R.nb > 0) {
-      const int64_t ns = R.s1 - R.s0;
-      const int64_t b0 = ((lo + 1) * R.nb - 1) / rows, b1 = (hi * R.nb - 1) / rows;
-      for (int64_t b = b0; b <= b1; ++b) {
-        const int64_t j = R.item0 + b * ns + sl;
-        if (j != self && !wait_item(p, j, target, t_start)) return false;
+#pragma unroll
+  for (int i = 0; i < kMaxRects; ++i) {
+    if (i >= a.nrect) continue;
+    const TbRectArg R = a.rect[i];  // constant index (see tb_span)
+    const int64_t rows = R.r1 - R.r0;
+    const int64_t lo = max(t0 - K, R.r0) - R.r0, hi = min(t1 + K, R.r1) - R.r0;  // rect-local rows [lo, hi)
+    if (lo >= hi) continue;
+    for (int64_t s = max(strip - 1, R.s0); s <= min(strip + 1, R.s1 - 1); ++s) {
+      const int64_t sl = s - R.s0;
+      if (R.nb > 0) {
+        const int64_t ns = R.s1 - R.s0;
+        const int64_t b0 = ((lo + 1) * R.nb - 1) / rows, b1 = (hi * R.nb - 1) / rows;
+        for (int64_t b = b0; b <= b1; ++b) {
+          const int64_t j = R.item0 + b * ns + sl;
+          if (j != self && !wait_item(p, j, target, t_start)) return false;
+        }
+      } else {
+        for (int64_t j = item_of(R, sl, lo); j <= item_of(R, sl, hi - 1); ++j)
+          if (j != self && !wait_item(p, j, target, t_start)) return false;
       }
-    } else {
-      for (int64_t j = item_of(R, sl, lo); j <= item_of(R, sl, hi - 1); ++j)
-        if (j != self && !wait_item(p, j, target, t_start)) return false;
     }
   }
   return true;

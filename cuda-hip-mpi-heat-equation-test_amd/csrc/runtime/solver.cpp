@@ -1481,10 +1481,6 @@ const kern::SplitPlan* Solver::persist_plan(int k) {
   if (p.k != k) {
     const kern::SplitPlan& t = split_plan(k);
     kern::SplitPlan c = t.valid == 2 ? t : kern::plan_single(dtype(), L_, k, 0, 0, 0, cfg_.arith);
-    if (c.nfused > 0) {  // the persistent kernel runs one rect: drop the frame-strip weighting
-      c.nfused = 0;
-      c.main_items = c.main.nb > 0 ? c.main.nb * (c.main.s1 - c.main.s0) : -c.main.nb;
-    }
     const int64_t cap = kern::persist_capacity(dtype(), c.ring, k, cfg_.arith);
     if (c.main_items > cap) c = kern::plan_single(dtype(), L_, k, 0, c.ring, -cap, cfg_.arith);
     if (!c.valid || c.main_items > cap || c.main_items < 1) c.valid = 0;
