@@ -52,7 +52,7 @@ typedef struct heat2d_split_plan {
   heat2d_rect main;
   heat2d_rect edge[4];
   int64_t main_waves, edge_waves, main_items, edge_items;
-  int32_t nfused, pad;
+  int32_t nfused, pair;
   heat2d_rect fused[6];
   int64_t sig_items;
 } heat2d_split_plan;

@@ -78,7 +78,10 @@ struct SplitPlan {
   // then the interior — and `edge` holds only bands on the Dirichlet frame.
   // valid = 1..3 with nfused > 0 (arith 2): `main` cut into frame-strip-
   // weighted rects, launched instead of `main` (stencil_tb.hip weight_main).
-  int32_t nfused, pad;
+  // pair = 1 (valid = 2, fp32): the single launch runs the wave-pair kernel
+  // (tb_pair_kernel: two waves per item, the levels split between them);
+  // main_waves then counts PAIRS.
+  int32_t nfused, pair;
   TbRect fused[kMaxFused];
   int64_t sig_items;
 };
@@ -91,6 +94,10 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
 // where the second launch costs more than it saves.
 SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int ring_override = 0, int64_t bands = 0,
                       int arith = 0);
+// Co-resident wave pairs of the fp32 wave-pair kernel (0: not available for
+// this dtype / depth); pair_plan(p) = p run by that kernel (valid = 0 if not).
+int64_t pair_capacity(DType dt, int ring, int k, int arith);
+SplitPlan pair_plan(DType dt, const SplitPlan& p, int arith);
 // Fused cycle (valid = 4) for slabs whose halo exchange can be gated on a
 // device counter (Transport::gates()): ONE interior-kernel launch whose first
 // items are the boundary bands the exchange sends (top if send_top, bottom if

@@ -193,7 +193,7 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t simds, int k, int64_t pri
 // partials != nullptr: the fused-statistics kernel (general, ring 4). Returns the waves launched.
 int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
                      const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith,
-                     double* partials = nullptr, int64_t sig_items = 0, uint32_t* sig = nullptr) {
+                     double* partials = nullptr, int64_t sig_items = 0, uint32_t* sig = nullptr, bool pair = false) {
   HEAT2D_REQUIRE(nrect >= 1 && nrect <= (main ? kMainRects : kMaxRects), "bad rect count");
   TbArgs a{};
   a.pitch = L.pitch;
@@ -224,9 +224,19 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   HEAT2D_REQUIRE(sig_items == 0 || (main && sig != nullptr && sig_items <= items), "bad band-signal items");
   a.sig_items = sig_items;
   a.sig = sig;
-  const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
+  // (pair: nwaves counts wave pairs, two per 256-thread block)
+  const unsigned nblocks = pair ? (unsigned)((a.nwaves + 1) / 2) : (unsigned)((a.nwaves + 3) / 4);
   const int64_t o = L.origin();
-  if (partials) {
+  if (pair) {
+    HEAT2D_REQUIRE(dt == DType::F32 && !main && !partials && !sig && k >= 2, "wave pairs: fp32 general launches, k >= 2");
+    const float* s32 = static_cast<const float*>(src) + o;
+    float* d32 = static_cast<float*>(dst) + o;
+    with_ar(arith, [&](auto ar) {
+      constexpr int AR = decltype(ar)::value;
+      if (ring == 4) dispatch_pair<4, AR>(k, nblocks, s32, d32, a, (float)r, stream);
+      else dispatch_pair<6, AR>(k, nblocks, s32, d32, a, (float)r, stream);
+    });
+  } else if (partials) {
     HEAT2D_REQUIRE(a.nwaves <= max_stats_waves(), "statistics partials buffer too small");
     const float* s32 = static_cast<const float*>(src) + o;
     const double* s64 = static_cast<const double*>(src) + o;
@@ -360,8 +370,11 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 double pinned_weight(DType dt, bool row) {
   const char* env = std::getenv(row ? "HEAT2D_W_ROW" : "HEAT2D_W_COL");
   if (env && std::atof(env) >= 1.0) return std::atof(env);
+  // fp32 columns: 1.4 measured best over 1.0-2.3 (4096^2 K = 16, 1007
+  // segments: 58.7-59.1 us per cycle against 60.1 at 1.5 and 60.7 at 1.75,
+  // profiles/r3/sweep5/); the rest are the VALU-op ratios
   if (row) return dt == DType::F32 ? 1.5 : 1.4;
-  return dt == DType::F32 ? 1.75 : 1.6;
+  return dt == DType::F32 ? 1.4 : 1.6;
 }
 
 int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect out[kMaxFused]) {
@@ -578,6 +591,27 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   return p;
 }
 
+int64_t pair_capacity(DType dt, int ring, int k, int arith) {
+  if (dt != DType::F32 || k < 2 || k > max_tb(dt) || (ring != 4 && ring != 6)) return 0;
+  const int bpc = with_ar(arith, [&](auto ar) {
+    constexpr int AR = decltype(ar)::value;
+    return ring == 4 ? occupancy_pair<4, AR>(k) : occupancy_pair<6, AR>(k);
+  });
+  return (int64_t)cu_count() * bpc * 2;
+}
+
+SplitPlan pair_plan(DType dt, const SplitPlan& p, int arith) {
+  SplitPlan q = p;
+  const int64_t cap = p.valid == 2 ? pair_capacity(dt, p.ring, p.k, arith) : 0;
+  if (cap <= 0) {
+    q.valid = 0;
+    return q;
+  }
+  q.pair = 1;
+  q.main_waves = std::min<int64_t>(q.main_items, cap);  // pairs
+  return q;
+}
+
 int64_t persist_capacity(DType dt, int ring, int k, int arith) {
   HEAT2D_REQUIRE(ring == 4 || ring == 6, "ring must be 4 or 6");
   const int bpc = with_ar(arith, [&](auto ar) {
@@ -678,7 +712,9 @@ void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, con
   const TbRect* mr = p.nfused > 0 ? p.fused : &p.main;
   const int nm = p.nfused > 0 ? p.nfused : 1;
   if (p.valid == 2) {  // single general launch over the whole slab (no edge part)
-    if (main_part) launch_rects(dt, src, dst, L, p.k, p.ring, false, mr, nm, p.main_waves, r, stream, arith);
+    if (main_part)
+      launch_rects(dt, src, dst, L, p.k, p.ring, false, mr, nm, p.main_waves, r, stream, arith, nullptr, 0, nullptr,
+                   p.pair != 0);
     return;
   }
   if (main_part)

@@ -536,7 +536,31 @@ struct March {
 // ~2x the registers: 209 VGPRs at K = 10). Same operation order and rounding
 // per element as March (bitwise identical); the loads / stores / ring /
 // descriptors / edge kinds are March's.
-template <int K, int EK, int RING, int AR, bool ST = false, int CL = K, int CP = 0>
+// Wave pair (tb_pair_kernel): IO 1 = the producer (levels 1..K of the pair's
+// first half: global loads, its last level handed to the consumer through an
+// LDS row ring, still scaled), IO 2 = the consumer (its rows come from that
+// ring; LIN levels already applied to them). kPairRing rows per pair.
+constexpr int kPairRing = 16;
+// polls before a ring wait gives up (~2 s of s_sleep 1): a wrong result, never a hang
+constexpr uint32_t kPairSpin = 1u << 25;
+
+__device__ __forceinline__ uint32_t lds_ctr_load(const uint32_t* c) {
+  return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_ctr_store(uint32_t* c, uint32_t v) {
+  __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait until *c >= need (wrap-safe); returns the value seen
+__device__ __forceinline__ uint32_t lds_wait_ge(const uint32_t* c, uint32_t need) {
+  uint32_t v = lds_ctr_load(c);
+  for (uint32_t n = 0; (int32_t)(v - need) < 0 && n < kPairSpin; ++n) {
+    __builtin_amdgcn_s_sleep(1);
+    v = lds_ctr_load(c);
+  }
+  return v;
+}
+
+template <int K, int EK, int RING, int AR, bool ST = false, int CL = K, int CP = 0, int IO = 0, int LIN = 0>
 struct MarchF32 {
   using F2 = float __attribute__((ext_vector_type(2)));
   using VT = float __attribute__((ext_vector_type(4)));
@@ -560,6 +584,14 @@ struct MarchF32 {
   int32_t st_off;
   Row rl;  // EK & 2: r per element (0 in Dirichlet / pad columns)
   static constexpr bool kScaled = AR == 2 && EK == 0;  // levels carried x 4^level (see March)
+  // IO 1 / 2: the pair's LDS row ring (kPairRing rows of 64 lanes) and its
+  // counters {rows produced, rows consumed}, monotone over the pair's items:
+  // row `row` of this piece is ring entry qbase + (qtop - row)
+  VT* pring;
+  uint32_t* pctr;
+  uint32_t qbase;
+  int32_t qtop, qlast;
+  uint32_t have;  // last counter value seen (producer: consumed, consumer: produced)
 
   using Ch = ChainShape<K, CL>;
   static constexpr int L = Ch::unroll(RING);
@@ -572,14 +604,41 @@ struct MarchF32 {
   // of a rebuild at each of its three uses.
   Row Lb[RING];
 
-  __device__ __forceinline__ void load_row(int32_t m, Row& out) const {
-    const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + (int64_t)m * pitch_b, nrec);
-    const VT v = __builtin_bit_cast(VT, __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off, 0, kLoadAux<CP>));
-    out = Row{F2{v.x, v.y}, F2{v.z, v.w}};
+  __device__ __forceinline__ void load_row(int32_t m, Row& out) {
+    if constexpr (IO == 2) {  // consumer: the producer's row, once it is in the ring
+      int32_t q = qtop - m;
+      q = q > qlast ? qlast : q;  // clamped rows below the last one only feed priming values
+      const uint32_t e = qbase + (uint32_t)q;
+      if ((int32_t)(have - (e + 1u)) < 0) have = lds_wait_ge(pctr, e + 1u);
+      asm volatile("" ::: "memory");
+      const int lane = (int)(threadIdx.x & 63);
+      const VT v = pring[(e & (kPairRing - 1)) * 64 + lane];
+      out = Row{F2{v.x, v.y}, F2{v.z, v.w}};
+      asm volatile("" ::: "memory");
+      // LDS executes one wave's operations in order: the producer sees this
+      // count only after the read above has taken the row
+      if (lane == 0) lds_ctr_store(pctr + 1, e + 1u);
+    } else {
+      const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + (int64_t)m * pitch_b, nrec);
+      const VT v = __builtin_bit_cast(VT, __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off, 0, kLoadAux<CP>));
+      out = Row{F2{v.x, v.y}, F2{v.z, v.w}};
+    }
   }
-  __device__ __forceinline__ void store_row(int32_t row, bool live, const VT& w) const {
-    const __amdgpu_buffer_rsrc_t rs = row_rsrc(drow + (int64_t)row * pitch_b, live ? nrec : 0u);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off, 0, kStoreAux<CP>);
+  __device__ __forceinline__ void store_row(int32_t row, bool live, const VT& w) {
+    if constexpr (IO == 1) {  // producer: into the ring once its slot's previous row was consumed
+      if (live) {             // wave-uniform
+        const uint32_t e = qbase + (uint32_t)(qtop - row);
+        if ((int32_t)(have - (e + 1u - kPairRing)) < 0) have = lds_wait_ge(pctr + 1, e + 1u - kPairRing);
+        asm volatile("" ::: "memory");
+        const int lane = (int)(threadIdx.x & 63);
+        pring[(e & (kPairRing - 1)) * 64 + lane] = w;
+        asm volatile("" ::: "memory");
+        if (lane == 0) lds_ctr_store(pctr, e + 1u);
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t rs = row_rsrc(drow + (int64_t)row * pitch_b, live ? nrec : 0u);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off, 0, kStoreAux<CP>);
+    }
   }
   static __device__ __forceinline__ Row split(const Row& v) { return Row{F2{v.a.x, v.b.x}, F2{v.a.y, v.b.y}}; }
 
@@ -649,8 +708,11 @@ struct MarchF32 {
   __device__ __forceinline__ VT update_last(const Row& part, const Row& C, const Row& N, int32_t row) const {
     if constexpr (AR == 2) {
       const Row sum = sum4(part, C, N);
-      if constexpr (EK == 0) {  // unscale 4^K T once, at the store (exact)
-        constexpr float u = inv_pow4<float>(K);
+      if constexpr (EK == 0) {
+        // unscale 4^K T once, at the store (exact); the producer of a pair
+        // hands its rows on scaled, its consumer unscales the pair's LIN + K
+        if constexpr (IO == 1) return VT{sum.a.x, sum.b.x, sum.a.y, sum.b.y};
+        constexpr float u = inv_pow4<float>(LIN + K);
         return VT{sum.a.x * u, sum.b.x * u, sum.a.y * u, sum.b.y * u};
       }
       const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
@@ -828,6 +890,65 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
     *acc = w.acc;
   } else {
     w.template run<PS>();
+  }
+}
+
+// Wave-pair march of one piece (tb_pair_kernel, fp32): the producer (role 0)
+// runs levels 1..KA over the piece's rows widened by KB on both sides (its
+// march covers rows [t0 - K, t1 + K), as a single wave of depth K would), the
+// consumer (role 1) levels KA+1..K over the piece itself, its input rows the
+// producer's level KA, taken from the pair's LDS ring as they appear. Strip
+// geometry (halo columns, useful width) is that of the whole depth K. Same
+// operations in the same order per point as one wave of depth K: bitwise
+// identical. qbase: ring entries of the pair's earlier pieces.
+template <int K, int EK, int RING, int AR>
+__device__ __forceinline__ void march_pair(const float* src, float* dst, const TbArgs& a, float r, int64_t strip,
+                                           int64_t t0, int64_t t1, int lane, int role,
+                                           float __attribute__((ext_vector_type(4))) * ring, uint32_t* ctr,
+                                           uint32_t qbase) {
+  constexpr int KA = K / 2, KB = K - KA;
+  using S = TbShape<float, 1, K>;
+  constexpr int V = S::V;
+  const int64_t u0 = strip * S::U;
+  const int64_t mycol = u0 - S::KA + (int64_t)lane * V;
+  const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
+  const int32_t off = (int32_t)((mycol - a.col_lo) * 4);
+  const bool in_alloc = (mycol >= a.col_lo) && (mycol + V <= a.col_hi);
+  const bool useful = (mycol >= u0) && (mycol < ustop);
+  auto setup = [&](auto& w) {
+    w.srow = reinterpret_cast<const char*>(src + a.col_lo);
+    w.drow = reinterpret_cast<char*>(dst + a.col_lo);
+    w.pitch_b = a.pitch * 4;
+    w.nrec = (uint32_t)(a.pitch * 4);
+    w.r = r;
+    w.fixed_lo = (int32_t)a.fixed_lo;
+    w.fixed_hi = (int32_t)a.fixed_hi;
+    w.ld_off = in_alloc ? off : kOob;
+    w.st_off = useful && in_alloc ? off : kOob;
+    if constexpr ((EK & 2) != 0) {
+      auto rcol = [&](int e) { return (mycol + e < 0 || mycol + e >= a.ncols) ? 0.f : r; };
+      w.rl.a = {rcol(0), rcol(2)};
+      w.rl.b = {rcol(1), rcol(3)};
+    }
+    w.pring = ring;
+    w.pctr = ctr;
+    w.qbase = qbase;
+    w.qtop = (int32_t)(t1 + KB - 1);
+    w.qlast = (int32_t)(t1 - t0 + 2 * KB - 1);
+    w.have = 0;
+  };
+  if (role == 0) {
+    MarchF32<KA, EK, RING, AR, false, KA, 0, 1, 0> w;
+    setup(w);
+    w.t0 = (int32_t)(t0 - KB);
+    w.t1 = (int32_t)(t1 + KB);
+    w.run();
+  } else {
+    MarchF32<KB, EK, RING, AR, false, KB, 0, 2, KA> w;
+    setup(w);
+    w.t0 = (int32_t)t0;
+    w.t1 = (int32_t)t1;
+    w.run();
   }
 }
 
@@ -1052,6 +1173,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
 #pragma unroll
       for (int j = 0; j < kNStatFused; ++j) a.partials[j * a.nwaves + wid] = v[j];
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-pair kernel (fp32 single launches of small grids). With one march wave
+// per SIMD (the 4096^2 grid: ~1000 items, no second wave without doubling the
+// priming rows), every non-VALU instruction of that wave — loads, stores,
+// waits, scalar address work, DPP hazard nops — is a VALU issue slot lost
+// (VALU ~74 % busy: profiles/small_grid/). Here each item is marched by TWO
+// waves, the K levels split between them (producer KA = K/2, consumer K - KA),
+// handing rows over through a 16-row LDS ring with two counters: 2 waves per
+// SIMD for the same item count and (slightly fewer) level-rows. A 256-thread
+// block holds 2 pairs; the waves of a pair agree on the item sequence, and the
+// only cross-wave waits are the ring's (bounded: kPairSpin).
+template <int K, int RING, int AR>
+__global__ __launch_bounds__(256) void tb_pair_kernel(const float* __restrict__ src, float* __restrict__ dst, TbArgs a,
+                                                      float r) {
+  using VT4 = float __attribute__((ext_vector_type(4)));
+  constexpr int KB = K - K / 2;
+  __shared__ VT4 ring[2][kPairRing * 64];
+  __shared__ uint32_t ctr[2][2];
+  if (threadIdx.x < 4) ctr[threadIdx.x >> 1][threadIdx.x & 1] = 0u;
+  __syncthreads();
+  using S = TbShape<float, 1, K>;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int pr = w >> 1, role = w & 1;
+  const int64_t pid = (int64_t)blockIdx.x * 2 + pr;
+  if (pid >= a.nwaves) return;  // nwaves = pairs launched
+  uint32_t qbase = 0;
+  int64_t it = pid;
+  int32_t lin = tb_span(a, it).lin;
+  while (it < a.nitems) {
+    int64_t strip, t0, t1;
+    if (!tb_piece(a, it, lin, strip, t0, t1)) {
+      it += a.nwaves;
+      if (it < a.nitems) lin = tb_span(a, it).lin;
+      continue;
+    }
+    lin += (int32_t)(t1 - t0);
+    const int64_t c0 = strip * S::U - S::KA;
+    const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
+                   (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
+    switch (ek) {
+      case 0: march_pair<K, 0, RING, AR>(src, dst, a, r, strip, t0, t1, lane, role, ring[pr], ctr[pr], qbase); break;
+      case 1: march_pair<K, 1, RING, AR>(src, dst, a, r, strip, t0, t1, lane, role, ring[pr], ctr[pr], qbase); break;
+      case 2: march_pair<K, 2, RING, AR>(src, dst, a, r, strip, t0, t1, lane, role, ring[pr], ctr[pr], qbase); break;
+      default: march_pair<K, 3, RING, AR>(src, dst, a, r, strip, t0, t1, lane, role, ring[pr], ctr[pr], qbase); break;
+    }
+    qbase += (uint32_t)(t1 - t0 + 2 * KB);
   }
 }
 
@@ -1359,6 +1530,61 @@ int occupancy_blocks_stats(int k);
         break;                                                                                             \
     }                                                                                                      \
     return 1;                                                                                              \
+  }
+// wave-pair kernels (fp32, K = 2..16): tb_f32_r<RING>_pair[_fma|_jac].hip
+template <int RING, int AR>
+void dispatch_pair(int k, unsigned nblocks, const float* src, float* dst, const TbArgs& a, float r, hipStream_t s);
+template <int RING, int AR>
+int occupancy_pair(int k);  // resident 256-thread blocks (2 pairs each) per CU
+template <int K, int RING, int AR>
+int pair_blocks_per_cu() {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&tb_pair_kernel<K, RING, AR>), 256,
+                                                   0) != hipSuccess ||
+      nb <= 0)
+    nb = 1;
+  cache[dev] = nb;
+  return nb;
+}
+#define H2D_PR_CASE(T, RING, MAIN, AR, KK)                                                              \
+  case KK:                                                                                              \
+    hipLaunchKernelGGL((tb_pair_kernel<KK, RING, AR>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
+    return;
+#define H2D_PR_OCC_CASE(T, RING, MAIN, AR, KK) \
+  case KK:                                     \
+    return pair_blocks_per_cu<KK, RING, AR>();
+// K = 2..16 (a pair splits the levels)
+#define H2D_TB_CASES_PAIR(M, T, RING, MAIN, AR)                                                         \
+  M(T, RING, MAIN, AR, 2) M(T, RING, MAIN, AR, 3) M(T, RING, MAIN, AR, 4) M(T, RING, MAIN, AR, 5)       \
+  M(T, RING, MAIN, AR, 6) M(T, RING, MAIN, AR, 7) M(T, RING, MAIN, AR, 8) M(T, RING, MAIN, AR, 9)       \
+  M(T, RING, MAIN, AR, 10) M(T, RING, MAIN, AR, 11) M(T, RING, MAIN, AR, 12) M(T, RING, MAIN, AR, 13)   \
+  M(T, RING, MAIN, AR, 14) M(T, RING, MAIN, AR, 15) M(T, RING, MAIN, AR, 16)
+#define H2D_PR_UNIT(RING, AR)                                                                                  \
+  template <>                                                                                                  \
+  void dispatch_pair<RING, AR>(int k, unsigned nblocks, const float* src, float* dst, const TbArgs& a, float r, \
+                               hipStream_t s) {                                                                \
+    switch (k) {                                                                                               \
+      H2D_TB_CASES_PAIR(H2D_PR_CASE, float, RING, false, AR)                                                        \
+      default:                                                                                                 \
+        break;                                                                                                 \
+    }                                                                                                          \
+    HEAT2D_REQUIRE(false, "temporal depth not instantiated for the wave-pair kernel (K = 2..16)");             \
+  }                                                                                                            \
+  template <>                                                                                                  \
+  int occupancy_pair<RING, AR>(int k) {                                                                        \
+    switch (k) {                                                                                               \
+      H2D_TB_CASES_PAIR(H2D_PR_OCC_CASE, float, RING, false, AR)                                                    \
+      default:                                                                                                 \
+        break;                                                                                                 \
+    }                                                                                                          \
+    return 1;                                                                                                  \
   }
 #define H2D_TB_UNIT(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_NO_CASES)
 #define H2D_TB_UNIT_F64(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_DEEP)

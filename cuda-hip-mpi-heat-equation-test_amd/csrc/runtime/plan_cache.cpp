@@ -135,10 +135,12 @@ bool get_plan(const std::string& ctx, int k, int64_t band, kern::SplitPlan* p, f
     for (auto& x : r) in >> x;
     e = kern::TbRect{r[0], r[1], r[2], r[3], r[4]};
   }
-  in >> sig;
+  long long pr = 0;
+  in >> sig >> pr;
   q.nfused = (int32_t)nf;
   q.sig_items = sig;
-  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > kern::kMaxFused) return false;
+  q.pair = (int32_t)pr;
+  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > kern::kMaxFused || q.pair < 0 || q.pair > 1) return false;
   *p = q;
   *ms = t;
   return true;
@@ -153,7 +155,7 @@ void put_plan(const std::string& ctx, int k, int64_t band, const kern::SplitPlan
   o << ' ' << p.main_waves << ' ' << p.edge_waves << ' ' << p.main_items << ' ' << p.edge_items << ' ' << ms;
   o << ' ' << p.nfused;
   for (const auto& e : p.fused) rect(e);
-  o << ' ' << p.sig_items;
+  o << ' ' << p.sig_items << ' ' << p.pair;
   store(plan_key(ctx, k, band), o.str());
 }
 

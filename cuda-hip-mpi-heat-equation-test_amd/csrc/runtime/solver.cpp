@@ -477,6 +477,11 @@ const kern::SplitPlan& Solver::split_plan(int k) {
         p.k = k;
       }
     }
+    // HEAT2D_PAIR=1: a single-launch plan runs as the wave-pair kernel (tests, A/B)
+    if (const char* e = std::getenv("HEAT2D_PAIR"); e && std::atoi(e) == 1 && p.valid == 2 && !p.pair) {
+      const kern::SplitPlan q = kern::pair_plan(dtype(), p, cfg_.arith);
+      if (q.valid) p = q;
+    }
   }
   return p;
 }
@@ -528,6 +533,14 @@ static int device_cus_of(int device) {
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
   return ncu;
+}
+
+static bool pair_candidates() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_PAIR");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
 }
 
 static bool tune_segments() {
@@ -672,6 +685,16 @@ void Solver::autotune_split(int k) {
   // exchange of the bands running beside the interior (valid = 3)
   bool top = false, bot = false;
   sent_sides(&top, &bot);
+  // every candidate; a single launch (fp32) also as the wave-pair kernel
+  // (tb_pair_kernel: two waves per item, for grids whose items leave one
+  // wave per SIMD); HEAT2D_PAIR=0 skips those
+  auto add = [&](const kern::SplitPlan& c) {
+    timed.emplace_back(time_plan(c, 4), c);
+    if (c.valid == 2 && pair_candidates()) {
+      const kern::SplitPlan q = kern::pair_plan(dtype(), c, cfg_.arith);
+      if (q.valid) timed.emplace_back(time_plan(q, 4), q);
+    }
+  };
   for (int mode : {1, 2, 3, 4}) {
     if (mode == 2 && !single_ok) continue;
     if (mode == 4) {
@@ -702,7 +725,7 @@ void Solver::autotune_split(int k) {
         if (mode == 3) c.valid = 3;
         if (mode == 1)  // more items than waves only via explicit band counts above the default
           c.main_waves = std::min<int64_t>(c.main_items, std::max<int64_t>(c.main_waves, best.main_waves));
-        timed.emplace_back(time_plan(c, 4), c);
+        add(c);
       }
       // segment work items (TbRect nb < 0): the interior cut into equal runs of
       // strip rows, 1/2 .. 2 per persistent wave — balanced whatever the strip
@@ -734,7 +757,7 @@ void Solver::autotune_split(int k) {
                                                          cfg_.arith);
         if (!c.valid) continue;
         if (mode == 3) c.valid = 3;
-        timed.emplace_back(time_plan(c, 4), c);
+        add(c);
       }
     }
   }
@@ -1481,6 +1504,10 @@ const kern::SplitPlan* Solver::persist_plan(int k) {
   if (p.k != k) {
     const kern::SplitPlan& t = split_plan(k);
     kern::SplitPlan c = t.valid == 2 ? t : kern::plan_single(dtype(), L_, k, 0, 0, 0, cfg_.arith);
+    if (c.pair) {  // one wave per item here
+      c.pair = 0;
+      c.main_waves = c.main_items;
+    }
     const int64_t cap = kern::persist_capacity(dtype(), c.ring, k, cfg_.arith);
     if (c.main_items > cap) c = kern::plan_single(dtype(), L_, k, 0, c.ring, -cap, cfg_.arith);
     if (!c.valid || c.main_items > cap || c.main_items < 1) c.valid = 0;

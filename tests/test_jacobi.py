@@ -207,3 +207,28 @@ def test_hip_jacobi_single_launch_frame_rects(gpu, native, monkeypatch, dtype, t
     assert top[0] == 0 and top[4] == 1 and bot[1] == p.n_owned and bot[4] == 1, pl
     assert top[1] - top[0] >= tb and bot[1] - bot[0] >= tb
     assert np.array_equal(got, golden(p, npdt, T0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arith", ["jacobi", "fma", "exact"])
+@pytest.mark.parametrize("tb,env", [(16, {"HEAT2D_SEGMENTS": "30"}), (15, {"HEAT2D_BANDS": "4"}), (2, {}),
+                                    (3, {"HEAT2D_SEGMENTS": "7"}), (8, {"HEAT2D_SEGMENTS": "600"})])
+def test_hip_pair_kernel(gpu, native, monkeypatch, arith, tb, env):
+    """Wave-pair kernel (tb_pair_kernel: two waves per item, the levels split
+    between a producer and a consumer through an LDS row ring): every edge
+    kind, segments crossing strip ends (7 / 600 segments), several items per
+    pair (600 > co-resident pairs is not needed: grid stride), bitwise."""
+    monkeypatch.setenv("HEAT2D_SPLIT_ORDER", "single")
+    monkeypatch.setenv("HEAT2D_PAIR", "1")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    p = prob(1100, 2 * tb + 3)
+    T0 = rough(p, np.float32)
+    s = HeatSolver(p, dtype="fp32", backend="hip", tb=tb, device=0, autotune=0, arith=arith)
+    s.upload(T0)
+    s.step(p.ntime)
+    got = s.download()
+    pl = s.plan(tb)
+    s.close()
+    assert pl["order"] == "single" and pl["pair"] == 1, pl
+    assert np.array_equal(got, golden(p, np.float32, T0, arith=arith))
