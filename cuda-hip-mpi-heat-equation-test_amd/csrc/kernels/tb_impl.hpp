@@ -308,6 +308,18 @@ struct March {
 
   const char* srow;  // byte address of (row 0, column -cpad) in src   [wave-uniform]
   char* drow;        // same in dst                                      [wave-uniform]
+  // Row pointers of the steady march, stepped by one row per march row: the
+  // prefetch row (m + 2 - RING) and the stored row (m + off(K)). A row address
+  // recomputed from its index costs ~12 scalar ops (64-bit multiply, sign,
+  // descriptor) per access — with one wave per SIMD every one an issue slot
+  // the VALU loses (31 SALU per march row against 136 VALU at fp32 K = 16,
+  // rocprofv3 SQ_INSTS_SALU, profiles/r3/pairprof/).
+  const char* lp;
+  char* sp;
+  // ... except in the fp64 K >= 20 ring-4 kernels, where the two loop-carried
+  // pointers push the interior kernel past 256 VGPRs (SGPR spills into VGPR
+  // lanes: 1 wave/SIMD instead of 2); those keep the per-row recomputation
+  static constexpr bool kIncPtr = !(std::is_same<T, double>::value && K >= 20 && RING == 4);
   int64_t pitch_b;   // bytes per row                                    [wave-uniform]
   uint32_t nrec;     // descriptor size (= pitch_b)
   T r;
@@ -327,8 +339,11 @@ struct March {
   StatAcc acc;       // ST: statistics of the stored rows
   uint32_t colmask;  // ST: bit e = element e is an owned output column of this lane
 
-  __device__ __forceinline__ void load_row(int32_t m, VT (&out)[NV]) const {
-    const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + (int64_t)m * pitch_b, nrec);
+  __device__ __forceinline__ void load_row(int32_t m, VT (&out)[NV]) const { load_row_p(srow + (int64_t)m * pitch_b, true, out); }
+  // live == false: a row below the item's lowest loaded row (it only feeds
+  // priming values): num_records 0, the load returns 0 without a memory access
+  __device__ __forceinline__ void load_row_p(const char* p, bool live, VT (&out)[NV]) const {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(p, live ? nrec : 0u);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       U4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off + v * 16, 0, kLoadAux<CP>);
@@ -337,8 +352,8 @@ struct March {
   }
 
   // live == false (priming rows): num_records 0 drops the whole store.
-  __device__ __forceinline__ void store_row(int32_t row, bool live, const T (&out)[V]) const {
-    const __amdgpu_buffer_rsrc_t rs = row_rsrc(drow + (int64_t)row * pitch_b, live ? nrec : 0u);
+  __device__ __forceinline__ void store_row(char* p, bool live, const T (&out)[V]) const {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(p, live ? nrec : 0u);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       VT w;
@@ -367,7 +382,7 @@ struct March {
   __device__ __forceinline__ void update(const T (&part)[V], const T (&C)[V], const T (&N)[V], int32_t row,
                                          T (&out)[V]) const {
     const T west0 = from_lower(C[V - 1]);
-    const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
+    const bool frame_row = (EK & 1) && ((uint32_t)(row - fixed_lo) >= (uint32_t)(fixed_hi - fixed_lo));  // wave-uniform
     const T rs = frame_row ? T(0) : r;                                      // EK 1: scalar select
 #pragma unroll
     for (int e = 0; e < V; ++e) {
@@ -419,7 +434,12 @@ struct March {
       // latch (which waits for the load and serialises the ring).
       const int32_t nxt = m + 2 - RING;
       __builtin_amdgcn_sched_barrier(0);
-      load_row(nxt >= mload ? nxt : mload, Lb[sS]);
+      if constexpr (kIncPtr) {
+        load_row_p(lp, nxt >= mload, Lb[sS]);
+        lp -= pitch_b;
+      } else {
+        load_row(nxt >= mload ? nxt : mload, Lb[sS]);
+      }
     }
     unpack(Lb[sN], N0);
 #pragma unroll
@@ -448,12 +468,12 @@ struct March {
         for (int e = 0; e < V; ++e) part[e] = nxtpart[e];
       } else {
         const int32_t row = m + Ch::off(K);
-        const bool live = row < t1 && row >= t0;  // wave-uniform
+        const bool live = (uint32_t)(row - t0) < (uint32_t)(t1 - t0);  // row in [t0, t1), wave-uniform
         if constexpr (kScaled) {
 #pragma unroll
           for (int e = 0; e < V; ++e) out[e] *= inv_pow4<T>(K);
         }
-        store_row(row, live, out);
+        store_row(kIncPtr ? sp : drow + (int64_t)row * pitch_b, live, out);
         if constexpr (ST) {
           if (live) {
             constexpr T cu = kScaled ? inv_pow4<T>(K - 1) : T(1);  // level K-1 scale
@@ -463,6 +483,7 @@ struct March {
         }
       }
     }
+    if constexpr (kIncPtr) sp -= pitch_b;
   }
 
   template <int... I>
@@ -489,6 +510,8 @@ struct March {
     mload = t0 - K;
     mlo = t0 - Ch::off(K);
     const int32_t mtop = t1 + K - 1;
+    lp = srow + (int64_t)(mtop + 2 - RING) * pitch_b;
+    sp = drow + (int64_t)(mtop + Ch::off(K)) * pitch_b;
     // slots 0..RING-3: rows mtop, mtop-1, ...; slots RING-2 / RING-1 stand for
     // rows mtop+2 / mtop+1 (priming only: their results are never stored)
 #pragma unroll
@@ -573,6 +596,8 @@ struct MarchF32 {
 
   const char* srow;
   char* drow;
+  const char* lp;  // steady-march row pointers (see March)
+  char* sp;
   int64_t pitch_b;
   uint32_t nrec;
   float r;
@@ -619,10 +644,14 @@ struct MarchF32 {
       // count only after the read above has taken the row
       if (lane == 0) lds_ctr_store(pctr + 1, e + 1u);
     } else {
-      const __amdgpu_buffer_rsrc_t rs = row_rsrc(srow + (int64_t)m * pitch_b, nrec);
-      const VT v = __builtin_bit_cast(VT, __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off, 0, kLoadAux<CP>));
-      out = Row{F2{v.x, v.y}, F2{v.z, v.w}};
+      load_row_p(srow + (int64_t)m * pitch_b, true, out);
     }
+  }
+  // live == false: below the item's lowest loaded row (priming values only): returns 0
+  __device__ __forceinline__ void load_row_p(const char* p, bool live, Row& out) const {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(p, live ? nrec : 0u);
+    const VT v = __builtin_bit_cast(VT, __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off, 0, kLoadAux<CP>));
+    out = Row{F2{v.x, v.y}, F2{v.z, v.w}};
   }
   __device__ __forceinline__ void store_row(int32_t row, bool live, const VT& w) {
     if constexpr (IO == 1) {  // producer: into the ring once its slot's previous row was consumed
@@ -636,7 +665,7 @@ struct MarchF32 {
         if (lane == 0) lds_ctr_store(pctr, e + 1u);
       }
     } else {
-      const __amdgpu_buffer_rsrc_t rs = row_rsrc(drow + (int64_t)row * pitch_b, live ? nrec : 0u);
+      const __amdgpu_buffer_rsrc_t rs = row_rsrc(sp, live ? nrec : 0u);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off, 0, kStoreAux<CP>);
     }
   }
@@ -665,7 +694,7 @@ struct MarchF32 {
     const Row sum = sum4(part, C, N);
     const F2 m4 = {-4.f, -4.f};
     in = Row{__builtin_elementwise_fma(m4, C.a, sum.a), __builtin_elementwise_fma(m4, C.b, sum.b)};
-    const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
+    const bool frame_row = (EK & 1) && ((uint32_t)(row - fixed_lo) >= (uint32_t)(fixed_hi - fixed_lo));  // wave-uniform
     if constexpr (EK == 0) {
       re = Row{F2{r, r}, F2{r, r}};
     } else if constexpr (EK == 1) {
@@ -682,7 +711,7 @@ struct MarchF32 {
     if constexpr (AR == 2) {
       const Row sum = sum4(part, C, N);
       if constexpr (EK == 0) return sum;  // scaled: 4^s T
-      const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
+      const bool frame_row = (EK & 1) && ((uint32_t)(row - fixed_lo) >= (uint32_t)(fixed_hi - fixed_lo));  // wave-uniform
       if constexpr (EK == 1) {  // fma(ke, C, re * sum), scalar (re, ke) (see March::update)
         const F2 re = {frame_row ? 0.f : r, frame_row ? 0.f : r}, ke = {frame_row ? 1.f : 0.f, frame_row ? 1.f : 0.f};
         return Row{__builtin_elementwise_fma(ke, C.a, re * sum.a), __builtin_elementwise_fma(ke, C.b, re * sum.b)};
@@ -715,7 +744,7 @@ struct MarchF32 {
         constexpr float u = inv_pow4<float>(LIN + K);
         return VT{sum.a.x * u, sum.b.x * u, sum.a.y * u, sum.b.y * u};
       }
-      const bool frame_row = (EK & 1) && (row < fixed_lo || row >= fixed_hi);  // wave-uniform
+      const bool frame_row = (EK & 1) && ((uint32_t)(row - fixed_lo) >= (uint32_t)(fixed_hi - fixed_lo));  // wave-uniform
       if constexpr (EK == 1) {
         const float re = frame_row ? 0.f : r, ke = frame_row ? 1.f : 0.f;
         return VT{__builtin_fmaf(ke, C.a.x, re * sum.a.x), __builtin_fmaf(ke, C.b.x, re * sum.b.x),
@@ -741,7 +770,12 @@ struct MarchF32 {
     {
       const int32_t nxt = m + 2 - RING;
       __builtin_amdgcn_sched_barrier(0);
-      load_row(nxt >= mload ? nxt : mload, Lb[sS]);
+      if constexpr (IO == 2) {
+        load_row(nxt >= mload ? nxt : mload, Lb[sS]);
+      } else {
+        load_row_p(lp, nxt >= mload, Lb[sS]);
+        lp -= pitch_b;
+      }
     }
     Lb[sN] = split(Lb[sN]);  // first use of this row: to even/odd form, in place
     const Row N0 = Lb[sN];
@@ -760,7 +794,7 @@ struct MarchF32 {
         part = nxtpart;
       } else {
         const int32_t row = m + Ch::off(K);
-        const bool live = row < t1 && row >= t0;  // wave-uniform
+        const bool live = (uint32_t)(row - t0) < (uint32_t)(t1 - t0);  // row in [t0, t1), wave-uniform
         const VT w = update_last(part, C, N, row);
         store_row(row, live, w);
         if constexpr (ST) {
@@ -774,6 +808,7 @@ struct MarchF32 {
         }
       }
     }
+    if constexpr (IO != 1) sp -= pitch_b;
   }
 
   template <int... I>
@@ -793,6 +828,8 @@ struct MarchF32 {
     mload = t0 - K;
     mlo = t0 - Ch::off(K);
     const int32_t mtop = t1 + K - 1;
+    lp = srow + (int64_t)(mtop + 2 - RING) * pitch_b;
+    sp = drow + (int64_t)(mtop + Ch::off(K)) * pitch_b;
 #pragma unroll
     for (int q = 0; q < RING - 2; ++q) load_row(mtop - q >= mload ? mtop - q : mload, Lb[q]);
 #pragma unroll
