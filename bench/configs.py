@@ -21,14 +21,17 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(name, n, dtype, steps, warmup, backend, tb, graph=False):
+def run(name, n, dtype, steps, warmup, backend, tb, graph=False, arith="bench"):
     import heat2d
     from heat2d.models.heat2d import HeatSolver
     from heat2d.utils.metrics import plan_hbm_bytes
     inp = heat2d.InputDat(n=n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=steps, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
+    # bench: the r = 1/4 form when r == 1/4 (every config here), as bench.py
+    ar = ("jacobi" if prob.r == 0.25 else "auto") if arith == "bench" else arith
     t_init = time.perf_counter()
-    s = HeatSolver(prob, dtype=dtype, backend=backend, tb=tb, graph=graph, device=0 if backend == "hip" else None)
+    s = HeatSolver(prob, dtype=dtype, backend=backend, tb=tb, graph=graph, device=0 if backend == "hip" else None,
+                   arith=ar)
     s.synchronize()
     t_init = time.perf_counter() - t_init
     # as bench.py: warm-up, then plan / autotune / pick the cycle schedule of the
@@ -47,7 +50,7 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False):
     es = 8 if dtype == "fp64" else 4
     gpts = float(n) * n * steps / dt / 1e9
     hist = s.cycle_hist()
-    rec = {"config": name, "n": n, "dtype": dtype, "backend": backend, "tb_max": s.tb, "graph": graph,
+    rec = {"config": name, "n": n, "dtype": dtype, "backend": backend, "arith": ar, "tb_max": s.tb, "graph": graph,
            "steps": steps, "s": round(dt, 6), "ms_per_step": round(dt / steps * 1e3, 5), "gpts": round(gpts, 2),
            "cycles": {str(k): c for k, c in sorted(hist.items())}, "field_gb": round(s.layout.elems() * es / 1e9, 2),
            "init_s": round(t_init, 3), "prepare_s": round(prepare_s, 2), "finite": bool(math.isfinite(st["sum"]))}
@@ -55,7 +58,7 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False):
         plans, traffic = {}, 0.0
         for k, c in sorted(hist.items()):
             pl = s.plan(k)
-            plans[str(k)] = {kk: pl[kk] for kk in ("order", "ring", "main_bands", "main_waves", "tuned_ms")}
+            plans[str(k)] = {kk: pl[kk] for kk in ("order", "pair", "ring", "main_bands", "main_waves", "tuned_ms")}
             traffic += c * plan_hbm_bytes(pl, es, n, n)["total"]
         rec["launch_plans"] = plans
         rec["hbm_gb_per_s_plan"] = round(traffic / dt / 1e9, 1)
@@ -67,6 +70,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--max-gb", type=float, default=240.0)
+    ap.add_argument("--arith", default="bench", choices=["bench", "auto", "exact", "fma", "jacobi"],
+                    help="update form (bench.py --arith): bench = jacobi where r == 1/4")
     a = ap.parse_args()
     import torch
     have_gpu = torch.cuda.is_available()
@@ -90,7 +95,7 @@ def main():
             continue
         if be == "hip" and not have_gpu:
             continue
-        print(json.dumps(run(name, n, dt, steps, warm, be, tb, graph)), flush=True)
+        print(json.dumps(run(name, n, dt, steps, warm, be, tb, graph, a.arith)), flush=True)
         if have_gpu:
             torch.cuda.empty_cache()
 

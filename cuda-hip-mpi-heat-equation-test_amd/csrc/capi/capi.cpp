@@ -78,6 +78,10 @@ int heat2d_device_count(int* n) {
   });
 }
 
+int heat2d_wave_times(uint64_t* out, int64_t max_waves, int64_t* n) {
+  return guarded([&] { *n = kern::wave_times(out, max_waves); });
+}
+
 int heat2d_device_limits(int device, int64_t* out10) {
   return guarded([&] {
     const hipDeviceAttribute_t attrs[10] = {

@@ -70,6 +70,9 @@ int heat2d_device_count(int* n);
 // out = [max_block_dim_x, _y, _z, max_grid_dim_x, _y, _z, total_constant_memory,
 //        max_threads_per_block, warp_size, multiprocessor_count]
 int heat2d_device_limits(int device, int64_t* out10);
+// Diagnostics (HEAT2D_WAVE_TIMES=1): per-wave {start, end, wave, 0} wall-clock
+// ticks of the last stencil launch; *n = waves copied.
+int heat2d_wave_times(uint64_t* out, int64_t max_waves, int64_t* n);
 
 int heat2d_make_layout(int64_t nrows, int64_t ncols, int64_t halo, int64_t row0,
                        int64_t nrows_global, heat2d_layout* out);

@@ -182,6 +182,9 @@ void launch_stats(DType dt, const void* field, const void* other, const SlabLayo
 // (>= kNStat * max_stats_waves() doubles), then a fixed-order reduce into
 // out6 (device). Deterministic for a given slab and device.
 int64_t max_stats_waves();
+// Diagnostics: per-wave {start, end, wave id, 0} (wall clock ticks) of the
+// last tb_kernel launch when HEAT2D_WAVE_TIMES=1; returns the waves copied.
+int64_t wave_times(uint64_t* out, int64_t max_waves);
 void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, int k, double r, double* partials,
                      double* out6, hipStream_t stream, int arith = 0);
 void launch_reduce_partials(const double* partials, int64_t nparts, double* out6, hipStream_t stream);

@@ -168,6 +168,37 @@ int64_t balance_units(DType dt, int cus, int bpc) {
   return dt == DType::F32 ? c * 4 : c * bpc * 4;
 }
 
+// HEAT2D_WAVE_TIMES=1 (diagnostics, eager runs only): every tb_kernel launch
+// records per-wave start / end times into one device buffer (the last launch
+// wins); kern::wave_times copies it out.
+struct WaveTimes {
+  uint64_t* buf = nullptr;
+  int64_t cap = 0, n = 0;
+};
+WaveTimes& wave_times_state() {
+  static WaveTimes w;
+  return w;
+}
+uint64_t* wave_times_buf(int64_t nwaves) {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_WAVE_TIMES");
+    return e && std::atoi(e) != 0;
+  }();
+  if (!on) return nullptr;
+  WaveTimes& w = wave_times_state();
+  if (w.cap < nwaves) {
+    if (w.buf) (void)hipFree(w.buf);
+    w.cap = std::max<int64_t>(nwaves, 65536);
+    if (hipMalloc(reinterpret_cast<void**>(&w.buf), (size_t)w.cap * 4 * sizeof(uint64_t)) != hipSuccess) {
+      w.buf = nullptr;
+      w.cap = 0;
+      return nullptr;
+    }
+  }
+  w.n = nwaves;
+  return w.buf;
+}
+
 int64_t choose_bands(int64_t rows, int64_t ns, int64_t simds, int k, int64_t prime_rows = -1) {
   const int64_t slots = std::max<int64_t>(simds, 1);
   if (prime_rows < 0) prime_rows = 2 * (int64_t)k;
@@ -224,6 +255,7 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   HEAT2D_REQUIRE(sig_items == 0 || (main && sig != nullptr && sig_items <= items), "bad band-signal items");
   a.sig_items = sig_items;
   a.sig = sig;
+  a.wtimes = wave_times_buf(a.nwaves);
   // (pair: nwaves counts wave pairs, two per 256-thread block)
   const unsigned nblocks = pair ? (unsigned)((a.nwaves + 1) / 2) : (unsigned)((a.nwaves + 3) / 4);
   const int64_t o = L.origin();
@@ -370,11 +402,14 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 double pinned_weight(DType dt, bool row) {
   const char* env = std::getenv(row ? "HEAT2D_W_ROW" : "HEAT2D_W_COL");
   if (env && std::atof(env) >= 1.0) return std::atof(env);
-  // fp32 columns: 1.4 measured best over 1.0-2.3 (4096^2 K = 16, 1007
+  // Measured: fp32 columns 1.4 best over 1.0-2.3 (4096^2 K = 16, 1007
   // segments: 58.7-59.1 us per cycle against 60.1 at 1.5 and 60.7 at 1.75,
-  // profiles/r3/sweep5/); the rest are the VALU-op ratios
-  if (row) return dt == DType::F32 ? 1.5 : 1.4;
-  return dt == DType::F32 ? 1.4 : 1.6;
+  // profiles/r3/sweep5/); rows from per-wave timelines (tools/wave_times.py,
+  // profiles/r3/wt2/): fp32 1.3 puts the frame-row items at 45.8 us against
+  // 46.9 for the interior ones (1.5: 40.5); fp64 4096^2 K = 12 at 1.4 / 1.6
+  // left the frame rows at 68 and the frame columns at 61 us against 75
+  if (row) return 1.3;
+  return dt == DType::F32 ? 1.4 : 1.3;
 }
 
 int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect out[kMaxFused]) {
@@ -685,6 +720,16 @@ void launch_tb_persist(DType dt, void* buf0, void* buf1, const SlabLayout& L, co
                           : dispatch_persist<double, 6, AR>(k, nblocks, d0, d1, a, r, p, stream);
   });
   if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("persistent launch: ") + hipGetErrorString(e));
+}
+
+int64_t wave_times(uint64_t* out, int64_t max_waves) {
+  WaveTimes& w = wave_times_state();
+  if (!w.buf || w.n == 0) return 0;
+  HEAT2D_REQUIRE(hipDeviceSynchronize() == hipSuccess, "wave_times: device synchronisation failed");
+  const int64_t n = std::min(w.n, max_waves);
+  HEAT2D_REQUIRE(hipMemcpy(out, w.buf, (size_t)n * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess,
+                 "wave_times: copy failed");
+  return n;
 }
 
 int64_t max_stats_waves() { return (int64_t)cu_count() * 32; }  // 8 x 256-thread blocks per CU

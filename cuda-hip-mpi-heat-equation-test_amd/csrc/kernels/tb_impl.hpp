@@ -108,6 +108,9 @@ struct TbArgs {
   // (gated on the count) starts while the rest of the launch runs.
   int64_t sig_items;
   uint32_t* sig;
+  // Diagnostics (HEAT2D_WAVE_TIMES, kern::wave_times): per launched wave
+  // {start, end (wall clock, 100 MHz), first item, its edge kind}; nullptr off
+  uint64_t* wtimes;
 };
 
 // Fused statistics of the stored (last) level (ST kernels): sum T, sum T^2,
@@ -1005,6 +1008,18 @@ struct TbSpan {
   int32_t lin, lin_end, rows;
   int64_t r0, s0;
 };
+// floor(a * b / c) for 0 <= a, b and 0 < c with a result below 2^31 (host
+// checks: strip rows < 2^31): a double-precision quotient corrected to the
+// exact one (its error is below 1), instead of a 64-bit integer division —
+// ~100 scalar ops each, four per item lookup, on waves that are alone on
+// their SIMD.
+__device__ __forceinline__ int64_t muldiv(int64_t a, int64_t b, int64_t c) {
+  const int64_t p = a * b;
+  int64_t q = (int64_t)((double)p / (double)c);
+  while (q > 0 && q * c > p) --q;
+  while ((q + 1) * c <= p) ++q;
+  return q;
+}
 // NR: rects the kernel instance can be handed (the interior kernels take at
 // most 4: a larger scan costs the deep fp64 ones SGPRs that spill to scratch).
 template <int NR = kMaxRects>
@@ -1020,13 +1035,13 @@ __device__ __forceinline__ TbSpan tb_span(const TbArgs& a, int64_t it) {
   const int64_t rows = R.r1 - R.r0;
   TbSpan g{0, 0, (int32_t)rows, R.r0, R.s0};
   if (R.nb > 0) {
-    const int64_t band = local / ns, sl = local - band * ns;
-    g.lin = (int32_t)(sl * rows + band * rows / R.nb);
-    g.lin_end = (int32_t)(sl * rows + (band + 1) * rows / R.nb);
+    const int64_t band = muldiv(local, 1, ns), sl = local - band * ns;
+    g.lin = (int32_t)(sl * rows + muldiv(band, rows, R.nb));
+    g.lin_end = (int32_t)(sl * rows + muldiv(band + 1, rows, R.nb));
   } else {
     const int64_t total = ns * rows, nseg = -R.nb;
-    g.lin = (int32_t)(local * total / nseg);
-    g.lin_end = (int32_t)((local + 1) * total / nseg);
+    g.lin = (int32_t)muldiv(local, total, nseg);
+    g.lin_end = (int32_t)muldiv(local + 1, total, nseg);
   }
   return g;
 }
@@ -1113,6 +1128,8 @@ __device__ __forceinline__ double wave_max(double v) {
   return v;
 }
 
+__device__ __forceinline__ bool lane_id_is0() { return (threadIdx.x & 63) == 0; }
+
 // Kernel variants (VAR): 0 plain; 1 fused statistics (StatAcc; general kernel).
 // (A third, latency-oriented variant for the boundary-band launch — priming
 // skip + dependency chains — measured slower everywhere and was removed:
@@ -1146,6 +1163,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
   }
   const int64_t wid = (int64_t)blk * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (wid >= a.nwaves) return;  // whole wave exits; no barriers in this kernel
+  if (a.wtimes && lane_id_is0()) a.wtimes[wid * 4] = wall_clock64();
   // Band items are band-major within a rect: consecutive waves take adjacent
   // strips of the same band, so the waves in flight stream whole contiguous
   // rows (HBM page locality) and all march in step.
@@ -1202,6 +1220,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
         default: march<T, NV, K, 3, RING, AR>(src, dst, a, r, strip, t0, t1, lane); break;
       }
     }
+  }
+  if (a.wtimes && lane_id_is0()) {
+    a.wtimes[wid * 4 + 1] = wall_clock64();
+    a.wtimes[wid * 4 + 2] = (uint64_t)wid;
   }
   if constexpr (ST) {
     const double v[kNStatFused] = {wave_sum(acc.s), wave_sum(acc.ss), wave_min(acc.mn),

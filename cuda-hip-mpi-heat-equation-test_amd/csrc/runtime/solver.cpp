@@ -535,10 +535,15 @@ static int device_cus_of(int device) {
   return ncu;
 }
 
+// Wave-pair candidates (HEAT2D_PAIR=2; =1 forces the pair kernel on a
+// single-launch plan). Off by default: once the march's scalar address work
+// was cut (31 -> 12.5 SALU per row) the pair ran 3.5 % behind one wave per
+// item on 4096^2 fp32 K = 16 (58.4 vs 56.4 us per cycle, profiles/r3/salu/):
+// its LDS hand-off and ring waits cost what the second wave hides.
 static bool pair_candidates() {
   static const bool on = [] {
     const char* e = std::getenv("HEAT2D_PAIR");
-    return !e || std::atoi(e) != 0;
+    return e && std::atoi(e) == 2;
   }();
   return on;
 }

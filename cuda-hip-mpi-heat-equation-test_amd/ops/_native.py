@@ -121,6 +121,7 @@ _SIGS = {
     "heat2d_max_tb": (C.c_int, []),
     "heat2d_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "heat2d_device_limits": (C.c_int, [C.c_int, C.POINTER(C.c_int64)]),
+    "heat2d_wave_times": (C.c_int, [C.POINTER(C.c_uint64), C.c_int64, C.POINTER(C.c_int64)]),
     "heat2d_make_layout": (C.c_int, [_I64, _I64, _I64, _I64, _I64, _LP]),
     "heat2d_parse_input": (C.c_int, [C.c_char_p, C.POINTER(C.c_double)]),
     "heat2d_decompose": (C.c_int, [_I64, C.c_int, C.c_int, C.POINTER(_I64), C.POINTER(_I64)]),
@@ -313,6 +314,17 @@ def device_count() -> int:
 
 LIMIT_NAMES = ("MAX_BLOCK_DIM_X", "MAX_BLOCK_DIM_Y", "MAX_BLOCK_DIM_Z", "MAX_GRID_DIM_X", "MAX_GRID_DIM_Y",
                "MAX_GRID_DIM_Z", "TOTAL_CONSTANT_MEMORY", "MAX_THREADS_PER_BLOCK", "WARP_SIZE", "MULTIPROCESSOR_COUNT")
+
+
+def wave_times(max_waves: int = 1 << 16):
+    """Per-wave [start, end, wave, 0] wall-clock ticks (100 MHz on MI355X) of
+    the last stencil launch, when the process runs with HEAT2D_WAVE_TIMES=1
+    (diagnostics; eager launches). numpy array of shape (n, 4)."""
+    import numpy as np
+    buf = (C.c_uint64 * (4 * max_waves))()
+    n = C.c_int64()
+    call("heat2d_wave_times", buf, int(max_waves), C.byref(n))
+    return np.frombuffer(buf, dtype=np.uint64, count=4 * n.value).reshape(-1, 4).copy()
 
 
 def device_limits(device: int = 0) -> dict:
