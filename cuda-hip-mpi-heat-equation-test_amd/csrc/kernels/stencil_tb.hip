@@ -399,7 +399,7 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 // frame row, the interior strips get a top / bottom rect of one short band
 // each, (h + 2k) w1 = Li + 2k, and the segments / bands in between: 5 rects.
 // Weights: HEAT2D_W_ROW / HEAT2D_W_COL override (A/B).
-double pinned_weight(DType dt, bool row) {
+double pinned_weight(DType dt, bool row, bool single) {
   const char* env = std::getenv(row ? "HEAT2D_W_ROW" : "HEAT2D_W_COL");
   if (env && std::atof(env) >= 1.0) return std::atof(env);
   // Measured: fp32 columns 1.4 best over 1.0-2.3 (4096^2 K = 16, 1007
@@ -407,15 +407,20 @@ double pinned_weight(DType dt, bool row) {
   // profiles/r3/sweep5/); rows from per-wave timelines (tools/wave_times.py,
   // profiles/r3/wt2/): fp32 1.3 puts the frame-row items at 45.8 us against
   // 46.9 for the interior ones (1.5: 40.5); fp64 4096^2 K = 12 at 1.4 / 1.6
-  // left the frame rows at 68 and the frame columns at 61 us against 75
+  // left the frame rows at 68 and the frame columns at 61 us against 75. A
+  // wave alone on its SIMD hides part of the pinned kinds' extra ops in its own
+  // stalls; in the 2-waves/SIMD interior launch of a split plan they cost their
+  // full VALU ratio: fp64 columns 1.6 there (32768^2 K = 20: 4310-4332 Gpts/s
+  // against 4071-4153 at 1.3, same box, profiles/r3/abwcol/)
   if (row) return 1.3;
-  return dt == DType::F32 ? 1.4 : 1.3;
+  if (dt == DType::F32) return 1.4;
+  return single ? 1.3 : 1.6;
 }
 
-int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect out[kMaxFused]) {
+int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect out[kMaxFused], bool single) {
   const int64_t ns = R.s1 - R.s0, rows = R.r1 - R.r0;
   if (ns < 3 || rows < 2) return 0;
-  const double w = pinned_weight(dt, false), w1 = pinned_weight(dt, true), prime = 2.0 * k;
+  const double w = pinned_weight(dt, false, single), w1 = pinned_weight(dt, true, single), prime = 2.0 * k;
   auto edge_items = [&](double li) {  // items of one frame strip for interior items of li rows
     const double le = std::max(8.0, (li + prime) / w - prime);
     return std::min<int64_t>(rows, (int64_t)std::ceil((double)rows / le));
@@ -484,9 +489,9 @@ int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect 
 int64_t rect_items(const TbRect& R) { return R.nb > 0 ? R.nb * (R.s1 - R.s0) : -R.nb; }
 
 // arith 2: put the weighted rects of p.main into p.fused (see weighted_main)
-void weight_main(DType dt, const SlabLayout& L, SplitPlan& p, int arith, int64_t slots) {
+void weight_main(DType dt, const SlabLayout& L, SplitPlan& p, int arith, int64_t slots, bool single) {
   if (arith != 2) return;
-  const int n = weighted_main(dt, p.k, p.main, L, p.fused);
+  const int n = weighted_main(dt, p.k, p.main, L, p.fused, single);
   if (n == 0) return;
   p.nfused = n;
   p.main_items = 0;
@@ -517,7 +522,7 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   p.main = TbRect{B, n - B, 0, ns, nb_m};
   p.main_items = nb_m > 0 ? nb_m * ns : -nb_m;
   p.main_waves = std::min<int64_t>(p.main_items, mw);  // > one item per wave if main_bands asks for it
-  weight_main(dt, L, p, arith, mw);
+  weight_main(dt, L, p, arith, mw, false);
   // EDGE: the two boundary bands (one band each), general kernel. Short
   // (B + 2k march rows per item): beside MAIN where wave slots allow, else
   // right after it — either way the halo exchange that follows overlaps the
@@ -620,7 +625,7 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   p.main = TbRect{0, L.nrows, 0, ns, nb};
   p.main_items = nb > 0 ? nb * ns : -nb;
   p.main_waves = std::min<int64_t>(p.main_items, slots);
-  weight_main(dt, L, p, arith, slots);
+  weight_main(dt, L, p, arith, slots, true);
   p.nedge = 0;
   p.valid = 2;
   return p;
