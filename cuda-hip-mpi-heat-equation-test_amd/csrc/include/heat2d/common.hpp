@@ -44,12 +44,13 @@ struct Error : std::runtime_error {
 // temporal-block depth (rounded to the vector width) and keep rows aligned.
 constexpr int64_t kColPad = 32;
 // Largest supported temporal-block depth (time steps fused per HBM pass):
-// 24 for fp64, 16 for fp32 (max_tb). The fp64 interior kernel keeps 2
-// waves/SIMD up to K = 24 with ring 4 (193 VGPRs at K = 20, 225 at 24, no
-// scratch), so a short run can take one HBM pass; the packed fp32 march
-// needs AGPRs and drops to 1 wave/SIMD beyond 16.
+// 24 for fp64, 20 for fp32 (max_tb). The fp64 interior kernel keeps 2
+// waves/SIMD up to K = 24 with ring 4, so a short run can take one HBM pass;
+// the packed fp32 interior kernel keeps 2 waves/SIMD up to K = 20 with ring 4
+// (a floor: tb_impl.hpp kMinWaves) — deeper passes for the HBM-bound big fp32
+// grids (one read + one write of the field per K steps).
 constexpr int kMaxTB = 24;
-constexpr int kMaxTBF32 = 16;
+constexpr int kMaxTBF32 = 20;
 inline int max_tb(DType dt) { return dt == DType::F64 ? kMaxTB : kMaxTBF32; }
 // Default halo depth (ghost rows per side). Must be >= temporal depth used.
 constexpr int64_t kDefaultHalo = kMaxTB;

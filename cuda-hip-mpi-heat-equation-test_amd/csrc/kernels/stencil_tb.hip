@@ -90,8 +90,12 @@ int default_ring(DType dt, int k) {
   }
   // measured on MI355X (bench/sweep.py, 32768^2, profiles/sweep_split_32768.txt)
   if (dt == DType::F64) return k <= 10 ? 6 : 4;
-  return (k == 10 || k == 11) ? 6 : 4;
+  return (k == 10 || k == 11) ? 6 : 4;  // (K > 16: ring 4, see ring_ok)
 }
+
+// fp32 K = 17..20 exist with ring 4 only (ring 6 needs > 256 VGPRs there and
+// spilled in the general kernel): every plan of those depths uses ring 4.
+int ring_ok(DType dt, int k, int ring) { return (dt == DType::F32 && k > 16) ? 4 : ring; }
 
 // arith code -> the kernels' AR template argument (0 reference rounding,
 // 1 contracted fma, 2 r = 1/4: tb_impl.hpp); f is called with
@@ -143,7 +147,7 @@ void dispatch_t(int ring, bool main, int arith, int k, unsigned nblocks, const T
 }
 
 void check_layout(DType dt, const SlabLayout& L, int k) {
-  HEAT2D_REQUIRE(k >= 1 && k <= max_tb(dt), "k must be in [1, max_tb(dtype)] (fp64 24, fp32 16)");
+  HEAT2D_REQUIRE(k >= 1 && k <= max_tb(dt), "k must be in [1, max_tb(dtype)] (fp64 24, fp32 20)");
   HEAT2D_REQUIRE(k <= L.halo, "temporal depth exceeds the halo depth");
   HEAT2D_REQUIRE(L.cpad >= (k + 1) / 2 * 2 + 4, "column padding too small for the strip halo");
   // the march keeps row indices in 32 bits (scalar compares)
@@ -318,7 +322,7 @@ TbPlan plan_tb(DType dt, const SlabLayout& L, int64_t row_begin, int64_t row_end
   p.useful_w = useful_width(dt, k);
   p.nstrips = (L.ncols + p.useful_w - 1) / p.useful_w;
   const int64_t rows = row_end - row_begin;
-  p.prefetch = default_ring(dt, k);
+  p.prefetch = ring_ok(dt, k, default_ring(dt, k));
   p.main = 0;
   const int bpc = occupancy(dt, p.prefetch, false, k, arith);
   p.blocks_per_cu = bpc;
@@ -504,7 +508,7 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   check_layout(dt, L, k);
   SplitPlan p{};
   p.k = k;
-  p.ring = (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k);
+  p.ring = ring_ok(dt, k, (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k));
   const int64_t n = L.nrows, B = std::max<int64_t>(band, k);
   const int64_t U = useful_width(dt, k);
   const int64_t ns = (L.ncols + U - 1) / U;
@@ -543,8 +547,8 @@ SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool se
   SplitPlan p{};
   p.k = k;
   // default ring: the fused fp64 K >= 17 interior keeps 2 waves/SIMD only at ring 6
-  p.ring = (ring_override == 4 || ring_override == 6) ? ring_override
-                                                      : (dt == DType::F64 && k >= 17 ? 6 : default_ring(dt, k));
+  p.ring = ring_ok(dt, k, (ring_override == 4 || ring_override == 6) ? ring_override
+                                                                     : (dt == DType::F64 && k >= 17 ? 6 : default_ring(dt, k)));
   const int64_t n = L.nrows, B = std::max<int64_t>(band, k);
   const int64_t U = useful_width(dt, k);
   const int64_t ns = (L.ncols + U - 1) / U;
@@ -614,7 +618,7 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   check_layout(dt, L, k);
   SplitPlan p{};
   p.k = k;
-  p.ring = (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k);
+  p.ring = ring_ok(dt, k, (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k));
   const int64_t U = useful_width(dt, k);
   const int64_t ns = (L.ncols + U - 1) / U;
   const int bpc = occupancy(dt, p.ring, false, k, arith);
@@ -632,7 +636,7 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
 }
 
 int64_t pair_capacity(DType dt, int ring, int k, int arith) {
-  if (dt != DType::F32 || k < 2 || k > max_tb(dt) || (ring != 4 && ring != 6)) return 0;
+  if (dt != DType::F32 || k < 2 || k > 16 || (ring != 4 && ring != 6)) return 0;  // pair kernels: K = 2..16
   const int bpc = with_ar(arith, [&](auto ar) {
     constexpr int AR = decltype(ar)::value;
     return ring == 4 ? occupancy_pair<4, AR>(k) : occupancy_pair<6, AR>(k);

@@ -5,7 +5,7 @@
 namespace heat2d {
 namespace kern {
 namespace tbimpl {
-H2D_TB_UNIT(float, 4, false, 1)
+H2D_TB_UNIT_F32(float, 4, false, 1)
 }  // namespace tbimpl
 }  // namespace kern
 }  // namespace heat2d

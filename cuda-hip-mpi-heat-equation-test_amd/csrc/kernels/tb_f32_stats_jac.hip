@@ -5,7 +5,7 @@
 namespace heat2d {
 namespace kern {
 namespace tbimpl {
-H2D_ST_UNIT(float, 2, H2D_NO_CASES)
+H2D_ST_UNIT(float, 2, H2D_TB_CASES_F32DEEP)
 }  // namespace tbimpl
 }  // namespace kern
 }  // namespace heat2d

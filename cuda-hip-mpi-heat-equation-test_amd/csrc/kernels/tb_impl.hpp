@@ -1070,12 +1070,14 @@ __device__ __forceinline__ bool tb_piece(const TbArgs& a, int64_t it, int32_t li
 // fp32 march with the single across-lane adds spills under a 3-wave floor from
 // K = 12 on, so it has none.) The r = 1/4 (AR 2) fp64 interior kernel keeps 2
 // waves/SIMD at K = 18..19 under a floor; at K = 20 ring 4 a floor spills (its
-// ring-6 twin fits 241 VGPRs, which the autotuner weighs). The fused-cycle
+// ring-6 twin fits 241 VGPRs, which the autotuner weighs). The fp32 interior
+// kernels at K = 17..20 (ring 4) keep 2 waves/SIMD under a floor. The fused-cycle
 // variant (more state) takes no floor. Checked per build:
 // ScratchSize = 0 in the ISA (tools/isa_report.py, tests/test_isa.py).
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
 constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K >= 11 && K <= 12) ? 4
                           : (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 2 && K >= 18 && K <= 19) ? 2
+                          : (std::is_same<T, float>::value && MAIN && RING == 4 && K >= 17)                        ? 2
                                                                                                                   : 1;
 
 // Rows [t0, t1) of `strip` that this wave just stored: re-read (sc0: past the
@@ -1533,7 +1535,11 @@ int occupancy_blocks_stats(int k);
   M(T, RING, MAIN, AR, 5) M(T, RING, MAIN, AR, 6) M(T, RING, MAIN, AR, 7) M(T, RING, MAIN, AR, 8)       \
   M(T, RING, MAIN, AR, 9) M(T, RING, MAIN, AR, 10) M(T, RING, MAIN, AR, 11) M(T, RING, MAIN, AR, 12)    \
   M(T, RING, MAIN, AR, 13) M(T, RING, MAIN, AR, 14) M(T, RING, MAIN, AR, 15) M(T, RING, MAIN, AR, 16)
-// fp64 only: K = 17..24 (kMaxTB; fp32 stops at kMaxTBF32 = 16, common.hpp)
+// fp32: K = 17..20 (kMaxTBF32, common.hpp): the big fp32 grids are HBM-bound
+// at K = 16, and the packed march fits K = 20 in 2 waves/SIMD
+#define H2D_TB_CASES_F32DEEP(M, T, RING, MAIN, AR)                                                     \
+  M(T, RING, MAIN, AR, 17) M(T, RING, MAIN, AR, 18) M(T, RING, MAIN, AR, 19) M(T, RING, MAIN, AR, 20)
+// fp64 only: K = 17..24 (kMaxTB)
 #define H2D_TB_CASES_DEEP(M, T, RING, MAIN, AR)                                                        \
   M(T, RING, MAIN, AR, 17) M(T, RING, MAIN, AR, 18) M(T, RING, MAIN, AR, 19) M(T, RING, MAIN, AR, 20)   \
   M(T, RING, MAIN, AR, 21) M(T, RING, MAIN, AR, 22) M(T, RING, MAIN, AR, 23) M(T, RING, MAIN, AR, 24)
@@ -1647,6 +1653,7 @@ int pair_blocks_per_cu() {
   }
 #define H2D_TB_UNIT(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_NO_CASES)
 #define H2D_TB_UNIT_F64(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_DEEP)
+#define H2D_TB_UNIT_F32(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_F32DEEP)
 #define H2D_ST_CASE(T, RING, MAIN, AR, KK)                                                                        \
   case KK:                                                                                                        \
     hipLaunchKernelGGL((tb_kernel<T, 1, KK, 4, false, AR, kVarStats>), dim3(nblocks), dim3(256), 0, s, src, dst, a, \

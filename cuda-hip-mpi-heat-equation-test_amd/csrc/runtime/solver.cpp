@@ -72,7 +72,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
   // MI355X, profiles/README.md §11: fp64 14 — equal to 12 on a whole 32768²
   // grid, 3-6 % faster on the slabs of 2/4/8-rank runs — fp32 16 with the
   // packed fp32 march); 8 on the CPU twin.
-  // tb <= 0 on the HIP engine: depths up to max_tb (fp64 24, fp32 16) are
+  // tb <= 0 on the HIP engine: depths up to max_tb (fp64 24, fp32 20) are
   // available to the measured schedules of prepare(); the balanced fallback
   // uses the steady-state best.
   const bool tb_given = cfg_.tb > 0;

@@ -69,7 +69,7 @@ class HeatSolver:
         dtype: "fp64" (reference precision) or "fp32".
         backend: "hip", "cpu" or "auto".
         tb: largest temporal-block depth K (time steps fused per HBM pass; fp64
-            1..24, fp32 1..16). 0: all depths up to that limit for the measured
+            1..24, fp32 1..20). 0: all depths up to that limit for the measured
             schedules of prepare() (autotuned slabs), balanced cycles of the
             steady-state best (fp64 14 / fp32 16) otherwise; 8 on the CPU twin.
         overlap: boundary/interior split with the halo exchange on a comm stream.

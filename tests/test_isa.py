@@ -28,10 +28,11 @@ def tb():
         p = isa_report.tb_params(k["name"])
         if p:
             ks[p] = k
-    # 2 rings x main/gen x 3 arith x (fp32 K 1..16 + fp64 K 1..24), plus the
-    # fused-statistics variants (general, ring 4, 3 arith)
-    assert sum(len(p) == 6 for p in ks) == 12 * (16 + 24), len(ks)
-    assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 3 * (16 + 24), len(ks)
+    # main/gen x 3 arith x (ring 4: fp32 K 1..20 + fp64 K 1..24; ring 6: fp32
+    # K 1..16 + fp64 K 1..24), plus the fused-statistics variants (general,
+    # ring 4, 3 arith)
+    assert sum(len(p) == 6 for p in ks) == 6 * (20 + 24) + 6 * (16 + 24), len(ks)
+    assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 3 * (20 + 24), len(ks)
     return ks
 
 
@@ -56,7 +57,10 @@ def test_deep_fp64_interior_two_waves(tb):
         for ar in (0, 1, 2):
             ring = 6 if (ar, k) == (2, 20) else 4  # r = 1/4, K = 20: ring 4 needs 258 VGPRs, ring 6 fits
             assert tb[("fp64", 1, k, ring, True, ar)]["waves_per_simd"] >= 2, (k, ar)
-    assert not any(p[0] == "fp32" and p[2] > 16 for p in tb)
+    assert not any(p[0] == "fp32" and p[2] > 20 for p in tb)
+    for k in range(17, 21):  # fp32 K = 17..20: the interior kernel keeps 2 waves/SIMD at ring 4 (floor)
+        for ar in (0, 1, 2):
+            assert tb[("fp32", 1, k, 4, True, ar)]["waves_per_simd"] >= 2, (k, ar)
 
 
 def test_packed_fp32_compact(tb):
