@@ -86,7 +86,7 @@ int useful_width(DType dt, int k) { return 64 * vec_elems(dt) - 2 * halo_cols(dt
 int default_ring(DType dt, int k) {
   if (const char* env = std::getenv("HEAT2D_TB_RING")) {
     const int r = std::atoi(env);
-    if (r == 4 || r == 6) return r;
+    if (r == 4 || r == 6 || r == 8) return r;
   }
   // measured on MI355X (bench/sweep.py, 32768^2, profiles/sweep_split_32768.txt)
   if (dt == DType::F64) return k <= 10 ? 6 : 4;
@@ -95,7 +95,16 @@ int default_ring(DType dt, int k) {
 
 // fp32 K = 17..20 exist with ring 4 only (ring 6 needs > 256 VGPRs there and
 // spilled in the general kernel): every plan of those depths uses ring 4.
-int ring_ok(DType dt, int k, int ring) { return (dt == DType::F32 && k > 16) ? 4 : ring; }
+// Ring 8 (6 rows in flight) exists only for the fp32 general kernel at K <= 16,
+// for single launches (plan_single): one wave per SIMD there, whose loads wait
+// on memory ~20 % of its life with 4 rows in flight (SQ_WAIT_ANY,
+// profiles/r3/pairprof/); other plans fall back to ring 6.
+int ring_ok(DType dt, int k, int ring, bool single = false) {
+  if (dt == DType::F32 && k > 16) return 4;
+  if (ring == 8 && !(single && dt == DType::F32)) return 6;
+  return ring;
+}
+bool ring_valid(int r) { return r == 4 || r == 6 || r == 8; }
 
 // arith code -> the kernels' AR template argument (0 reference rounding,
 // 1 contracted fma, 2 r = 1/4: tb_impl.hpp); f is called with
@@ -111,6 +120,13 @@ decltype(auto) with_ar(int arith, F&& f) {
 template <typename T, int AR>
 int occupancy_t(int ring, bool main, int k) {
   if (ring == 4) return main ? occupancy_blocks<T, 4, true, AR>(k) : occupancy_blocks<T, 4, false, AR>(k);
+  if constexpr (std::is_same<T, float>::value) {
+    if (ring == 8) {
+      HEAT2D_REQUIRE(!main && k <= 16, "ring 8: fp32 general kernel, K <= 16");
+      return occupancy_blocks<T, 8, false, AR>(k);
+    }
+  }
+  HEAT2D_REQUIRE(ring == 6, "ring must be 4, 6 (or 8: fp32 general kernel)");
   return main ? occupancy_blocks<T, 6, true, AR>(k) : occupancy_blocks<T, 6, false, AR>(k);
 }
 
@@ -131,6 +147,13 @@ int occupancy(DType dt, int ring, bool main, int k, int arith) {
 template <typename T, int AR>
 void dispatch_ar(int ring, bool main, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
                  hipStream_t st) {
+  if constexpr (std::is_same<T, float>::value) {
+    if (ring == 8) {
+      HEAT2D_REQUIRE(!main && k <= 16, "ring 8: fp32 general kernel, K <= 16");
+      dispatch<T, 8, false, AR>(k, nblocks, s, d, a, r, st);
+      return;
+    }
+  }
   if (ring == 4) {
     if (main) dispatch<T, 4, true, AR>(k, nblocks, s, d, a, r, st);
     else dispatch<T, 4, false, AR>(k, nblocks, s, d, a, r, st);
@@ -618,7 +641,7 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   check_layout(dt, L, k);
   SplitPlan p{};
   p.k = k;
-  p.ring = ring_ok(dt, k, (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k));
+  p.ring = ring_ok(dt, k, ring_valid(ring_override) ? ring_override : default_ring(dt, k), true);
   const int64_t U = useful_width(dt, k);
   const int64_t ns = (L.ncols + U - 1) / U;
   const int bpc = occupancy(dt, p.ring, false, k, arith);

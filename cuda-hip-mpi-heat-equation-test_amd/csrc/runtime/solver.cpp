@@ -719,7 +719,10 @@ void Solver::autotune_split(int k) {
     // fp64 slabs of 4096-16384 rows +2-4 %; a 4096-row fp32 slab, whose
     // interior cycle is 0.28 ms, lost 7 % to an exposed exchange)
     if (mode == 3 && (single_ok || best.valid != 1 || timed.front().first < kEdgeFirstMinCycleMs)) continue;
-    for (int ring : {4, 6}) {
+    // ring 8 (6 rows in flight): fp32 single launches only (stencil_tb.hip ring_ok)
+    const std::vector<int> rings = (mode == 2 && dtype() == DType::F32 && k <= 16) ? std::vector<int>{4, 6, 8}
+                                                                                     : std::vector<int>{4, 6};
+    for (int ring : rings) {
       for (double f : {1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 1.25, 1.5, 2.0}) {
         const int64_t nb = std::max<int64_t>(1, (int64_t)((mode == 2 ? nb1 : nb0) * f + 0.5));
         if (mode == 1 && ring == best.ring && nb == best.main.nb) continue;
@@ -1513,6 +1516,7 @@ const kern::SplitPlan* Solver::persist_plan(int k) {
       c.pair = 0;
       c.main_waves = c.main_items;
     }
+    if (c.ring == 8) c = kern::plan_single(dtype(), L_, k, 0, 6, c.main.nb, cfg_.arith);  // rings 4 / 6 only
     const int64_t cap = kern::persist_capacity(dtype(), c.ring, k, cfg_.arith);
     if (c.main_items > cap) c = kern::plan_single(dtype(), L_, k, 0, c.ring, -cap, cfg_.arith);
     if (!c.valid || c.main_items > cap || c.main_items < 1) c.valid = 0;

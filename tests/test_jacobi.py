@@ -232,3 +232,23 @@ def test_hip_pair_kernel(gpu, native, monkeypatch, arith, tb, env):
     s.close()
     assert pl["order"] == "single" and pl["pair"] == 1, pl
     assert np.array_equal(got, golden(p, np.float32, T0, arith=arith))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arith,tb", [("jacobi", 16), ("fma", 15), ("exact", 3)])
+def test_hip_ring8_single_launch(gpu, native, monkeypatch, arith, tb):
+    """Ring 8 (6 level-0 rows in flight; fp32 general kernel, single launches):
+    frame-weighted segments, bitwise."""
+    monkeypatch.setenv("HEAT2D_SPLIT_ORDER", "single")
+    monkeypatch.setenv("HEAT2D_TB_RING", "8")
+    monkeypatch.setenv("HEAT2D_SEGMENTS", "30")
+    p = prob(1100, 2 * tb + 3)
+    T0 = rough(p, np.float32)
+    s = HeatSolver(p, dtype="fp32", backend="hip", tb=tb, device=0, autotune=0, arith=arith)
+    s.upload(T0)
+    s.step(p.ntime)
+    got = s.download()
+    pl = s.plan(tb)
+    s.close()
+    assert pl["order"] == "single" and pl["ring"] == 8, pl
+    assert np.array_equal(got, golden(p, np.float32, T0, arith=arith))
