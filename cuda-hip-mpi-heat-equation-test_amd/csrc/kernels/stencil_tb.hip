@@ -426,7 +426,7 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 // frame row, the interior strips get a top / bottom rect of one short band
 // each, (h + 2k) w1 = Li + 2k, and the segments / bands in between: 5 rects.
 // Weights: HEAT2D_W_ROW / HEAT2D_W_COL override (A/B).
-double pinned_weight(DType dt, bool row, bool single) {
+double pinned_weight(DType dt, bool row, bool single, int ring) {
   const char* env = std::getenv(row ? "HEAT2D_W_ROW" : "HEAT2D_W_COL");
   if (env && std::atof(env) >= 1.0) return std::atof(env);
   // Measured: fp32 columns 1.4 best over 1.0-2.3 (4096^2 K = 16, 1007
@@ -439,15 +439,20 @@ double pinned_weight(DType dt, bool row, bool single) {
   // stalls; in the 2-waves/SIMD interior launch of a split plan they cost their
   // full VALU ratio: fp64 columns 1.6 there (32768^2 K = 20: 4310-4332 Gpts/s
   // against 4071-4153 at 1.3, same box, profiles/r3/abwcol/)
+  // The fp32 ring-8 general kernel (294 VGPRs at K = 16) runs interior items
+  // 8 % faster than ring 6 but its pinned kinds not (ring8/: 43.7 us interior,
+  // 53.5 frame rows, 47.5 frame columns at 1.3 / 1.4): 1.6 / 1.55 there
+  if (dt == DType::F32 && ring == 8) return row ? 1.6 : 1.55;
   if (row) return 1.3;
   if (dt == DType::F32) return 1.4;
   return single ? 1.3 : 1.6;
 }
 
-int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect out[kMaxFused], bool single) {
+int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect out[kMaxFused], bool single,
+                  int ring) {
   const int64_t ns = R.s1 - R.s0, rows = R.r1 - R.r0;
   if (ns < 3 || rows < 2) return 0;
-  const double w = pinned_weight(dt, false, single), w1 = pinned_weight(dt, true, single), prime = 2.0 * k;
+  const double w = pinned_weight(dt, false, single, ring), w1 = pinned_weight(dt, true, single, ring), prime = 2.0 * k;
   auto edge_items = [&](double li) {  // items of one frame strip for interior items of li rows
     const double le = std::max(8.0, (li + prime) / w - prime);
     return std::min<int64_t>(rows, (int64_t)std::ceil((double)rows / le));
@@ -518,7 +523,7 @@ int64_t rect_items(const TbRect& R) { return R.nb > 0 ? R.nb * (R.s1 - R.s0) : -
 // arith 2: put the weighted rects of p.main into p.fused (see weighted_main)
 void weight_main(DType dt, const SlabLayout& L, SplitPlan& p, int arith, int64_t slots, bool single) {
   if (arith != 2) return;
-  const int n = weighted_main(dt, p.k, p.main, L, p.fused, single);
+  const int n = weighted_main(dt, p.k, p.main, L, p.fused, single, p.ring);
   if (n == 0) return;
   p.nfused = n;
   p.main_items = 0;
