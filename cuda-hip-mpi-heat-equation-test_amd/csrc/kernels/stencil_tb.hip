@@ -99,9 +99,11 @@ int default_ring(DType dt, int k) {
 // for single launches (plan_single): one wave per SIMD there, whose loads wait
 // on memory ~20 % of its life with 4 rows in flight (SQ_WAIT_ANY,
 // profiles/r3/pairprof/); other plans fall back to ring 6.
+// (Ring 10, and ring 8 for the fp64 general kernel, measured no better:
+// profiles/r3/ring10/.)
 int ring_ok(DType dt, int k, int ring, bool single = false) {
   if (dt == DType::F32 && k > 16) return 4;
-  if (ring == 8 && !(single && dt == DType::F32)) return 6;
+  if (ring == 8 && !(single && k <= 16 && dt == DType::F32)) return 6;
   return ring;
 }
 bool ring_valid(int r) { return r == 4 || r == 6 || r == 8; }
@@ -126,7 +128,7 @@ int occupancy_t(int ring, bool main, int k) {
       return occupancy_blocks<T, 8, false, AR>(k);
     }
   }
-  HEAT2D_REQUIRE(ring == 6, "ring must be 4, 6 (or 8: fp32 general kernel)");
+  HEAT2D_REQUIRE(ring == 6, "ring must be 4, 6 (8: fp32 general kernel of single launches)");
   return main ? occupancy_blocks<T, 6, true, AR>(k) : occupancy_blocks<T, 6, false, AR>(k);
 }
 

@@ -1516,7 +1516,7 @@ const kern::SplitPlan* Solver::persist_plan(int k) {
       c.pair = 0;
       c.main_waves = c.main_items;
     }
-    if (c.ring == 8) c = kern::plan_single(dtype(), L_, k, 0, 6, c.main.nb, cfg_.arith);  // rings 4 / 6 only
+    if (c.ring > 6) c = kern::plan_single(dtype(), L_, k, 0, 6, c.main.nb, cfg_.arith);  // rings 4 / 6 only
     const int64_t cap = kern::persist_capacity(dtype(), c.ring, k, cfg_.arith);
     if (c.main_items > cap) c = kern::plan_single(dtype(), L_, k, 0, c.ring, -cap, cfg_.arith);
     if (!c.valid || c.main_items > cap || c.main_items < 1) c.valid = 0;

@@ -29,8 +29,9 @@ def tb():
         if p:
             ks[p] = k
     # main/gen x 3 arith x (ring 4: fp32 K 1..20 + fp64 K 1..24; ring 6: fp32
-    # K 1..16 + fp64 K 1..24), the fp32 general ring-8 kernels (3 arith x K
-    # 1..16), plus the fused-statistics variants (general, ring 4, 3 arith)
+    # K 1..16 + fp64 K 1..24), the fp32 general ring-8 kernels of single
+    # launches (3 arith x K 1..16), plus the fused-statistics variants
+    # (general, ring 4, 3 arith)
     assert sum(len(p) == 6 for p in ks) == 6 * (20 + 24) + 6 * (16 + 24) + 3 * 16, len(ks)
     assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 3 * (20 + 24), len(ks)
     return ks

@@ -235,20 +235,22 @@ def test_hip_pair_kernel(gpu, native, monkeypatch, arith, tb, env):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("arith,tb", [("jacobi", 16), ("fma", 15), ("exact", 3)])
-def test_hip_ring8_single_launch(gpu, native, monkeypatch, arith, tb):
-    """Ring 8 (6 level-0 rows in flight; fp32 general kernel, single launches):
-    frame-weighted segments, bitwise."""
+@pytest.mark.parametrize("dtype,ring,arith,tb", [("fp32", 8, "jacobi", 16), ("fp32", 8, "fma", 15), ("fp32", 8, "exact", 3),
+                                                ("fp32", 8, "jacobi", 9)])
+def test_hip_ring8_single_launch(gpu, native, monkeypatch, dtype, ring, arith, tb):
+    """Ring 8 for single launches (fp32 general kernel: 6 level-0 rows in
+    flight instead of 4): frame-weighted segments, bitwise."""
     monkeypatch.setenv("HEAT2D_SPLIT_ORDER", "single")
-    monkeypatch.setenv("HEAT2D_TB_RING", "8")
-    monkeypatch.setenv("HEAT2D_SEGMENTS", "30")
+    monkeypatch.setenv("HEAT2D_TB_RING", str(ring))
+    monkeypatch.setenv("HEAT2D_SEGMENTS", "30" if dtype == "fp32" else "44")
     p = prob(1100, 2 * tb + 3)
-    T0 = rough(p, np.float32)
-    s = HeatSolver(p, dtype="fp32", backend="hip", tb=tb, device=0, autotune=0, arith=arith)
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    T0 = rough(p, npdt)
+    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0, arith=arith)
     s.upload(T0)
     s.step(p.ntime)
     got = s.download()
     pl = s.plan(tb)
     s.close()
-    assert pl["order"] == "single" and pl["ring"] == 8, pl
-    assert np.array_equal(got, golden(p, np.float32, T0, arith=arith))
+    assert pl["order"] == "single" and pl["ring"] == ring, pl
+    assert np.array_equal(got, golden(p, npdt, T0, arith=arith))
