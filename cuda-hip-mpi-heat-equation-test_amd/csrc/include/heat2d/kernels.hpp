@@ -78,9 +78,10 @@ struct SplitPlan {
   // then the interior — and `edge` holds only bands on the Dirichlet frame.
   // valid = 1..3 with nfused > 0 (arith 2): `main` cut into frame-strip-
   // weighted rects, launched instead of `main` (stencil_tb.hip weight_main).
-  // pair = 1 (valid = 2, fp32): the single launch runs the wave-pair kernel
+  // pair bit 0 (valid = 2, fp32): the single launch runs the wave-pair kernel
   // (tb_pair_kernel: two waves per item, the levels split between them);
-  // main_waves then counts PAIRS.
+  // main_waves then counts PAIRS. Bit 1: the main launch takes its items
+  // from a dynamic queue (more items than waves; TbArgs::queue).
   int32_t nfused, pair;
   TbRect fused[kMaxFused];
   int64_t sig_items;
@@ -119,8 +120,9 @@ void launch_fused_main(DType dt, const void* src, void* dst, const SlabLayout& L
 // timeout_ticks sets *err and returns.
 void launch_wait_counter(const uint32_t* counter, uint32_t target, uint64_t timeout_ticks, unsigned int* err,
                          hipStream_t stream);
+// queue: 2 device counters (zeroed once) for plans with pair bit 1 (dynamic items)
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
-                  double r, hipStream_t stream, int arith = 0);
+                  double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr);
 
 // Persistent multi-cycle launch (tb_impl.hpp tb_persist_kernel): `ncycles`
 // cycles of depth plan.k over the whole slab in ONE cooperative dispatch, one

@@ -458,6 +458,7 @@ class Solver {
   uint32_t done_base_ = 0;                // their value at the next launch
   unsigned int* h_err_ = nullptr;         // pinned, host-visible error word (persistent kernel, exchange gates)
   uint32_t* d_sig_ = nullptr;             // [0]: band items of the running fused cycle; [1]: trial scratch
+  uint32_t* d_queue_ = nullptr;           // dynamic item queue of the main launches (SplitPlan::pair bit 1)
   int64_t pend_sig_ = 0;                  // band items the pending fused cycle signals
   uint64_t gate_timeout_ticks_ = 0;
   uint64_t persist_timeout_ticks_ = 0;

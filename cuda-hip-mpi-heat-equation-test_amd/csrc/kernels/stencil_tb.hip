@@ -253,7 +253,8 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t simds, int k, int64_t pri
 // partials != nullptr: the fused-statistics kernel (general, ring 4). Returns the waves launched.
 int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
                      const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith,
-                     double* partials = nullptr, int64_t sig_items = 0, uint32_t* sig = nullptr, bool pair = false) {
+                     double* partials = nullptr, int64_t sig_items = 0, uint32_t* sig = nullptr, bool pair = false,
+                     uint32_t* queue = nullptr) {
   HEAT2D_REQUIRE(nrect >= 1 && nrect <= (main ? kMainRects : kMaxRects), "bad rect count");
   TbArgs a{};
   a.pitch = L.pitch;
@@ -285,6 +286,8 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   a.sig_items = sig_items;
   a.sig = sig;
   a.wtimes = wave_times_buf(a.nwaves);
+  // the dynamic queue only pays with more items than waves (plain kernels)
+  a.queue = (queue && !pair && !partials && !sig && items > a.nwaves) ? queue : nullptr;
   // (pair: nwaves counts wave pairs, two per 256-thread block)
   const unsigned nblocks = pair ? (unsigned)((a.nwaves + 1) / 2) : (unsigned)((a.nwaves + 3) / 4);
   const int64_t o = L.origin();
@@ -788,7 +791,9 @@ void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, 
 }
 
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
-                  double r, hipStream_t stream, int arith) {
+                  double r, hipStream_t stream, int arith, uint32_t* queue) {
+  // (SplitPlan::pair bit 1: the main part takes its items from the dynamic queue)
+  uint32_t* q = (p.pair & 2) ? queue : nullptr;
   HEAT2D_REQUIRE(p.valid, "invalid split plan");
   HEAT2D_REQUIRE(p.valid != 4 || !main_part, "a fused plan's main part needs its band counter (launch_fused_main)");
   if (p.valid == 4 && p.nedge == 0) return;  // no band on the frame
@@ -798,11 +803,12 @@ void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, con
   if (p.valid == 2) {  // single general launch over the whole slab (no edge part)
     if (main_part)
       launch_rects(dt, src, dst, L, p.k, p.ring, false, mr, nm, p.main_waves, r, stream, arith, nullptr, 0, nullptr,
-                   p.pair != 0);
+                   (p.pair & 1) != 0, q);
     return;
   }
   if (main_part)
-    launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith);
+    launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith, nullptr, 0, nullptr, false,
+                 q);
   else
     launch_rects(dt, src, dst, L, p.k, p.ring, false, p.edge, p.nedge, p.edge_waves, r, stream, arith);
 }

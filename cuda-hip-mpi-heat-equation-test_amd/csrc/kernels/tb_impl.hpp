@@ -111,6 +111,12 @@ struct TbArgs {
   // Diagnostics (HEAT2D_WAVE_TIMES, kern::wave_times): per launched wave
   // {start, end (wall clock, 100 MHz), first item, its edge kind}; nullptr off
   uint64_t* wtimes;
+  // Dynamic item queue (SplitPlan::pair bit 1): {next item beyond the first
+  // round, waves finished}; a wave takes its first item statically (wid) and
+  // then the next free one, so waves that run faster take more items. The
+  // last wave to finish resets both counters for the next launch. nullptr:
+  // static grid stride.
+  uint32_t* queue;
 };
 
 // Fused statistics of the stored (last) level (ST kernels): sum T, sum T^2,
@@ -1065,8 +1071,9 @@ __device__ __forceinline__ bool tb_piece(const TbArgs& a, int64_t it, int32_t li
 // kernel (no per-level row tests, no corner selects). MAIN = false: the general
 // kernel classifies each item (edge kinds 0..3, see March).
 // Occupancy floor handed to the register allocator: the fp64 fma interior
-// kernel at K = 11..12 lands at 129 VGPRs and fits 128 (4 waves/SIMD instead
-// of 3) without spilling; its exact-arithmetic twin would spill. (The packed
+// kernel at K = 11 lands at 129 VGPRs and fits 128 (4 waves/SIMD instead of 3)
+// without spilling (K = 12 did until the dynamic item queue's code; now it
+// would spill 32 B); its exact-arithmetic twin would spill. (The packed
 // fp32 march with the single across-lane adds spills under a 3-wave floor from
 // K = 12 on, so it has none.) The r = 1/4 (AR 2) fp64 interior kernel keeps 2
 // waves/SIMD at K = 18..19 under a floor; at K = 20 ring 4 a floor spills (its
@@ -1075,7 +1082,7 @@ __device__ __forceinline__ bool tb_piece(const TbArgs& a, int64_t it, int32_t li
 // variant (more state) takes no floor. Checked per build:
 // ScratchSize = 0 in the ISA (tools/isa_report.py, tests/test_isa.py).
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
-constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K >= 11 && K <= 12) ? 4
+constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K == 11) ? 4
                           : (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 2 && K >= 18 && K <= 19) ? 2
                           : (std::is_same<T, float>::value && MAIN && RING == 4 && K >= 17)                        ? 2
                                                                                                                   : 1;
@@ -1132,6 +1139,22 @@ __device__ __forceinline__ double wave_max(double v) {
 
 __device__ __forceinline__ bool lane_id_is0() { return (threadIdx.x & 63) == 0; }
 
+// The wave's next work item after `it` (static grid stride, or the dynamic queue).
+__device__ __forceinline__ int64_t next_item(const TbArgs& a, int64_t it) {
+  if (!a.queue) return it + a.nwaves;
+  uint32_t v = 0;
+  if (lane_id_is0()) v = __hip_atomic_fetch_add(a.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return a.nwaves + (int64_t)__builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ void queue_exit(const TbArgs& a) {
+  if (!a.queue || !lane_id_is0()) return;
+  const uint32_t d = __hip_atomic_fetch_add(a.queue + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (d + 1u == (uint32_t)a.nwaves) {  // every wave has taken its last item: reset for the next launch
+    __hip_atomic_store(a.queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.queue + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Kernel variants (VAR): 0 plain; 1 fused statistics (StatAcc; general kernel).
 // (A third, latency-oriented variant for the boundary-band launch — priming
 // skip + dependency chains — measured slower everywhere and was removed:
@@ -1184,7 +1207,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
           if (lane == 0) __hip_atomic_fetch_add(a.sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-      it += a.nwaves;
+      it = next_item(a, it);
       if (it < a.nitems) lin = tb_span<NR>(a, it).lin;
       continue;
     }
@@ -1223,6 +1246,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
       }
     }
   }
+  queue_exit(a);
   if (a.wtimes && lane_id_is0()) {
     a.wtimes[wid * 4 + 1] = wall_clock64();
     a.wtimes[wid * 4 + 2] = (uint64_t)wid;

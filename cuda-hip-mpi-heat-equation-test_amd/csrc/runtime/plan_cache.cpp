@@ -140,7 +140,7 @@ bool get_plan(const std::string& ctx, int k, int64_t band, kern::SplitPlan* p, f
   q.nfused = (int32_t)nf;
   q.sig_items = sig;
   q.pair = (int32_t)pr;
-  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > kern::kMaxFused || q.pair < 0 || q.pair > 1) return false;
+  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > kern::kMaxFused || q.pair < 0 || q.pair > 3) return false;
   *p = q;
   *ms = t;
   return true;

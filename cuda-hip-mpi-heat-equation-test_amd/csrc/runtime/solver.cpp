@@ -123,6 +123,8 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     }
     H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_work_), (size_t)(kern::stats_work_elems() + 8) * sizeof(double)));
     H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_part_), (size_t)(6 * kern::max_stats_waves()) * sizeof(double)));
+    H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_queue_), 2 * sizeof(uint32_t)));
+    H2D_HIP(hipMemset(d_queue_, 0, 2 * sizeof(uint32_t)));
     if (external_stream) {
       s_compute_ = s_comm_ = external_stream;
       cfg_.overlap = 0;
@@ -189,6 +191,7 @@ Solver::~Solver() {
     if (d_part_) (void)hipFree(d_part_);
     if (d_done_) (void)hipFree(d_done_);
     if (d_sig_) (void)hipFree(d_sig_);
+    if (d_queue_) (void)hipFree(d_queue_);
     if (h_err_) (void)hipHostFree(h_err_);
     if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
@@ -477,8 +480,11 @@ const kern::SplitPlan& Solver::split_plan(int k) {
         p.k = k;
       }
     }
+    // HEAT2D_DYNAMIC=1: the main launch takes its items from the dynamic queue (tests, A/B)
+    if (const char* e = std::getenv("HEAT2D_DYNAMIC"); e && std::atoi(e) == 1 && p.valid >= 1 && p.valid <= 3)
+      p.pair |= 2;
     // HEAT2D_PAIR=1: a single-launch plan runs as the wave-pair kernel (tests, A/B)
-    if (const char* e = std::getenv("HEAT2D_PAIR"); e && std::atoi(e) == 1 && p.valid == 2 && !p.pair) {
+    if (const char* e = std::getenv("HEAT2D_PAIR"); e && std::atoi(e) == 1 && p.valid == 2 && !(p.pair & 1)) {
       const kern::SplitPlan q = kern::pair_plan(dtype(), p, cfg_.arith);
       if (q.valid) p = q;
     }
@@ -540,6 +546,16 @@ static int device_cus_of(int device) {
 // was cut (31 -> 12.5 SALU per row) the pair ran 3.5 % behind one wave per
 // item on 4096^2 fp32 K = 16 (58.4 vs 56.4 us per cycle, profiles/r3/salu/):
 // its LDS hand-off and ring waits cost what the second wave hides.
+// Dynamic-queue candidates (HEAT2D_DYNAMIC=0 skips them; =1 forces the queue
+// on plans with more items than waves).
+static bool dynamic_candidates() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_DYNAMIC");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 static bool pair_candidates() {
   static const bool on = [] {
     const char* e = std::getenv("HEAT2D_PAIR");
@@ -579,14 +595,14 @@ void Solver::trial_cycle(const kern::SplitPlan& c) {
   if (c.valid == 3) {  // edge-first: both parts in order on the compute stream
     H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
     kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_compute_, cfg_.arith);
-    kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith);
+    kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
     return;
   }
   H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
   H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
-  kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith);
+  kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
   H2D_HIP(hipEventRecord(ev_int_, s_compute_));
   kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_, cfg_.arith);
   H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
@@ -699,6 +715,14 @@ void Solver::autotune_split(int k) {
       const kern::SplitPlan q = kern::pair_plan(dtype(), c, cfg_.arith);
       if (q.valid) timed.emplace_back(time_plan(q, 4), q);
     }
+    // more items than waves: also with the dynamic item queue (faster waves
+    // take more items; per-wave timelines of the 32768^2 fp64 interior showed
+    // a bimodal spread of up to 25 % between equal items: profiles/r3/wt3/)
+    if (dynamic_candidates() && c.main_items > c.main_waves && c.valid >= 1 && c.valid <= 3) {
+      kern::SplitPlan d = c;
+      d.pair |= 2;
+      timed.emplace_back(time_plan(d, 4), d);
+    }
   };
   for (int mode : {1, 2, 3, 4}) {
     if (mode == 2 && !single_ok) continue;
@@ -746,6 +770,7 @@ void Solver::autotune_split(int k) {
                                    : best.main_waves;
       std::vector<int64_t> segs;
       for (double f : {0.5, 1.0, 1.5, 2.0}) segs.push_back(std::max<int64_t>(1, (int64_t)(w0 * f + 0.5)));
+      if (dynamic_candidates()) segs.push_back(4 * w0);  // (timed with the dynamic queue, add())
       if (mode == 2 && cfg_.arith == 2) {
         // r = 1/4 single launches: strip-aligned segment counts too (a whole
         // number per strip), whose frame-row items the plan can weight
@@ -828,7 +853,7 @@ void Solver::launch_overlap(int k, int64_t B) {
     H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
     if (tr_->exchanges()) tr_->post(dst, L_, ev_bnd_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
-    kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith);
+    kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     pend_ = Pending::EdgeFirst;
@@ -839,7 +864,7 @@ void Solver::launch_overlap(int k, int64_t B) {
   if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
   if (sp.valid) {
     if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
-    kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith);
+    kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_, cfg_.arith);

@@ -45,7 +45,7 @@ def _plan(h, k: int) -> dict:
     N.call("heat2d_solver_plan", h, int(k), C.byref(p), C.byref(ms))
     return {"k": p.k, "ring": p.ring, "valid": p.valid,
             "order": {1: "concurrent", 2: "single", 3: "edge-first", 4: "fused"}.get(p.valid, "serial"),
-            "pair": int(p.pair),
+            "pair": int(p.pair & 1), "dynamic": int((p.pair >> 1) & 1),
             "main_bands": p.main.nb, "main_items": p.main_items, "main_waves": p.main_waves,
             "edge_items": p.edge_items, "edge_waves": p.edge_waves, "tuned_ms": ms.value,
             "main_rect": [p.main.r0, p.main.r1, p.main.s0, p.main.s1, p.main.nb],

@@ -254,3 +254,31 @@ def test_hip_ring8_single_launch(gpu, native, monkeypatch, dtype, ring, arith, t
     s.close()
     assert pl["order"] == "single" and pl["ring"] == ring, pl
     assert np.array_equal(got, golden(p, npdt, T0, arith=arith))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,tb,order,nseg,graph", [("fp64", 12, "single", 400, False), ("fp32", 16, "single", 300, True),
+                                                       ("fp64", 20, "concurrent", 500, True),
+                                                       ("fp32", 20, "edge-first", 700, False)])
+def test_hip_dynamic_queue(gpu, native, monkeypatch, dtype, tb, order, nseg, graph):
+    """Dynamic item queue (HEAT2D_DYNAMIC=1: after its first item a wave takes
+    the next free one from a device counter, reset by the last wave): many
+    more segments than waves would be needed to show balance, but correctness
+    needs only > 1 item per wave — forced here by planning for 16 CUs (the
+    compute stream CU-masked: comm_cus=240); several cycles (the reset between
+    launches), graph replays, bitwise."""
+    monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
+    monkeypatch.setenv("HEAT2D_DYNAMIC", "1")
+    monkeypatch.setenv("HEAT2D_SEGMENTS", str(nseg))
+    p = prob(1100, 3 * tb + 5)
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    T0 = rough(p, npdt)
+    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0, arith="jacobi", graph=graph,
+                   comm_cus=240)
+    s.upload(T0)
+    s.step(p.ntime)
+    got = s.download()
+    pl = s.plan(tb)
+    s.close()
+    assert pl["dynamic"] == 1 and pl["main_items"] > pl["main_waves"], pl
+    assert np.array_equal(got, golden(p, npdt, T0))

@@ -51,9 +51,18 @@ for lo, hi, r in bounds:
         per.append({"rect": r, "waves": int(sel.sum()), "dur_mean_us": round(float(d.mean()), 2),
                     "dur_max_us": round(float(d.max()), 2), "dur_min_us": round(float(d.min()), 2),
                     "end_max_us": round(float(end[sel].max()), 2)})
+# by XCD (blocks are dealt round-robin over the 8 XCDs: block = wave // 4) and
+# by the wave's slot in its block (its SIMD)
+wid = w[:, 2]
+xcd = {int(x): round(float(dur[(wid // 4) % 8 == x].mean()), 2) for x in range(8) if ((wid // 4) % 8 == x).any()}
+slot = {int(x): round(float(dur[wid % 4 == x].mean()), 2) for x in range(4)}
+# waves in eighths of the launch order (item order: strip-major segments / band-major bands)
+n8 = max(1, len(w) // 8)
+order = [round(float(dur[(wid >= i * n8) & (wid < (i + 1) * n8)].mean()), 2) for i in range(8)]
 q = np.percentile(end, [50, 90, 99, 100])
 print(json.dumps({"dtype": dtype, "n": n, "k": k, "waves": int(len(w)), "plan": {kk: pl[kk] for kk in ("order", "pair", "ring", "main_bands", "main_items")},
                   "span_us": round(float(end.max()), 2), "start_spread_us": round(float(start.max()), 2),
                   "start_p90_us": round(float(np.percentile(start, 90)), 2),
                   "dur_mean_us": round(float(dur.mean()), 2), "dur_max_us": round(float(dur.max()), 2),
-                  "end_p50_p90_p99_max_us": [round(float(x), 2) for x in q], "per_rect": per}))
+                  "end_p50_p90_p99_max_us": [round(float(x), 2) for x in q], "dur_by_xcd": xcd,
+                  "dur_by_slot": slot, "dur_by_order_eighth": order, "per_rect": per}))
