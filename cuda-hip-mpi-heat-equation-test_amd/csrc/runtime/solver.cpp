@@ -546,12 +546,13 @@ static int device_cus_of(int device) {
 // was cut (31 -> 12.5 SALU per row) the pair ran 3.5 % behind one wave per
 // item on 4096^2 fp32 K = 16 (58.4 vs 56.4 us per cycle, profiles/r3/salu/):
 // its LDS hand-off and ring waits cost what the second wave hides.
-// Dynamic-queue candidates (HEAT2D_DYNAMIC=0 skips them; =1 forces the queue
-// on plans with more items than waves).
+// Dynamic-queue candidates (HEAT2D_DYNAMIC=2 adds them to the autotuner; =1
+// forces the queue on plans with more items than waves). Opt-in until measured
+// end to end.
 static bool dynamic_candidates() {
   static const bool on = [] {
     const char* e = std::getenv("HEAT2D_DYNAMIC");
-    return !e || std::atoi(e) != 0;
+    return e && std::atoi(e) == 2;
   }();
   return on;
 }

@@ -16,7 +16,7 @@ for f in $O/wt*.json; do python -c "
 import json; d=json.load(open('$f')); print('$f', d['waves'], d['span_us'], d['dur_mean_us'], d['end_p50_p90_p99_max_us'], 'xcd', d['dur_by_xcd'], 'slot', d['dur_by_slot'], 'order', d['dur_by_order_eighth'])"; done
 for i in 1 2; do
   timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 > $O/b20_$i.json 2> $O/b20_$i.err || exit 1
-  HEAT2D_DYNAMIC=0 timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 > $O/b20_static_$i.json 2> $O/b20_static_$i.err || exit 1
+  HEAT2D_DYNAMIC=2 timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 > $O/b20_dyncand_$i.json 2> $O/b20_dyncand_$i.err || exit 1
 done
 timeout -k 10 300 python -u bench.py --dtype fp32 --steps 480 --warmup 20 > $O/f32.json 2> $O/f32.err || exit 1
 timeout -k 10 200 python -u bench.py --grid 4096 --dtype fp32 --steps 1000 --warmup 100 > $O/s4096.json 2> $O/s4096.err || exit 1
