@@ -480,6 +480,9 @@ const kern::SplitPlan& Solver::split_plan(int k) {
         p.k = k;
       }
     }
+    // HEAT2D_MAX_WAVES=n: at most n waves for the main launch (tests: several items per wave)
+    if (const char* e = std::getenv("HEAT2D_MAX_WAVES"); e && std::atoll(e) > 0 && p.valid >= 1 && p.valid <= 3)
+      p.main_waves = std::min<int64_t>(p.main_waves, std::atoll(e));
     // HEAT2D_DYNAMIC=1: the main launch takes its items from the dynamic queue (tests, A/B)
     if (const char* e = std::getenv("HEAT2D_DYNAMIC"); e && std::atoi(e) == 1 && p.valid >= 1 && p.valid <= 3)
       p.pair |= 2;

@@ -264,17 +264,16 @@ def test_hip_dynamic_queue(gpu, native, monkeypatch, dtype, tb, order, nseg, gra
     """Dynamic item queue (HEAT2D_DYNAMIC=1: after its first item a wave takes
     the next free one from a device counter, reset by the last wave): many
     more segments than waves would be needed to show balance, but correctness
-    needs only > 1 item per wave — forced here by planning for 16 CUs (the
-    compute stream CU-masked: comm_cus=240); several cycles (the reset between
-    launches), graph replays, bitwise."""
+    needs only > 1 item per wave — forced here with HEAT2D_MAX_WAVES=96;
+    several cycles (the reset between launches), graph replays, bitwise."""
     monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
     monkeypatch.setenv("HEAT2D_DYNAMIC", "1")
     monkeypatch.setenv("HEAT2D_SEGMENTS", str(nseg))
+    monkeypatch.setenv("HEAT2D_MAX_WAVES", "96")
     p = prob(1100, 3 * tb + 5)
     npdt = np.float64 if dtype == "fp64" else np.float32
     T0 = rough(p, npdt)
-    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0, arith="jacobi", graph=graph,
-                   comm_cus=240)
+    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0, arith="jacobi", graph=graph)
     s.upload(T0)
     s.step(p.ntime)
     got = s.download()
