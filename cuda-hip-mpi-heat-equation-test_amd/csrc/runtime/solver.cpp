@@ -549,13 +549,17 @@ static int device_cus_of(int device) {
 // was cut (31 -> 12.5 SALU per row) the pair ran 3.5 % behind one wave per
 // item on 4096^2 fp32 K = 16 (58.4 vs 56.4 us per cycle, profiles/r3/salu/):
 // its LDS hand-off and ring waits cost what the second wave hides.
-// Dynamic-queue candidates (HEAT2D_DYNAMIC=2 adds them to the autotuner; =1
-// forces the queue on plans with more items than waves). Opt-in until measured
-// end to end.
+// Dynamic-queue candidates (HEAT2D_DYNAMIC=0 keeps them out of the autotuner;
+// =1 forces the queue on plans with more items than waves). With 2 waves per
+// SIMD the older wave issues first: on the headline's interior launch the
+// first 1024 of 2048 equal waves end at 3.67 ms, the other 1024 at 5.43 ms,
+// which then run alone on their SIMDs (profiles/r3/dyn/). A queue lets the
+// early waves take more items: 32768^2 fp64 20 steps 4358 -> 4820 Gpts/s on
+// one box.
 static bool dynamic_candidates() {
   static const bool on = [] {
     const char* e = std::getenv("HEAT2D_DYNAMIC");
-    return e && std::atoi(e) == 2;
+    return !e || std::atoi(e) != 0;
   }();
   return on;
 }
