@@ -83,7 +83,7 @@ def test_hip_autotune_keeps_state_bitwise(gpu, native, dtype, tb):
     s.upload(R.owned(R.initial_field(p, npdt)))
     s.prepare(p.ntime)
     pl = s.plan()
-    assert pl["valid"] in (1, 2, 3) and pl["tuned_ms"] > 0.0 and pl["ring"] in (4, 6)  # split or single launch
+    assert pl["valid"] in (1, 2, 3) and pl["tuned_ms"] > 0.0 and pl["ring"] in (4, 6, 8)  # split or single launch (8: fp32 single)
     s.step(p.ntime)
     ref = R.owned(R.ftcs(p, dtype=npdt))
     got = s.download()
