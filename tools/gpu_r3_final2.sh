@@ -8,7 +8,7 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeou
 rc=$?; echo "tests rc=$rc"; tail -3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log || exit 1
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench20.json 2> $O/bench20.err && cat $O/bench20.json || exit 1
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench20_cached.json 2> $O/bench20_cached.err && cat $O/bench20_cached.json || exit 1
+HEAT2D_DYNAMIC=0 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench20_static.json 2> $O/bench20_static.err && cat $O/bench20_static.json || exit 1
 timeout -k 10 900 python -u bench/configs.py > $O/configs.jsonl 2> $O/configs.err || exit 1
 cat $O/configs.jsonl | python -c "import sys,json; [print(d['config'], d['gpts'], d['cycles'], d['prepare_s']) for d in map(json.loads, sys.stdin)]"
 timeout -k 10 200 python -u bench.py --rehearse-comm --rows 4096 --steps 20 --warmup 5 > $O/reh64_20.json 2> $O/reh64_20.err || exit 1
