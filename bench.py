@@ -275,8 +275,8 @@ def main():
     for k, c in sorted(hist.items()):
         pl = s.plan(k) if hip else {"k": k, "valid": 0}
         if hip:
-            plans[str(k)] = {kk: pl[kk] for kk in ("order", "pair", "dynamic", "ring", "main_bands", "main_waves", "edge_items",
-                                                    "tuned_ms")}
+            plans[str(k)] = {kk: pl[kk] for kk in ("order", "dynamic", "origin", "ring", "main_bands", "main_waves",
+                                                    "edge_items", "tuned_ms")}
         traffic += c * plan_hbm_bytes(pl, es, s.nrows, s.ncols)["total"]
     # halo traffic of the timed region: each exchange moves the NEXT cycle's
     # depth in whole padded rows, one message per neighbour
@@ -320,7 +320,6 @@ def main():
                 "arith": arith_name(prob.r, arith) + {"auto": " (auto)", "bench": " (r = 1/4)"}.get(args.arith, ""),
                 "overlap": not args.no_overlap,
                 "graph": bool(graph),
-                "persistent": bool(s.persistent(args.steps)) if hip else False,
                 "launch_plans": plans or None,
                 "backend": args.backend,
             },

@@ -58,7 +58,7 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False, arith="bench"):
         plans, traffic = {}, 0.0
         for k, c in sorted(hist.items()):
             pl = s.plan(k)
-            plans[str(k)] = {kk: pl[kk] for kk in ("order", "pair", "ring", "main_bands", "main_waves", "tuned_ms")}
+            plans[str(k)] = {kk: pl[kk] for kk in ("order", "dynamic", "origin", "ring", "main_bands", "main_waves", "tuned_ms")}
             traffic += c * plan_hbm_bytes(pl, es, n, n)["total"]
         rec["launch_plans"] = plans
         rec["hbm_gb_per_s_plan"] = round(traffic / dt / 1e9, 1)

@@ -497,8 +497,8 @@ int heat2d_plan_cache_path(char* buf, int64_t cap) {
   });
 }
 
-int heat2d_solver_persistent(void* s, int64_t n, int32_t* out) {
-  return guarded([&] { *out = static_cast<Solver*>(s)->persistent(n) ? 1 : 0; });
+int heat2d_solver_plan_origin(void* s, int k, int32_t* out) {
+  return guarded([&] { *out = static_cast<Solver*>(s)->plan_origin(k); });
 }
 
 int heat2d_autotune_slabs(int64_t n_rows, int64_t n_cols, int nranks, int autotune, int32_t* out) {

@@ -52,7 +52,7 @@ typedef struct heat2d_split_plan {
   heat2d_rect main;
   heat2d_rect edge[4];
   int64_t main_waves, edge_waves, main_items, edge_items;
-  int32_t nfused, pair;
+  int32_t nfused, flags;  // flags & 2: dynamic item queue
   heat2d_rect fused[6];
   int64_t sig_items;
 } heat2d_split_plan;
@@ -186,8 +186,9 @@ int heat2d_solver_ghost_rows(void* s, int32_t* out);
 // Plans / schedules the solver took from the persistent plan cache; the cache file path.
 int heat2d_solver_plan_cache_hits(void* s, int64_t* out);
 int heat2d_plan_cache_path(char* buf, int64_t cap);
-// 1 if prepare(n) chose persistent multi-cycle launches for step(n).
-int heat2d_solver_persistent(void* s, int64_t n, int32_t* out);
+// Where the depth-k split plan came from: 0 planned (not autotuned), 1 autotuned in
+// this process, 2 the plan cache (re-validated), -1 not planned yet.
+int heat2d_solver_plan_origin(void* s, int k, int32_t* out);
 // Autotune / measured-schedule eligibility of a decomposition (the same on every rank).
 int heat2d_autotune_slabs(int64_t n_rows, int64_t n_cols, int nranks, int autotune, int32_t* out);
 /* the schedule search itself on given cycle times t_ms[k] (k = 1..kmax; t_ms[0] unused): depths in out */

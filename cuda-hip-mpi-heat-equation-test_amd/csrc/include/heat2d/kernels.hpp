@@ -68,6 +68,7 @@ struct TbRect {
 };
 // rects of one launch (SplitPlan::fused, the kernel's TbArgs::rect)
 constexpr int kMaxFused = 6;
+constexpr int32_t kPlanDynamic = 2;  // SplitPlan::flags
 struct SplitPlan {
   int32_t k, ring, valid, nedge;
   TbRect main;
@@ -78,11 +79,9 @@ struct SplitPlan {
   // then the interior — and `edge` holds only bands on the Dirichlet frame.
   // valid = 1..3 with nfused > 0 (arith 2): `main` cut into frame-strip-
   // weighted rects, launched instead of `main` (stencil_tb.hip weight_main).
-  // pair bit 0 (valid = 2, fp32): the single launch runs the wave-pair kernel
-  // (tb_pair_kernel: two waves per item, the levels split between them);
-  // main_waves then counts PAIRS. Bit 1: the main launch takes its items
-  // from a dynamic queue (more items than waves; TbArgs::queue).
-  int32_t nfused, pair;
+  // flags & kPlanDynamic: the main launch takes its items from a dynamic
+  // queue (more items than waves; TbArgs::queue).
+  int32_t nfused, flags;
   TbRect fused[kMaxFused];
   int64_t sig_items;
 };
@@ -95,10 +94,6 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
 // where the second launch costs more than it saves.
 SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int ring_override = 0, int64_t bands = 0,
                       int arith = 0);
-// Co-resident wave pairs of the fp32 wave-pair kernel (0: not available for
-// this dtype / depth); pair_plan(p) = p run by that kernel (valid = 0 if not).
-int64_t pair_capacity(DType dt, int ring, int k, int arith);
-SplitPlan pair_plan(DType dt, const SplitPlan& p, int arith);
 // Fused cycle (valid = 4) for slabs whose halo exchange can be gated on a
 // device counter (Transport::gates()): ONE interior-kernel launch whose first
 // items are the boundary bands the exchange sends (top if send_top, bottom if
@@ -120,28 +115,9 @@ void launch_fused_main(DType dt, const void* src, void* dst, const SlabLayout& L
 // timeout_ticks sets *err and returns.
 void launch_wait_counter(const uint32_t* counter, uint32_t target, uint64_t timeout_ticks, unsigned int* err,
                          hipStream_t stream);
-// queue: 2 device counters (zeroed once) for plans with pair bit 1 (dynamic items)
+// queue: 2 device counters (zeroed once) for plans with flags & kPlanDynamic (dynamic items)
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr);
-
-// Persistent multi-cycle launch (tb_impl.hpp tb_persist_kernel): `ncycles`
-// cycles of depth plan.k over the whole slab in ONE cooperative dispatch, one
-// co-resident wave per item of a single-launch plan (plan_single), items
-// synchronised by per-item completion counters (a wavefront, no grid barrier)
-// instead of kernel boundaries.
-// alternate = 1: cycle c reads buffer c & 1 and writes the other (the real
-// loop: the result lands in buf0 / buf1 by the parity of ncycles); 0: every
-// cycle buf0 -> buf1 (timing trials; buf0 untouched).
-struct PersistCtl {
-  uint32_t* done;          // device, >= nitems_cap per-item completion counters
-  int64_t nitems_cap;
-  uint32_t base;           // the counters' value at launch (advance by ncycles after each launch)
-  uint64_t timeout_ticks;  // a dependency wait longer than this fails the launch (*err = 1)
-  unsigned int* err;       // host-visible
-};
-int64_t persist_capacity(DType dt, int ring, int k, int arith);  // co-resident waves of the persistent kernel
-void launch_tb_persist(DType dt, void* buf0, void* buf1, const SlabLayout& L, const SplitPlan& plan, double r,
-                       const PersistCtl& ctl, int ncycles, int alternate, hipStream_t stream, int arith = 0);
 
 // Initial / boundary condition kinds (covers every IC of the reference
 // variants, see models/presets.py for the mapping).

@@ -7,12 +7,15 @@
 // winners on disk, keyed by everything the measurement depended on — GPU
 // architecture and CU count, dtype, arithmetic, the slab's rows / columns /
 // pitch / position in the domain, the depth and band, the compute stream's CU
-// budget, the exchange kind, and the build (a hash of the kernel and runtime
-// sources, HEAT2D_BUILD_ID) — and a hit is re-validated by ONE short re-time
-// of the cached plan (a drift of more than 10 % re-tunes).
+// budget, the exchange kind, the transport (name, gated exchanges), a hash of
+// the plan-shaping HEAT2D_* environment knobs, and the build (a hash of the
+// kernel and runtime sources, HEAT2D_BUILD_ID; a build without one, "dev",
+// disables the cache) — and a hit is checked semantically (a plan kind this
+// run may not use is refused) and re-validated by ONE short re-time of the
+// cached plan (a drift of more than 10 % re-tunes).
 //
 // File: $HEAT2D_PLAN_CACHE (path; "off" disables), default
-// $XDG_CACHE_HOME/heat2d/plans-v1.txt or ~/.cache/heat2d/plans-v1.txt. One
+// $XDG_CACHE_HOME/heat2d/plans-v3.txt or ~/.cache/heat2d/plans-v3.txt. One
 // "key<TAB>value" line per entry, appended (O_APPEND: concurrent rank
 // processes add whole lines); the last line of a key wins.
 #pragma once

@@ -337,11 +337,9 @@ class Solver {
   int64_t plans_made() const { return plans_made_; }
   // plans and schedules taken from the persistent plan cache (plan_cache.hpp)
   int64_t plan_cache_hits() const { return plan_cache_hits_; }
-  // step(n) runs as persistent multi-cycle launches (prepare() decided)
-  bool persistent(int64_t n) const {
-    auto it = persist_.find(n);
-    return it != persist_.end() && it->second;
-  }
+  // origin of the depth-k split plan: -1 not planned, 0 planned (no autotune),
+  // 1 autotuned here, 2 taken from the plan cache (re-validated)
+  int plan_origin(int k) const { return k >= 1 && k <= kMaxTB ? plan_origin_[k] : -1; }
   int spare_waves() const;
   // Phase timers (hipEvents on the GPU timeline) for every cycle while
   // enabled: [main ms, edge ms, exchange ms, whole-cycle ms (serial schedule),
@@ -385,21 +383,12 @@ class Solver {
   std::string sched_ctx() const;   // ... of the decomposition's schedules
   bool cached_split(int k);        // plan of depth k from the cache, re-validated
   bool cached_schedule(int64_t n); // measured schedule of n steps from the cache (collective)
-  // Persistent multi-cycle launches (kern::launch_tb_persist): single-rank
-  // runs of many short cycles (small grids), one dispatch per run of equal
-  // depths instead of a launch (or graph node) per cycle. HEAT2D_PERSIST:
-  // 0 off, 1 on where possible, unset = auto (prepare() times both).
-  bool persist_eligible() const;
   // fused cycles (kern::plan_fused): the exchange gated on the interior
   // launch's band items (HEAT2D_FUSED=0 disables)
   bool fused_ok() const;
   void sent_sides(bool* top, bool* bottom) const;
   void ensure_err();
   void ensure_sig();
-  const kern::SplitPlan* persist_plan(int k);  // nullptr: too many items to be co-resident
-  void ensure_persist_ctl();
-  void run_persist(const std::vector<int>& seq, bool trial);
-  float time_persist(const std::vector<int>& seq);  // ms of one trial run (solution untouched)
   void run_schedule_graph(int64_t n);
   float depth_ms(int k);
   std::vector<int> choose_schedule(int64_t n);
@@ -450,18 +439,12 @@ class Solver {
   float tuned_ms_[kMaxTB + 1] = {};           // autotuned cycle time (ms), 0 if not tuned
   int64_t plans_made_ = 0;
   int64_t plan_cache_hits_ = 0;
-  int persist_mode_ = -1;                 // HEAT2D_PERSIST (-1 auto, 0 off, 1 on)
-  std::map<int64_t, bool> persist_;       // step(n) runs persistent launches (decided in prepare)
-  kern::SplitPlan persist_plans_[kMaxTB + 1] = {};
-  uint32_t* d_done_ = nullptr;            // persistent launches: per-item completion counters
-  int64_t done_cap_ = 0;
-  uint32_t done_base_ = 0;                // their value at the next launch
-  unsigned int* h_err_ = nullptr;         // pinned, host-visible error word (persistent kernel, exchange gates)
+  int plan_origin_[kMaxTB + 1];           // plan_origin(), initialised to -1
+  unsigned int* h_err_ = nullptr;         // pinned, host-visible error word (exchange gates)
   uint32_t* d_sig_ = nullptr;             // [0]: band items of the running fused cycle; [1]: trial scratch
   uint32_t* d_queue_ = nullptr;           // dynamic item queue of the main launches (SplitPlan::pair bit 1)
   int64_t pend_sig_ = 0;                  // band items the pending fused cycle signals
   uint64_t gate_timeout_ticks_ = 0;
-  uint64_t persist_timeout_ticks_ = 0;
   hipEvent_t ev_t0_ = nullptr, ev_t1_ = nullptr;  // time_plan
   hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K
   int graph_k_ = 0;

@@ -23,7 +23,7 @@
 //     voffsets for masked lanes (and num_records = 0 for priming rows): no
 //     memory op under control flow, so the RING-row prefetch is waited for
 //     with counted vmcnt(N);
-//   * persistent schedule: as many waves as the chip holds resident
+//   * persistent grid: as many waves as the chip holds resident
 //     (occupancy API x CUs), work items = (row band, strip), band-major;
 //   * the arithmetic order is exactly the reference's
 //     c + r*((((S + E) + N) + W) - 4c) (fortran/hip/heat_kernel.cpp:43, with
@@ -253,7 +253,7 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t simds, int k, int64_t pri
 // partials != nullptr: the fused-statistics kernel (general, ring 4). Returns the waves launched.
 int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
                      const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith,
-                     double* partials = nullptr, int64_t sig_items = 0, uint32_t* sig = nullptr, bool pair = false,
+                     double* partials = nullptr, int64_t sig_items = 0, uint32_t* sig = nullptr,
                      uint32_t* queue = nullptr) {
   HEAT2D_REQUIRE(nrect >= 1 && nrect <= (main ? kMainRects : kMaxRects), "bad rect count");
   TbArgs a{};
@@ -287,20 +287,10 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   a.sig = sig;
   a.wtimes = wave_times_buf(a.nwaves);
   // the dynamic queue only pays with more items than waves (plain kernels)
-  a.queue = (queue && !pair && !partials && !sig && items > a.nwaves) ? queue : nullptr;
-  // (pair: nwaves counts wave pairs, two per 256-thread block)
-  const unsigned nblocks = pair ? (unsigned)((a.nwaves + 1) / 2) : (unsigned)((a.nwaves + 3) / 4);
+  a.queue = (queue && !partials && !sig && items > a.nwaves) ? queue : nullptr;
+  const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
   const int64_t o = L.origin();
-  if (pair) {
-    HEAT2D_REQUIRE(dt == DType::F32 && !main && !partials && !sig && k >= 2, "wave pairs: fp32 general launches, k >= 2");
-    const float* s32 = static_cast<const float*>(src) + o;
-    float* d32 = static_cast<float*>(dst) + o;
-    with_ar(arith, [&](auto ar) {
-      constexpr int AR = decltype(ar)::value;
-      if (ring == 4) dispatch_pair<4, AR>(k, nblocks, s32, d32, a, (float)r, stream);
-      else dispatch_pair<6, AR>(k, nblocks, s32, d32, a, (float)r, stream);
-    });
-  } else if (partials) {
+  if (partials) {
     HEAT2D_REQUIRE(a.nwaves <= max_stats_waves(), "statistics partials buffer too small");
     const float* s32 = static_cast<const float*>(src) + o;
     const double* s64 = static_cast<const double*>(src) + o;
@@ -668,102 +658,6 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_ov
   return p;
 }
 
-int64_t pair_capacity(DType dt, int ring, int k, int arith) {
-  if (dt != DType::F32 || k < 2 || k > 16 || (ring != 4 && ring != 6)) return 0;  // pair kernels: K = 2..16
-  const int bpc = with_ar(arith, [&](auto ar) {
-    constexpr int AR = decltype(ar)::value;
-    return ring == 4 ? occupancy_pair<4, AR>(k) : occupancy_pair<6, AR>(k);
-  });
-  return (int64_t)cu_count() * bpc * 2;
-}
-
-SplitPlan pair_plan(DType dt, const SplitPlan& p, int arith) {
-  SplitPlan q = p;
-  const int64_t cap = p.valid == 2 ? pair_capacity(dt, p.ring, p.k, arith) : 0;
-  if (cap <= 0) {
-    q.valid = 0;
-    return q;
-  }
-  q.pair = 1;
-  q.main_waves = std::min<int64_t>(q.main_items, cap);  // pairs
-  return q;
-}
-
-int64_t persist_capacity(DType dt, int ring, int k, int arith) {
-  HEAT2D_REQUIRE(ring == 4 || ring == 6, "ring must be 4 or 6");
-  const int bpc = with_ar(arith, [&](auto ar) {
-    constexpr int AR = decltype(ar)::value;
-    if (dt == DType::F32) return ring == 4 ? occupancy_persist<float, 4, AR>(k) : occupancy_persist<float, 6, AR>(k);
-    return ring == 4 ? occupancy_persist<double, 4, AR>(k) : occupancy_persist<double, 6, AR>(k);
-  });
-  return (int64_t)cu_count() * bpc * 4;
-}
-
-void launch_tb_persist(DType dt, void* buf0, void* buf1, const SlabLayout& L, const SplitPlan& plan, double r,
-                       const PersistCtl& ctl, int ncycles, int alternate, hipStream_t stream, int arith) {
-  const int k = plan.k;
-  check_layout(dt, L, k);
-  HEAT2D_REQUIRE(plan.valid == 2, "the persistent launch runs a single-launch plan (plan_single)");
-  HEAT2D_REQUIRE(ncycles >= 1, "ncycles >= 1");
-  const TbRect& R = plan.main;
-  HEAT2D_REQUIRE(R.r0 == 0 && R.r1 == L.nrows && R.nb != 0 && R.s1 > R.s0, "persistent plan must cover the slab");
-  TbArgs a{};
-  a.pitch = L.pitch;
-  a.ncols = L.ncols;
-  a.col_lo = -L.cpad;
-  a.col_hi = L.col_hi();
-  a.fixed_lo = -L.row0;
-  a.fixed_hi = L.nrows_global - L.row0;
-  // the plan's rects (frame-weighted, weight_main) or its one main rect; they
-  // tile the slab, which the kernel's neighbour waits rely on
-  const TbRect* rects = plan.nfused > 0 ? plan.fused : &plan.main;
-  const int nr = plan.nfused > 0 ? plan.nfused : 1;
-  HEAT2D_REQUIRE(nr <= kMaxRects, "bad rect count");
-  int64_t items = 0, covered = 0;
-  for (int i = 0; i < nr; ++i) {
-    const TbRect& Q = rects[i];
-    const int64_t rows = Q.r1 - Q.r0, ns = Q.s1 - Q.s0;
-    HEAT2D_REQUIRE(rows > 0 && ns > 0 && Q.nb != 0 && Q.r0 >= 0 && Q.r1 <= L.nrows && Q.s0 >= R.s0 && Q.s1 <= R.s1,
-                   "persistent rect outside the slab");
-    HEAT2D_REQUIRE(Q.nb > 0 || -Q.nb <= rows * ns, "more segments than strip rows");
-    HEAT2D_REQUIRE(rows * ns < (int64_t(1) << 31), "rect exceeds 2^31 strip rows");
-    a.rect[i] = TbRectArg{Q.r0, Q.r1, Q.s0, Q.s1, Q.nb, items};
-    items += Q.nb > 0 ? Q.nb * ns : -Q.nb;
-    covered += rows * ns;
-  }
-  HEAT2D_REQUIRE(covered == (R.r1 - R.r0) * (R.s1 - R.s0), "persistent rects must tile the slab");
-  a.nrect = nr;
-  a.nitems = items;
-  a.nwaves = a.nitems;
-  // every item's wave must be resident at once (they wait on each other)
-  HEAT2D_REQUIRE(a.nitems <= persist_capacity(dt, plan.ring, k, arith) && a.nitems <= ctl.nitems_cap,
-                 "persistent launch: more items than co-resident waves / counters");
-  PersistArgs p{};
-  p.done = ctl.done;
-  p.base = ctl.base;
-  p.ncycles = ncycles;
-  p.alternate = alternate;
-  p.timeout_ticks = ctl.timeout_ticks;
-  p.err = ctl.err;
-  const unsigned nblocks = (unsigned)((a.nitems + 3) / 4);
-  const int64_t o = L.origin();
-  const hipError_t e = with_ar(arith, [&](auto ar) {
-    constexpr int AR = decltype(ar)::value;
-    if (dt == DType::F32) {
-      float* f0 = static_cast<float*>(buf0) + o;
-      float* f1 = static_cast<float*>(buf1) + o;
-      const float rf = (float)r;
-      return plan.ring == 4 ? dispatch_persist<float, 4, AR>(k, nblocks, f0, f1, a, rf, p, stream)
-                            : dispatch_persist<float, 6, AR>(k, nblocks, f0, f1, a, rf, p, stream);
-    }
-    double* d0 = static_cast<double*>(buf0) + o;
-    double* d1 = static_cast<double*>(buf1) + o;
-    return plan.ring == 4 ? dispatch_persist<double, 4, AR>(k, nblocks, d0, d1, a, r, p, stream)
-                          : dispatch_persist<double, 6, AR>(k, nblocks, d0, d1, a, r, p, stream);
-  });
-  if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("persistent launch: ") + hipGetErrorString(e));
-}
-
 int64_t wave_times(uint64_t* out, int64_t max_waves) {
   WaveTimes& w = wave_times_state();
   if (!w.buf || w.n == 0) return 0;
@@ -792,8 +686,8 @@ void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, 
 
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith, uint32_t* queue) {
-  // (SplitPlan::pair bit 1: the main part takes its items from the dynamic queue)
-  uint32_t* q = (p.pair & 2) ? queue : nullptr;
+  // (SplitPlan::flags & kPlanDynamic: the main part takes its items from the dynamic queue)
+  uint32_t* q = (p.flags & kPlanDynamic) ? queue : nullptr;
   HEAT2D_REQUIRE(p.valid, "invalid split plan");
   HEAT2D_REQUIRE(p.valid != 4 || !main_part, "a fused plan's main part needs its band counter (launch_fused_main)");
   if (p.valid == 4 && p.nedge == 0) return;  // no band on the frame
@@ -802,13 +696,11 @@ void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, con
   const int nm = p.nfused > 0 ? p.nfused : 1;
   if (p.valid == 2) {  // single general launch over the whole slab (no edge part)
     if (main_part)
-      launch_rects(dt, src, dst, L, p.k, p.ring, false, mr, nm, p.main_waves, r, stream, arith, nullptr, 0, nullptr,
-                   (p.pair & 1) != 0, q);
+      launch_rects(dt, src, dst, L, p.k, p.ring, false, mr, nm, p.main_waves, r, stream, arith, nullptr, 0, nullptr, q);
     return;
   }
   if (main_part)
-    launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith, nullptr, 0, nullptr, false,
-                 q);
+    launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith, nullptr, 0, nullptr, q);
   else
     launch_rects(dt, src, dst, L, p.k, p.ring, false, p.edge, p.nedge, p.edge_waves, r, stream, arith);
 }

@@ -111,7 +111,7 @@ struct TbArgs {
   // Diagnostics (HEAT2D_WAVE_TIMES, kern::wave_times): per launched wave
   // {start, end (wall clock, 100 MHz), first item, its edge kind}; nullptr off
   uint64_t* wtimes;
-  // Dynamic item queue (SplitPlan::pair bit 1): {next item beyond the first
+  // Dynamic item queue (SplitPlan::flags & kPlanDynamic): {next item beyond the first
   // round, waves finished}; a wave takes its first item statically (wid) and
   // then the next free one, so waves that run faster take more items. The
   // last wave to finish resets both counters for the next launch. nullptr:
@@ -294,18 +294,7 @@ constexpr int chain_len() {
 #define HEAT2D_STORE_AUX 2
 #endif
 
-// CP (cache policy of the field loads / stores): 0 = default (stores nt); 1 =
-// device-coherent (sc1 loads, nt sc1 stores): the values go to / come from the
-// memory side, coherent across the 8 XCDs' L2s without cache maintenance —
-// the persistent kernel's cross-wave hand-off (tb_persist_kernel); 2 =
-// device-coherent stores only (the band items of a fused cycle, read by the
-// exchange while the launch still runs).
-template <int CP>
-constexpr int kLoadAux = CP == 1 ? 16 : 0;
-template <int CP>
-constexpr int kStoreAux = CP ? (16 | 2) : HEAT2D_STORE_AUX;
-
-template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, int CL = K, int CP = 0>
+template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, int CL = K>
 struct March {
   using S = TbShape<T, NV, K>;
   static constexpr int V = S::V;
@@ -355,7 +344,7 @@ struct March {
     const __amdgpu_buffer_rsrc_t rs = row_rsrc(p, live ? nrec : 0u);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      U4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off + v * 16, 0, kLoadAux<CP>);
+      U4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off + v * 16, 0, 0);
       out[v] = __builtin_bit_cast(VT, b);
     }
   }
@@ -368,7 +357,7 @@ struct March {
       VT w;
 #pragma unroll
       for (int e = 0; e < VM; ++e) w[e] = out[v * VM + e];
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off + v * 16, 0, kStoreAux<CP>);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off + v * 16, 0, HEAT2D_STORE_AUX);
     }
   }
 
@@ -568,31 +557,7 @@ struct March {
 // ~2x the registers: 209 VGPRs at K = 10). Same operation order and rounding
 // per element as March (bitwise identical); the loads / stores / ring /
 // descriptors / edge kinds are March's.
-// Wave pair (tb_pair_kernel): IO 1 = the producer (levels 1..K of the pair's
-// first half: global loads, its last level handed to the consumer through an
-// LDS row ring, still scaled), IO 2 = the consumer (its rows come from that
-// ring; LIN levels already applied to them). kPairRing rows per pair.
-constexpr int kPairRing = 16;
-// polls before a ring wait gives up (~2 s of s_sleep 1): a wrong result, never a hang
-constexpr uint32_t kPairSpin = 1u << 25;
-
-__device__ __forceinline__ uint32_t lds_ctr_load(const uint32_t* c) {
-  return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_ctr_store(uint32_t* c, uint32_t v) {
-  __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// wait until *c >= need (wrap-safe); returns the value seen
-__device__ __forceinline__ uint32_t lds_wait_ge(const uint32_t* c, uint32_t need) {
-  uint32_t v = lds_ctr_load(c);
-  for (uint32_t n = 0; (int32_t)(v - need) < 0 && n < kPairSpin; ++n) {
-    __builtin_amdgcn_s_sleep(1);
-    v = lds_ctr_load(c);
-  }
-  return v;
-}
-
-template <int K, int EK, int RING, int AR, bool ST = false, int CL = K, int CP = 0, int IO = 0, int LIN = 0>
+template <int K, int EK, int RING, int AR, bool ST = false, int CL = K>
 struct MarchF32 {
   using F2 = float __attribute__((ext_vector_type(2)));
   using VT = float __attribute__((ext_vector_type(4)));
@@ -618,15 +583,6 @@ struct MarchF32 {
   int32_t st_off;
   Row rl;  // EK & 2: r per element (0 in Dirichlet / pad columns)
   static constexpr bool kScaled = AR == 2 && EK == 0;  // levels carried x 4^level (see March)
-  // IO 1 / 2: the pair's LDS row ring (kPairRing rows of 64 lanes) and its
-  // counters {rows produced, rows consumed}, monotone over the pair's items:
-  // row `row` of this piece is ring entry qbase + (qtop - row)
-  VT* pring;
-  uint32_t* pctr;
-  uint32_t qbase;
-  int32_t qtop, qlast;
-  uint32_t have;  // last counter value seen (producer: consumed, consumer: produced)
-
   using Ch = ChainShape<K, CL>;
   static constexpr int L = Ch::unroll(RING);
   Row X[3][KX];  // slot 2 only below chain boundaries (see March)
@@ -638,45 +594,16 @@ struct MarchF32 {
   // of a rebuild at each of its three uses.
   Row Lb[RING];
 
-  __device__ __forceinline__ void load_row(int32_t m, Row& out) {
-    if constexpr (IO == 2) {  // consumer: the producer's row, once it is in the ring
-      int32_t q = qtop - m;
-      q = q > qlast ? qlast : q;  // clamped rows below the last one only feed priming values
-      const uint32_t e = qbase + (uint32_t)q;
-      if ((int32_t)(have - (e + 1u)) < 0) have = lds_wait_ge(pctr, e + 1u);
-      asm volatile("" ::: "memory");
-      const int lane = (int)(threadIdx.x & 63);
-      const VT v = pring[(e & (kPairRing - 1)) * 64 + lane];
-      out = Row{F2{v.x, v.y}, F2{v.z, v.w}};
-      asm volatile("" ::: "memory");
-      // LDS executes one wave's operations in order: the producer sees this
-      // count only after the read above has taken the row
-      if (lane == 0) lds_ctr_store(pctr + 1, e + 1u);
-    } else {
-      load_row_p(srow + (int64_t)m * pitch_b, true, out);
-    }
-  }
+  __device__ __forceinline__ void load_row(int32_t m, Row& out) const { load_row_p(srow + (int64_t)m * pitch_b, true, out); }
   // live == false: below the item's lowest loaded row (priming values only): returns 0
   __device__ __forceinline__ void load_row_p(const char* p, bool live, Row& out) const {
     const __amdgpu_buffer_rsrc_t rs = row_rsrc(p, live ? nrec : 0u);
-    const VT v = __builtin_bit_cast(VT, __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off, 0, kLoadAux<CP>));
+    const VT v = __builtin_bit_cast(VT, __builtin_amdgcn_raw_buffer_load_b128(rs, ld_off, 0, 0));
     out = Row{F2{v.x, v.y}, F2{v.z, v.w}};
   }
-  __device__ __forceinline__ void store_row(int32_t row, bool live, const VT& w) {
-    if constexpr (IO == 1) {  // producer: into the ring once its slot's previous row was consumed
-      if (live) {             // wave-uniform
-        const uint32_t e = qbase + (uint32_t)(qtop - row);
-        if ((int32_t)(have - (e + 1u - kPairRing)) < 0) have = lds_wait_ge(pctr + 1, e + 1u - kPairRing);
-        asm volatile("" ::: "memory");
-        const int lane = (int)(threadIdx.x & 63);
-        pring[(e & (kPairRing - 1)) * 64 + lane] = w;
-        asm volatile("" ::: "memory");
-        if (lane == 0) lds_ctr_store(pctr, e + 1u);
-      }
-    } else {
-      const __amdgpu_buffer_rsrc_t rs = row_rsrc(sp, live ? nrec : 0u);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off, 0, kStoreAux<CP>);
-    }
+  __device__ __forceinline__ void store_row(bool live, const VT& w) const {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(sp, live ? nrec : 0u);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, w), rs, st_off, 0, HEAT2D_STORE_AUX);
   }
   static __device__ __forceinline__ Row split(const Row& v) { return Row{F2{v.a.x, v.b.x}, F2{v.a.y, v.b.y}}; }
 
@@ -747,10 +674,8 @@ struct MarchF32 {
     if constexpr (AR == 2) {
       const Row sum = sum4(part, C, N);
       if constexpr (EK == 0) {
-        // unscale 4^K T once, at the store (exact); the producer of a pair
-        // hands its rows on scaled, its consumer unscales the pair's LIN + K
-        if constexpr (IO == 1) return VT{sum.a.x, sum.b.x, sum.a.y, sum.b.y};
-        constexpr float u = inv_pow4<float>(LIN + K);
+        // unscale 4^K T once, at the store (exact)
+        constexpr float u = inv_pow4<float>(K);
         return VT{sum.a.x * u, sum.b.x * u, sum.a.y * u, sum.b.y * u};
       }
       const bool frame_row = (EK & 1) && ((uint32_t)(row - fixed_lo) >= (uint32_t)(fixed_hi - fixed_lo));  // wave-uniform
@@ -779,12 +704,8 @@ struct MarchF32 {
     {
       const int32_t nxt = m + 2 - RING;
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (IO == 2) {
-        load_row(nxt >= mload ? nxt : mload, Lb[sS]);
-      } else {
-        load_row_p(lp, nxt >= mload, Lb[sS]);
-        lp -= pitch_b;
-      }
+      load_row_p(lp, nxt >= mload, Lb[sS]);
+      lp -= pitch_b;
     }
     Lb[sN] = split(Lb[sN]);  // first use of this row: to even/odd form, in place
     const Row N0 = Lb[sN];
@@ -805,7 +726,7 @@ struct MarchF32 {
         const int32_t row = m + Ch::off(K);
         const bool live = (uint32_t)(row - t0) < (uint32_t)(t1 - t0);  // row in [t0, t1), wave-uniform
         const VT w = update_last(part, C, N, row);
-        store_row(row, live, w);
+        store_row(live, w);
         if constexpr (ST) {
           if (live) {  // C in even/odd form: a = (c0, c2), b = (c1, c3)
             constexpr float cu = kScaled ? inv_pow4<float>(K - 1) : 1.f;  // level K-1 scale
@@ -817,7 +738,7 @@ struct MarchF32 {
         }
       }
     }
-    if constexpr (IO != 1) sp -= pitch_b;
+    sp -= pitch_b;
   }
 
   template <int... I>
@@ -877,8 +798,7 @@ template <typename T, int NV>
 constexpr bool kPackedF32 = false;
 #endif
 
-template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, bool PS = false, int CLX = 0,
-          int CP = 0>
+template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, bool PS = false, int CLX = 0>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
                                       int64_t t1, int lane, StatAcc* acc = nullptr) {
   using S = TbShape<T, NV, K>;
@@ -892,8 +812,8 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   // the chains' extra rows spill at fp64 K >= 21
   // (CLX > 0: an explicit chain length — the boundary-band kernel)
   constexpr int CL = CLX > 0 ? (CLX < K ? CLX : K) : (ST ? K : chain_len<T, K>());
-  using W = typename std::conditional<kPackedF32<T, NV>, MarchF32<K, EK, RING, AR, ST, CL, CP>,
-                                      March<T, NV, K, EK, RING, AR, ST, CL, CP>>::type;
+  using W = typename std::conditional<kPackedF32<T, NV>, MarchF32<K, EK, RING, AR, ST, CL>,
+                                      March<T, NV, K, EK, RING, AR, ST, CL>>::type;
   W w;
   // row base = column col_lo (= -cpad) of row 0; offsets are relative to it
   w.srow = reinterpret_cast<const char*>(src + a.col_lo);
@@ -936,65 +856,6 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
     *acc = w.acc;
   } else {
     w.template run<PS>();
-  }
-}
-
-// Wave-pair march of one piece (tb_pair_kernel, fp32): the producer (role 0)
-// runs levels 1..KA over the piece's rows widened by KB on both sides (its
-// march covers rows [t0 - K, t1 + K), as a single wave of depth K would), the
-// consumer (role 1) levels KA+1..K over the piece itself, its input rows the
-// producer's level KA, taken from the pair's LDS ring as they appear. Strip
-// geometry (halo columns, useful width) is that of the whole depth K. Same
-// operations in the same order per point as one wave of depth K: bitwise
-// identical. qbase: ring entries of the pair's earlier pieces.
-template <int K, int EK, int RING, int AR>
-__device__ __forceinline__ void march_pair(const float* src, float* dst, const TbArgs& a, float r, int64_t strip,
-                                           int64_t t0, int64_t t1, int lane, int role,
-                                           float __attribute__((ext_vector_type(4))) * ring, uint32_t* ctr,
-                                           uint32_t qbase) {
-  constexpr int KA = K / 2, KB = K - KA;
-  using S = TbShape<float, 1, K>;
-  constexpr int V = S::V;
-  const int64_t u0 = strip * S::U;
-  const int64_t mycol = u0 - S::KA + (int64_t)lane * V;
-  const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
-  const int32_t off = (int32_t)((mycol - a.col_lo) * 4);
-  const bool in_alloc = (mycol >= a.col_lo) && (mycol + V <= a.col_hi);
-  const bool useful = (mycol >= u0) && (mycol < ustop);
-  auto setup = [&](auto& w) {
-    w.srow = reinterpret_cast<const char*>(src + a.col_lo);
-    w.drow = reinterpret_cast<char*>(dst + a.col_lo);
-    w.pitch_b = a.pitch * 4;
-    w.nrec = (uint32_t)(a.pitch * 4);
-    w.r = r;
-    w.fixed_lo = (int32_t)a.fixed_lo;
-    w.fixed_hi = (int32_t)a.fixed_hi;
-    w.ld_off = in_alloc ? off : kOob;
-    w.st_off = useful && in_alloc ? off : kOob;
-    if constexpr ((EK & 2) != 0) {
-      auto rcol = [&](int e) { return (mycol + e < 0 || mycol + e >= a.ncols) ? 0.f : r; };
-      w.rl.a = {rcol(0), rcol(2)};
-      w.rl.b = {rcol(1), rcol(3)};
-    }
-    w.pring = ring;
-    w.pctr = ctr;
-    w.qbase = qbase;
-    w.qtop = (int32_t)(t1 + KB - 1);
-    w.qlast = (int32_t)(t1 - t0 + 2 * KB - 1);
-    w.have = 0;
-  };
-  if (role == 0) {
-    MarchF32<KA, EK, RING, AR, false, KA, 0, 1, 0> w;
-    setup(w);
-    w.t0 = (int32_t)(t0 - KB);
-    w.t1 = (int32_t)(t1 + KB);
-    w.run();
-  } else {
-    MarchF32<KB, EK, RING, AR, false, KB, 0, 2, KA> w;
-    setup(w);
-    w.t0 = (int32_t)t0;
-    w.t1 = (int32_t)t1;
-    w.run();
   }
 }
 
@@ -1261,250 +1122,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
   }
 }
 
-// ---------------------------------------------------------------------------
-// Wave-pair kernel (fp32 single launches of small grids). With one march wave
-// per SIMD (the 4096^2 grid: ~1000 items, no second wave without doubling the
-// priming rows), every non-VALU instruction of that wave — loads, stores,
-// waits, scalar address work, DPP hazard nops — is a VALU issue slot lost
-// (VALU ~74 % busy: profiles/small_grid/). Here each item is marched by TWO
-// waves, the K levels split between them (producer KA = K/2, consumer K - KA),
-// handing rows over through a 16-row LDS ring with two counters: 2 waves per
-// SIMD for the same item count and (slightly fewer) level-rows. A 256-thread
-// block holds 2 pairs; the waves of a pair agree on the item sequence, and the
-// only cross-wave waits are the ring's (bounded: kPairSpin).
-template <int K, int RING, int AR>
-__global__ __launch_bounds__(256) void tb_pair_kernel(const float* __restrict__ src, float* __restrict__ dst, TbArgs a,
-                                                      float r) {
-  using VT4 = float __attribute__((ext_vector_type(4)));
-  constexpr int KB = K - K / 2;
-  __shared__ VT4 ring[2][kPairRing * 64];
-  __shared__ uint32_t ctr[2][2];
-  if (threadIdx.x < 4) ctr[threadIdx.x >> 1][threadIdx.x & 1] = 0u;
-  __syncthreads();
-  using S = TbShape<float, 1, K>;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int pr = w >> 1, role = w & 1;
-  const int64_t pid = (int64_t)blockIdx.x * 2 + pr;
-  if (pid >= a.nwaves) return;  // nwaves = pairs launched
-  uint32_t qbase = 0;
-  int64_t it = pid;
-  int32_t lin = tb_span(a, it).lin;
-  while (it < a.nitems) {
-    int64_t strip, t0, t1;
-    if (!tb_piece(a, it, lin, strip, t0, t1)) {
-      it += a.nwaves;
-      if (it < a.nitems) lin = tb_span(a, it).lin;
-      continue;
-    }
-    lin += (int32_t)(t1 - t0);
-    const int64_t c0 = strip * S::U - S::KA;
-    const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
-                   (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
-    switch (ek) {
-      case 0: march_pair<K, 0, RING, AR>(src, dst, a, r, strip, t0, t1, lane, role, ring[pr], ctr[pr], qbase); break;
-      case 1: march_pair<K, 1, RING, AR>(src, dst, a, r, strip, t0, t1, lane, role, ring[pr], ctr[pr], qbase); break;
-      case 2: march_pair<K, 2, RING, AR>(src, dst, a, r, strip, t0, t1, lane, role, ring[pr], ctr[pr], qbase); break;
-      default: march_pair<K, 3, RING, AR>(src, dst, a, r, strip, t0, t1, lane, role, ring[pr], ctr[pr], qbase); break;
-    }
-    qbase += (uint32_t)(t1 - t0 + 2 * KB);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent multi-cycle launch (small grids / short cycles).
-//
-// One dispatch runs `ncycles` cycles of depth K over the whole slab: exactly
-// one wave per work item (all resident: the grid is sized to the occupancy),
-// each wave marching ITS item in every cycle. Between cycles there is no
-// kernel boundary — no dispatch ramp, no drain into an empty queue, no
-// inter-launch gap (~11 + 8-10 us of a ~61 us 4096^2 fp32 cycle,
-// profiles/small_grid/) — and no grid barrier either: an item of cycle c waits
-// only for the items whose cycle-(c-1) output it reads (the K rows above and
-// below it in its strip and the two neighbour strips: read-after-write on the
-// source), which are also the only items that read the rows its cycle
-// overwrites (write-after-read on the destination). A wavefront through the
-// grid, synchronised by one completion counter per item (epoch-based: it holds
-// base + cycles completed).
-//
-// Coherence across the 8 XCDs (separate, mutually non-coherent L2s) without
-// cache maintenance: the field loads / stores of this kernel carry device
-// scope (march CP = 1: sc1 loads, nt sc1 stores), so a row a wave stored is at
-// the memory side once its vmcnt drains, and a row a wave loads comes from
-// there. Whole-L2 maintenance (buffer_wbl2 / buffer_inv per wave or per XCD,
-// the usual release / acquire) measured 3x slower (profiles/r3/persist_v1/).
-// A wait longer than timeout_ticks of the wall clock (a wave that never became
-// resident) sets *err and the wave returns: the launch fails loudly instead of
-// hanging the GPU.
-struct PersistArgs {
-  uint32_t* done;          // per item
-  uint32_t base;           // value every item's counter holds at launch
-  int32_t ncycles;
-  int32_t alternate;       // 1: cycle c reads buf[c & 1], writes buf[(c + 1) & 1]; 0: buf0 -> buf1 each cycle (trials)
-  int32_t pad;
-  uint64_t timeout_ticks;  // wall_clock64 ticks
-  unsigned int* err;       // host-visible error word (1: a dependency wait timed out)
-};
-
-// Item of rect R holding strip-local row `row` of strip-local strip `sl`.
-__device__ __forceinline__ int64_t item_of(const TbRectArg& R, int64_t sl, int64_t row) {
-  const int64_t rows = R.r1 - R.r0, ns = R.s1 - R.s0;
-  if (R.nb > 0) return R.item0 + ((row + 1) * R.nb - 1) / rows * ns + sl;  // band-major (tb_span)
-  const int64_t total = ns * rows, nseg = -R.nb, lin = sl * rows + row;
-  return R.item0 + ((lin + 1) * nseg - 1) / total;
-}
-
-__device__ __forceinline__ bool wait_item(const PersistArgs& p, int64_t j, uint32_t target, uint64_t t_start) {
-  while ((int32_t)(__hip_atomic_load(&p.done[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-    if (wall_clock64() - t_start > p.timeout_ticks) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return true;
-}
-
-// Wait until every item whose cycle-(c-1) output the piece (strip, rows
-// [t0, t1)) reads — rows [t0 - K, t1 + K) of strips strip - 1 .. strip + 1 —
-// has counter >= target. The rects of a launch tile the slab without overlap
-// (a single-launch plan, or its frame-weighted rects: stencil_tb.hip
-// weighted_main), so those items are found rect by rect.
-template <int K>
-__device__ bool wait_piece(const TbArgs& a, const PersistArgs& p, int64_t self, int64_t strip, int64_t t0, int64_t t1,
-                           uint32_t target, uint64_t t_start) {
-#pragma unroll
-  for (int i = 0; i < kMaxRects; ++i) {
-    if (i >= a.nrect) continue;
-    const TbRectArg R = a.rect[i];  // constant index (see tb_span)
-    const int64_t rows = R.r1 - R.r0;
-    const int64_t lo = max(t0 - K, R.r0) - R.r0, hi = min(t1 + K, R.r1) - R.r0;  // rect-local rows [lo, hi)
-    if (lo >= hi) continue;
-    for (int64_t s = max(strip - 1, R.s0); s <= min(strip + 1, R.s1 - 1); ++s) {
-      const int64_t sl = s - R.s0;
-      if (R.nb > 0) {
-        const int64_t ns = R.s1 - R.s0;
-        const int64_t b0 = ((lo + 1) * R.nb - 1) / rows, b1 = (hi * R.nb - 1) / rows;
-        for (int64_t b = b0; b <= b1; ++b) {
-          const int64_t j = R.item0 + b * ns + sl;
-          if (j != self && !wait_item(p, j, target, t_start)) return false;
-        }
-      } else {
-        for (int64_t j = item_of(R, sl, lo); j <= item_of(R, sl, hi - 1); ++j)
-          if (j != self && !wait_item(p, j, target, t_start)) return false;
-      }
-    }
-  }
-  return true;
-}
-
-template <typename T, int NV, int K, int RING, int AR>
-__global__ __launch_bounds__(256) void tb_persist_kernel(T* __restrict__ b0, T* __restrict__ b1, TbArgs a, T r,
-                                                         PersistArgs p) {
-  using S = TbShape<T, NV, K>;
-  const int lane = threadIdx.x & 63;
-  const int64_t it = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  if (it >= a.nitems) return;  // one item per wave, for every cycle
-  for (int32_t c = 0; c < p.ncycles; ++c) {
-    const bool odd = p.alternate && (c & 1);
-    const T* src = odd ? b1 : b0;
-    T* dst = odd ? b0 : b1;
-    int64_t strip, t0, t1;
-    if (c > 0) {
-      const uint32_t target = p.base + (uint32_t)c;
-      const uint64_t t_start = wall_clock64();  // this cycle's waits
-      int32_t lin = tb_span(a, it).lin;
-      bool ok = true;
-      while (ok && tb_piece(a, it, lin, strip, t0, t1)) {
-        lin += (int32_t)(t1 - t0);
-        ok = wait_piece<K>(a, p, it, strip, t0, t1, target, t_start);
-      }
-      if (!ok) {
-        if (lane == 0) __hip_atomic_store(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return;
-      }
-      asm volatile("buffer_inv sc0" ::: "memory");  // nothing of this CU's L1 survives into the next reads
-    }
-    int32_t lin = tb_span(a, it).lin;
-    while (tb_piece(a, it, lin, strip, t0, t1)) {
-      lin += (int32_t)(t1 - t0);
-      const int64_t c0 = strip * S::U - S::KA;
-      const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
-                     (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
-      switch (ek) {
-        case 0: march<T, NV, K, 0, RING, AR, false, false, 0, 1>(src, dst, a, r, strip, t0, t1, lane); break;
-        case 1: march<T, NV, K, 1, RING, AR, false, false, 0, 1>(src, dst, a, r, strip, t0, t1, lane); break;
-        case 2: march<T, NV, K, 2, RING, AR, false, false, 0, 1>(src, dst, a, r, strip, t0, t1, lane); break;
-        default: march<T, NV, K, 3, RING, AR, false, false, 0, 1>(src, dst, a, r, strip, t0, t1, lane); break;
-      }
-    }
-    // this item's rows are at the device-coherent level once the stores drain
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(&p.done[it], p.base + (uint32_t)c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-template <typename T, int K, int RING, int AR>
-int persist_blocks_per_cu() {
-  static std::mutex mu;
-  static std::map<int, int> cache;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> g(mu);
-  auto it = cache.find(dev);
-  if (it != cache.end()) return it->second;
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&tb_persist_kernel<T, 1, K, RING, AR>),
-                                                   256, 0) != hipSuccess || nb <= 0)
-    nb = 1;
-  cache[dev] = nb;
-  return nb;
-}
-
-// A plain launch on the caller's stream: a cooperative launch guarantees
-// co-residency too, but went through a separate hardware queue with ~1 ms of
-// launch latency per dispatch (rocprofv3 trace, profiles/r3/persist_v2/); the
-// host sizes the grid to the occupancy instead, and the kernel's wait timeout
-// turns a non-resident wave into an error, not a hang.
-template <typename T, int K, int RING, int AR>
-hipError_t persist_launch(unsigned nblocks, T* b0, T* b1, const TbArgs& a, T r, const PersistArgs& p, hipStream_t s) {
-  hipLaunchKernelGGL((tb_persist_kernel<T, 1, K, RING, AR>), dim3(nblocks), dim3(256), 0, s, b0, b1, a, r, p);
-  return hipGetLastError();
-}
-
-// Per-(T, RING, AR) entry points, instantiated in tb_<dtype>_r<RING>_persist[_fma].hip.
-template <typename T, int RING, int AR>
-hipError_t dispatch_persist(int k, unsigned nblocks, T* b0, T* b1, const TbArgs& a, T r, const PersistArgs& p,
-                            hipStream_t s);
-template <typename T, int RING, int AR>
-int occupancy_persist(int k);
-#define H2D_PS_CASE(T, RING, MAIN, AR, KK) \
-  case KK:                                 \
-    return persist_launch<T, KK, RING, AR>(nblocks, b0, b1, a, r, p, s);
-#define H2D_PS_OCC_CASE(T, RING, MAIN, AR, KK) \
-  case KK:                                     \
-    return persist_blocks_per_cu<T, KK, RING, AR>();
-#define H2D_PS_UNIT(T, RING, AR, DEEP)                                                                              \
-  template <>                                                                                                        \
-  hipError_t dispatch_persist<T, RING, AR>(int k, unsigned nblocks, T* b0, T* b1, const TbArgs& a, T r,              \
-                                           const PersistArgs& p, hipStream_t s) {                                    \
-    switch (k) {                                                                                                     \
-      H2D_TB_CASES(H2D_PS_CASE, T, RING, false, AR)                                                                  \
-      DEEP(H2D_PS_CASE, T, RING, false, AR)                                                                          \
-      default:                                                                                                       \
-        break;                                                                                                       \
-    }                                                                                                                \
-    HEAT2D_REQUIRE(false, "temporal depth not instantiated for the persistent kernel");                              \
-    return hipErrorInvalidValue;                                                                                     \
-  }                                                                                                                  \
-  template <>                                                                                                        \
-  int occupancy_persist<T, RING, AR>(int k) {                                                                        \
-    switch (k) {                                                                                                     \
-      H2D_TB_CASES(H2D_PS_OCC_CASE, T, RING, false, AR)                                                              \
-      DEEP(H2D_PS_OCC_CASE, T, RING, false, AR)                                                                      \
-      default:                                                                                                       \
-        break;                                                                                                       \
-    }                                                                                                                \
-    return 1;                                                                                                        \
-  }
-
 template <typename T, int NV, int K, int RING, bool MAIN, int AR, int VAR = kVarPlain>
 constexpr auto kernel_ptr() {
   return &tb_kernel<T, NV, K, RING, MAIN, AR, VAR>;
@@ -1619,61 +1236,6 @@ int occupancy_blocks_stats(int k);
         break;                                                                                             \
     }                                                                                                      \
     return 1;                                                                                              \
-  }
-// wave-pair kernels (fp32, K = 2..16): tb_f32_r<RING>_pair[_fma|_jac].hip
-template <int RING, int AR>
-void dispatch_pair(int k, unsigned nblocks, const float* src, float* dst, const TbArgs& a, float r, hipStream_t s);
-template <int RING, int AR>
-int occupancy_pair(int k);  // resident 256-thread blocks (2 pairs each) per CU
-template <int K, int RING, int AR>
-int pair_blocks_per_cu() {
-  static std::mutex mu;
-  static std::map<int, int> cache;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> g(mu);
-  auto it = cache.find(dev);
-  if (it != cache.end()) return it->second;
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&tb_pair_kernel<K, RING, AR>), 256,
-                                                   0) != hipSuccess ||
-      nb <= 0)
-    nb = 1;
-  cache[dev] = nb;
-  return nb;
-}
-#define H2D_PR_CASE(T, RING, MAIN, AR, KK)                                                              \
-  case KK:                                                                                              \
-    hipLaunchKernelGGL((tb_pair_kernel<KK, RING, AR>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
-    return;
-#define H2D_PR_OCC_CASE(T, RING, MAIN, AR, KK) \
-  case KK:                                     \
-    return pair_blocks_per_cu<KK, RING, AR>();
-// K = 2..16 (a pair splits the levels)
-#define H2D_TB_CASES_PAIR(M, T, RING, MAIN, AR)                                                         \
-  M(T, RING, MAIN, AR, 2) M(T, RING, MAIN, AR, 3) M(T, RING, MAIN, AR, 4) M(T, RING, MAIN, AR, 5)       \
-  M(T, RING, MAIN, AR, 6) M(T, RING, MAIN, AR, 7) M(T, RING, MAIN, AR, 8) M(T, RING, MAIN, AR, 9)       \
-  M(T, RING, MAIN, AR, 10) M(T, RING, MAIN, AR, 11) M(T, RING, MAIN, AR, 12) M(T, RING, MAIN, AR, 13)   \
-  M(T, RING, MAIN, AR, 14) M(T, RING, MAIN, AR, 15) M(T, RING, MAIN, AR, 16)
-#define H2D_PR_UNIT(RING, AR)                                                                                  \
-  template <>                                                                                                  \
-  void dispatch_pair<RING, AR>(int k, unsigned nblocks, const float* src, float* dst, const TbArgs& a, float r, \
-                               hipStream_t s) {                                                                \
-    switch (k) {                                                                                               \
-      H2D_TB_CASES_PAIR(H2D_PR_CASE, float, RING, false, AR)                                                        \
-      default:                                                                                                 \
-        break;                                                                                                 \
-    }                                                                                                          \
-    HEAT2D_REQUIRE(false, "temporal depth not instantiated for the wave-pair kernel (K = 2..16)");             \
-  }                                                                                                            \
-  template <>                                                                                                  \
-  int occupancy_pair<RING, AR>(int k) {                                                                        \
-    switch (k) {                                                                                               \
-      H2D_TB_CASES_PAIR(H2D_PR_OCC_CASE, float, RING, false, AR)                                                    \
-      default:                                                                                                 \
-        break;                                                                                                 \
-    }                                                                                                          \
-    return 1;                                                                                                  \
   }
 #define H2D_TB_UNIT(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_NO_CASES)
 #define H2D_TB_UNIT_F64(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_DEEP)

@@ -33,7 +33,7 @@ std::string default_path() {
   if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) base = x;
   else if (const char* h = std::getenv("HOME"); h && *h) base = std::string(h) + "/.cache";
   else return "";
-  return base + "/heat2d/plans-v2.txt";
+  return base + "/heat2d/plans-v3.txt";
 }
 
 void mkdirs(const std::string& file) {
@@ -46,6 +46,9 @@ void load() {
   if (g_loaded) return;
   g_loaded = true;
   g_path = default_path();
+  // a build without a source hash (HEAT2D_BUILD_ID unset: "dev") cannot tell
+  // plans of older sources from its own: no cache
+  if (std::string(HEAT2D_BUILD_ID) == "dev") g_path = "off";
   if (g_path.empty() || g_path == "off") return;
   std::ifstream f(g_path);
   std::string line;
@@ -139,8 +142,8 @@ bool get_plan(const std::string& ctx, int k, int64_t band, kern::SplitPlan* p, f
   in >> sig >> pr;
   q.nfused = (int32_t)nf;
   q.sig_items = sig;
-  q.pair = (int32_t)pr;
-  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > kern::kMaxFused || q.pair < 0 || q.pair > 3) return false;
+  q.flags = (int32_t)pr;
+  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > kern::kMaxFused || q.flags < 0 || q.flags > kern::kPlanDynamic) return false;
   *p = q;
   *ms = t;
   return true;
@@ -155,7 +158,7 @@ void put_plan(const std::string& ctx, int k, int64_t band, const kern::SplitPlan
   o << ' ' << p.main_waves << ' ' << p.edge_waves << ' ' << p.main_items << ' ' << p.edge_items << ' ' << ms;
   o << ' ' << p.nfused;
   for (const auto& e : p.fused) rect(e);
-  o << ' ' << p.sig_items << ' ' << p.pair;
+  o << ' ' << p.sig_items << ' ' << p.flags;
   store(plan_key(ctx, k, band), o.str());
 }
 

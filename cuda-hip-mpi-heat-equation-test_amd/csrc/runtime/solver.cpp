@@ -65,6 +65,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
   HEAT2D_REQUIRE(cfg_.n_rows >= 1 && cfg_.n_cols >= 1, "empty grid");
   HEAT2D_REQUIRE(cfg_.dtype == 0 || cfg_.dtype == 1, "dtype must be 0 (fp32) or 1 (fp64)");
   hip_ = cfg_.backend == (int32_t)Backend::Hip;
+  std::fill(plan_origin_, plan_origin_ + kMaxTB + 1, -1);
   const int P = tr_->size(), rank = tr_->rank();
   HEAT2D_REQUIRE(cfg_.n_rows >= P, "fewer rows than ranks");
 
@@ -175,7 +176,6 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     cfg_.use_graph = 0;
   }
   tr_->attach(buf_[0], buf_[1], L_, dtype());
-  if (const char* e = std::getenv("HEAT2D_PERSIST")) persist_mode_ = std::atoi(e) != 0 ? 1 : 0;
 }
 
 Solver::~Solver() {
@@ -189,7 +189,6 @@ Solver::~Solver() {
       if (b) (void)hipFree(b);
     if (d_work_) (void)hipFree(d_work_);
     if (d_part_) (void)hipFree(d_part_);
-    if (d_done_) (void)hipFree(d_done_);
     if (d_sig_) (void)hipFree(d_sig_);
     if (d_queue_) (void)hipFree(d_queue_);
     if (h_err_) (void)hipHostFree(h_err_);
@@ -445,8 +444,14 @@ const kern::SplitPlan& Solver::split_plan(int k) {
     p = kern::plan_split(dtype(), L_, k, k, compute_cus_, spare, 0, 0, cfg_.arith);
     p.k = k;
     ++plans_made_;
-    if (p.valid && autotune_slabs(cfg_.n_rows, cfg_.n_cols, tr_->size(), cfg_.autotune) && !cached_split(k))
-      autotune_split(k);
+    plan_origin_[k] = 0;
+    if (p.valid && autotune_slabs(cfg_.n_rows, cfg_.n_cols, tr_->size(), cfg_.autotune)) {
+      if (cached_split(k)) plan_origin_[k] = 2;
+      else {
+        autotune_split(k);
+        plan_origin_[k] = 1;
+      }
+    }
     // HEAT2D_SPLIT_ORDER=edge-first | concurrent overrides the split's ordering (tests, A/B);
     // HEAT2D_SPLIT_ORDER=single forces one general launch per cycle (no exchange only)
     if (const char* env = std::getenv("HEAT2D_SPLIT_ORDER")) {
@@ -485,12 +490,7 @@ const kern::SplitPlan& Solver::split_plan(int k) {
       p.main_waves = std::min<int64_t>(p.main_waves, std::atoll(e));
     // HEAT2D_DYNAMIC=1: the main launch takes its items from the dynamic queue (tests, A/B)
     if (const char* e = std::getenv("HEAT2D_DYNAMIC"); e && std::atoi(e) == 1 && p.valid >= 1 && p.valid <= 3)
-      p.pair |= 2;
-    // HEAT2D_PAIR=1: a single-launch plan runs as the wave-pair kernel (tests, A/B)
-    if (const char* e = std::getenv("HEAT2D_PAIR"); e && std::atoi(e) == 1 && p.valid == 2 && !(p.pair & 1)) {
-      const kern::SplitPlan q = kern::pair_plan(dtype(), p, cfg_.arith);
-      if (q.valid) p = q;
-    }
+      p.flags |= kern::kPlanDynamic;
   }
   return p;
 }
@@ -544,11 +544,6 @@ static int device_cus_of(int device) {
   return ncu;
 }
 
-// Wave-pair candidates (HEAT2D_PAIR=2; =1 forces the pair kernel on a
-// single-launch plan). Off by default: once the march's scalar address work
-// was cut (31 -> 12.5 SALU per row) the pair ran 3.5 % behind one wave per
-// item on 4096^2 fp32 K = 16 (58.4 vs 56.4 us per cycle, profiles/r3/salu/):
-// its LDS hand-off and ring waits cost what the second wave hides.
 // Dynamic-queue candidates (HEAT2D_DYNAMIC=0 keeps them out of the autotuner;
 // =1 forces the queue on plans with more items than waves). With 2 waves per
 // SIMD the older wave issues first: on the headline's interior launch the
@@ -564,18 +559,22 @@ static bool dynamic_candidates() {
   return on;
 }
 
-static bool pair_candidates() {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_PAIR");
-    return e && std::atoi(e) == 2;
-  }();
-  return on;
-}
-
 static bool tune_segments() {
   static const bool on = [] {
     const char* e = std::getenv("HEAT2D_TUNE_SEGMENTS");
     return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+// Fused plans among the autotuner's candidates: opt-in (HEAT2D_FUSED=1). The
+// trials cannot see the exchange, and end to end the fused cycle measured
+// level with or behind the edge-first order on the rehearsed slabs
+// (profiles/r3/fused_v2/README.md); HEAT2D_SPLIT_ORDER=fused forces it.
+static bool fused_candidates() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_FUSED");
+    return e && std::atoi(e) != 0;
   }();
   return on;
 }
@@ -639,8 +638,29 @@ float Solver::time_plan(const kern::SplitPlan& c, int kTimed) {
   return ms / kTimed;
 }
 
+// The environment knobs that shape the autotuner's candidate set or the plans
+// it returns (a run with any of them set must neither reuse plans tuned without
+// it nor leave plans for runs without it): an FNV-1a hash of their values,
+// part of every cache key.
+static uint64_t plan_env_hash() {
+  static const uint64_t h = [] {
+    uint64_t v = 1469598103934665603ull;
+    for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_TUNE_SEGMENTS", "HEAT2D_FUSED", "HEAT2D_W_ROW", "HEAT2D_W_COL",
+                             "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
+                             "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES"}) {
+      const char* e = std::getenv(name);
+      const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
+      for (unsigned char c : kv) v = (v ^ c) * 1099511628211ull;
+    }
+    return v;
+  }();
+  return h;
+}
+
 // Plan-cache context of this slab: what a tuned plan's timing depends on
-// besides the depth (plan_cache.hpp).
+// besides the depth (plan_cache.hpp), including the transport (its name and
+// whether it gates: the fused candidates exist only for gating transports)
+// and the plan-shaping environment knobs.
 std::string Solver::cache_ctx() const {
   hipDeviceProp_t prop{};
   std::string arch = "unknown";
@@ -650,10 +670,11 @@ std::string Solver::cache_ctx() const {
     ncu = prop.multiProcessorCount;
   }
   const int pos = (L_.row0 == 0 ? 1 : 0) | (L_.row0 + L_.nrows == L_.nrows_global ? 2 : 0);
-  char b[512];
-  std::snprintf(b, sizeof(b), "%s|cu%d|%s|ar%d|%lldx%lld|p%lld|h%lld|pos%d|ccu%d|sp%d|x%d", arch.c_str(), ncu,
-                dtype_name(dtype()), cfg_.arith, (long long)L_.nrows, (long long)L_.ncols, (long long)L_.pitch,
-                (long long)L_.halo, pos, compute_cus_, spare_waves(), tr_->exchanges() ? 1 : 0);
+  char b[640];
+  std::snprintf(b, sizeof(b), "%s|cu%d|%s|ar%d|%lldx%lld|p%lld|h%lld|pos%d|ccu%d|sp%d|x%d|tr=%s|g%d|env%016llx",
+                arch.c_str(), ncu, dtype_name(dtype()), cfg_.arith, (long long)L_.nrows, (long long)L_.ncols,
+                (long long)L_.pitch, (long long)L_.halo, pos, compute_cus_, spare_waves(), tr_->exchanges() ? 1 : 0,
+                tr_->name().c_str(), tr_->gates() ? 1 : 0, (unsigned long long)plan_env_hash());
   return b;
 }
 
@@ -668,6 +689,12 @@ bool Solver::cached_split(int k) {
   const kern::SplitPlan fresh = kern::plan_split(dtype(), L_, k, k, compute_cus_, spare_waves(), c.ring,
                                                  c.main.nb, cfg_.arith);
   if (!c.valid || (c.valid != 2 && !fresh.valid) || c.main.r1 > L_.nrows || c.nedge > 4) return false;
+  // semantic checks on top of the key: a plan kind this run may not use
+  // (fused cycles need a gating transport and HEAT2D_FUSED; the dynamic queue
+  // is off under HEAT2D_DYNAMIC=0; a single launch cannot exchange)
+  if (c.valid == 4 && (!fused_ok() || !fused_candidates())) return false;
+  if ((c.flags & kern::kPlanDynamic) && !dynamic_candidates()) return false;
+  if (c.valid == 2 && tr_->exchanges()) return false;
   synchronize();
   const float t = time_plan(c, 4);
   H2D_HIP(hipEventRecord(ev_int_, s_compute_));
@@ -679,18 +706,6 @@ bool Solver::cached_split(int k) {
   tuned_ms_[k] = t;
   ++plan_cache_hits_;
   return true;
-}
-
-// Fused plans among the autotuner's candidates: opt-in (HEAT2D_FUSED=1). The
-// trials cannot see the exchange, and end to end the fused cycle measured
-// level with or behind the edge-first order on the rehearsed slabs
-// (profiles/r3/fused_v2/README.md); HEAT2D_SPLIT_ORDER=fused forces it.
-static bool fused_candidates() {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_FUSED");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
 }
 
 void Solver::autotune_split(int k) {
@@ -714,21 +729,14 @@ void Solver::autotune_split(int k) {
   // exchange of the bands running beside the interior (valid = 3)
   bool top = false, bot = false;
   sent_sides(&top, &bot);
-  // every candidate; a single launch (fp32) also as the wave-pair kernel
-  // (tb_pair_kernel: two waves per item, for grids whose items leave one
-  // wave per SIMD); HEAT2D_PAIR=0 skips those
   auto add = [&](const kern::SplitPlan& c) {
     timed.emplace_back(time_plan(c, 4), c);
-    if (c.valid == 2 && pair_candidates()) {
-      const kern::SplitPlan q = kern::pair_plan(dtype(), c, cfg_.arith);
-      if (q.valid) timed.emplace_back(time_plan(q, 4), q);
-    }
     // more items than waves: also with the dynamic item queue (faster waves
     // take more items; per-wave timelines of the 32768^2 fp64 interior showed
     // a bimodal spread of up to 25 % between equal items: profiles/r3/wt3/)
     if (dynamic_candidates() && c.main_items > c.main_waves && c.valid >= 1 && c.valid <= 3) {
       kern::SplitPlan d = c;
-      d.pair |= 2;
+      d.flags |= kern::kPlanDynamic;
       timed.emplace_back(time_plan(d, 4), d);
     }
   };
@@ -1049,10 +1057,6 @@ void Solver::step(int64_t n) {
   if (cfg_.copy_swap) {
     for (int64_t i = 0; i < n; ++i) cycle_copy_swap();
     steps_ += n;
-    return;
-  }
-  if (persistent(n)) {
-    run_persist(step_cycles(n), false);
     return;
   }
   const std::vector<CycleRun> runs = step_runs(n, cur_);
@@ -1452,30 +1456,6 @@ void Solver::prepare_plans(int64_t n) {
       cur_ ^= p;
     }
   }
-  if (persist_eligible() && !persist_.count(n)) {
-    // persistent launches vs the schedule's graph replay (or eager cycles):
-    // both timed as trial runs of the same cycles, the faster one kept
-    const std::vector<int> seq = step_cycles(n);
-    bool ok = !seq.empty();
-    for (int k : seq) ok = ok && persist_plan(k) != nullptr;
-    bool use = false;
-    if (ok && persist_mode_ == 1) {
-      use = true;
-    } else if (ok && schedule(n)) {
-      const float tp = time_persist(seq);
-      float tg;
-      if (schedule_graphs()) {
-        tg = time_trial_schedule(seq);
-      } else {
-        tg = 0.f;
-        for (int k : seq) tg += depth_ms(k);
-      }
-      // a clear win only: on MI355X the persistent kernel's cross-XCD hand-off
-      // costs about what a launch boundary does (profiles/r3/persist_v3/)
-      use = tp < 0.97f * tg;
-    }
-    persist_[n] = use;
-  }
   if (const std::vector<int>* s = schedule(n)) {
     for (size_t i = 0; i < s->size(); ++i)
       (void)split_plan_banded((*s)[i], std::max((*s)[i], exchange_depth(*s, i, (*s)[0])));
@@ -1533,105 +1513,12 @@ void Solver::ensure_sig() {
   gate_timeout_ticks_ = (uint64_t)((to > 0 ? to * 1.5 + 5.0 : 3600.0) * 1e3 * (double)khz);
 }
 
-bool Solver::persist_eligible() const {
-  return hip_ && !jit_ && !cfg_.copy_swap && !tr_->exchanges() && persist_mode_ != 0;
-}
-
-// Single-launch plan of depth k for the persistent kernel: the autotuned one
-// when the autotuner chose a single launch, else plan_single's default, cut
-// to at most the co-resident waves.
-const kern::SplitPlan* Solver::persist_plan(int k) {
-  kern::SplitPlan& p = persist_plans_[k];
-  if (p.k != k) {
-    const kern::SplitPlan& t = split_plan(k);
-    kern::SplitPlan c = t.valid == 2 ? t : kern::plan_single(dtype(), L_, k, 0, 0, 0, cfg_.arith);
-    if (c.pair) {  // one wave per item here
-      c.pair = 0;
-      c.main_waves = c.main_items;
-    }
-    if (c.ring > 6) c = kern::plan_single(dtype(), L_, k, 0, 6, c.main.nb, cfg_.arith);  // rings 4 / 6 only
-    const int64_t cap = kern::persist_capacity(dtype(), c.ring, k, cfg_.arith);
-    if (c.main_items > cap) c = kern::plan_single(dtype(), L_, k, 0, c.ring, -cap, cfg_.arith);
-    if (!c.valid || c.main_items > cap || c.main_items < 1) c.valid = 0;
-    c.k = k;
-    p = c;
-  }
-  return p.valid == 2 ? &p : nullptr;
-}
-
-void Solver::ensure_persist_ctl() {
-  if (d_done_) return;
-  int ncu = 0;
-  H2D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg_.device));
-  done_cap_ = (int64_t)ncu * 32;  // per-item counters: 8 workgroups of 4 waves per CU at most
-  H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_done_), (size_t)done_cap_ * sizeof(uint32_t)));
-  H2D_HIP(hipMemsetAsync(d_done_, 0, (size_t)done_cap_ * sizeof(uint32_t), s_compute_));
-  done_base_ = 0;
-  ensure_err();
-  int khz = 0;
-  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg_.device) != hipSuccess || khz <= 0) khz = 100000;
-  persist_timeout_ticks_ = (uint64_t)khz * 2000;  // 2 s: a healthy wait lasts about one cycle
-}
-
-// seq's cycles as one persistent launch per run of equal depths. trial: every
-// cycle reads the current buffer and writes the other (timing; the solution
-// and the step / histogram counters are untouched).
-void Solver::run_persist(const std::vector<int>& seq, bool trial) {
-  ensure_persist_ctl();
-  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
-  H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
-  for (size_t i = 0; i < seq.size();) {
-    size_t j = i;
-    while (j < seq.size() && seq[j] == seq[i]) ++j;
-    const int k = seq[i];
-    const int nc = (int)(j - i);
-    const kern::SplitPlan* p = persist_plan(k);
-    HEAT2D_REQUIRE(p != nullptr, "persistent launch: no co-resident plan for this depth");
-    kern::PersistCtl ctl{d_done_, done_cap_, done_base_, persist_timeout_ticks_, h_err_};
-    kern::launch_tb_persist(dtype(), buf_[cur_], buf_[cur_ ^ 1], L_, *p, cfg_.r, ctl, nc, trial ? 0 : 1, s_compute_,
-                            cfg_.arith);
-    done_base_ += (uint32_t)nc;
-    if (trial) {
-      last_k_ = 0;  // the other buffer was overwritten
-    } else {
-      if (nc & 1) cur_ ^= 1;
-      steps_ += (int64_t)k * nc;
-      hist_[k] += nc;
-      last_k_ = k;
-    }
-    i = j;
-  }
-  // later eager cycles order against the launches' end
-  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-  H2D_HIP(hipEventRecord(ev_bnd_, s_compute_));
-  H2D_HIP(hipEventRecord(ev_comm_, s_compute_));
-  H2D_HIP(hipStreamWaitEvent(s_comm_, ev_comm_, 0));
-}
-
-float Solver::time_persist(const std::vector<int>& seq) {
-  synchronize();
-  run_persist(seq, true);  // warm (clocks, code objects)
-  if (!ev_t0_) {
-    H2D_HIP(hipEventCreate(&ev_t0_));
-    H2D_HIP(hipEventCreate(&ev_t1_));
-  }
-  H2D_HIP(hipEventRecord(ev_t0_, s_compute_));
-  run_persist(seq, true);
-  H2D_HIP(hipEventRecord(ev_t1_, s_compute_));
-  synchronize();
-  float ms = 0.f;
-  H2D_HIP(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));
-  return ms;
-}
-
 void Solver::synchronize() {
   if (!hip_) return;
   H2D_HIP(hipSetDevice(cfg_.device));
   if (!tr_->exchanges()) {
     H2D_HIP(hipStreamSynchronize(s_compute_));
     if (s_comm_ != s_compute_) H2D_HIP(hipStreamSynchronize(s_comm_));
-    if (h_err_ && __atomic_load_n(h_err_, __ATOMIC_ACQUIRE) != 0)
-      fail(__FILE__, __LINE__, "persistent launch: a wave timed out waiting for its neighbours (not co-resident?)");
     tr_->check();
     return;
   }

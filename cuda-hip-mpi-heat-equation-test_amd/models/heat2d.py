@@ -40,12 +40,16 @@ def resolve_backend(backend: str) -> str:
     return backend
 
 
+PLAN_ORIGINS = {-1: "none", 0: "planned", 1: "tuned", 2: "cache"}
+
+
 def _plan(h, k: int) -> dict:
-    p, ms = N.SplitPlan(), C.c_float()
+    p, ms, org = N.SplitPlan(), C.c_float(), C.c_int32()
     N.call("heat2d_solver_plan", h, int(k), C.byref(p), C.byref(ms))
+    N.call("heat2d_solver_plan_origin", h, int(k), C.byref(org))
     return {"k": p.k, "ring": p.ring, "valid": p.valid,
             "order": {1: "concurrent", 2: "single", 3: "edge-first", 4: "fused"}.get(p.valid, "serial"),
-            "pair": int(p.pair & 1), "dynamic": int((p.pair >> 1) & 1),
+            "dynamic": int((p.flags >> 1) & 1), "origin": PLAN_ORIGINS.get(org.value, "?"),
             "main_bands": p.main.nb, "main_items": p.main_items, "main_waves": p.main_waves,
             "edge_items": p.edge_items, "edge_waves": p.edge_waves, "tuned_ms": ms.value,
             "main_rect": [p.main.r0, p.main.r1, p.main.s0, p.main.s1, p.main.nb],
@@ -238,14 +242,6 @@ class HeatSolver:
         v = C.c_int64()
         N.call("heat2d_solver_halo_rows", self._h, int(bool(reset)), C.byref(v))
         return v.value
-
-    def persistent(self, n: int) -> bool:
-        """True if prepare(n) chose persistent multi-cycle launches for step(n)
-        (one cooperative dispatch per run of equal depths, items synchronised by
-        neighbour completion counters: kern::launch_tb_persist)."""
-        v = C.c_int32()
-        N.call("heat2d_solver_persistent", self._h, int(n), C.byref(v))
-        return bool(v.value)
 
     @property
     def plan_cache_hits(self) -> int:

@@ -93,7 +93,7 @@ class SplitPlan(C.Structure):
         ("k", C.c_int32), ("ring", C.c_int32), ("valid", C.c_int32), ("nedge", C.c_int32),
         ("main", Rect), ("edge", Rect * 4),
         ("main_waves", C.c_int64), ("edge_waves", C.c_int64), ("main_items", C.c_int64), ("edge_items", C.c_int64),
-        ("nfused", C.c_int32), ("pair", C.c_int32), ("fused", Rect * 6), ("sig_items", C.c_int64),
+        ("nfused", C.c_int32), ("flags", C.c_int32), ("fused", Rect * 6), ("sig_items", C.c_int64),
     ]
 
 
@@ -195,7 +195,7 @@ _SIGS = {
     "heat2d_autotune_slabs": (C.c_int, [_I64, _I64, C.c_int, C.c_int, C.POINTER(C.c_int32)]),
     "heat2d_solver_plan_cache_hits": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "heat2d_plan_cache_path": (C.c_int, [C.c_char_p, _I64]),
-    "heat2d_solver_persistent": (C.c_int, [_P, _I64, C.POINTER(C.c_int32)]),
+    "heat2d_solver_plan_origin": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int32)]),
 }
 
 _lib = None

@@ -134,13 +134,14 @@ def test_bench_plan_cache_second_run(tmp_path):
     plans and measured schedule from the cache (each re-validated by one short
     re-time) — prepare() under a second, the same throughput."""
     env_cache = str(tmp_path / "plans.txt")
+    old = os.environ.get("HEAT2D_PLAN_CACHE")
     os.environ["HEAT2D_PLAN_CACHE"] = env_cache
     try:
         args = ["--gpus", "1", "--grid", "8192", "--steps", "20", "--warmup", "5"]
         first = run_plain(*args)
         second = run_plain(*args)
     finally:
-        os.environ.pop("HEAT2D_PLAN_CACHE", None)
+        os.environ["HEAT2D_PLAN_CACHE"] = old if old is not None else "off"
     assert first["config"]["plan_cache"]["path"] == env_cache and os.path.getsize(env_cache) > 0
     assert first["config"]["plan_cache"]["hits"] == 0 and second["config"]["plan_cache"]["hits"] >= 2
     assert second["config"]["prepare_s"] < 1.0, second["config"]

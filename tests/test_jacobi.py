@@ -11,7 +11,7 @@ Oracles:
   * the reference rounding itself, bitwise, where every sum - 4c is exact
     (Sterbenz: the reference IC, values in [1, 2]) — the bench configuration.
 GPU cases cover every edge kind, the split schedule + autotuner, the fused
-statistics, the persistent launch, the hipRTC engine and multi-rank slabs."""
+statistics, the hipRTC engine and multi-rank slabs."""
 import numpy as np
 import pytest
 
@@ -149,22 +149,6 @@ def test_hip_jacobi_step_stats(gpu, native, dtype, tb):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype,tb,n,steps", [("fp64", 8, 301, 37), ("fp32", 16, 515, 45)])
-def test_hip_jacobi_persistent(gpu, native, monkeypatch, dtype, tb, n, steps):
-    monkeypatch.setenv("HEAT2D_PERSIST", "1")
-    p = prob(n, steps)
-    npdt = np.float64 if dtype == "fp64" else np.float32
-    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0, arith="jacobi")
-    s.upload(R.owned(R.initial_field(p, npdt)))
-    s.prepare(steps)
-    assert s.persistent(steps)
-    s.step(steps)
-    got = s.download()
-    s.close()
-    assert np.array_equal(got, golden(p, npdt))
-
-
-@pytest.mark.gpu
 def test_hip_jacobi_jit_and_ranks(gpu, native):
     """hipRTC engine and a 3-rank loopback group == the temporal-blocked engine."""
     p = prob(257, 9)
@@ -207,31 +191,6 @@ def test_hip_jacobi_single_launch_frame_rects(gpu, native, monkeypatch, dtype, t
     assert top[0] == 0 and top[4] == 1 and bot[1] == p.n_owned and bot[4] == 1, pl
     assert top[1] - top[0] >= tb and bot[1] - bot[0] >= tb
     assert np.array_equal(got, golden(p, npdt, T0))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("arith", ["jacobi", "fma", "exact"])
-@pytest.mark.parametrize("tb,env", [(16, {"HEAT2D_SEGMENTS": "30"}), (15, {"HEAT2D_BANDS": "4"}), (2, {}),
-                                    (3, {"HEAT2D_SEGMENTS": "7"}), (8, {"HEAT2D_SEGMENTS": "600"})])
-def test_hip_pair_kernel(gpu, native, monkeypatch, arith, tb, env):
-    """Wave-pair kernel (tb_pair_kernel: two waves per item, the levels split
-    between a producer and a consumer through an LDS row ring): every edge
-    kind, segments crossing strip ends (7 / 600 segments), several items per
-    pair (600 > co-resident pairs is not needed: grid stride), bitwise."""
-    monkeypatch.setenv("HEAT2D_SPLIT_ORDER", "single")
-    monkeypatch.setenv("HEAT2D_PAIR", "1")
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    p = prob(1100, 2 * tb + 3)
-    T0 = rough(p, np.float32)
-    s = HeatSolver(p, dtype="fp32", backend="hip", tb=tb, device=0, autotune=0, arith=arith)
-    s.upload(T0)
-    s.step(p.ntime)
-    got = s.download()
-    pl = s.plan(tb)
-    s.close()
-    assert pl["order"] == "single" and pl["pair"] == 1, pl
-    assert np.array_equal(got, golden(p, np.float32, T0, arith=arith))
 
 
 @pytest.mark.gpu

@@ -54,13 +54,13 @@ def sq(d):
     acc = defaultdict(float)
     n = 0
     for r in rows(d, "counter_collection"):
-        if "tb_kernel" in r["Kernel_Name"] or "tb_pair_kernel" in r["Kernel_Name"]:
+        if "tb_kernel" in r["Kernel_Name"]:
             acc[r["Counter_Name"]] += float(r["Counter_Value"])
             n += 1
     wc = acc["SQ_WAVE_CYCLES"] or 1
     # dispatches / mean duration of the same run's tb_kernel dispatches (kernel
     # trace beside the counters): GRBM_GUI_ACTIVE per dispatch / duration = clock
-    ks = [r for r in rows(d, "kernel_trace") if "tb_kernel" in r["Kernel_Name"] or "tb_pair_kernel" in r["Kernel_Name"]]
+    ks = [r for r in rows(d, "kernel_trace") if "tb_kernel" in r["Kernel_Name"]]
     dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in ks]
     extra = {}
     if dur and acc.get("GRBM_GUI_ACTIVE"):

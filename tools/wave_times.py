@@ -60,7 +60,7 @@ slot = {int(x): round(float(dur[wid % 4 == x].mean()), 2) for x in range(4)}
 n8 = max(1, len(w) // 8)
 order = [round(float(dur[(wid >= i * n8) & (wid < (i + 1) * n8)].mean()), 2) for i in range(8)]
 q = np.percentile(end, [50, 90, 99, 100])
-print(json.dumps({"dtype": dtype, "n": n, "k": k, "waves": int(len(w)), "plan": {kk: pl[kk] for kk in ("order", "pair", "ring", "main_bands", "main_items")},
+print(json.dumps({"dtype": dtype, "n": n, "k": k, "waves": int(len(w)), "plan": {kk: pl[kk] for kk in ("order", "dynamic", "ring", "main_bands", "main_items")},
                   "span_us": round(float(end.max()), 2), "start_spread_us": round(float(start.max()), 2),
                   "start_p90_us": round(float(np.percentile(start, 90)), 2),
                   "dur_mean_us": round(float(dur.mean()), 2), "dur_max_us": round(float(dur.max()), 2),
