@@ -125,6 +125,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=48)
     ap.add_argument("--n", "--grid", dest="n", type=int, default=32768,
                     help="grid edge (use --grid under torchrun: its parser takes --n as an abbreviation)")
+    ap.add_argument("--sigma", type=float, default=0.25,
+                    help="input.dat sigma (= r, the FTCS coefficient); the reference's inputs all use 0.25")
     ap.add_argument("--weak", action="store_true",
                     help="weak scaling: --n is the 1-GPU grid edge; the global square grid grows to n*sqrt(N) so "
                          "every rank keeps ~n^2 points (e.g. --dtype fp32 --n 173056: the full-HBM 240 GB per GPU)")
@@ -133,16 +135,16 @@ def main():
                     help="largest time-step depth fused per HBM pass (0: every depth the kernels have, fp64 24 / "
                          "fp32 20; prepare() picks the cycle schedule of the timed steps by measurement)")
     ap.add_argument("--tile-rows", type=int, default=0)
-    ap.add_argument("--arith", default="bench", choices=["bench", "auto", "exact", "fma", "jacobi"],
+    ap.add_argument("--arith", default="bench", choices=["bench", "auto", "exact", "fma", "jacobi", "fast"],
                     help="fma: contracted update (one op fewer per point); exact: every op rounded; auto: fma when "
                          "bitwise identical to exact (r a power of two, as here), else exact; jacobi: r == 1/4 "
                          "only, r * (S + E + N + W) (3 adds per point; bitwise == exact on this benchmark's IC); "
-                         "bench (default): jacobi when r == 1/4, else auto")
+                         "fast: any r, levels carried as T / r^level (3 adds + 1 fma per point, within a stated "
+                         "error bound of exact); bench (default): jacobi when r == 1/4, else auto")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="replay the timed schedule from one hipGraph captured in prepare() (auto: single-rank runs, "
-                         "whose transport is capturable; RCCL exchanges stay eager). 4096^2 fp32, 1000 steps: "
-                         "4343 vs 3859 Gpts/s eager; neutral for the 1-cycle 20-step run")
+                    help="replay the timed schedule from one hipGraph captured in prepare() (auto: whenever the "
+                         "transport's exchange captures: single-rank runs and IPC; RCCL exchanges stay eager)")
     ap.add_argument("--comm-cus", type=int, default=0, help="CUs reserved for bands + RCCL (0: default, -1: none)")
     ap.add_argument("--check", action="store_true", help="print field statistics after the run")
     ap.add_argument("--phase-timers", action="store_true",
@@ -152,19 +154,27 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"],
                     help="cpu: the same harness on the native CPU twin over gloo (CI rehearsal of the "
                          "multi-process path: tests/test_bench_contract.py); not a performance number")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "peer"],
-                    help="halo exchange between rank processes: rccl (RCCL send/recv over xGMI) or peer (no RCCL: "
-                         "the neighbours' fields mapped through hipIpc handles, halos pulled by device copies "
-                         "ordered by stream-side counters; host collectives over gloo; capturable into hipGraphs)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "ipc", "peer"],
+                    help="halo exchange between rank processes: rccl (RCCL send/recv over xGMI), ipc (alias peer: "
+                         "no RCCL, the neighbours' fields mapped through hipIpc handles, halos pulled by device "
+                         "copies ordered by stream-side counters; capturable into hipGraphs), or auto (default): "
+                         "build both, time the real timed loop with each (MAX over ranks) and keep the faster; a "
+                         "transport that fails to initialise on any rank is skipped on every rank")
     ap.add_argument("--share-gpu", action="store_true",
-                    help="every rank on GPU 0 (--transport peer): the exact multi-process path on a 1-GPU box "
-                         "(a correctness / overhead rehearsal, not a node throughput)")
+                    help="every rank on GPU 0: the exact multi-process path on a 1-GPU box (RCCL refuses two ranks "
+                         "on one GPU, so auto falls back to ipc); a correctness / overhead rehearsal, not a node "
+                         "throughput")
+    ap.add_argument("--verify", default="on", choices=["on", "off"],
+                    help="after the timed run: a small uneven rough-data problem on the same transport kind and "
+                         "rank layout, gathered and compared bitwise with the NumPy golden (JSON 'verified')")
     ap.add_argument("--rehearse-comm", action="store_true",
                     help="1 GPU only: run the multi-GPU schedule (bands + RCCL self-exchange beside a CU-masked "
                          "interior) to measure its per-rank cost; not the headline (periodic halo)")
     args = ap.parse_args()
-    if args.share_gpu and args.transport != "peer":
-        ap.error("--share-gpu needs --transport peer (RCCL refuses two ranks on one GPU)")
+    if args.transport == "peer":
+        args.transport = "ipc"
+    if args.share_gpu and args.transport == "rccl":
+        ap.error("--share-gpu needs --transport ipc or auto (RCCL refuses two ranks on one GPU)")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_launch_ranks(args.gpus, args.backend, args.share_gpu))
     out_fd = _claim_stdout()
@@ -180,27 +190,40 @@ def main():
         sys.exit(2)
     hip = args.backend == "hip"
     device = 0 if args.share_gpu else local
-    peer = args.transport == "peer" and world > 1 and hip
     if hip:
         torch.cuda.set_device(device)
     if world > 1:
-        # a dead peer fails the run instead of hanging it: torch's own collectives
-        # time out, and the native RCCL transport's watchdog uses the same limit
+        # Host collectives (barriers, the timing MAX, the transport choice, the
+        # RCCL unique id) over gloo: the halo fabric is the native transport's
+        # own (an RCCL communicator or IPC mappings), whichever wins. A dead
+        # peer fails the run instead of hanging it: the native transports'
+        # watchdogs use the same limit.
         from datetime import timedelta
         to = timedelta(seconds=float(os.environ.get("HEAT2D_COMM_TIMEOUT", "600")))
-        if hip and not peer:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=to)
-        else:  # host collectives only (CPU twin, or the IPC transport's handle exchange / all-reduces)
-            dist.init_process_group("gloo", timeout=to)
-    # device of the torch collectives below (RCCL: device tensors; gloo: host tensors)
-    cdev = "cuda" if (hip and world > 1 and not peer) else "cpu"
+        dist.init_process_group("gloo", timeout=to)
+
+    def reduce(v, op):
+        if world == 1:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    amin = (lambda v: reduce(v, dist.ReduceOp.MIN))
+    amax = (lambda v: reduce(v, dist.ReduceOp.MAX))
 
     def sync():
         if hip:
             torch.cuda.synchronize()
 
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        sync()
+
     import heat2d
     from heat2d.models.heat2d import HeatSolver
+    from heat2d.parallel import select
     from heat2d.parallel.transport import (IpcLoopTransport, IpcTransport, RcclLoopTransport, RcclTransport,
                                            SelfTransport, TorchDistTransport)
 
@@ -208,56 +231,110 @@ def main():
     if args.weak:
         import math
         n_glob = int(round(args.n * math.sqrt(world)))
-    inp = heat2d.InputDat(n=n_glob, sigma=0.25, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
+    inp = heat2d.InputDat(n=n_glob, sigma=args.sigma, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     arith = args.arith if args.arith != "bench" else ("jacobi" if prob.r == 0.25 else "auto")
-    if world > 1:
-        tr = (IpcTransport(device) if peer else RcclTransport(rank, world, local)) if hip else TorchDistTransport()
-    elif args.rehearse_comm and hip:  # one rank's exchange with itself: RCCL kernels or IPC pulls
-        tr = IpcLoopTransport(device) if args.transport == "peer" else RcclLoopTransport(local)
-    else:
-        tr = SelfTransport()
     rows = args.rows if (args.rows and world == 1) else None
     # a rehearsal of one rank's slab is a MIDDLE slab of the grid (interior
     # boundary bands, as on rank 3 of 8); --rows alone is a standalone rows x n grid
     slab_row0 = (prob.n_owned - rows) // 2 if (rows and args.rehearse_comm) else None
-    # graphs: single-rank runs, and multi-rank runs whose exchange captures (the IPC transport; RCCL's does not)
-    ipc = peer or (args.rehearse_comm and args.transport == "peer")
-    graph = hip and (args.graph == "on" or (args.graph == "auto" and ((world == 1 and not args.rehearse_comm) or ipc)))
-    s = HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb, overlap=not args.no_overlap, graph=graph,
-                   tile_rows=args.tile_rows, transport=tr, device=device if hip else None, rows=rows,
-                   comm_cus=args.comm_cus, arith=arith, slab_row0=slab_row0)
 
-    def barrier():
-        if world > 1:
-            tr_vals = torch.zeros(1, device=cdev)
-            dist.all_reduce(tr_vals)
+    def make_transport(kind):
+        if kind == "rccl":
+            return RcclTransport(rank, world, device)
+        if kind == "ipc":
+            return IpcTransport(device)
+        if kind == "torch-dist":
+            return TorchDistTransport()
+        if kind == "rccl-loop":
+            return RcclLoopTransport(device)
+        if kind == "ipc-loop":
+            return IpcLoopTransport(device)
+        return SelfTransport()
+
+    def uses_graph(kind):
+        # graphs whenever the exchange captures: single-rank runs and the IPC transport (RCCL's does not)
+        capt = kind in ("self", "ipc", "ipc-loop")
+        return hip and (args.graph == "on" or (args.graph == "auto" and capt))
+
+    def build(kind, tr):
+        return HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb, overlap=not args.no_overlap,
+                          graph=uses_graph(kind), tile_rows=args.tile_rows, transport=tr,
+                          device=device if hip else None, rows=rows, comm_cus=args.comm_cus, arith=arith,
+                          slab_row0=slab_row0)
+
+    def timed(s):
+        barrier()
+        t0 = time.perf_counter()
+        s.step(args.steps)
+        s.synchronize()
         sync()
+        t1 = time.perf_counter()
+        barrier()
+        return amax(t1 - t0)
 
-    s.step(args.warmup)
-    s.synchronize()
-    # plan / autotune every depth the timed run uses, pick its cycle schedule by
-    # measurement, and end on non-mutating trial cycles of that schedule (GPU
-    # clocks as in a long run) — outside the timed region, after the warmup
-    tp = time.perf_counter()
-    s.prepare(args.steps)
-    prepare_s = time.perf_counter() - tp
+    live = {}  # kind -> (transport, solver, prepare seconds)
+
+    def setup(kind):
+        """Transport + solver + warm-up + prepare(steps), each phase collective:
+        a failure on any rank raises Skip on every rank."""
+        tr, why = select.try_collective(lambda: make_transport(kind), amin,
+                                        cleanup=lambda t: (t.abort("another rank failed to initialise"), t.close()))
+        if why is not None:
+            raise select.Skip(why)
+        s, why = select.try_collective(lambda: build(kind, tr), amin, cleanup=lambda x: x.close())
+        if why is not None:
+            tr.close()
+            raise select.Skip(why)
+        s.step(args.warmup)
+        s.synchronize()
+        # plan / autotune every depth the timed run uses, pick its cycle schedule
+        # by measurement, and end on non-mutating trial cycles of that schedule
+        # (GPU clocks as in a long run) — outside the timed region, after the warmup
+        tp = time.perf_counter()
+        s.prepare(args.steps)
+        live[kind] = (tr, s, time.perf_counter() - tp)
+        return s
+
+    def release(kind):
+        tr, s, _ = live.pop(kind)
+        s.close()
+        tr.close()
+
+    cands = select.candidate_transports(args.transport, world, hip)
+    choice_report = None
+    if cands:
+        field_bytes = 2.0 * (prob.n_owned / world + 48) * (prob.n_owned + 128) * (8 if args.dtype == "fp64" else 4)
+
+        def trial(kind):
+            s = setup(kind)
+            ms = min(timed(s) for _ in range(2)) * 1e3
+            if hip and kind != cands[-1]:
+                # keep this candidate for the timed run only if another solver fits beside it
+                free = torch.cuda.mem_get_info(device)[0] / (world if args.share_gpu else 1)
+                if amin(free) < 1.5 * field_bytes:
+                    release(kind)
+            return ms
+
+        chosen, choice_report = select.choose_transport(cands, trial, amin, amax)
+        if chosen is None:
+            raise SystemExit(f"bench.py: no transport works on every rank: {choice_report}")
+        for k in list(live):
+            if k != chosen:
+                release(k)
+        if chosen not in live:
+            setup(chosen)
+        kind = chosen
+    else:
+        kind = ("torch-dist" if world > 1 else
+                (("ipc-loop" if args.transport == "ipc" else "rccl-loop") if (args.rehearse_comm and hip) else "self"))
+        setup(kind)
+    tr, s, prepare_s = live[kind]
     s.cycle_hist(reset=True)
     s.halo_rows_exchanged(reset=True)
     if args.phase_timers:
         s.set_timing(True)
-    barrier()
-    t0 = time.perf_counter()
-    s.step(args.steps)
-    s.synchronize()
-    sync()
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed(s)
 
     pts = float(prob.n_owned) * float(rows or prob.n_owned)
     gpts = pts * args.steps / elapsed / 1e9
@@ -283,11 +360,24 @@ def main():
     nmsg = 2 if (args.rehearse_comm and world == 1) else (rank > 0) + (rank < world - 1)
     halo_bytes = float(s.halo_rows_exchanged()) * s.layout.pitch * es * nmsg
     if world > 1:
-        tt = torch.tensor([traffic, halo_bytes], device=cdev, dtype=torch.float64)
+        tt = torch.tensor([traffic, halo_bytes], dtype=torch.float64)
         dist.all_reduce(tt)
         traffic, halo_bytes = float(tt[0].item()), float(tt[1].item())
     stats = s.stats() if args.check else None
     phases = s.phase_times() if args.phase_timers else None
+    plan_cache = {"hits": s.plan_cache_hits, "path": N.plan_cache_path()} if hip else None
+    measured = s.schedule(args.steps) is not None
+    s.close()
+    tr.close()
+    live.clear()
+    verify = None
+    if args.verify == "on":
+        # the chosen transport kind and rank layout on a small uneven problem
+        # (a rehearsal's self-exchange is not physics: its slab verifies alone)
+        vkind = kind if kind not in ("rccl-loop", "ipc-loop") else "self"
+        verify = select.verify_decomposition(lambda: make_transport(vkind), rank=rank, world=world,
+                                             dtype=args.dtype, arith=arith, backend=args.backend,
+                                             device=device if hip else None, graph=uses_graph(vkind), r=prob.r)
     if rank == 0:
         out = {
             "metric": "stencil Gpoints/sec (whole node)",
@@ -304,22 +394,27 @@ def main():
             "data": "synthetic (reference benchmark IC: T=2 interior, Dirichlet T=1 frame)",
             "config": {
                 "model": (f"heat2d FTCS 5-point, weak scaling: {args.n}^2 points per GPU (global {n_glob}^2)" if args.weak
-                          else "heat2d FTCS 5-point, fortran/hip/input.dat (32768 0.25 0.05 1.0 25000 0)" if n_glob == 32768
-                          else f"heat2d FTCS 5-point, {n_glob}^2 (sigma 0.25, nu 0.05, L 1.0)"),
+                          else "heat2d FTCS 5-point, fortran/hip/input.dat (32768 0.25 0.05 1.0 25000 0)"
+                          if n_glob == 32768 and args.sigma == 0.25
+                          else f"heat2d FTCS 5-point, {n_glob}^2 (sigma {args.sigma:g}, nu 0.05, L 1.0)"),
                 "grid": [rows or prob.n_owned, prob.n_owned],
                 "global_batch": 1,
                 "seq_len": prob.n_owned,
+                "sigma": args.sigma,
                 "parallelism": f"slab{world}" + ("-rehearsal" if args.rehearse_comm and world == 1 else "")
                                + ("-shared-gpu" if args.share_gpu and world > 1 else ""),
                 "transport": tr.name,
+                "transport_choice": (dict(choice_report, chosen=kind, requested=args.transport)
+                                     if choice_report is not None else None),
                 "tb_max": tb,
                 "cycles": {str(k): c for k, c in sorted(hist.items())},
-                "schedule": "measured" if s.schedule(args.steps) else "balanced",
+                "schedule": "measured" if measured else "balanced",
                 "prepare_s": round(prepare_s, 2),
-                "plan_cache": {"hits": s.plan_cache_hits, "path": N.plan_cache_path()} if hip else None,
-                "arith": arith_name(prob.r, arith) + {"auto": " (auto)", "bench": " (r = 1/4)"}.get(args.arith, ""),
+                "plan_cache": plan_cache,
+                "arith": arith_name(prob.r, arith) + {"auto": " (auto)", "bench": " (r = 1/4)" if prob.r == 0.25
+                                                      else " (auto)"}.get(args.arith, ""),
                 "overlap": not args.no_overlap,
-                "graph": bool(graph),
+                "graph": bool(uses_graph(kind)),
                 "launch_plans": plans or None,
                 "backend": args.backend,
             },
@@ -327,6 +422,8 @@ def main():
             # halo bytes moved by all ranks in the timed region, and per cycle (whole node)
             "halo_bytes": halo_bytes,
             "halo_bytes_per_cycle": round(halo_bytes / max(1, sum(hist.values())), 1),
+            "verified": None if verify is None else verify["verified"],
+            "verify": verify,
             "baseline_basis": "BASELINE.md derived ceiling 50 Gpts/s per MI250X GCD x n_gpus",
         }
         if stats:
@@ -334,8 +431,6 @@ def main():
         if phases:
             out["phase_ms"] = phases
         os.write(out_fd, (json.dumps(out) + "\n").encode())
-    s.close()
-    tr.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -165,14 +165,24 @@ class IpcTransport final : public Transport {
     HEAT2D_REQUIRE(ops_.allreduce(ops_.ctx, &ok, 1, 1) == 0, "IPC transport: allreduce callback failed");
     if (rank_ == 0) ::shm_unlink(all[0].shm);
     HEAT2D_REQUIRE(ok == 0.0, "IPC transport: a rank could not map the counter block" + (err.empty() ? "" : ": " + err));
-    // open the neighbours' fields
-    for (int p : {rank_ - 1, rank_ + 1}) {
-      if (p < 0 || p >= size_) continue;
-      HEAT2D_REQUIRE(all[(size_t)p].L.pitch == L.pitch, "IPC transport: slabs of different pitch");
-      peer_L_[p > rank_] = all[(size_t)p].L;
-      for (int b = 0; b < 2; ++b)
-        H2D_HIP(hipIpcOpenMemHandle(&peer_buf_[p > rank_][b], all[(size_t)p].buf[b], hipIpcMemLazyEnablePeerAccess));
+    // open the neighbours' fields; every rank learns whether all of them could
+    // (a rank failing alone would leave the others waiting in the next
+    // collective: bench.py's transport fallback needs a collective verdict)
+    err.clear();
+    try {
+      for (int p : {rank_ - 1, rank_ + 1}) {
+        if (p < 0 || p >= size_) continue;
+        HEAT2D_REQUIRE(all[(size_t)p].L.pitch == L.pitch, "IPC transport: slabs of different pitch");
+        peer_L_[p > rank_] = all[(size_t)p].L;
+        for (int b = 0; b < 2; ++b)
+          H2D_HIP(hipIpcOpenMemHandle(&peer_buf_[p > rank_][b], all[(size_t)p].buf[b], hipIpcMemLazyEnablePeerAccess));
+      }
+    } catch (const std::exception& e) {
+      err = e.what();
     }
+    ok = err.empty() ? 0.0 : 1.0;
+    HEAT2D_REQUIRE(ops_.allreduce(ops_.ctx, &ok, 1, 1) == 0, "IPC transport: allreduce callback failed");
+    HEAT2D_REQUIRE(ok == 0.0, "IPC transport: a rank could not map its neighbours' fields" + (err.empty() ? "" : ": " + err));
     barrier();
     if (timeout_s_ > 0)
       wd_.reset(new Watchdog(

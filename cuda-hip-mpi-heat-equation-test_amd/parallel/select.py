@@ -1,0 +1,153 @@
+"""Collective transport selection and a bitwise self-check of a decomposition.
+
+The reference has exactly one way to move halos: host-staged MPI_Sendrecv
+(fortran/hip/heat.F90:196-230) over whatever MPI the job was linked with.
+Here a multi-GPU run can exchange halos through RCCL send/recv or through the
+IPC transport (hipIpc mappings of the neighbours' fields, device copies
+ordered by stream-side counters), and which one is faster depends on the node
+(xGMI topology, RCCL's channel kernels sharing the CUs with the interior
+launch, whether the exchange can be graph-captured: IPC's can, RCCL's cannot).
+So the first run on a node decides by measurement, collectively:
+
+* :func:`collective_ok` — a step that may fail on some ranks (e.g. RCCL
+  refusing two ranks on one GPU) succeeds only if it succeeded on every rank;
+  every rank then takes the same branch.
+* :func:`choose_transport` — try each candidate (build + time the real timed
+  loop), MAX over ranks per candidate, keep the fastest; a candidate that
+  fails anywhere is skipped on every rank (the fallback).
+* :func:`verify_decomposition` — a small uneven, rough-data problem run with
+  the chosen transport and rank layout through the same engine paths
+  (autotuned split plans, measured schedule, graphs where the transport
+  captures), gathered to rank 0 and compared bitwise with the NumPy golden
+  model (models/reference.py).
+
+The selection logic takes its collectives as callables, so it is tested on CPU
+with plain functions and with gloo ranks (tests/test_select.py).
+"""
+from __future__ import annotations
+
+import traceback
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+
+class Skip(Exception):
+    """A candidate failed a collective phase on some rank: raised on EVERY
+    rank (after the phase's agreement), so all of them skip it alike."""
+
+
+def collective_ok(local_ok: bool, allreduce_min: Callable[[float], float]) -> bool:
+    """True iff ``local_ok`` holds on every rank (one MIN all-reduce)."""
+    return allreduce_min(1.0 if local_ok else 0.0) >= 1.0
+
+
+def try_collective(fn: Callable[[], object], allreduce_min: Callable[[float], float],
+                   cleanup: Optional[Callable[[object], None]] = None) -> Tuple[Optional[object], Optional[str]]:
+    """Run ``fn`` on every rank; if it raised on ANY rank, undo it where it
+    succeeded (``cleanup``) and return (None, reason) everywhere, else
+    (result, None). Exceptions are caught, never propagated: the caller picks
+    the next candidate on every rank alike."""
+    obj, why = None, None
+    try:
+        obj = fn()
+    except Skip as e:  # a nested phase already agreed (and reported) that it failed
+        why = str(e)
+    except Exception as e:  # noqa: BLE001 - any failure of a candidate is a fallback, reported
+        why = f"{type(e).__name__}: {e}".strip()
+        traceback.print_exc()
+    if collective_ok(why is None, allreduce_min):
+        return obj, None
+    if obj is not None and cleanup is not None:
+        try:
+            cleanup(obj)
+        except Exception:  # noqa: BLE001
+            traceback.print_exc()
+    return None, why or "failed on another rank"
+
+
+def choose_transport(candidates: Sequence[str], trial: Callable[[str], float],
+                     allreduce_min: Callable[[float], float],
+                     allreduce_max: Callable[[float], float]) -> Tuple[Optional[str], Dict[str, dict]]:
+    """Try every candidate transport with ``trial(kind) -> ms`` (it builds the
+    transport and the solver and times the real loop; raising = unusable),
+    reduce each time with MAX over ranks, and return (fastest kind, report).
+    The report holds {"ms": max-over-ranks ms} or {"error": reason} per kind,
+    identical on every rank (a failure anywhere skips the kind everywhere).
+    None if no candidate works."""
+    report: Dict[str, dict] = {}
+    best, best_ms = None, float("inf")
+    for kind in candidates:
+        ms, why = try_collective(lambda: trial(kind), allreduce_min)
+        if why is not None:
+            report[kind] = {"error": why}
+            continue
+        ms = allreduce_max(float(ms))
+        report[kind] = {"ms": round(ms, 4)}
+        if ms < best_ms:
+            best, best_ms = kind, ms
+    return best, report
+
+
+def candidate_transports(requested: str, world: int, hip: bool) -> List[str]:
+    """Transports a run may use: one forced kind, or every GPU transport for
+    "auto" (RCCL first: the reference's own model of an MPI-style fabric; IPC
+    second). Single-rank and CPU runs have nothing to choose."""
+    if not hip or world <= 1:
+        return []
+    if requested == "auto":
+        return ["rccl", "ipc"]
+    return ["ipc" if requested in ("ipc", "peer") else "rccl"]
+
+
+def verify_decomposition(make_transport: Callable[[], object], *, rank: int, world: int, dtype: str, arith: str,
+                         backend: str = "hip", device: Optional[int] = None, n: Optional[int] = None,
+                         steps: int = 57, graph: bool = False, seed: int = 1234, r: float = 0.25) -> dict:
+    """Run a small problem with a fresh transport of the chosen kind on every
+    rank — n x n (default 256 * world + 5: uneven slabs), rough random data
+    (sum - 4c is not exact, so the arithmetic is really checked), ``steps``
+    steps through the autotuned split plans and measured schedule — gather it
+    to rank 0 and compare it BITWISE with the NumPy golden model of the same
+    arithmetic, with the run's FTCS coefficient ``r`` (the same update bits as
+    the run: r = nu dt / delta^2 is sigma only up to rounding, which differs
+    with n). Returns {"verified": bool, "n": n, "steps": steps,
+    "max_abs_diff": float} (the verdict is broadcast: the same on every rank)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import heat2d
+    from ..models import reference as R
+    from ..models.heat2d import HeatSolver
+
+    n = int(n or 256 * world + 5)
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    import dataclasses
+    prob = heat2d.make_problem(heat2d.InputDat(n=n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=steps, soln=0, nfields=6),
+                               "ghost", "uniform")
+    prob = dataclasses.replace(prob, r=float(r))
+    T0 = np.random.default_rng(seed).random((n, n)).astype(npdt) + npdt(1.0)
+    tr = make_transport()
+    s = None
+    try:
+        s = HeatSolver(prob, dtype=dtype, backend=backend, transport=tr, device=device, autotune=1, graph=graph,
+                       arith=arith)
+        s.upload(T0[s.row0:s.row0 + s.nrows])
+        s.prepare(steps)
+        s.step(steps)
+        s.synchronize()
+        got = s.gather()
+    finally:
+        if s is not None:
+            s.close()
+        tr.close()
+    verdict = torch.zeros(2, dtype=torch.float64)
+    if rank == 0:
+        full = R.initial_field(prob, npdt)
+        full[1:-1, 1:-1] = T0
+        ref = R.owned(R.ftcs(prob, steps, dtype=npdt, T0=full, arith=arith))
+        diff = float(np.max(np.abs(got.astype(np.float64) - ref.astype(np.float64))))
+        verdict[0] = 1.0 if np.array_equal(got, ref) else 0.0
+        verdict[1] = diff
+    if world > 1:
+        dist.broadcast(verdict, src=0)
+    return {"verified": bool(verdict[0].item() == 1.0), "n": n, "steps": steps,
+            "max_abs_diff": float(verdict[1].item())}

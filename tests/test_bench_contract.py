@@ -36,6 +36,9 @@ def test_bench_json_line_multi_rank(nproc, dtype):
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
     assert d["scaling"] == "strong" and d["config"]["parallelism"] == f"slab{nproc}"
     assert d["config"]["grid"] == [100, 100]
+    # the self-check after the timed run: an uneven rough-data problem over the
+    # same ranks and transport kind, gathered and compared bitwise to the golden
+    assert d["verified"] is True and d["verify"]["n"] == 256 * nproc + 5 and d["verify"]["max_abs_diff"] == 0.0
 
 
 def test_bench_weak_mode():
@@ -91,12 +94,12 @@ def run_plain(*args, timeout=600):
     return json.loads(lines[0])
 
 
-def test_bench_share_gpu_needs_peer():
+def test_bench_share_gpu_refuses_forced_rccl():
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu"],
-                       capture_output=True, text=True, timeout=300, env=env)
-    assert p.returncode != 0 and "--share-gpu needs --transport peer" in p.stderr
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--transport",
+                        "rccl"], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode != 0 and "--share-gpu needs --transport ipc or auto" in p.stderr
 
 
 def test_bench_reports_halo_traffic_cpu():
@@ -126,6 +129,25 @@ def test_bench_ipc_transport_share_gpu_matches_one_rank(dtype, steps):
     assert a["min"] == b["min"] and a["max"] == b["max"]
     assert b["sum"] == pytest.approx(a["sum"], rel=1e-12, abs=0)
     assert four["halo_bytes"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_auto_transport_falls_back_to_ipc_share_gpu():
+    """`bench.py --gpus 4 --share-gpu` with the default --transport auto: RCCL
+    refuses four ranks on one GPU, every rank skips it alike and the run
+    proceeds on the IPC transport (the fallback a node whose RCCL cannot
+    initialise takes), then verifies the decomposition bitwise."""
+    common = ["--grid", "8192", "--steps", "20", "--warmup", "5", "--check"]
+    four = run_plain("--gpus", "4", "--share-gpu", *common)
+    ch = four["config"]["transport_choice"]
+    assert four["config"]["transport"] == "ipc" and ch["chosen"] == "ipc" and ch["requested"] == "auto", ch
+    assert "error" in ch["rccl"] and ch["ipc"]["ms"] > 0, ch
+    assert four["verified"] is True and four["verify"]["max_abs_diff"] == 0.0, four["verify"]
+    one = run_plain("--gpus", "1", *common)
+    assert one["verified"] is True and one["config"]["transport_choice"] is None
+    a, b = one["field_stats"], four["field_stats"]
+    assert a["min"] == b["min"] and a["max"] == b["max"]
+    assert b["sum"] == pytest.approx(a["sum"], rel=1e-12, abs=0)
 
 
 @pytest.mark.gpu

@@ -1,0 +1,107 @@
+"""Collective transport selection (parallel/select.py) and the bench's
+self-verification, on CPU: the logic bench.py runs on a multi-GPU node before
+its timed region (try RCCL and IPC, skip whatever fails on any rank, keep the
+faster by the MAX over ranks, then check a small decomposition bitwise).
+
+Pure-function cases use single-rank collectives; the multi-rank cases run gloo
+ranks (tests/select_worker.py), where a failure on ONE rank must make every
+rank skip the candidate alike."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from heat2d.parallel import select
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ident = (lambda v: v)  # noqa: E731  (a 1-rank all-reduce)
+
+
+def test_choose_fastest():
+    chosen, rep = select.choose_transport(["rccl", "ipc"], lambda k: {"rccl": 2.0, "ipc": 1.5}[k], ident, ident)
+    assert chosen == "ipc" and rep == {"rccl": {"ms": 2.0}, "ipc": {"ms": 1.5}}
+
+
+def test_choose_skips_failing_candidate():
+    def trial(kind):
+        if kind == "rccl":
+            raise RuntimeError("ncclCommInitRank failed")
+        return 3.0
+    chosen, rep = select.choose_transport(["rccl", "ipc"], trial, ident, ident)
+    assert chosen == "ipc" and "ncclCommInitRank failed" in rep["rccl"]["error"] and rep["ipc"] == {"ms": 3.0}
+
+
+def test_choose_none_when_all_fail():
+    def trial(kind):
+        raise select.Skip("no fabric")
+    chosen, rep = select.choose_transport(["rccl", "ipc"], trial, ident, ident)
+    assert chosen is None and set(rep) == {"rccl", "ipc"}
+
+
+def test_try_collective_cleans_up_on_remote_failure():
+    """Local success but a failure elsewhere (the MIN all-reduce says 0):
+    the local object is cleaned up and the caller sees the failure."""
+    cleaned = []
+    obj, why = select.try_collective(lambda: "comm", lambda v: 0.0, cleanup=cleaned.append)
+    assert obj is None and why == "failed on another rank" and cleaned == ["comm"]
+
+
+@pytest.mark.parametrize("requested,world,hip,expect", [("auto", 8, True, ["rccl", "ipc"]), ("peer", 2, True, ["ipc"]),
+                                                        ("rccl", 2, True, ["rccl"]), ("auto", 1, True, []),
+                                                        ("auto", 4, False, [])])
+def test_candidates(requested, world, hip, expect):
+    assert select.candidate_transports(requested, world, hip) == expect
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(tmp_path, world, scenario, timeout=240):
+    port = free_port()
+    env = dict(os.environ, OMP_NUM_THREADS="1", HEAT2D_CPU_THREADS="2")
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "select_worker.py"), str(r), str(world), str(port),
+                               str(tmp_path), scenario], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=timeout)[0].decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-3000:]
+    res = []
+    for r in range(world):
+        with open(tmp_path / f"rank{r}.json") as f:
+            res.append(json.load(f))
+    return res
+
+
+def test_gloo_failure_on_one_rank_falls_back_everywhere(tmp_path):
+    res = run_ranks(tmp_path, 3, "fail_rccl_on_1")
+    for r in res:
+        assert r["chosen"] == "ipc", r
+        assert "duplicate GPU" in r["report"]["rccl"]["error"] or r["report"]["rccl"]["error"] == "failed on another rank"
+        assert r["report"]["ipc"] == {"ms": 2.0}
+    # ranks that did build an RCCL object released it
+    assert res[0]["built"] == ["rccl", "cleanup-rccl", "ipc"] and res[1]["built"] == ["ipc"]
+
+
+def test_gloo_choice_uses_the_slowest_rank(tmp_path):
+    """rccl is faster on rank 0 but slow on rank 1: MAX over ranks decides."""
+    res = run_ranks(tmp_path, 2, "slow_rank")
+    assert all(r["chosen"] == "ipc" and r["report"] == {"rccl": {"ms": 5.0}, "ipc": {"ms": 3.0}} for r in res), res
+
+
+def test_gloo_verify_decomposition_bitwise(tmp_path):
+    res = run_ranks(tmp_path, 3, "verify")
+    for r in res:
+        assert r["verify"] == {"verified": True, "n": 113, "steps": 29, "max_abs_diff": 0.0}, r
