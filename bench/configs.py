@@ -10,6 +10,8 @@ serial case). Prints one JSON line per configuration.
   gpu-32768-fp64    32768x32768 fp64 — the reference's benchmark input (fortran/hip/input.dat)
   gpu-32768-fp32    32768x32768 fp32 (the 8-GPU config of BASELINE.json, here on 1 GPU)
   gpu-max-fp32      the largest fp32 grid two fields fit in --max-gb of HBM (weak-scaling unit)
+  gpu-32768-fp64-s0.2  the reference input with sigma = 0.2 (r != 1/4): the scaled-level
+                       "fast" arithmetic (any r) and the exact reference rounding, 20 steps
 """
 import argparse
 import json
@@ -21,11 +23,11 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(name, n, dtype, steps, warmup, backend, tb, graph=False, arith="bench"):
+def run(name, n, dtype, steps, warmup, backend, tb, graph=False, arith="bench", sigma=0.25):
     import heat2d
     from heat2d.models.heat2d import HeatSolver
     from heat2d.utils.metrics import plan_hbm_bytes
-    inp = heat2d.InputDat(n=n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=steps, nfields=6)
+    inp = heat2d.InputDat(n=n, sigma=sigma, nu=0.05, dom_len=1.0, ntime=steps, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     # bench: the r = 1/4 form when r == 1/4 (every config here), as bench.py
     ar = ("jacobi" if prob.r == 0.25 else "auto") if arith == "bench" else arith
@@ -50,7 +52,8 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False, arith="bench"):
     es = 8 if dtype == "fp64" else 4
     gpts = float(n) * n * steps / dt / 1e9
     hist = s.cycle_hist()
-    rec = {"config": name, "n": n, "dtype": dtype, "backend": backend, "arith": ar, "tb_max": s.tb, "graph": graph,
+    rec = {"config": name, "n": n, "dtype": dtype, "backend": backend, "arith": ar, "sigma": sigma, "tb_max": s.tb,
+           "graph": graph,
            "steps": steps, "s": round(dt, 6), "ms_per_step": round(dt / steps * 1e3, 5), "gpts": round(gpts, 2),
            "cycles": {str(k): c for k, c in sorted(hist.items())}, "field_gb": round(s.layout.elems() * es / 1e9, 2),
            "init_s": round(t_init, 3), "prepare_s": round(prepare_s, 2), "finite": bool(math.isfinite(st["sum"]))}
@@ -70,7 +73,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--max-gb", type=float, default=240.0)
-    ap.add_argument("--arith", default="bench", choices=["bench", "auto", "exact", "fma", "jacobi"],
+    ap.add_argument("--arith", default="bench", choices=["bench", "auto", "exact", "fma", "jacobi", "fast"],
                     help="update form (bench.py --arith): bench = jacobi where r == 1/4")
     a = ap.parse_args()
     import torch
@@ -89,13 +92,18 @@ def main():
         ("gpu-32768-fp64", 32768, "fp64", 480, 48, "hip", 0, False),
         ("gpu-32768-fp32", 32768, "fp32", 480, 48, "hip", 0, False),
         ("gpu-max-fp32", nmax, "fp32", 64, 16, "hip", 0, False),
+        # sigma 0.2 (any r): the scaled-level arithmetic against the reference rounding
+        ("gpu-32768-fp64-s0.2-fast", 32768, "fp64", 20, 5, "hip", 0, True, "fast", 0.2),
+        ("gpu-32768-fp64-s0.2-exact", 32768, "fp64", 20, 5, "hip", 0, True, "exact", 0.2),
     ]
-    for name, n, dt, steps, warm, be, tb, graph in plan:
+    for entry in plan:
+        name, n, dt, steps, warm, be, tb, graph = entry[:8]
+        arith, sigma = (entry[8], entry[9]) if len(entry) > 8 else (a.arith, 0.25)
         if a.only and not any(name.startswith(o) for o in a.only):
             continue
         if be == "hip" and not have_gpu:
             continue
-        print(json.dumps(run(name, n, dt, steps, warm, be, tb, graph, a.arith)), flush=True)
+        print(json.dumps(run(name, n, dt, steps, warm, be, tb, graph, arith, sigma)), flush=True)
         if have_gpu:
             torch.cuda.empty_cache()
 

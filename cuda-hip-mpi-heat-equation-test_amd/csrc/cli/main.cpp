@@ -58,7 +58,12 @@ struct Args {
   bool quiet = false;
   bool timers = false;
   std::string engine = "tb";
-  std::string arith = "auto";  // auto | exact | fma | jacobi (SolverConfig::arith; auto: fma iff bitwise-identical)
+  // auto | exact | fma | jacobi | fast (SolverConfig::arith). auto: jacobi when
+  // r == 1/4 and the IC keeps every value in [m, 2m] (bitwise the reference
+  // rounding then, ic_sterbenz_safe), else fma when r is a power of two
+  // (bitwise identical too), else exact
+  std::string arith = "auto";
+  bool time_transfers = false;  // --time-transfers: H2D of the IC and D2H of the result inside the timed region
   std::string checkpoint;       // --checkpoint DIR (utils/checkpoint.py format)
   int64_t checkpoint_every = 0;
   std::string restart;          // --restart DIR (any writer rank count)
@@ -72,7 +77,8 @@ void usage() {
       "usage: heat2d [input.dat] [--variant mpi|serial|cuda] [--gpus N | --cpu] [--dtype fp64|fp32]\n"
       "              [--tb K] [--no-overlap] [--copy-swap] [--managed] [--graph] [--ic NAME]\n"
       "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
-      "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith auto|exact|fma|jacobi]\n"
+      "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith auto|exact|fma|jacobi|fast]\n"
+      "              [--time-transfers]\n"
       "              [--checkpoint DIR [--checkpoint-every N]] [--restart DIR]\n"
       "              [--transport rccl|peer] [--share-gpu] [--autotune auto|on|off]\n");
 }
@@ -103,6 +109,7 @@ Args parse_args(int argc, char** argv) {
     else if (s == "--graph") a.graph = true;
     else if (s == "--engine") a.engine = need("--engine");
     else if (s == "--arith") a.arith = need("--arith");
+    else if (s == "--time-transfers") a.time_transfers = true;
     else if (s == "--print-every") a.print_every = std::atoll(need("--print-every").c_str());
     else if (s == "--check-every") a.check_every = std::atoll(need("--check-every").c_str());
     else if (s == "--ntime") a.ntime = std::atoll(need("--ntime").c_str());
@@ -148,6 +155,8 @@ struct Shared {
   std::vector<int64_t> rank_halo_rows;          // halo rows exchanged per side by each rank's timed loop
   bool measured = false;  // a chunk of the timed loop runs a measured cycle schedule (Solver::prepare)
   int64_t start_step = 0;  // > 0 after --restart
+  std::string arith_used;  // the arithmetic the run used (auto resolved)
+  double t_h2d = 0, t_d2h = 0;  // --time-transfers: rank 0's whole-field copies inside the timed region
 };
 
 // Collective checkpoint (every rank its slab, then rank 0 publishes meta.json).
@@ -233,9 +242,24 @@ void run_rank(Shared& sh, int rank) {
     cfg.autotune = a.autotune;
     if (a.engine != "tb" && a.engine != "jit") fail(__FILE__, __LINE__, "--engine must be tb or jit");
     cfg.engine = a.engine == "jit" ? 1 : 0;  // jit: hipRTC kernel rendered for this slab (python/cuda/cuda.py)
-    if (a.arith != "exact" && a.arith != "fma" && a.arith != "jacobi" && a.arith != "auto")
-      fail(__FILE__, __LINE__, "--arith must be auto, exact, fma or jacobi");
-    cfg.arith = a.arith == "jacobi" ? 2 : a.arith == "fma" ? 1 : (a.arith == "exact" ? 0 : -1);
+    if (a.arith != "exact" && a.arith != "fma" && a.arith != "jacobi" && a.arith != "fast" && a.arith != "auto")
+      fail(__FILE__, __LINE__, "--arith must be auto, exact, fma, jacobi or fast");
+    cfg.arith = a.arith == "fast" ? 3 : a.arith == "jacobi" ? 2 : a.arith == "fma" ? 1 : (a.arith == "exact" ? 0 : -1);
+    std::string arith_used = a.arith;
+    if (cfg.arith < 0) {
+      // auto: the r = 1/4 form when it rounds exactly like the reference for
+      // the whole run — the IC in [m, 2m] (the reference's: 1 and 2) keeps
+      // every sum - 4c exact; a restart's data is not known to be
+      if (sh.prob.r == 0.25 && ic_sterbenz_safe(sh.prob.ic) && a.restart.empty() && cfg.engine == 0) {
+        cfg.arith = 2;
+        arith_used = "jacobi (auto)";
+      } else {
+        int e = 0;
+        const bool pow2 = sh.prob.r > 0 && std::frexp(sh.prob.r, &e) == 0.5;
+        arith_used = pow2 ? "fma (auto)" : "exact (auto)";
+      }
+    }
+    if (root) sh.arith_used = arith_used;
     Solver s(cfg, tr);
     s.init(sh.prob.ic, sh.prob.x.data(), sh.prob.x.data());
     const bool inclusive = sh.prob.conv == Convention::Inclusive;
@@ -306,9 +330,26 @@ void run_rank(Shared& sh, int rank) {
       s.cycle_hist(h, true);  // count the timed loop's cycles only
       (void)s.halo_rows_exchanged(true);
     }
+    // --time-transfers: the reference's timed region also moves the whole
+    // field host -> device before the loop and back after it
+    // (fortran/hip/heat.F90:284-295); the host copy of the IC is taken here,
+    // outside it (pinned memory: the copies run at DMA speed)
+    void* host_field = nullptr;
+    bool host_pinned = false;
+    const size_t host_bytes = (size_t)(s.layout().nrows * s.layout().ncols) * dtype_size(s.dtype());
+    if (a.time_transfers) {
+      if (!a.cpu && hipHostMalloc(&host_field, host_bytes, 0) == hipSuccess) host_pinned = true;
+      else host_field = std::malloc(host_bytes);
+      HEAT2D_REQUIRE(host_field != nullptr, "host buffer for --time-transfers");
+      s.download(host_field, s.layout().ncols);
+    }
     tr->barrier();
     s.synchronize();
     const auto t0 = std::chrono::steady_clock::now();
+    if (a.time_transfers) {
+      s.upload(host_field, s.layout().ncols);  // H2D + the halo exchange of the uploaded field
+      if (root) sh.t_h2d = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
     int64_t done = start;
     const bool ckpt_periodic = !a.checkpoint.empty() && a.checkpoint_every > 0;
     while (done < ntime) {
@@ -336,8 +377,17 @@ void run_rank(Shared& sh, int rank) {
       if (ckpt_periodic && done % a.checkpoint_every == 0 && done < ntime) save_checkpoint(sh, s, *tr, rank, done);
     }
     s.synchronize();
+    if (a.time_transfers) {
+      const auto td = std::chrono::steady_clock::now();
+      s.download(host_field, s.layout().ncols);  // D2H of the result
+      if (root) sh.t_d2h = std::chrono::duration<double>(std::chrono::steady_clock::now() - td).count();
+    }
     tr->barrier();
     const auto t1 = std::chrono::steady_clock::now();
+    if (host_field) {
+      if (host_pinned) (void)hipHostFree(host_field);
+      else std::free(host_field);
+    }
     sh.t_elapsed[(size_t)rank] = std::chrono::duration<double>(t1 - t0).count();
     if (a.timers) {
       double ph[5];
@@ -469,6 +519,8 @@ int main(int argc, char** argv) {
   const double bpp = a.copy_swap ? 4.0 * es
                                  : (passes > 0 && ntime > 0 ? 2.0 * es * (double)passes / (double)ntime : 2.0 * es / K);
   std::printf(" simulation completed!!!!\n");
+  if (a.time_transfers && !a.quiet)
+    std::printf(" heat2d: timed region includes the whole-field H2D (%.6f s) and D2H (%.6f s)\n", sh.t_h2d, sh.t_d2h);
   if (a.variant == "mpi")
     std::printf(" Average time: %24.16g\n", ntime > 0 ? tmax / (double)ntime : 0.0);
   else
@@ -497,11 +549,13 @@ int main(int argc, char** argv) {
                    "{\"n\": %lld, \"nranks\": %d, \"dtype\": \"%s\", \"tb\": %d, \"cycles\": {%s}, \"steps\": %lld, \"wall_s\": %.9g, "
                    "\"gpts_per_s\": %.9g, \"model_gb_per_s\": %.9g, \"sum\": %.17g, \"min\": %.17g, \"max\": %.17g, "
                    "\"backend\": \"%s\", \"variant\": \"%s\", \"arith\": \"%s\", \"cycles_per_rank\": [%s], "
-                   "\"halo_rows_per_rank\": [%s], \"schedule\": \"%s\"}\n",
+                   "\"halo_rows_per_rank\": [%s], \"schedule\": \"%s\", \"arith_used\": \"%s\", "
+                   "\"time_transfers\": %s, \"h2d_s\": %.9g, \"d2h_s\": %.9g}\n",
                    (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, depths.c_str(), (long long)ntime, tmax,
                    gpts, gpts * bpp,
                    sh.final_stats[0], sh.final_stats[2], sh.final_stats[3], a.cpu ? "cpu" : "hip", a.variant.c_str(),
-                   a.arith.c_str(), per_rank.c_str(), halo.c_str(), sh.measured ? "measured" : "balanced");
+                   a.arith.c_str(), per_rank.c_str(), halo.c_str(), sh.measured ? "measured" : "balanced",
+                   sh.arith_used.c_str(), a.time_transfers ? "true" : "false", sh.t_h2d, sh.t_d2h);
       std::fclose(f);
     }
   }

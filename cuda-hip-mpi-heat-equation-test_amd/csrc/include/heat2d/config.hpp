@@ -46,4 +46,12 @@ struct Problem {
 // reference's order (fortran/hip/heat.F90:178-182), so r == sigma up to rounding.
 Problem make_problem(const InputDat& in, Convention conv, const std::string& ic_name);
 
+// True if every value this IC puts in the field (interior, frame, pad) lies in
+// [m, 2m] for some m > 0. FTCS with r <= 1/4 is a convex combination, so the
+// field stays in that range forever (maximum principle), and every sum - 4c of
+// the update is then exact (Sterbenz): at r = 1/4 the r * sum form (arith 2,
+// "jacobi") rounds bitwise like the reference's c + r*(sum - 4c). The CLI's
+// --arith auto uses it (the reference IC: 2 inside, 1 on the frame).
+bool ic_sterbenz_safe(const kern::IcParams& ic);
+
 }  // namespace heat2d

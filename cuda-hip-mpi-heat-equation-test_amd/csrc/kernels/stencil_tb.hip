@@ -109,11 +109,21 @@ int ring_ok(DType dt, int k, int ring, bool single = false) {
 bool ring_valid(int r) { return r == 4 || r == 6 || r == 8; }
 
 // arith code -> the kernels' AR template argument (0 reference rounding,
-// 1 contracted fma, 2 r = 1/4: tb_impl.hpp); f is called with
-// std::integral_constant<int, AR>.
+// 1 contracted fma, 2 r = 1/4, 3 any r with scaled levels: tb_impl.hpp); f is
+// called with std::integral_constant<int, AR>.
 template <class F>
 decltype(auto) with_ar(int arith, F&& f) {
-  HEAT2D_REQUIRE(arith >= 0 && arith <= 2, "arith must be 0 (exact), 1 (fma) or 2 (r = 1/4)");
+  HEAT2D_REQUIRE(arith >= 0 && arith <= 3, "arith must be 0 (exact), 1 (fma), 2 (r = 1/4) or 3 (fast)");
+  if (arith == 3) return f(std::integral_constant<int, 3>{});
+  if (arith == 2) return f(std::integral_constant<int, 2>{});
+  if (arith == 1) return f(std::integral_constant<int, 1>{});
+  return f(std::integral_constant<int, 0>{});
+}
+// the fused cycle's interior kernel exists for arith 0..2 only (opt-in; not
+// instantiated for the scaled-level arithmetic 3)
+template <class F>
+decltype(auto) with_ar_fused(int arith, F&& f) {
+  HEAT2D_REQUIRE(arith >= 0 && arith <= 2, "fused cycles: arith 0, 1 or 2");
   if (arith == 2) return f(std::integral_constant<int, 2>{});
   if (arith == 1) return f(std::integral_constant<int, 1>{});
   return f(std::integral_constant<int, 0>{});
@@ -286,6 +296,12 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   a.sig_items = sig_items;
   a.sig = sig;
   a.wtimes = wave_times_buf(a.nwaves);
+  if (arith == 3) {  // scaled levels (tb_impl.hpp AR 3): coefficients of this depth, in double
+    HEAT2D_REQUIRE(r > 0.0, "arith 3 (fast) needs r > 0");
+    a.fb = (1.0 - 4.0 * r) / r;
+    a.fu = std::pow(r, (double)k);
+    a.fu1 = std::pow(r, (double)(k - 1));
+  }
   // the dynamic queue only pays with more items than waves (plain kernels)
   a.queue = (queue && !partials && !sig && items > a.nwaves) ? queue : nullptr;
   const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
@@ -304,7 +320,7 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
     const double* s64 = static_cast<const double*>(src) + o;
     float* d32 = static_cast<float*>(dst) + o;
     double* d64 = static_cast<double*>(dst) + o;
-    with_ar(arith, [&](auto ar) {
+    with_ar_fused(arith, [&](auto ar) {
       constexpr int AR = decltype(ar)::value;
       if (dt == DType::F32) {
         if (ring == 4) dispatch_fused<float, 4, AR>(k, nblocks, s32, d32, a, (float)r, stream);
@@ -582,7 +598,8 @@ SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool se
   if ((send_top && frame_top) || (send_bottom && frame_bottom)) return p;
   const int nsig = (send_top ? 1 : 0) + (send_bottom ? 1 : 0);
   if (nsig == 0) return p;
-  const int bpc = with_ar(arith, [&](auto ar) {
+  if (arith == 3) return p;  // no fused kernel for the scaled-level arithmetic
+  const int bpc = with_ar_fused(arith, [&](auto ar) {
     constexpr int AR = decltype(ar)::value;
     if (dt == DType::F32) return p.ring == 4 ? occupancy_fused<float, 4, AR>(k) : occupancy_fused<float, 6, AR>(k);
     return p.ring == 4 ? occupancy_fused<double, 4, AR>(k) : occupancy_fused<double, 6, AR>(k);

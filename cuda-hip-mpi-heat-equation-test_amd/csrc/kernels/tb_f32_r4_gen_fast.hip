@@ -1,0 +1,11 @@
+// Instantiation unit (scaled-level arithmetic for any r, AR = 3): temporal-blocked stencil, float, 16 B per lane, ring of
+// 4 level-0 rows, general (edge-classifying) kernel, K = 1..16 (see tb_impl.hpp).
+#include "tb_impl.hpp"
+
+namespace heat2d {
+namespace kern {
+namespace tbimpl {
+H2D_TB_UNIT_F32(float, 4, false, 3)
+}  // namespace tbimpl
+}  // namespace kern
+}  // namespace heat2d

@@ -111,6 +111,11 @@ struct TbArgs {
   // Diagnostics (HEAT2D_WAVE_TIMES, kern::wave_times): per launched wave
   // {start, end (wall clock, 100 MHz), first item, its edge kind}; nullptr off
   uint64_t* wtimes;
+  // arith 3 (any r): scaled-level coefficients, computed on the host in
+  // double for this launch's depth k: fb = (1 - 4r) / r (the centre weight of
+  // a level carried as T / r^level), fu = r^k (unscales the stored level),
+  // fu1 = r^(k-1) (level k-1, the statistics' residual)
+  double fb, fu, fu1;
   // Dynamic item queue (SplitPlan::flags & kPlanDynamic): {next item beyond the first
   // round, waves finished}; a wave takes its first item statically (wid) and
   // then the next free one, so waves that run faster take more items. The
@@ -214,6 +219,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uin
 // pair lies within a factor of two (smooth positive data, e.g. the reference IC
 // with values in [1, 2]), sum - 4C is exact (Sterbenz) and the reference
 // rounding gives the same bits too.
+// 3 = any r (SolverConfig::arith 3, "fast"): the same scaling with 1 / r in
+// place of 4. With X_s = T_s / r^s the update T' = (1 - 4r) C + r (S+E+N+W)
+// becomes X_{s+1} = fma(b, X_s(C), ((S + E) + N) + W), b = (1 - 4r) / r: 3 adds
+// + 1 fma per point and level instead of 5 ops (arith 1); the stored level is
+// multiplied by r^K once. Kind-0 items only; pinned kinds run arith 1's
+// contracted form unscaled (the frame must stay bit-exact). Not the
+// reference's rounding: within a stated bound of it (tests/test_arith_fast.py,
+// |T_fast - T_exact| <= 16 n u max|T_0| after n steps, u the unit roundoff),
+// and, since interior and pinned items round differently, the bits depend on
+// the launch plan. At r = 1/4 (b = 0, r^K a power of two) it IS arith 2.
 template <typename T>
 constexpr T inv_pow4(int l) {
   T s = T(1);
@@ -328,7 +343,8 @@ struct March {
   int32_t ld_off;    // per-lane load byte offset (kOob outside the allocation)
   int32_t st_off;    // per-lane vector store offset (kOob unless the lane holds output columns)
   T rl[(EK & 2) ? V : 1];  // EK & 2: r per element, 0 in Dirichlet / pad columns
-  static constexpr bool kScaled = AR == 2 && EK == 0;  // levels carried x 4^level (AR 2)
+  T fb, fu, fu1;           // AR 3: TbArgs::fb / fu / fu1
+  static constexpr bool kScaled = (AR == 2 || AR == 3) && EK == 0;  // levels carried scaled (AR 2: x 4^level, 3: / r^level)
 
   using Ch = ChainShape<K, CL>;
   static constexpr int L = Ch::unroll(RING);  // march rows per loop body
@@ -394,7 +410,9 @@ struct March {
       else if constexpr (EK == 1) re = rs;
       else if constexpr (EK == 2) re = rl[e];
       else re = frame_row ? T(0) : rl[e];
-      if constexpr (AR == 2) {
+      if constexpr (AR == 3 && EK == 0) {
+        out[e] = fma_t(fb, C[e], sum);  // scaled: T / r^s
+      } else if constexpr (AR == 2) {
         // scaled kind 0: the plain sum (4^s T). Pinned kinds (re = 0 where
         // pinned), unscaled: kind 1 (frame rows: wave-uniform) fma(ke, C, re *
         // sum) with scalar ke = 1 - 4 re; kinds 2 / 3 (per-element re)
@@ -403,7 +421,7 @@ struct March {
         if constexpr (EK == 0) out[e] = sum;
         else if constexpr (EK == 1) out[e] = fma_t(frame_row ? T(1) : T(0), C[e], re * sum);
         else out[e] = fma_t(re, sum, fma_t(re, T(-4) * C[e], C[e]));
-      } else if constexpr (AR == 1) {
+      } else if constexpr (AR == 1 || AR == 3) {  // (AR 3 pinned kinds: unscaled, contracted)
         out[e] = fma_t(re, fma_t(T(-4), C[e], sum), C[e]);
       } else {
         out[e] = C[e] + re * fma_t(T(-4), C[e], sum);
@@ -468,13 +486,14 @@ struct March {
         const int32_t row = m + Ch::off(K);
         const bool live = (uint32_t)(row - t0) < (uint32_t)(t1 - t0);  // row in [t0, t1), wave-uniform
         if constexpr (kScaled) {
+          const T u = AR == 2 ? inv_pow4<T>(K) : fu;
 #pragma unroll
-          for (int e = 0; e < V; ++e) out[e] *= inv_pow4<T>(K);
+          for (int e = 0; e < V; ++e) out[e] *= u;
         }
         store_row(kIncPtr ? sp : drow + (int64_t)row * pitch_b, live, out);
         if constexpr (ST) {
           if (live) {
-            constexpr T cu = kScaled ? inv_pow4<T>(K - 1) : T(1);  // level K-1 scale
+            const T cu = kScaled ? (AR == 2 ? inv_pow4<T>(K - 1) : fu1) : T(1);  // level K-1 scale
 #pragma unroll
             for (int e = 0; e < V; ++e) acc.add((colmask >> e) & 1u, (double)out[e], (double)(C[e] * cu));
           }
@@ -582,7 +601,8 @@ struct MarchF32 {
   int32_t ld_off;
   int32_t st_off;
   Row rl;  // EK & 2: r per element (0 in Dirichlet / pad columns)
-  static constexpr bool kScaled = AR == 2 && EK == 0;  // levels carried x 4^level (see March)
+  float fb, fu, fu1;  // AR 3: TbArgs::fb / fu / fu1
+  static constexpr bool kScaled = (AR == 2 || AR == 3) && EK == 0;  // levels carried scaled (see March)
   using Ch = ChainShape<K, CL>;
   static constexpr int L = Ch::unroll(RING);
   Row X[3][KX];  // slot 2 only below chain boundaries (see March)
@@ -644,6 +664,11 @@ struct MarchF32 {
     }
   }
   __device__ __forceinline__ Row update(const Row& part, const Row& C, const Row& N, int32_t row) const {
+    if constexpr (AR == 3 && EK == 0) {  // scaled: fma(b, C, sum) on packed pairs
+      const Row sum = sum4(part, C, N);
+      const F2 b2 = {fb, fb};
+      return Row{__builtin_elementwise_fma(b2, C.a, sum.a), __builtin_elementwise_fma(b2, C.b, sum.b)};
+    }
     if constexpr (AR == 2) {
       const Row sum = sum4(part, C, N);
       if constexpr (EK == 0) return sum;  // scaled: 4^s T
@@ -658,19 +683,24 @@ struct MarchF32 {
     }
     Row in, re;
     terms(part, C, N, row, in, re);
-    if constexpr (AR == 1)
+    if constexpr (AR == 1 || AR == 3)
       return Row{__builtin_elementwise_fma(re.a, in.a, C.a), __builtin_elementwise_fma(re.b, in.b, C.b)};
     else
       return Row{C.a + re.a * in.a, C.b + re.b * in.b};
   }
   static __device__ __forceinline__ float fin(float re, float in, float c) {
-    if constexpr (AR == 1) return __builtin_fmaf(re, in, c);
+    if constexpr (AR == 1 || AR == 3) return __builtin_fmaf(re, in, c);
     else return c + re * in;
   }
   // The stored (last) level: its 4 final ops as scalar fp32 ops writing the
   // store vector in memory order (c0, c1, c2, c3) — a packed op would produce
   // the even/odd pairs and need a transpose before the 16-B store.
   __device__ __forceinline__ VT update_last(const Row& part, const Row& C, const Row& N, int32_t row) const {
+    if constexpr (AR == 3 && EK == 0) {  // scaled level K, unscaled by r^K at the store
+      const Row sum = sum4(part, C, N);
+      return VT{__builtin_fmaf(fb, C.a.x, sum.a.x) * fu, __builtin_fmaf(fb, C.b.x, sum.b.x) * fu,
+                __builtin_fmaf(fb, C.a.y, sum.a.y) * fu, __builtin_fmaf(fb, C.b.y, sum.b.y) * fu};
+    }
     if constexpr (AR == 2) {
       const Row sum = sum4(part, C, N);
       if constexpr (EK == 0) {
@@ -729,7 +759,7 @@ struct MarchF32 {
         store_row(live, w);
         if constexpr (ST) {
           if (live) {  // C in even/odd form: a = (c0, c2), b = (c1, c3)
-            constexpr float cu = kScaled ? inv_pow4<float>(K - 1) : 1.f;  // level K-1 scale
+            const float cu = kScaled ? (AR == 2 ? inv_pow4<float>(K - 1) : fu1) : 1.f;  // level K-1 scale
             acc.add(colmask & 1u, (double)w.x, (double)(C.a.x * cu));
             acc.add((colmask >> 1) & 1u, (double)w.y, (double)(C.b.x * cu));
             acc.add((colmask >> 2) & 1u, (double)w.z, (double)(C.a.y * cu));
@@ -821,6 +851,11 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   w.pitch_b = a.pitch * ES;
   w.nrec = (uint32_t)(a.pitch * ES);
   w.r = r;
+  if constexpr (AR == 3) {
+    w.fb = (T)a.fb;
+    w.fu = (T)a.fu;
+    w.fu1 = (T)a.fu1;
+  }
   w.t0 = (int32_t)t0;
   w.t1 = (int32_t)t1;
   w.fixed_lo = (int32_t)a.fixed_lo;

@@ -135,4 +135,23 @@ Problem make_problem(const InputDat& in, Convention conv, const std::string& ic_
   return p;
 }
 
+bool ic_sterbenz_safe(const kern::IcParams& ic) {
+  double lo = 0, hi = 0;
+  switch ((kern::IcKind)ic.kind) {
+    case kern::IcKind::Uniform:
+    case kern::IcKind::Box:
+    case kern::IcKind::IndexBox:
+      lo = std::min({ic.a, ic.b, ic.pad});
+      hi = std::max({ic.a, ic.b, ic.pad});
+      break;
+    case kern::IcKind::Const:
+      lo = std::min(ic.a, ic.pad);
+      hi = std::max(ic.a, ic.pad);
+      break;
+    default:  // sine: zero frame
+      return false;
+  }
+  return lo > 0 && hi <= 2 * lo;
+}
+
 }  // namespace heat2d

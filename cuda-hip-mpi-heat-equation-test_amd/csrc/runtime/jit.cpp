@@ -96,7 +96,10 @@ JitStencil::JitStencil(DType dt, const SlabLayout& L, double r, int device, int 
   HEAT2D_REQUIRE(L.nrows >= 1 && L.ncols >= 1 && L.halo >= 1 && L.cpad >= 1, "layout needs a ghost frame");
   if (device >= 0) H2D_HIP(hipSetDevice(device));
   H2D_HIP(hipGetDevice(&device_));
-  HEAT2D_REQUIRE(arith >= 0 && arith <= 2, "arith must be 0, 1 or 2");
+  HEAT2D_REQUIRE(arith >= 0 && arith <= 3, "arith must be 0, 1, 2 or 3");
+  // arith 3 (scaled levels) has nothing to scale at one step per launch: the
+  // contracted form is its one-level case up to the rounding of b and r
+  if (arith == 3) arith = 1;
   HEAT2D_REQUIRE(arith != 2 || r == 0.25, "arith 2 (jacobi) needs r == 1/4 exactly");
   src_ = jit_render(dt, L, r, arith);
   std::lock_guard<std::mutex> g(g_mu);

@@ -89,13 +89,21 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     int e = 0;
     cfg_.arith = (cfg_.r > 0 && std::frexp(cfg_.r, &e) == 0.5) ? 1 : 0;
   }
-  HEAT2D_REQUIRE(cfg_.arith >= 0 && cfg_.arith <= 2,
-                 "arith must be 0 (reference rounding), 1 (fma), 2 (jacobi, r = 1/4) or -1 (auto)");
+  HEAT2D_REQUIRE(cfg_.arith >= 0 && cfg_.arith <= 3,
+                 "arith must be 0 (reference rounding), 1 (fma), 2 (jacobi, r = 1/4), 3 (fast) or -1 (auto)");
   HEAT2D_REQUIRE(cfg_.arith != 2 || cfg_.r == 0.25, "arith 2 (jacobi) needs r == 1/4 exactly (sigma = 0.25)");
+  HEAT2D_REQUIRE(cfg_.arith != 3 || cfg_.r > 0, "arith 3 (fast) needs r > 0");
   if (cfg_.engine == 1) {
     HEAT2D_REQUIRE(hip_, "the jit engine runs on the HIP backend");
     HEAT2D_REQUIRE(!cfg_.copy_swap, "the jit engine has no copy-swap mode");
     K = 1;  // one step per launch, like the reference's JIT program
+  }
+  if (cfg_.arith == 3 && cfg_.r < 0.25) {
+    // scaled levels carry T / r^s: keep r^K and max|T| / r^K well inside the
+    // exponent range (fp32: r^K >= 2^-60; fp64: 2^-480), shallower passes else
+    const double lim = cfg_.dtype == 0 ? -60.0 : -480.0;
+    const int kmax = (int)std::floor(lim / std::log2(cfg_.r));
+    K = std::max(1, std::min(K, kmax));
   }
   // every rank must own >= K rows so a neighbour's K ghost rows come from one rank
   K = (int)std::min<int64_t>(K, cfg_.n_rows / P);
@@ -1481,7 +1489,8 @@ void Solver::prepare_plans(int64_t n) {
 }
 
 bool Solver::fused_ok() const {
-  return hip_ && cfg_.overlap && !cfg_.copy_swap && !jit_ && tr_->exchanges() && tr_->gates() && s_comm_ != s_compute_;
+  return hip_ && cfg_.overlap && !cfg_.copy_swap && !jit_ && tr_->exchanges() && tr_->gates() && s_comm_ != s_compute_ &&
+         cfg_.arith != 3;
 }
 
 

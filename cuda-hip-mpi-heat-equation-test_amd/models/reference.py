@@ -77,6 +77,22 @@ def ftcs(problem: Problem, nsteps: int | None = None, dtype=np.float64, T0: np.n
     return T
 
 
+def fast_error_bound(nsteps: int, dtype, tmax: float) -> float:
+    """Stated bound of the scaled-level arithmetic ("fast", the kernels' AR 3)
+    against the reference rounding ("exact") after ``nsteps`` steps from a
+    field with max |T0| = tmax, for r <= 1/4:
+
+        max |T_fast - T_exact| <= 16 * nsteps * u * tmax,   u = eps / 2.
+
+    Per step the reference form rounds ~6 times on values <= tmax (the sum,
+    sum - 4c, r * (...), c + ...) and the scaled form ~5 times (sum, fma, and
+    the rounded coefficient b = (1 - 4r) / r), plus 2 per pass for r^K and the
+    unscaling multiply; FTCS with r <= 1/4 is non-expansive in the max norm, so
+    per-step errors add up at most linearly (16 > 6 + 5 + 2 covers both)."""
+    u = float(np.finfo(dtype).eps) / 2.0
+    return 16.0 * nsteps * u * tmax
+
+
 def owned(T: np.ndarray) -> np.ndarray:
     return T[1:-1, 1:-1]
 

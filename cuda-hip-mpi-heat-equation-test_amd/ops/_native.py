@@ -28,7 +28,7 @@ CLI_PATH = os.path.join(NATIVE_DIR, "heat2d")
 F32, F64 = 0, 1
 # SolverConfig::arith: reference rounding (bitwise == NumPy golden) | contracted fma(r, sum - 4c, c) |
 # jacobi: r == 1/4 only, r * sum (the zero centre weight folded away)
-ARITH = {"exact": 0, "fma": 1, "jacobi": 2, "auto": -1}
+ARITH = {"exact": 0, "fma": 1, "jacobi": 2, "fast": 3, "auto": -1}
 
 
 def arith_code(arith: str, r: float) -> int:

@@ -40,7 +40,7 @@ def build_parser():
     ap.add_argument("--engine", default=None, choices=["tb", "jit"],
                     help="tb: temporal-blocked kernels; jit: hipRTC kernel rendered at run time "
                          "(default: jit for --variant pycuda on a GPU, else tb)")
-    ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma", "jacobi"],
+    ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma", "jacobi", "fast"],
                     help="exact: reference rounding (bitwise == NumPy golden); fma: contracted update, one op fewer; "
                          "jacobi: r == 1/4 only, r * (S + E + N + W), 3 adds per point")
     ap.add_argument("--n", type=int, default=None)
@@ -123,9 +123,12 @@ def run(argv=None) -> int:
     else:
         tr = T.SelfTransport()
     engine = a.engine or ("jit" if var.name == "pycuda" and backend == "hip" else "tb")
+    arith = a.arith
+    if arith == "auto" and prob.r == 0.25 and prob.ic.sterbenz_safe() and not a.restart and engine == "tb":
+        arith = "jacobi"  # bitwise the reference rounding on this IC (the CLI's auto does the same)
     s = HeatSolver(prob, dtype=a.dtype, backend=backend, tb=a.tb, overlap=not a.no_overlap, copy_swap=a.copy_swap,
                    managed=a.managed or var.managed, graph=a.graph, transport=tr,
-                   device=local if backend == "hip" else None, engine=engine, arith=a.arith)
+                   device=local if backend == "hip" else None, engine=engine, arith=arith)
     if root and not a.quiet:
         if world > 1 or var.outputs == "mpi":
             print(f" Automatic MPI decomposition: {world:12d}  x 1")
@@ -212,7 +215,7 @@ def run(argv=None) -> int:
         else:
             print(f" total time: {elapsed:24.16g}")
         rec = metrics.record(prob.n_owned, ran, elapsed, world, a.dtype, s.tb, backend, a.copy_swap,
-                             {"variant": var.name, "arith": a.arith, "sum": st["sum"], "min": st["min"], "max": st["max"]},
+                             {"variant": var.name, "arith": arith, "sum": st["sum"], "min": st["min"], "max": st["max"]},
                              cycles=cycles)
         if not a.quiet:
             print(f" heat2d: n={prob.n_owned} P={world} {a.dtype} K<={s.tb} passes={sum(cycles.values())} "

@@ -139,15 +139,22 @@ def verify_decomposition(make_transport: Callable[[], object], *, rank: int, wor
         if s is not None:
             s.close()
         tr.close()
+    # "fast" (scaled levels) is not the reference rounding: checked against the
+    # exact golden within its stated bound (models/reference.fast_error_bound)
+    bound = R.fast_error_bound(steps, npdt, float(np.max(np.abs(T0)))) if arith == "fast" else 0.0
     verdict = torch.zeros(2, dtype=torch.float64)
     if rank == 0:
         full = R.initial_field(prob, npdt)
         full[1:-1, 1:-1] = T0
-        ref = R.owned(R.ftcs(prob, steps, dtype=npdt, T0=full, arith=arith))
+        ref = R.owned(R.ftcs(prob, steps, dtype=npdt, T0=full, arith="exact" if arith == "fast" else arith))
         diff = float(np.max(np.abs(got.astype(np.float64) - ref.astype(np.float64))))
-        verdict[0] = 1.0 if np.array_equal(got, ref) else 0.0
+        ok = diff <= bound if arith == "fast" else np.array_equal(got, ref)
+        verdict[0] = 1.0 if ok else 0.0
         verdict[1] = diff
     if world > 1:
         dist.broadcast(verdict, src=0)
-    return {"verified": bool(verdict[0].item() == 1.0), "n": n, "steps": steps,
-            "max_abs_diff": float(verdict[1].item())}
+    out = {"verified": bool(verdict[0].item() == 1.0), "n": n, "steps": steps,
+           "max_abs_diff": float(verdict[1].item())}
+    if arith == "fast":
+        out["bound"] = bound
+    return out

@@ -113,6 +113,19 @@ class IcSpec:
     ky: float = 1.0
     pad: float = 1.0
 
+    def sterbenz_safe(self) -> bool:
+        """Every value this IC puts in the field lies in [m, 2m], m > 0 (the
+        C++ twin: config.hpp ic_sterbenz_safe). FTCS at r <= 1/4 keeps the
+        field in that range, so every sum - 4c is exact and the r = 1/4 form
+        ("jacobi") rounds bitwise like the reference update."""
+        if self.kind in (IC_UNIFORM, IC_BOX, IC_INDEX_BOX):
+            vals = (self.a, self.b, self.pad)
+        elif self.kind == IC_CONST:
+            vals = (self.a, self.pad)
+        else:
+            return False
+        return min(vals) > 0 and max(vals) <= 2 * min(vals)
+
     def to_native(self):
         from ..ops import _native as N
         p = N.IcParams()

@@ -28,12 +28,13 @@ def tb():
         p = isa_report.tb_params(k["name"])
         if p:
             ks[p] = k
-    # main/gen x 3 arith x (ring 4: fp32 K 1..20 + fp64 K 1..24; ring 6: fp32
+    # main/gen x 4 arith x (ring 4: fp32 K 1..20 + fp64 K 1..24; ring 6: fp32
     # K 1..16 + fp64 K 1..24), the fp32 general ring-8 kernels of single
-    # launches (3 arith x K 1..16), plus the fused-statistics variants
-    # (general, ring 4, 3 arith)
-    assert sum(len(p) == 6 for p in ks) == 6 * (20 + 24) + 6 * (16 + 24) + 3 * 16, len(ks)
-    assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 3 * (20 + 24), len(ks)
+    # launches (4 arith x K 1..16), plus the fused-statistics variants
+    # (general, ring 4, 4 arith); the fused-cycle interior kernels (3 arith)
+    assert sum(len(p) == 6 for p in ks) == 8 * (20 + 24) + 8 * (16 + 24) + 4 * 16, len(ks)
+    assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 4 * (20 + 24), len(ks)
+    assert sum(len(p) == 7 and p[6] == "fused" for p in ks) == 3 * ((20 + 24) + (16 + 24)), len(ks)
     return ks
 
 
@@ -46,7 +47,7 @@ def test_occupancy_floors(tb):
     for k in (11,):
         assert tb[("fp64", 1, k, 4, True, 1)]["waves_per_simd"] >= 4, k
     for k in range(1, 12):  # the packed fp32 interior kernel keeps >= 3 waves/SIMD up to K = 11
-        for ar in (0, 1, 2):
+        for ar in (0, 1, 2, 3):
             assert tb[("fp32", 1, k, 4, True, ar)]["waves_per_simd"] >= 3, k
 
 
@@ -55,12 +56,12 @@ def test_deep_fp64_interior_two_waves(tb):
     must keep 2 waves/SIMD with ring 4 there (the general one may drop to 1;
     the r = 1/4 K = 20 kernel with ring 6)."""
     for k in range(17, 25):
-        for ar in (0, 1, 2):
+        for ar in (0, 1, 2, 3):
             ring = 6 if (ar, k) == (2, 20) else 4  # r = 1/4, K = 20: ring 4 needs 258 VGPRs, ring 6 fits
             assert tb[("fp64", 1, k, ring, True, ar)]["waves_per_simd"] >= 2, (k, ar)
     assert not any(p[0] == "fp32" and p[2] > 20 for p in tb)
     for k in range(17, 21):  # fp32 K = 17..20: the interior kernel keeps 2 waves/SIMD at ring 4 (floor)
-        for ar in (0, 1, 2):
+        for ar in (0, 1, 2, 3):
             assert tb[("fp32", 1, k, 4, True, ar)]["waves_per_simd"] >= 2, (k, ar)
 
 

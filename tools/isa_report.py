@@ -44,19 +44,24 @@ def kernels(so_path):
             f = os.path.join(td, f"co{i}.o")
             open(f, "wb").write(blob)
             txt = subprocess.run([READELF, "--notes", f], capture_output=True, text=True, check=True).stdout
-            for block in txt.split("  - .")[1:]:
-                block = "." + block
-                name = re.search(r"\.name:\s+(\S+)", block)
-                if not name or name.group(1).endswith(".kd"):
+            # one metadata map per kernel, keys in alphabetical order:
+            # .agpr_count ... .name ... .private_segment_fixed_size ... .vgpr_count
+            for m in re.finditer(r"\.name:\s+(\S+)", txt):
+                name = m.group(1)
+                if name.endswith(".kd") or not name.startswith("_Z"):
                     continue
+                end = txt.find(".vgpr_count", m.end())
+                end = txt.find("\n", end) if end >= 0 else len(txt)
+                start = txt.rfind(".agpr_count", 0, m.start())
+                block = txt[start if start >= 0 else m.start():end]
 
-                def field(key, default=0):
-                    m = re.search(r"\." + key + r":\s+(\d+)", block)
-                    return int(m.group(1)) if m else default
+                def field(key, default=0, block=block):
+                    f = re.search(r"\." + key + r":\s+(\d+)", block)
+                    return int(f.group(1)) if f else default
                 vg, ag = field("vgpr_count"), field("agpr_count")
                 # unified register file: 512 per SIMD lane, 8-register granule
                 regs = ((vg + 7) // 8) * 8 + ((ag + 3) // 4) * 4
-                out.append({"name": name.group(1), "triple": triple, "vgpr": vg, "agpr": ag,
+                out.append({"name": name, "triple": triple, "vgpr": vg, "agpr": ag,
                             "sgpr": field("sgpr_count"), "scratch": field("private_segment_fixed_size"),
                             "waves_per_simd": min(8, 512 // max(regs, 1))})
     return out
@@ -89,7 +94,7 @@ def main():
             continue
         p = tb_params(k["name"])
         tag = (f"tb_kernel<{p[0]}, NV={p[1]}, K={p[2]:2d}, RING={p[3]}, {'main' if p[4] else 'gen '}, "
-               f"{('exact', 'fma', 'jacobi')[p[5]]}>") if p else k["name"][:60]
+               f"{('exact', 'fma', 'jacobi', 'fast')[p[5]]}{', ' + p[6] if len(p) > 6 else ''}>") if p else k["name"][:60]
         print(f"{tag:55s} vgpr {k['vgpr']:3d} agpr {k['agpr']:3d} scratch {k['scratch']:4d} "
               f"waves/SIMD {k['waves_per_simd']}")
 
