@@ -78,7 +78,7 @@ def test_cpu_fma_decomposition_bitwise(native, P):
 
 def test_bad_arith(native):
     with pytest.raises(ValueError):
-        HeatSolver(prob(8, 1), backend="cpu", arith="fast")
+        HeatSolver(prob(8, 1), backend="cpu", arith="fastest")
 
 
 @pytest.mark.gpu
