@@ -366,6 +366,7 @@ def main():
     stats = s.stats() if args.check else None
     phases = s.phase_times() if args.phase_timers else None
     plan_cache = {"hits": s.plan_cache_hits, "path": N.plan_cache_path()} if hip else None
+    tune = s.tune_stats if hip else None
     measured = s.schedule(args.steps) is not None
     s.close()
     tr.close()
@@ -411,6 +412,7 @@ def main():
                 "schedule": "measured" if measured else "balanced",
                 "prepare_s": round(prepare_s, 2),
                 "plan_cache": plan_cache,
+                "autotune": tune,
                 "arith": arith_name(prob.r, arith) + {"auto": " (auto)", "bench": " (r = 1/4)" if prob.r == 0.25
                                                       else " (auto)"}.get(args.arith, ""),
                 "overlap": not args.no_overlap,

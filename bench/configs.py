@@ -58,6 +58,8 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False, arith="bench", 
            "cycles": {str(k): c for k, c in sorted(hist.items())}, "field_gb": round(s.layout.elems() * es / 1e9, 2),
            "init_s": round(t_init, 3), "prepare_s": round(prepare_s, 2), "finite": bool(math.isfinite(st["sum"]))}
     if backend == "hip":
+        rec["autotune"] = s.tune_stats
+    if backend == "hip":
         plans, traffic = {}, 0.0
         for k, c in sorted(hist.items()):
             pl = s.plan(k)

@@ -482,6 +482,13 @@ int heat2d_solver_ghost_rows(void* s, int32_t* out) {
   return guarded([&] { *out = static_cast<Solver*>(s)->ghost_rows(); });
 }
 
+int heat2d_solver_tune_stats(void* s, int64_t* depths, int64_t* candidates) {
+  return guarded([&] {
+    *depths = static_cast<Solver*>(s)->depths_tuned();
+    *candidates = static_cast<Solver*>(s)->tune_trials();
+  });
+}
+
 int heat2d_solver_plan_cache_hits(void* s, int64_t* out) {
   return guarded([&] { *out = static_cast<Solver*>(s)->plan_cache_hits(); });
 }

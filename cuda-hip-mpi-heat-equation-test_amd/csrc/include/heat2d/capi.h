@@ -185,6 +185,8 @@ int heat2d_solver_halo_rows(void* s, int reset, int64_t* out);
 int heat2d_solver_ghost_rows(void* s, int32_t* out);
 // Plans / schedules the solver took from the persistent plan cache; the cache file path.
 int heat2d_solver_plan_cache_hits(void* s, int64_t* out);
+// Depths autotuned in this process and candidate plans screened for them.
+int heat2d_solver_tune_stats(void* s, int64_t* depths, int64_t* candidates);
 int heat2d_plan_cache_path(char* buf, int64_t cap);
 // Where the depth-k split plan came from: 0 planned (not autotuned), 1 autotuned in
 // this process, 2 the plan cache (re-validated), -1 not planned yet.

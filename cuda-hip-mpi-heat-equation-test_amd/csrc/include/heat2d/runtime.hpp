@@ -340,6 +340,13 @@ class Solver {
   // origin of the depth-k split plan: -1 not planned, 0 planned (no autotune),
   // 1 autotuned here, 2 taken from the plan cache (re-validated)
   int plan_origin(int k) const { return k >= 1 && k <= kMaxTB ? plan_origin_[k] : -1; }
+  // depths autotuned in this process and candidate plans screened for them
+  int64_t depths_tuned() const {
+    int64_t n = 0;
+    for (int k = 1; k <= kMaxTB; ++k) n += plan_origin_[k] == 1;
+    return n;
+  }
+  int64_t tune_trials() const { return tune_trials_; }
   int spare_waves() const;
   // Phase timers (hipEvents on the GPU timeline) for every cycle while
   // enabled: [main ms, edge ms, exchange ms, whole-cycle ms (serial schedule),
@@ -391,6 +398,7 @@ class Solver {
   void ensure_sig();
   void run_schedule_graph(int64_t n);
   float depth_ms(int k);
+  float prescan_ms(int k);  // default-plan cycle time of depth k, max over ranks (schedule prescan)
   std::vector<int> choose_schedule(int64_t n);
 
   SolverConfig cfg_;
@@ -434,6 +442,8 @@ class Solver {
   // (both streams), keyed by (steps, starting buffer parity)
   std::map<std::pair<int64_t, int>, hipGraphExec_t> sched_graph_;
   float depth_ms_[kMaxTB + 1] = {};            // cycle ms per depth, max over ranks (schedule search)
+  float pre_ms_[kMaxTB + 1] = {};              // default-plan cycle ms per depth, max over ranks (prescan)
+  int64_t tune_trials_ = 0;                    // candidate plans the autotuner screened
   int compute_cus_ = 0;  // CUs of the (possibly CU-masked) compute stream; 0 = all
   kern::SplitPlan split_[kMaxTB + 1] = {};  // per temporal depth (k == 0: not planned yet)
   float tuned_ms_[kMaxTB + 1] = {};           // autotuned cycle time (ms), 0 if not tuned

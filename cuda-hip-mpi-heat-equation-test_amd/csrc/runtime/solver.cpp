@@ -655,7 +655,8 @@ static uint64_t plan_env_hash() {
     uint64_t v = 1469598103934665603ull;
     for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_TUNE_SEGMENTS", "HEAT2D_FUSED", "HEAT2D_W_ROW", "HEAT2D_W_COL",
                              "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
-                             "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES"}) {
+                             "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
+                             "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN"}) {
       const char* e = std::getenv(name);
       const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
       for (unsigned char c : kv) v = (v ^ c) * 1099511628211ull;
@@ -716,17 +717,28 @@ bool Solver::cached_split(int k) {
   return true;
 }
 
+// Staged screening (HEAT2D_TUNE_STAGED=0: every candidate over 4 cycles, the 4
+// best over 12, as round 3): stage A times every candidate over ONE cycle
+// (after one warm-up cycle), stage B the 6 best of A over 4, stage C the 3 best
+// of B over 12 — about half the trial cycles at the same winner (the leaders
+// are 1-2 % apart, which stage C resolves). Cycles longer than kLongCycleMs
+// (the full-HBM grids: ~50 ms per pass) screen a reduced candidate family.
+static bool staged_tuning() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_TUNE_STAGED");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+constexpr float kLongCycleMs = 8.0f;
+
 void Solver::autotune_split(int k) {
   const int spare = spare_waves();
   synchronize();
-  auto time_plan = [&](const kern::SplitPlan& c, int kTimed) { return this->time_plan(c, kTimed); };
-  // pass 1: every candidate over 4 steady-state cycles; pass 2: the 4 fastest
-  // re-timed over 12 cycles each (the spread between the leaders is ~1-2 %,
-  // about the noise of a 4-cycle sample)
-  std::vector<std::pair<float, kern::SplitPlan>> timed;
+  const bool staged = staged_tuning();
   kern::SplitPlan best = split_[k];
-  float best_ms = time_plan(best, 4);
-  timed.emplace_back(best_ms, best);
+  const float base_ms = time_plan(best, staged ? 2 : 4);
+  const bool long_cycles = staged && base_ms > kLongCycleMs;
   const int64_t nb0 = best.main.nb;
   // without an exchange to hide, a single general launch per cycle competes too
   const bool single_ok = !tr_->exchanges();
@@ -737,27 +749,34 @@ void Solver::autotune_split(int k) {
   // exchange of the bands running beside the interior (valid = 3)
   bool top = false, bot = false;
   sent_sides(&top, &bot);
+  std::vector<kern::SplitPlan> cands{best};
   auto add = [&](const kern::SplitPlan& c) {
-    timed.emplace_back(time_plan(c, 4), c);
+    cands.push_back(c);
     // more items than waves: also with the dynamic item queue (faster waves
     // take more items; per-wave timelines of the 32768^2 fp64 interior showed
     // a bimodal spread of up to 25 % between equal items: profiles/r3/wt3/)
     if (dynamic_candidates() && c.main_items > c.main_waves && c.valid >= 1 && c.valid <= 3) {
       kern::SplitPlan d = c;
       d.flags |= kern::kPlanDynamic;
-      timed.emplace_back(time_plan(d, 4), d);
+      cands.push_back(d);
     }
   };
+  if (dynamic_candidates() && best.main_items > best.main_waves && best.valid >= 1 && best.valid <= 3) {
+    kern::SplitPlan d = best;
+    d.flags |= kern::kPlanDynamic;
+    cands.push_back(d);
+  }
+  const std::vector<double> factors = long_cycles ? std::vector<double>{1.0, 0.5, 2.0}
+                                                  : std::vector<double>{1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 1.25, 1.5, 2.0};
   for (int mode : {1, 2, 3, 4}) {
     if (mode == 2 && !single_ok) continue;
     if (mode == 4) {
       // fused (exchange gated on the interior launch's band items): like the
       // edge-first order it needs an interior long enough to hide the exchange
-      if (!fused_candidates() || !fused_ok() || best.valid != 1 || timed.front().first < kEdgeFirstMinCycleMs)
-        continue;
+      if (!fused_candidates() || !fused_ok() || best.valid != 1 || base_ms < kEdgeFirstMinCycleMs) continue;
       for (int ring : {4, 6}) {
         kern::SplitPlan c = kern::plan_fused(dtype(), L_, k, k, top, bot, compute_cus_, spare, ring, cfg_.arith);
-        if (c.valid) timed.emplace_back(time_plan(c, 4), c);
+        if (c.valid) cands.push_back(c);
       }
       continue;
     }
@@ -766,12 +785,12 @@ void Solver::autotune_split(int k) {
     // hide it (measured on the 1-rank RCCL rehearsal, profiles/multi_gpu_rehearsal_v4.md:
     // fp64 slabs of 4096-16384 rows +2-4 %; a 4096-row fp32 slab, whose
     // interior cycle is 0.28 ms, lost 7 % to an exposed exchange)
-    if (mode == 3 && (single_ok || best.valid != 1 || timed.front().first < kEdgeFirstMinCycleMs)) continue;
+    if (mode == 3 && (single_ok || best.valid != 1 || base_ms < kEdgeFirstMinCycleMs)) continue;
     // ring 8 (6 rows in flight): fp32 single launches only (stencil_tb.hip ring_ok)
     const std::vector<int> rings = (mode == 2 && dtype() == DType::F32 && k <= 16) ? std::vector<int>{4, 6, 8}
                                                                                      : std::vector<int>{4, 6};
     for (int ring : rings) {
-      for (double f : {1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 1.25, 1.5, 2.0}) {
+      for (double f : factors) {
         const int64_t nb = std::max<int64_t>(1, (int64_t)((mode == 2 ? nb1 : nb0) * f + 0.5));
         if (mode == 1 && ring == best.ring && nb == best.main.nb) continue;
         kern::SplitPlan c = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, nb, cfg_.arith)
@@ -793,9 +812,10 @@ void Solver::autotune_split(int k) {
       const int64_t w0 = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, 0, cfg_.arith).main_waves
                                    : best.main_waves;
       std::vector<int64_t> segs;
-      for (double f : {0.5, 1.0, 1.5, 2.0}) segs.push_back(std::max<int64_t>(1, (int64_t)(w0 * f + 0.5)));
-      if (dynamic_candidates()) segs.push_back(4 * w0);  // (timed with the dynamic queue, add())
-      if (mode == 2 && cfg_.arith == 2) {
+      for (double f : long_cycles ? std::vector<double>{1.0} : std::vector<double>{0.5, 1.0, 1.5, 2.0})
+        segs.push_back(std::max<int64_t>(1, (int64_t)(w0 * f + 0.5)));
+      if (dynamic_candidates()) segs.push_back(4 * w0);  // (timed with the dynamic queue too, add())
+      if (mode == 2 && cfg_.arith == 2 && !long_cycles) {
         // r = 1/4 single launches: strip-aligned segment counts too (a whole
         // number per strip), whose frame-row items the plan can weight
         // (stencil_tb.hip weighted_main) — one per SIMD and one per wave
@@ -818,15 +838,20 @@ void Solver::autotune_split(int k) {
       }
     }
   }
-  std::sort(timed.begin(), timed.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-  best_ms = 1e30f;
-  for (size_t i = 0; i < std::min<size_t>(4, timed.size()); ++i) {
-    const float ms = time_plan(timed[i].second, 12);
-    if (ms < best_ms) {
-      best_ms = ms;
-      best = timed[i].second;
-    }
+  // screening: (cycles per trial, candidates kept) per stage
+  using Stage = std::pair<int, size_t>;
+  const std::vector<Stage> stages = staged ? std::vector<Stage>{{1, 6}, {4, 3}, {12, 1}}
+                                           : std::vector<Stage>{{4, 4}, {12, 1}};
+  std::vector<std::pair<float, kern::SplitPlan>> timed;
+  for (const auto& c : cands) timed.emplace_back(0.f, c);
+  for (const Stage& st : stages) {
+    for (auto& t : timed) t.first = time_plan(t.second, st.first);
+    std::stable_sort(timed.begin(), timed.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    timed.resize(std::min(timed.size(), st.second));
   }
+  best = timed.front().second;
+  const float best_ms = timed.front().first;
+  tune_trials_ += (int64_t)cands.size();
   synchronize();
   best.k = k;
   split_[k] = best;
@@ -1194,8 +1219,63 @@ float Solver::depth_ms(int k) {
 // depths (n/c, rounded) are the best split; scan c upward from ceil(n/Kmax)
 // and stop once the base depth's per-step cost is 25 % worse than the best
 // seen (deeper into the HBM-bound region it only gets worse).
+// Prescan (HEAT2D_SCHED_PRESCAN=0 disables): the scan above needs the cycle
+// time of every depth it visits — ~15 depths for 480 steps, each autotuned
+// (~30 trial cycles of ~100 candidates: 44 s at 32768^2 fp64 in round 3).
+// Instead the scan runs on each depth's DEFAULT plan (1 warm-up + 2 timed
+// cycles, max over ranks), keeps the schedules within 20 % of its best (up to
+// 4, one per base depth), and only their depths are autotuned; the schedule
+// with the smallest autotuned cost wins.
+static bool sched_prescan() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_SCHED_PRESCAN");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+float Solver::prescan_ms(int k) {
+  if (pre_ms_[k] == 0.f) {
+    double v = 0.0;
+    if (tuned_ms_[k] > 0.f) {
+      v = tuned_ms_[k];
+    } else {
+      const kern::SplitPlan base = kern::plan_split(dtype(), L_, k, k, compute_cus_, spare_waves(), 0, 0, cfg_.arith);
+      if (base.valid) {
+        synchronize();
+        v = time_plan(base, 2);
+        H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+        H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+        synchronize();
+      }
+    }
+    tr_->allreduce(&v, 1, 1);
+    pre_ms_[k] = v > 0 ? (float)v : -1.f;
+  }
+  return pre_ms_[k];
+}
+
 std::vector<int> Solver::choose_schedule(int64_t n) {
-  return cycle_schedule(n, cfg_.tb, [this](int k) { return (double)depth_ms(k); });
+  if (!sched_prescan()) return cycle_schedule(n, cfg_.tb, [this](int k) { return (double)depth_ms(k); });
+  const auto near = cycle_schedule_near(n, cfg_.tb, [this](int k) { return (double)prescan_ms(k); }, 0.20, 4);
+  std::vector<int> best;
+  double best_cost = 1e300;
+  for (const auto& sc : near) {  // the same order and depths on every rank: depth_ms is collective
+    double cost = 0.0;
+    for (int k : sc) {
+      const double t = depth_ms(k);
+      if (t < 0) {
+        cost = -1.0;
+        break;
+      }
+      cost += t;
+    }
+    if (cost >= 0.0 && cost < best_cost) {
+      best_cost = cost;
+      best = sc;
+    }
+  }
+  return best;
 }
 
 std::vector<int> cycle_schedule(int64_t n, int kmax, const std::function<double(int)>& t) {

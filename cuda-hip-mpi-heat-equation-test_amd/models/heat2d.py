@@ -251,6 +251,13 @@ class HeatSolver:
         return v.value
 
     @property
+    def tune_stats(self) -> dict:
+        """{"depths": depths autotuned in this process, "candidates": plans screened for them}."""
+        d, c = C.c_int64(), C.c_int64()
+        N.call("heat2d_solver_tune_stats", self._h, C.byref(d), C.byref(c))
+        return {"depths": d.value, "candidates": c.value}
+
+    @property
     def ghost_rows(self) -> int:
         """Valid ghost rows of the current field (the last exchange's depth)."""
         v = C.c_int32()

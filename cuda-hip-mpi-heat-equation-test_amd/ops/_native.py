@@ -194,6 +194,7 @@ _SIGS = {
     "heat2d_solver_ghost_rows": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "heat2d_autotune_slabs": (C.c_int, [_I64, _I64, C.c_int, C.c_int, C.POINTER(C.c_int32)]),
     "heat2d_solver_plan_cache_hits": (C.c_int, [_P, C.POINTER(C.c_int64)]),
+    "heat2d_solver_tune_stats": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "heat2d_plan_cache_path": (C.c_int, [C.c_char_p, _I64]),
     "heat2d_solver_plan_origin": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int32)]),
 }
