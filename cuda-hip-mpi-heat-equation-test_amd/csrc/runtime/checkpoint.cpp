@@ -50,8 +50,9 @@ void fsync_path(const std::string& path) {
   const int fd = ::open(path.c_str(), O_RDONLY);
   HEAT2D_REQUIRE(fd >= 0, "cannot open " + path + " to fsync");
   const int rc = ::fsync(fd);
+  const int err = errno;  // (close may overwrite it)
   ::close(fd);
-  HEAT2D_REQUIRE(rc == 0 || errno == EINVAL, "fsync failed on " + path);
+  HEAT2D_REQUIRE(rc == 0 || err == EINVAL, "fsync failed on " + path);
 }
 
 std::string parent_dir(const std::string& path) {
@@ -162,13 +163,31 @@ NpyInfo npy_header(FILE* f, const std::string& path) {
 
 }  // namespace
 
+// A name no earlier save of this step used, sorting after all of them (and
+// before the next step): `base` for the first save, then base-000001,
+// base-000002, ... one past the highest generation present — never a gap a
+// pruned generation left, so name order stays write order for pruning.
 std::string step_dir_name(const std::string& dir, int64_t step) {
   const std::string base = step_name(step);
-  if (!exists(join(dir, base))) return base;
-  for (int g = 1;; ++g) {  // sorts after `base` and before the next step: pruning order holds
-    const std::string name = base + "-" + std::to_string(g);
-    if (!exists(join(dir, name))) return name;
+  bool any = false;
+  long long gmax = 0;
+  if (DIR* d = ::opendir(dir.c_str())) {
+    while (dirent* e = ::readdir(d)) {
+      const std::string n = e->d_name;
+      if (n.compare(0, base.size(), base) != 0) continue;
+      if (n.size() == base.size()) {
+        any = true;
+      } else if (n.size() == base.size() + 7 && n[base.size()] == '-') {
+        any = true;
+        gmax = std::max(gmax, std::atoll(n.c_str() + base.size() + 1));
+      }
+    }
+    ::closedir(d);
   }
+  if (!any) return base;
+  char b[16];
+  std::snprintf(b, sizeof(b), "-%06lld", gmax + 1);
+  return base + b;
 }
 
 void write_rank(const std::string& dir, const std::string& name, int rank, Solver& s) {

@@ -38,15 +38,22 @@ def step_dir(directory: str, step: int) -> str:
 
 
 def fresh_step_dir(directory: str, step: int) -> str:
-    """A step directory name no earlier save used (sorts after the older
-    generations of the same step and before the next step)."""
+    """A step directory name no earlier save used, sorting after all of them
+    (and before the next step): the bare name first, then -000001, -000002,
+    ... one past the highest generation present (a pruned generation's name
+    is never reused, so name order stays write order; csrc twin:
+    checkpoint.cpp step_dir_name)."""
     base = step_dir(directory, step)
-    if not os.path.exists(base):
+    name = os.path.basename(base)
+    try:
+        entries = os.listdir(directory)
+    except FileNotFoundError:
+        entries = []
+    gens = [int(e[len(name) + 1:]) for e in entries
+            if e.startswith(name + "-") and len(e) == len(name) + 7 and e[len(name) + 1:].isdigit()]
+    if name not in entries and not gens:
         return base
-    g = 1
-    while os.path.exists(f"{base}-{g}"):
-        g += 1
-    return f"{base}-{g}"
+    return f"{base}-{max(gens, default=0) + 1:06d}"
 
 
 def _fsync_dir(path: str) -> None:

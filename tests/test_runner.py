@@ -224,7 +224,7 @@ def test_checkpoint_resave_same_step_never_overwrites(native, tmp_path, writer):
     (tmp_path / "input.dat").write_text("44 0.25 0.05 1.0 9 1\n")
     ck = tmp_path / "ck"
     prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
-    for _ in range(2):
+    for _ in range(4):
         if writer == "native":
             subprocess.run([N.CLI_PATH, "--cpu", "--quiet", "--tb", "3", "--checkpoint", "ck", "--output", "none"],
                            cwd=tmp_path, check=True, capture_output=True)
@@ -233,9 +233,11 @@ def test_checkpoint_resave_same_step_never_overwrites(native, tmp_path, writer):
             s.step(9)
             checkpoint.save(s, str(ck))
             s.close()
+    # generations are zero-padded and never reuse a pruned name: name order is
+    # write order, and pruning keeps the two newest
     names = sorted(d.name for d in ck.iterdir() if d.name.startswith("step-"))
-    assert names == ["step-000000000009", "step-000000000009-1"]
-    assert (ck / "latest").read_text().strip() == "step-000000000009-1"
+    assert names == ["step-000000000009-000002", "step-000000000009-000003"]
+    assert (ck / "latest").read_text().strip() == "step-000000000009-000003"
     assert checkpoint.load_meta(str(ck))["step"] == 9
     s = HeatSolver(prob, dtype="fp64", backend="cpu", tb=3)
     checkpoint.load(s, str(ck))

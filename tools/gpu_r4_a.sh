@@ -12,18 +12,12 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 rc=$?; echo "tests rc=$rc"; tail -3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log || exit 1
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench20.json 2> $O/bench20.err && cat $O/bench20.json || exit 1
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --sigma 0.2 --arith fast > $O/s02_fast.json 2> $O/s02_fast.err || exit 1
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --sigma 0.2 > $O/s02_auto.json 2> $O/s02_auto.err || exit 1
-mkdir -p $O/ref && cd $O/ref && printf "32768 0.25 0.05 1.0 25000 0\n" > input.dat
-timeout -k 10 300 $BIN input.dat --output none --json auto.json > auto.txt 2>&1 && tail -4 auto.txt || exit 1
-timeout -k 10 300 $BIN input.dat --output none --time-transfers --json auto_tt.json > auto_tt.txt 2>&1 && tail -4 auto_tt.txt || exit 1
-timeout -k 10 300 $BIN input.dat --output none --arith fma --json fma.json > fma.txt 2>&1 && tail -3 fma.txt || exit 1
-cd $GRAFT_REPO_ROOT
-for t in rccl ipc; do
-  timeout -k 10 200 python -u bench.py --rehearse-comm --transport $t --rows 4096 --steps 20 --warmup 5 --phase-timers > $O/reh64_$t.json 2> $O/reh64_$t.err || exit 1
-  timeout -k 10 200 python -u bench.py --dtype fp32 --rehearse-comm --transport $t --rows 4096 --steps 480 --warmup 20 > $O/reh32_$t.json 2> $O/reh32_$t.err || exit 1
+# prepare(): staged screening + prescan (new) vs the exhaustive search (old), interleaved
+for i in 1 2; do
+  HEAT2D_TUNE_STAGED=0 HEAT2D_SCHED_PRESCAN=0 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/b20_old_$i.json 2> $O/b20_old_$i.err || exit 1
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/b20_new_$i.json 2> $O/b20_new_$i.err || exit 1
 done
-for i in 1 2 3; do
-  timeout -k 10 200 python -u bench.py --grid 4096 --dtype fp32 --steps 1000 --warmup 100 > $O/small_$i.json 2> $O/small_$i.err || exit 1
-done
-for f in $O/*.json; do python -c "import json; d=json.load(open('$f')); c=d['config']; print('$f', d['value'], c['transport'], c['cycles'], c['prepare_s'], c['arith'], d.get('verified'))"; done
+HEAT2D_TUNE_STAGED=0 HEAT2D_SCHED_PRESCAN=0 timeout -k 10 400 python -u bench.py --steps 480 --warmup 48 > $O/b480_old.json 2> $O/b480_old.err || exit 1
+timeout -k 10 400 python -u bench.py --steps 480 --warmup 48 > $O/b480_new.json 2> $O/b480_new.err || exit 1
+timeout -k 10 400 python -u bench/configs.py --only gpu-max-fp32 > $O/max_new.json 2> $O/max_new.err || exit 1
+python tools/summarize_json.py $O/*.json
