@@ -223,8 +223,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base, uin
 // place of 4. With X_s = T_s / r^s the update T' = (1 - 4r) C + r (S+E+N+W)
 // becomes X_{s+1} = fma(b, X_s(C), ((S + E) + N) + W), b = (1 - 4r) / r: 3 adds
 // + 1 fma per point and level instead of 5 ops (arith 1); the stored level is
-// multiplied by r^K once. Kind-0 items only; pinned kinds run arith 1's
-// contracted form unscaled (the frame must stay bit-exact). Not the
+// multiplied by r^K once. Kind-0 items only; pinned kinds (the frame must stay
+// bit-exact) run arith 2's unscaled forms with the centre weight ke = 1 - 4r
+// instead of 0: kind 1 fma(ke, C, r * sum), kinds 2 / 3 r * sum + (C - 4rC)
+// as two fmas. Not the
 // reference's rounding: within a stated bound of it (tests/test_arith_fast.py,
 // |T_fast - T_exact| <= 16 n u max|T_0| after n steps, u the unit roundoff),
 // and, since interior and pinned items round differently, the bits depend on
@@ -344,6 +346,7 @@ struct March {
   int32_t st_off;    // per-lane vector store offset (kOob unless the lane holds output columns)
   T rl[(EK & 2) ? V : 1];  // EK & 2: r per element, 0 in Dirichlet / pad columns
   T fb, fu, fu1;           // AR 3: TbArgs::fb / fu / fu1
+  T fk;                    // AR 3: the centre weight 1 - 4r of the unscaled pinned kinds
   static constexpr bool kScaled = (AR == 2 || AR == 3) && EK == 0;  // levels carried scaled (AR 2: x 4^level, 3: / r^level)
 
   using Ch = ChainShape<K, CL>;
@@ -412,16 +415,17 @@ struct March {
       else re = frame_row ? T(0) : rl[e];
       if constexpr (AR == 3 && EK == 0) {
         out[e] = fma_t(fb, C[e], sum);  // scaled: T / r^s
-      } else if constexpr (AR == 2) {
+      } else if constexpr (AR == 2 || AR == 3) {
         // scaled kind 0: the plain sum (4^s T). Pinned kinds (re = 0 where
         // pinned), unscaled: kind 1 (frame rows: wave-uniform) fma(ke, C, re *
         // sum) with scalar ke = 1 - 4 re; kinds 2 / 3 (per-element re)
         // re * sum + (C - 4 re C). The added term is exactly 0 at updated
-        // points (re = 1/4) and C at pinned ones.
+        // points (re = 1/4) and C at pinned ones. (AR 3: ke = 1 - 4r at
+        // updated rows; at r = 1/4 the same bits as AR 2.)
         if constexpr (EK == 0) out[e] = sum;
-        else if constexpr (EK == 1) out[e] = fma_t(frame_row ? T(1) : T(0), C[e], re * sum);
+        else if constexpr (EK == 1) out[e] = fma_t(frame_row ? T(1) : (AR == 3 ? fk : T(0)), C[e], re * sum);
         else out[e] = fma_t(re, sum, fma_t(re, T(-4) * C[e], C[e]));
-      } else if constexpr (AR == 1 || AR == 3) {  // (AR 3 pinned kinds: unscaled, contracted)
+      } else if constexpr (AR == 1) {
         out[e] = fma_t(re, fma_t(T(-4), C[e], sum), C[e]);
       } else {
         out[e] = C[e] + re * fma_t(T(-4), C[e], sum);
@@ -602,6 +606,7 @@ struct MarchF32 {
   int32_t st_off;
   Row rl;  // EK & 2: r per element (0 in Dirichlet / pad columns)
   float fb, fu, fu1;  // AR 3: TbArgs::fb / fu / fu1
+  float fk;           // AR 3: the centre weight 1 - 4r of the unscaled pinned kinds (see March)
   static constexpr bool kScaled = (AR == 2 || AR == 3) && EK == 0;  // levels carried scaled (see March)
   using Ch = ChainShape<K, CL>;
   static constexpr int L = Ch::unroll(RING);
@@ -669,12 +674,13 @@ struct MarchF32 {
       const F2 b2 = {fb, fb};
       return Row{__builtin_elementwise_fma(b2, C.a, sum.a), __builtin_elementwise_fma(b2, C.b, sum.b)};
     }
-    if constexpr (AR == 2) {
+    if constexpr (AR == 2 || AR == 3) {  // (AR 3, kind 0: above)
       const Row sum = sum4(part, C, N);
       if constexpr (EK == 0) return sum;  // scaled: 4^s T
       const bool frame_row = (EK & 1) && ((uint32_t)(row - fixed_lo) >= (uint32_t)(fixed_hi - fixed_lo));  // wave-uniform
       if constexpr (EK == 1) {  // fma(ke, C, re * sum), scalar (re, ke) (see March::update)
-        const F2 re = {frame_row ? 0.f : r, frame_row ? 0.f : r}, ke = {frame_row ? 1.f : 0.f, frame_row ? 1.f : 0.f};
+        const float k0 = frame_row ? 1.f : (AR == 3 ? fk : 0.f);
+        const F2 re = {frame_row ? 0.f : r, frame_row ? 0.f : r}, ke = {k0, k0};
         return Row{__builtin_elementwise_fma(ke, C.a, re * sum.a), __builtin_elementwise_fma(ke, C.b, re * sum.b)};
       }
       const F2 z = {0.f, 0.f};
@@ -683,13 +689,13 @@ struct MarchF32 {
     }
     Row in, re;
     terms(part, C, N, row, in, re);
-    if constexpr (AR == 1 || AR == 3)
+    if constexpr (AR == 1)
       return Row{__builtin_elementwise_fma(re.a, in.a, C.a), __builtin_elementwise_fma(re.b, in.b, C.b)};
     else
       return Row{C.a + re.a * in.a, C.b + re.b * in.b};
   }
   static __device__ __forceinline__ float fin(float re, float in, float c) {
-    if constexpr (AR == 1 || AR == 3) return __builtin_fmaf(re, in, c);
+    if constexpr (AR == 1) return __builtin_fmaf(re, in, c);
     else return c + re * in;
   }
   // The stored (last) level: its 4 final ops as scalar fp32 ops writing the
@@ -701,7 +707,7 @@ struct MarchF32 {
       return VT{__builtin_fmaf(fb, C.a.x, sum.a.x) * fu, __builtin_fmaf(fb, C.b.x, sum.b.x) * fu,
                 __builtin_fmaf(fb, C.a.y, sum.a.y) * fu, __builtin_fmaf(fb, C.b.y, sum.b.y) * fu};
     }
-    if constexpr (AR == 2) {
+    if constexpr (AR == 2 || AR == 3) {  // (AR 3, kind 0: above)
       const Row sum = sum4(part, C, N);
       if constexpr (EK == 0) {
         // unscale 4^K T once, at the store (exact)
@@ -710,7 +716,7 @@ struct MarchF32 {
       }
       const bool frame_row = (EK & 1) && ((uint32_t)(row - fixed_lo) >= (uint32_t)(fixed_hi - fixed_lo));  // wave-uniform
       if constexpr (EK == 1) {
-        const float re = frame_row ? 0.f : r, ke = frame_row ? 1.f : 0.f;
+        const float re = frame_row ? 0.f : r, ke = frame_row ? 1.f : (AR == 3 ? fk : 0.f);
         return VT{__builtin_fmaf(ke, C.a.x, re * sum.a.x), __builtin_fmaf(ke, C.b.x, re * sum.b.x),
                   __builtin_fmaf(ke, C.a.y, re * sum.a.y), __builtin_fmaf(ke, C.b.y, re * sum.b.y)};
       }
@@ -852,6 +858,7 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
   w.nrec = (uint32_t)(a.pitch * ES);
   w.r = r;
   if constexpr (AR == 3) {
+    w.fk = (T)(1.0 - 4.0 * (double)r);
     w.fb = (T)a.fb;
     w.fu = (T)a.fu;
     w.fu1 = (T)a.fu1;
