@@ -90,9 +90,12 @@ def choose_transport(candidates: Sequence[str], trial: Callable[[str], float],
 def candidate_transports(requested: str, world: int, hip: bool) -> List[str]:
     """Transports a run may use: one forced kind, or every GPU transport for
     "auto" (RCCL first: the reference's own model of an MPI-style fabric; IPC
-    second). Single-rank and CPU runs have nothing to choose."""
-    if not hip or world <= 1:
+    second). Single-rank runs have nothing to choose; CPU ranks have one
+    transport (torch.distributed host callbacks), run through the same trial."""
+    if world <= 1:
         return []
+    if not hip:
+        return ["torch-dist"]
     if requested == "auto":
         return ["rccl", "ipc"]
     return ["ipc" if requested in ("ipc", "peer") else "rccl"]

@@ -41,6 +41,18 @@ def test_bench_json_line_multi_rank(nproc, dtype):
     assert d["verified"] is True and d["verify"]["n"] == 256 * nproc + 5 and d["verify"]["max_abs_diff"] == 0.0
 
 
+def test_bench_multi_rank_times_the_same_state_as_one_rank():
+    """The transport trials run the timed loop before the timed run; the field
+    then goes back to the IC and the warm-up, so the timed run ends on the same
+    state a single-rank run does (field statistics equal)."""
+    args = ["--grid", "100", "--steps", "24", "--warmup", "4", "--tb", "4", "--check"]
+    two = run_bench(2, *args, port=29566)
+    one = run_plain("--backend", "cpu", "--gpus", "1", *args)
+    assert two["config"]["transport_choice"]["chosen"] == "torch-dist"
+    a, b = one["field_stats"], two["field_stats"]
+    assert a["min"] == b["min"] and a["max"] == b["max"] and b["sum"] == pytest.approx(a["sum"], rel=1e-12, abs=0)
+
+
 def test_bench_weak_mode():
     d = run_bench(2, "--grid", "64", "--weak", "--steps", "8", "--warmup", "2", "--tb", "4", port=29570)
     assert d["scaling"] == "weak" and d["config"]["grid"] == [91, 91]  # round(64 * sqrt(2))

@@ -51,7 +51,7 @@ def test_try_collective_cleans_up_on_remote_failure():
 
 @pytest.mark.parametrize("requested,world,hip,expect", [("auto", 8, True, ["rccl", "ipc"]), ("peer", 2, True, ["ipc"]),
                                                         ("rccl", 2, True, ["rccl"]), ("auto", 1, True, []),
-                                                        ("auto", 4, False, [])])
+                                                        ("auto", 4, False, ["torch-dist"])])
 def test_candidates(requested, world, hip, expect):
     assert select.candidate_transports(requested, world, hip) == expect
 
