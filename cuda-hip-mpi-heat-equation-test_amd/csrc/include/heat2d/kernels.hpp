@@ -85,6 +85,11 @@ struct SplitPlan {
   TbRect fused[kMaxFused];
   int64_t sig_items;
 };
+// The same plan with its boundary-band (EDGE) rects cut into `nb` row bands
+// each (valid = 1 / 3; default 1): more, shorter band items — nb x as many
+// waves for the latency-bound band launch, each marching B/nb + 2k rows
+// instead of B + 2k.
+SplitPlan with_edge_bands(DType dt, const SplitPlan& p, int64_t nb, int arith = 0);
 // ring_override: 4 | 6 (0: default); main_bands: MAIN row bands (0: persistent default;
 // < 0: -main_bands segments, TbRect)
 SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus = 0, int spare_waves = 0,

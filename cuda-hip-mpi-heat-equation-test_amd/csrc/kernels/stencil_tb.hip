@@ -580,6 +580,20 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
   return p;
 }
 
+SplitPlan with_edge_bands(DType dt, const SplitPlan& p, int64_t nb, int arith) {
+  SplitPlan q = p;
+  if (!(p.valid == 1 || p.valid == 3) || nb < 1) return q;
+  q.edge_items = 0;
+  for (int i = 0; i < q.nedge; ++i) {
+    TbRect& e = q.edge[i];
+    e.nb = std::max<int64_t>(1, std::min<int64_t>(nb, e.r1 - e.r0));
+    q.edge_items += e.nb * (e.s1 - e.s0);
+  }
+  const int bpc_e = occupancy(dt, q.ring, false, q.k, arith);
+  q.edge_waves = std::min<int64_t>(q.edge_items, (int64_t)cu_count() * bpc_e * 4);
+  return q;
+}
+
 SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool send_top, bool send_bottom, int cus,
                      int spare_waves, int ring_override, int arith) {
   check_layout(dt, L, k);

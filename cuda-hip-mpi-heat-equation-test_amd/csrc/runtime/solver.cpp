@@ -493,6 +493,9 @@ const kern::SplitPlan& Solver::split_plan(int k) {
         p.k = k;
       }
     }
+    // HEAT2D_EDGE_BANDS=n: the boundary-band rects cut into n row bands each (tests, A/B)
+    if (const char* e = std::getenv("HEAT2D_EDGE_BANDS"); e && std::atoll(e) > 0 && (p.valid == 1 || p.valid == 3))
+      p = kern::with_edge_bands(dtype(), p, std::atoll(e), cfg_.arith);
     // HEAT2D_MAX_WAVES=n: at most n waves for the main launch (tests: several items per wave)
     if (const char* e = std::getenv("HEAT2D_MAX_WAVES"); e && std::atoll(e) > 0 && p.valid >= 1 && p.valid <= 3)
       p.main_waves = std::min<int64_t>(p.main_waves, std::atoll(e));
@@ -520,6 +523,8 @@ const kern::SplitPlan& Solver::split_plan_banded(int k, int64_t B) {
   kern::SplitPlan d = kern::plan_split(dtype(), L_, k, B, compute_cus_, spare_waves(), base.ring, base.main.nb,
                                        cfg_.arith);
   if (d.valid) {
+    if (base.nedge > 0 && base.edge[0].nb > 1) d = kern::with_edge_bands(dtype(), d, base.edge[0].nb, cfg_.arith);
+    d.flags = base.flags;
     d.valid = base.valid;
     d.main_waves = std::min<int64_t>(d.main_items, std::max<int64_t>(1, base.main_waves));
   }
@@ -656,7 +661,7 @@ static uint64_t plan_env_hash() {
     for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_TUNE_SEGMENTS", "HEAT2D_FUSED", "HEAT2D_W_ROW", "HEAT2D_W_COL",
                              "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
                              "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
-                             "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN"}) {
+                             "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN", "HEAT2D_EDGE_BANDS"}) {
       const char* e = std::getenv(name);
       const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
       for (unsigned char c : kv) v = (v ^ c) * 1099511628211ull;
@@ -850,7 +855,23 @@ void Solver::autotune_split(int k) {
     timed.resize(std::min(timed.size(), st.second));
   }
   best = timed.front().second;
-  const float best_ms = timed.front().first;
+  float best_ms = timed.front().first;
+  // the winner's boundary bands cut into 2..4 row bands each: the band launch
+  // is latency-bound (one wave per strip and band, ~1 wave per SIMD, each
+  // marching B + 2k rows) — more, shorter items where the split leaves the
+  // chip room (its time is on the cycle's critical path in the edge-first order)
+  if (best.valid == 1 || best.valid == 3) {
+    for (int64_t nb : {2, 3, 4}) {
+      const kern::SplitPlan c = kern::with_edge_bands(dtype(), best, nb, cfg_.arith);
+      if (c.edge_items == best.edge_items) continue;
+      const float ms = time_plan(c, 12);
+      ++tune_trials_;
+      if (ms < best_ms) {
+        best_ms = ms;
+        best = c;
+      }
+    }
+  }
   tune_trials_ += (int64_t)cands.size();
   synchronize();
   best.k = k;

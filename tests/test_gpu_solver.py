@@ -269,6 +269,28 @@ def test_split_orders_with_exchange_bitwise(gpu, native, order, P, tb, dtype, n,
     assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
 
 
+@pytest.mark.parametrize("order,nb", [("edge-first", 3), ("concurrent", 2), ("edge-first", 40)])
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+def test_edge_band_plans_bitwise(gpu, native, order, nb, dtype, monkeypatch):
+    """Boundary-band rects cut into nb row bands each (kern::with_edge_bands,
+    HEAT2D_EDGE_BANDS; 40 > band rows: one-row items), split orders with real
+    loopback exchanges: bitwise the golden."""
+    monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
+    monkeypatch.setenv("HEAT2D_EDGE_BANDS", str(nb))
+    tb = 12 if dtype == "fp64" else 16
+    p = prob(1100, 2 * tb + 3, "ghost", "sine")
+    npdt = np.float64 if dtype == "fp64" else np.float32
+    g = LoopbackGroup(p, 3, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0)
+    g.upload(R.owned(R.initial_field(p, npdt)))
+    g.step(p.ntime)
+    got = g.download()
+    plans = [g.plan(i, tb) for i in range(3)]
+    g.close()
+    for pl in plans:
+        assert all(e[4] == min(nb, e[1] - e[0]) for e in pl["edge_rects"]), pl
+    assert np.array_equal(got, R.owned(R.ftcs(p, dtype=npdt)))
+
+
 @pytest.mark.parametrize("order,nseg", [("edge-first", 37), ("concurrent", 1000), ("single", 5), ("single", 4097),
                                         ("concurrent", -3), ("single", -40)])
 @pytest.mark.parametrize("dtype", ["fp64", "fp32"])
