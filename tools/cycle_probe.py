@@ -10,7 +10,8 @@ exchanges the slab's band rows with itself over a 1-rank RCCL communicator
 (the multi-GPU schedule rehearsal of bench.py --rehearse-comm); CP_AUTOTUNE=1
 autotunes the plan first (its trial cycles appear in a profile before the
 timed ones); CP_TIMERS=1 prints the hipEvent phase times of the timed cycles;
-CP_ARITH=exact|fma|jacobi picks the update form (default auto).
+CP_ARITH=exact|fma|jacobi|fast picks the update form (default auto); CP_SIGMA=s
+the FTCS coefficient (default 0.25).
 """
 import json
 import os
@@ -28,7 +29,7 @@ dtype, n, k, cycles = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.a
 overlap = bool(int(sys.argv[5])) if len(sys.argv) > 5 else True
 graph = bool(int(sys.argv[6])) if len(sys.argv) > 6 else False
 torch.cuda.set_device(0)
-inp = heat2d.InputDat(n=n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=k * cycles, soln=0, nfields=6)
+inp = heat2d.InputDat(n=n, sigma=float(os.environ.get("CP_SIGMA", "0.25")), nu=0.05, dom_len=1.0, ntime=k * cycles, soln=0, nfields=6)
 prob = heat2d.make_problem(inp, "ghost", "uniform")
 rows = int(os.environ.get("CP_ROWS", "0")) or None
 tr = None
