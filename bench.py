@@ -274,6 +274,7 @@ def main():
         return amax(t1 - t0)
 
     live = {}  # kind -> (transport, solver, prepare seconds)
+    warm_s = {}  # kind -> warm-up seconds
 
     def setup(kind):
         """Transport + solver + warm-up + prepare(steps), each phase collective:
@@ -286,8 +287,10 @@ def main():
         if why is not None:
             tr.close()
             raise select.Skip(why)
+        tw = time.perf_counter()
         s.step(args.warmup)
         s.synchronize()
+        warm_s[kind] = time.perf_counter() - tw  # (the warm-up's own depths are planned / autotuned here)
         # plan / autotune every depth the timed run uses, pick its cycle schedule
         # by measurement, and end on non-mutating trial cycles of that schedule
         # (GPU clocks as in a long run) — outside the timed region, after the warmup
@@ -424,6 +427,7 @@ def main():
                 "cycles": {str(k): c for k, c in sorted(hist.items())},
                 "schedule": "measured" if measured else "balanced",
                 "prepare_s": round(prepare_s, 2),
+                "warmup_s": round(warm_s.get(kind, 0.0), 2),
                 "plan_cache": plan_cache,
                 "autotune": tune,
                 "arith": arith_name(prob.r, arith) + {"auto": " (auto)", "bench": " (r = 1/4)" if prob.r == 0.25

@@ -38,8 +38,10 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False, arith="bench", 
     t_init = time.perf_counter() - t_init
     # as bench.py: warm-up, then plan / autotune / pick the cycle schedule of the
     # timed run by measurement, outside the timed region
+    tw = time.perf_counter()
     s.step(warmup)
     s.synchronize()
+    warm_s = time.perf_counter() - tw  # (the warm-up's own depths are planned / autotuned here)
     tp = time.perf_counter()
     s.prepare(steps)
     prepare_s = time.perf_counter() - tp
@@ -56,7 +58,7 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False, arith="bench", 
            "graph": graph,
            "steps": steps, "s": round(dt, 6), "ms_per_step": round(dt / steps * 1e3, 5), "gpts": round(gpts, 2),
            "cycles": {str(k): c for k, c in sorted(hist.items())}, "field_gb": round(s.layout.elems() * es / 1e9, 2),
-           "init_s": round(t_init, 3), "prepare_s": round(prepare_s, 2), "finite": bool(math.isfinite(st["sum"]))}
+           "init_s": round(t_init, 3), "prepare_s": round(prepare_s, 2), "warmup_s": round(warm_s, 2), "finite": bool(math.isfinite(st["sum"]))}
     if backend == "hip":
         rec["autotune"] = s.tune_stats
     if backend == "hip":

@@ -1539,8 +1539,11 @@ void Solver::prepare_plans(int64_t n) {
     if (!s.empty() && schedule_graphs() && !tr_->exchanges()) {
       double est = 0.0;
       for (int k : s) est += depth_ms(k);
-      auto near = cycle_schedule_near(n, cfg_.tb, [this](int k) { return (double)depth_ms(k); }, 0.03, 3);
-      if (est < 50.0 && near.size() > 1) {
+      // (the near-tie scan autotunes every depth it visits: short runs only)
+      const auto near = est < 50.0 ? cycle_schedule_near(n, cfg_.tb, [this](int k) { return (double)depth_ms(k); },
+                                                         0.03, 3)
+                                   : std::vector<std::vector<int>>{};
+      if (near.size() > 1) {
         float best = 1e30f;
         for (auto& c : near) {
           const float ms = time_trial_schedule(c);

@@ -4,7 +4,7 @@
 # (rccl, ipc) and the small grid.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-export PYTHONUNBUFFERED=1
+export PYTHONUNBUFFERED=1 HEAT2D_PLAN_CACHE=off
 O=gpurun_out/r4b
 mkdir -p $O
 BIN=$GRAFT_REPO_ROOT/cuda-hip-mpi-heat-equation-test_amd/_native/heat2d
@@ -22,7 +22,11 @@ done
 for i in 1 2 3; do
   timeout -k 10 200 python -u bench.py --grid 4096 --dtype fp32 --steps 1000 --warmup 100 > $O/small_$i.json 2> $O/small_$i.err || exit 1
 done
-python tools/summarize_json.py $O/*.json
+# prepare(): staged screening + prescan (new) vs the round-3 search (old), cache off
+timeout -k 10 400 python -u bench.py --steps 480 --warmup 48 > $O/b480_new.json 2> $O/b480_new.err || exit 1
+HEAT2D_TUNE_STAGED=0 HEAT2D_SCHED_PRESCAN=0 timeout -k 10 400 python -u bench.py --steps 480 --warmup 48 > $O/b480_old.json 2> $O/b480_old.err || exit 1
+timeout -k 10 400 python -u bench/configs.py --only gpu-max-fp32 gpu-32768-fp64-s0.2 > $O/configs_new.jsonl 2> $O/configs_new.err || exit 1
+python tools/summarize_json.py $O/*.json $O/*.jsonl
 # thin-slab band phase: the fused cycle (band items first in the interior launch,
 # exchange gated on their count) against the autotuned order, r = 1/4 kernels
 for t in rccl ipc; do
