@@ -83,15 +83,17 @@ class IpcTransport final : public Transport {
     wd_.reset();
     for (auto& p : pend_) (void)hipEventDestroy(p.ev);
     for (auto e : pool_) (void)hipEventDestroy(e);
-    for (auto& pb : peer_buf_)
-      for (void* b : pb)
-        if (b) (void)hipIpcCloseMemHandle(b);
+    if (!loop_)  // (a loop rehearsal's "peers" are this rank's own buffers, not IPC mappings)
+      for (auto& pb : peer_buf_)
+        for (void* b : pb)
+          if (b) (void)hipIpcCloseMemHandle(b);
     if (host_ && loop_) {
       (void)hipHostFree(host_);
     } else if (host_) {
       (void)hipHostUnregister(host_);
       ::munmap(host_, shm_bytes_);
     }
+    (void)hipGetLastError();  // teardown errors must not surface as the next launch's
   }
   int rank() const override { return rank_; }
   int size() const override { return size_; }

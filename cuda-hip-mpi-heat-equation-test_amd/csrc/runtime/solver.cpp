@@ -212,6 +212,7 @@ Solver::~Solver() {
       (void)hipStreamDestroy(s_compute_);
       (void)hipStreamDestroy(s_comm_);
     }
+    (void)hipGetLastError();  // teardown errors must not surface as the next launch's
   } else {
     for (auto& b : buf_) std::free(b);
   }

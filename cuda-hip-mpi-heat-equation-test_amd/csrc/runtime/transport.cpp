@@ -88,6 +88,7 @@ class RcclTransport final : public Transport {
     for (auto e : pool_) (void)hipEventDestroy(e);
     if (d_scratch_) (void)hipFree(d_scratch_);
     if (aux_) (void)hipStreamDestroy(aux_);
+    (void)hipGetLastError();  // teardown errors must not surface as the next launch's
   }
   int rank() const override { return rank_; }
   int size() const override { return size_; }

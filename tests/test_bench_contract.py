@@ -163,6 +163,19 @@ def test_bench_auto_transport_falls_back_to_ipc_share_gpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
+def test_bench_rehearsal_then_verification(transport):
+    """A 1-GPU rehearsal of one rank's exchanging cycle (periodic self-exchange
+    over a 1-rank RCCL communicator / the IPC loop transport), then the
+    verification problem on a fresh solver: the loop transports' teardown
+    leaves no HIP error behind for the next launch."""
+    d = run_plain("--rehearse-comm", "--transport", transport, "--grid", "4096", "--rows", "1024", "--steps", "20",
+                  "--warmup", "5")
+    assert d["config"]["transport"] == f"{transport}-loop" and d["verified"] is True, d
+    assert d["halo_bytes"] > 0
+
+
+@pytest.mark.gpu
 def test_bench_plan_cache_second_run(tmp_path):
     """Persistent plan cache: the second identical bench run takes its split
     plans and measured schedule from the cache (each re-validated by one short
