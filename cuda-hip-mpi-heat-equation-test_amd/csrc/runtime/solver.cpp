@@ -725,7 +725,8 @@ bool Solver::cached_split(int k) {
 
 // Staged screening (HEAT2D_TUNE_STAGED=0: every candidate over 4 cycles, the 4
 // best over 12, as round 3): stage A times every candidate over ONE cycle
-// (after one warm-up cycle), stage B the 6 best of A over 4, stage C the 3 best
+// (after one warm-up cycle; up to 4 for cycles under 1 ms, where one sample is
+// noisy and cheap), stage B the 6 best of A over 4, stage C the 3 best
 // of B over 12 — about half the trial cycles at the same winner (the leaders
 // are 1-2 % apart, which stage C resolves). Cycles longer than kLongCycleMs
 // (the full-HBM grids: ~50 ms per pass) screen a reduced candidate family.
@@ -844,9 +845,11 @@ void Solver::autotune_split(int k) {
       }
     }
   }
-  // screening: (cycles per trial, candidates kept) per stage
+  // screening: (cycles per trial, candidates kept) per stage; stage A times
+  // short cycles over up to 4 (a single ~50 us cycle is noisy; they are cheap)
   using Stage = std::pair<int, size_t>;
-  const std::vector<Stage> stages = staged ? std::vector<Stage>{{1, 6}, {4, 3}, {12, 1}}
+  const int a_cycles = std::max(1, std::min(4, (int)std::ceil(1.0f / std::max(base_ms, 1e-3f))));
+  const std::vector<Stage> stages = staged ? std::vector<Stage>{{a_cycles, 6}, {4, 3}, {12, 1}}
                                            : std::vector<Stage>{{4, 4}, {12, 1}};
   std::vector<std::pair<float, kern::SplitPlan>> timed;
   for (const auto& c : cands) timed.emplace_back(0.f, c);
