@@ -364,6 +364,8 @@ class Solver {
   // (order, ring, interior bands) re-cut for the wider bands
   const kern::SplitPlan& split_plan_banded(int k, int64_t B);
   void autotune_split(int k);
+  // exposed-exchange estimate added to a candidate's trial time (exchanging slabs)
+  float exchange_penalty(const kern::SplitPlan& c, float trial_ms) const;
   void cycle_copy_swap();
   void launch_tb(const void* src, void* dst, int64_t rb, int64_t re, int k);
   void exchange_on(void* field, int64_t k, hipStream_t s);

@@ -739,6 +739,25 @@ static bool staged_tuning() {
 }
 constexpr float kLongCycleMs = 8.0f;
 
+// The trial cycles cannot run the halo exchange (it is collective, and the
+// ranks' candidate lists differ), so on an exchanging slab each candidate is
+// ranked by its trial time plus the part of the exchange its order cannot
+// hide: the concurrent order starts the exchange only after its band launch,
+// which runs beside the interior and ends with it (phase timers of the 4096-row
+// rehearsal: interior 0.61 ms, bands 0.66 ms) — the whole exchange is exposed;
+// the edge-first and fused orders run it beside the interior. The exchange is
+// modelled at 50 GB/s per message (an xGMI link, one direction) + 10 us.
+// Without it the no-exchange trials picked the concurrent order for the
+// 8-rank fp64 slab by 0.5 %, and the exchanging rehearsal ran 18 % slower than
+// with the edge-first order (profiles/r4/b/).
+float Solver::exchange_penalty(const kern::SplitPlan& c, float trial_ms) const {
+  if (!tr_->exchanges()) return 0.f;
+  const double bytes = (double)halo_msg_bytes(L_, c.k, dtype_size(dtype()));
+  const float tx = (float)(bytes / 50e6 + 0.010);  // ms
+  if (c.valid == 3 || c.valid == 4) return std::max(0.f, tx - 0.8f * trial_ms);
+  return tx;
+}
+
 void Solver::autotune_split(int k) {
   const int spare = spare_waves();
   synchronize();
@@ -851,15 +870,22 @@ void Solver::autotune_split(int k) {
   const int a_cycles = std::max(1, std::min(4, (int)std::ceil(1.0f / std::max(base_ms, 1e-3f))));
   const std::vector<Stage> stages = staged ? std::vector<Stage>{{a_cycles, 6}, {4, 3}, {12, 1}}
                                            : std::vector<Stage>{{4, 4}, {12, 1}};
-  std::vector<std::pair<float, kern::SplitPlan>> timed;
-  for (const auto& c : cands) timed.emplace_back(0.f, c);
+  struct Timed {
+    float score, ms;  // ranking score (trial + exposed exchange), trial ms per cycle
+    kern::SplitPlan plan;
+  };
+  std::vector<Timed> timed;
+  for (const auto& c : cands) timed.push_back(Timed{0.f, 0.f, c});
   for (const Stage& st : stages) {
-    for (auto& t : timed) t.first = time_plan(t.second, st.first);
-    std::stable_sort(timed.begin(), timed.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    for (auto& t : timed) {
+      t.ms = time_plan(t.plan, st.first);
+      t.score = t.ms + exchange_penalty(t.plan, t.ms);
+    }
+    std::stable_sort(timed.begin(), timed.end(), [](const Timed& x, const Timed& y) { return x.score < y.score; });
     timed.resize(std::min(timed.size(), st.second));
   }
-  best = timed.front().second;
-  float best_ms = timed.front().first;
+  best = timed.front().plan;
+  float best_score = timed.front().score, best_ms = timed.front().ms;
   // the winner's boundary bands cut into 2..4 row bands each: the band launch
   // is latency-bound (one wave per strip and band, ~1 wave per SIMD, each
   // marching B + 2k rows) — more, shorter items where the split leaves the
@@ -868,10 +894,12 @@ void Solver::autotune_split(int k) {
     for (int64_t nb : {2, 3, 4}) {
       const kern::SplitPlan c = kern::with_edge_bands(dtype(), best, nb, cfg_.arith);
       if (c.edge_items == best.edge_items) continue;
-      const float ms = time_plan(c, 12);
+      const float t = time_plan(c, 12);
+      const float score = t + exchange_penalty(c, t);
       ++tune_trials_;
-      if (ms < best_ms) {
-        best_ms = ms;
+      if (score < best_score) {
+        best_score = score;
+        best_ms = t;
         best = c;
       }
     }
