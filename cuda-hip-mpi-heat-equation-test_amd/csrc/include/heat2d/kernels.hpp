@@ -102,19 +102,21 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int rin
 // Fused cycle (valid = 4) for slabs whose halo exchange can be gated on a
 // device counter (Transport::gates()): ONE interior-kernel launch whose first
 // items are the boundary bands the exchange sends (top if send_top, bottom if
-// send_bottom; their rows stored at device scope, each item counted in a
-// device counter when its stores drain), the interior cut so that the waves
-// that took a band item get correspondingly less interior (every wave ends
-// together); bands on the Dirichlet frame (a first / last rank) go to a small
-// general launch beside it. The exchange starts as soon as the band count is
+// send_bottom; taken by wave id as the first items of waves 0 .. Nb-1, their
+// rows republished at device scope, each item counted in a device counter
+// when its stores drain), then the interior as row bands (main_bands; 0:
+// chosen as for the split plan) from the dynamic item queue, so the waves
+// that marched a band item take less interior; bands on the Dirichlet frame
+// (a first / last rank) go to a small general launch beside it. The exchange starts as soon as the band count is
 // reached instead of after a separate band launch (the edge-first order's
 // serial phase: 77 of 879 us on the 8-rank fp64 slab, profiles/r3/thin/).
 // valid = 0 if the slab is too thin or has more band items than waves.
 SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool send_top, bool send_bottom, int cus = 0,
-                     int spare_waves = 0, int ring_override = 0, int arith = 0);
-// Launch the MAIN part of a fused plan, counting band items into *sig.
+                     int spare_waves = 0, int ring_override = 0, int arith = 0, int64_t main_bands = 0);
+// Launch the MAIN part of a fused plan, counting band items into *sig (queue:
+// the dynamic item queue's counters, used when the plan has more items than waves).
 void launch_fused_main(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, uint32_t* sig,
-                       double r, hipStream_t stream, int arith = 0);
+                       double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr);
 // A one-wave kernel on `stream` that waits until *counter >= target (an
 // exchange gated on a fused cycle's band count); a wait longer than
 // timeout_ticks sets *err and returns.

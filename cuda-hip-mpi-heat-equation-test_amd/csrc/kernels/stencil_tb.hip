@@ -302,8 +302,11 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
     a.fu = std::pow(r, (double)k);
     a.fu1 = std::pow(r, (double)(k - 1));
   }
-  // the dynamic queue only pays with more items than waves (plain kernels)
-  a.queue = (queue && !partials && !sig && items > a.nwaves) ? queue : nullptr;
+  // the dynamic queue only pays with more items than waves (plain and fused
+  // interior kernels; a fused launch's band items are the first nwaves items,
+  // taken by wave id, so the queue hands out interior items only)
+  HEAT2D_REQUIRE(!sig || sig_items <= a.nwaves, "band-signal items must be first items of the waves");
+  a.queue = (queue && !partials && items > a.nwaves) ? queue : nullptr;
   const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
   const int64_t o = L.origin();
   if (partials) {
@@ -595,13 +598,11 @@ SplitPlan with_edge_bands(DType dt, const SplitPlan& p, int64_t nb, int arith) {
 }
 
 SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool send_top, bool send_bottom, int cus,
-                     int spare_waves, int ring_override, int arith) {
+                     int spare_waves, int ring_override, int arith, int64_t main_bands) {
   check_layout(dt, L, k);
   SplitPlan p{};
   p.k = k;
-  // default ring: the fused fp64 K >= 17 interior keeps 2 waves/SIMD only at ring 6
-  p.ring = ring_ok(dt, k, (ring_override == 4 || ring_override == 6) ? ring_override
-                                                                     : (dt == DType::F64 && k >= 17 ? 6 : default_ring(dt, k)));
+  p.ring = ring_ok(dt, k, (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k));
   const int64_t n = L.nrows, B = std::max<int64_t>(band, k);
   const int64_t U = useful_width(dt, k);
   const int64_t ns = (L.ncols + U - 1) / U;
@@ -621,34 +622,25 @@ SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool se
   const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
   const int64_t W = std::max<int64_t>(4, slots - std::max(0, spare_waves));
   const int64_t Nb = nsig * ns;
-  if (Nb >= W) return p;
-  // per-wave march rows: a band item B + prime, an interior segment of s rows
-  // s + prime; waves w < Nb take one band item and an interior segment of
-  // sA rows, the others one segment of sB rows: sA = sB - (B + prime) ends
-  // every wave together (the fp32 interior kernel skips ~k - 1 priming rows)
-  const double prime = dt == DType::F32 ? std::max(1, k - 1) : 2.0 * k;
-  const double cb = (double)B + prime;
-  const double S_int = (double)rows_m * (double)ns;
-  double sB = (S_int + (double)Nb * cb) / (double)W;
-  double sA = sB - cb;
-  int64_t hA = 0;
-  if (sA > 2.0 * k) hA = std::min<int64_t>(rows_m - 4 * k, (int64_t)((double)Nb * sA / (double)ns + 0.5));
-  if (hA * ns < Nb) hA = 0;  // too few strip rows for one segment per band wave
+  if (Nb >= W) return p;  // every band item must be a wave's FIRST item (taken by wave id)
+  // item order: the sent bands first — waves 0 .. Nb-1 take them by wave id
+  // and the exchange is gated on their count — then the interior as row
+  // bands (the split plan's interior, the same locality: waves in flight on the
+  // same rows of adjacent strips share the strip halos in L2), handed out by
+  // the dynamic queue, so the waves that marched a band item take less of it
+  int64_t nb = choose_bands(rows_m, ns, dt == DType::F32 ? balance_units(dt, cus, bpc) : W, k,
+                            dt == DType::F32 ? std::max(1, k - 1) : -1);
+  if (main_bands > 0) nb = std::min<int64_t>(main_bands, std::max<int64_t>(1, rows_m / (2 * (int64_t)k)));
   int nf = 0;
   if (send_top) p.fused[nf++] = TbRect{0, B, 0, ns, 1};
   if (send_bottom) p.fused[nf++] = TbRect{n - B, n, 0, ns, 1};
-  // item order = wave order of the grid stride (nwaves = W): band items
-  // [0, Nb) on waves 0 .. Nb-1; rect B (rows [B + hA, n - B)), one segment per
-  // wave Nb .. W-1; rect A (rows [B, B + hA)), items W .. W+Nb-1: the second
-  // item of waves 0 .. Nb-1
-  p.fused[nf++] = TbRect{B + hA, n - B, 0, ns, -std::min<int64_t>(W - Nb, (rows_m - hA) * ns)};
-  if (hA > 0) p.fused[nf++] = TbRect{B, B + hA, 0, ns, -Nb};
+  p.fused[nf++] = TbRect{B, n - B, 0, ns, nb};
   p.nfused = nf;
   p.sig_items = Nb;
   p.main = p.fused[nsig];
-  p.main_items = 0;
-  for (int i = 0; i < nf; ++i) p.main_items += p.fused[i].nb > 0 ? p.fused[i].nb * ns : -p.fused[i].nb;
-  p.main_waves = W;
+  p.main_items = Nb + nb * ns;
+  p.main_waves = std::min<int64_t>(W, p.main_items);
+  if (p.main_items > p.main_waves) p.flags |= kPlanDynamic;
   // bands on the frame (first / last rank): general kernel, beside the main launch
   int ne = 0;
   if (!send_top) p.edge[ne++] = TbRect{0, B, 0, ns, 1};
@@ -662,10 +654,10 @@ SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool se
 }
 
 void launch_fused_main(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, uint32_t* sig,
-                       double r, hipStream_t stream, int arith) {
-  HEAT2D_REQUIRE(p.valid == 4 && p.nfused >= 2 && p.nfused <= kMaxFused, "not a fused plan");
+                       double r, hipStream_t stream, int arith, uint32_t* queue) {
+  HEAT2D_REQUIRE(p.valid == 4 && p.nfused >= 2 && p.nfused <= kMainRects, "not a fused plan");
   launch_rects(dt, src, dst, L, p.k, p.ring, true, p.fused, p.nfused, p.main_waves, r, stream, arith, nullptr,
-               p.sig_items, sig);
+               p.sig_items, sig, (p.flags & kPlanDynamic) ? queue : nullptr);
 }
 
 SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_override, int64_t bands, int arith) {

@@ -515,7 +515,8 @@ const kern::SplitPlan& Solver::split_plan_banded(int k, int64_t B) {
   if (base.valid == 4) {  // fused: the same ring, the bands and the interior balance re-cut for B
     bool top, bot;
     sent_sides(&top, &bot);
-    kern::SplitPlan d = kern::plan_fused(dtype(), L_, k, B, top, bot, compute_cus_, spare_waves(), base.ring, cfg_.arith);
+    kern::SplitPlan d = kern::plan_fused(dtype(), L_, k, B, top, bot, compute_cus_, spare_waves(), base.ring, cfg_.arith,
+                                         base.main.nb > 0 ? base.main.nb : 0);
     d.k = k;
     return banded_.emplace(std::make_pair(k, B), d).first->second;
   }
@@ -607,7 +608,7 @@ void Solver::trial_cycle(const kern::SplitPlan& c) {
     ensure_sig();
     H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
     H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
-    kern::launch_fused_main(dtype(), src, dst, L_, c, d_sig_ + 1, cfg_.r, s_compute_, cfg_.arith);
+    kern::launch_fused_main(dtype(), src, dst, L_, c, d_sig_ + 1, cfg_.r, s_compute_, cfg_.arith, d_queue_);
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_, cfg_.arith);
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
@@ -800,10 +801,13 @@ void Solver::autotune_split(int k) {
       // fused (exchange gated on the interior launch's band items): like the
       // edge-first order it needs an interior long enough to hide the exchange
       if (!fused_candidates() || !fused_ok() || best.valid != 1 || base_ms < kEdgeFirstMinCycleMs) continue;
-      for (int ring : {4, 6}) {
-        kern::SplitPlan c = kern::plan_fused(dtype(), L_, k, k, top, bot, compute_cus_, spare, ring, cfg_.arith);
-        if (c.valid) cands.push_back(c);
-      }
+      for (int ring : {4, 6})
+        for (double f : long_cycles ? std::vector<double>{1.0} : std::vector<double>{1.0, 0.5, 2.0}) {
+          const int64_t nb = std::max<int64_t>(1, (int64_t)(std::max<int64_t>(nb0, 1) * f + 0.5));
+          kern::SplitPlan c = kern::plan_fused(dtype(), L_, k, k, top, bot, compute_cus_, spare, ring, cfg_.arith,
+                                               f == 1.0 ? 0 : nb);
+          if (c.valid) cands.push_back(c);
+        }
       continue;
     }
     // the trials run without the exchange, which the edge-first order puts
@@ -934,7 +938,7 @@ void Solver::launch_overlap(int k, int64_t B) {
     H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
     H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
     if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
-    kern::launch_fused_main(dtype(), src, dst, L_, sp, d_sig_, cfg_.r, s_compute_, cfg_.arith);
+    kern::launch_fused_main(dtype(), src, dst, L_, sp, d_sig_, cfg_.r, s_compute_, cfg_.arith, d_queue_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
     if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
