@@ -634,10 +634,30 @@ SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool se
   int nf = 0;
   if (send_top) p.fused[nf++] = TbRect{0, B, 0, ns, 1};
   if (send_bottom) p.fused[nf++] = TbRect{n - B, n, 0, ns, 1};
-  p.fused[nf++] = TbRect{B, n - B, 0, ns, nb};
+  // The waves that marched a band item (B + P march rows, P the priming rows
+  // of an item) take their interior item last, from the queue: unless those
+  // items are shorter by B + P rows, the cycle ends a band item after the rest
+  // (the serial band launch of the edge-first order, moved into the waves).
+  // So the last nsig bands of every strip are short (S = L - B - P,
+  // (nb - nsig) L + nsig S = rows_m) and come last in item order.
+  // HEAT2D_FUSED_BALANCE=0: equal bands (A/B).
+  const int64_t P = dt == DType::F32 ? std::max(1, k - 1) : 2 * (int64_t)k;
+  const int64_t nbl = nb - nsig;
+  const int64_t Lr = nbl > 0 ? (rows_m + nsig * (B + P) + nb - 1) / nb : 0;
+  const int64_t S = nbl > 0 ? (rows_m - nbl * Lr) / nsig : 0;
+  static const bool balance = [] {
+    const char* e = std::getenv("HEAT2D_FUSED_BALANCE");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (balance && nbl > 0 && S >= std::max<int64_t>(2 * P, 16)) {
+    p.fused[nf++] = TbRect{B, B + nbl * Lr, 0, ns, nbl};
+    p.fused[nf++] = TbRect{B + nbl * Lr, n - B, 0, ns, nsig};
+  } else {
+    p.fused[nf++] = TbRect{B, n - B, 0, ns, nb};
+  }
   p.nfused = nf;
   p.sig_items = Nb;
-  p.main = p.fused[nsig];
+  p.main = TbRect{B, n - B, 0, ns, nb};  // (the interior as a whole: its band count re-cuts it)
   p.main_items = Nb + nb * ns;
   p.main_waves = std::min<int64_t>(W, p.main_items);
   if (p.main_items > p.main_waves) p.flags |= kPlanDynamic;

@@ -663,7 +663,8 @@ static uint64_t plan_env_hash() {
     for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_TUNE_SEGMENTS", "HEAT2D_FUSED", "HEAT2D_W_ROW", "HEAT2D_W_COL",
                              "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
                              "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
-                             "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN", "HEAT2D_EDGE_BANDS"}) {
+                             "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN", "HEAT2D_EDGE_BANDS",
+                             "HEAT2D_FUSED_BALANCE"}) {
       const char* e = std::getenv(name);
       const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
       for (unsigned char c : kv) v = (v ^ c) * 1099511628211ull;

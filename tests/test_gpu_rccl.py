@@ -62,11 +62,13 @@ def periodic_golden(p, steps, k, dtype=np.float64):
 
 
 @pytest.mark.parametrize("order,graph", [("auto", False), ("edge-first", False), ("edge-first", True),
-                                         ("concurrent", True), ("concurrent", False)])
+                                         ("concurrent", True), ("concurrent", False), ("fused", False)])
 def test_rccl_loop_rehearsal(native, gpu, order, graph, monkeypatch):
     """The 1-GPU rehearsal of the multi-GPU schedule: bands + RCCL self
     send/recv on the comm stream beside the interior. Checked bitwise on ALL
-    rows against the periodic-in-x golden the self exchange implements."""
+    rows against the periodic-in-x golden the self exchange implements. The
+    fused order: both bands as the interior launch's first items, the exchange
+    gated on their count, the interior's short bands last (plan_fused)."""
     from heat2d.models.heat2d import HeatSolver
     from heat2d.parallel.transport import RcclLoopTransport
 
