@@ -69,6 +69,7 @@ struct TbRect {
 // rects of one launch (SplitPlan::fused, the kernel's TbArgs::rect)
 constexpr int kMaxFused = 6;
 constexpr int32_t kPlanDynamic = 2;  // SplitPlan::flags
+constexpr int32_t kPlanLead = 4;     // SplitPlan::flags (valid = 1)
 struct SplitPlan {
   int32_t k, ring, valid, nedge;
   TbRect main;
@@ -80,7 +81,11 @@ struct SplitPlan {
   // valid = 1..3 with nfused > 0 (arith 2): `main` cut into frame-strip-
   // weighted rects, launched instead of `main` (stencil_tb.hip weight_main).
   // flags & kPlanDynamic: the main launch takes its items from a dynamic
-  // queue (more items than waves; TbArgs::queue).
+  // queue (more items than waves; TbArgs::queue). flags & kPlanLead (valid 1,
+  // exchanging slabs): the concurrent order with the band launch issued
+  // FIRST — its waves take their slots before the interior's, the interior's
+  // last-dispatched waves (its one-item waves) start behind them, and the
+  // exchange follows the bands on the comm stream.
   int32_t nfused, flags;
   TbRect fused[kMaxFused];
   int64_t sig_items;

@@ -727,6 +727,22 @@ void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, 
   launch_reduce_partials(partials, nw, out6, stream);
 }
 
+// Boundary-band rects of a slab whose bands stay clear of the global frame
+// rows (every middle rank of a row decomposition): the interior kernel marches
+// them (item kinds 0 / 2 only), at its 2 waves per SIMD instead of the general
+// kernel's 1 (fp64 K = 20: 249 vs 374 + 118 acc VGPRs). HEAT2D_EDGE_MAIN=0: the
+// general kernel always (A/B).
+bool edges_on_main(const SlabLayout& L, int k, const TbRect* R, int n) {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_EDGE_MAIN");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (!on || n < 1 || n > kMainRects) return false;
+  for (int i = 0; i < n; ++i)
+    if (R[i].r1 > R[i].r0 && (R[i].r0 - k < -L.row0 || R[i].r1 + k > L.nrows_global - L.row0)) return false;
+  return true;
+}
+
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith, uint32_t* queue) {
   // (SplitPlan::flags & kPlanDynamic: the main part takes its items from the dynamic queue)
@@ -745,7 +761,8 @@ void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, con
   if (main_part)
     launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith, nullptr, 0, nullptr, q);
   else
-    launch_rects(dt, src, dst, L, p.k, p.ring, false, p.edge, p.nedge, p.edge_waves, r, stream, arith);
+    launch_rects(dt, src, dst, L, p.k, p.ring, edges_on_main(L, p.k, p.edge, p.nedge), p.edge, p.nedge, p.edge_waves,
+                 r, stream, arith);
 }
 
 }  // namespace kern

@@ -143,7 +143,7 @@ bool get_plan(const std::string& ctx, int k, int64_t band, kern::SplitPlan* p, f
   q.nfused = (int32_t)nf;
   q.sig_items = sig;
   q.flags = (int32_t)pr;
-  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > kern::kMaxFused || q.flags < 0 || q.flags > kern::kPlanDynamic) return false;
+  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > kern::kMaxFused || q.flags < 0 || q.flags > (kern::kPlanDynamic | kern::kPlanLead)) return false;
   *p = q;
   *ms = t;
   return true;

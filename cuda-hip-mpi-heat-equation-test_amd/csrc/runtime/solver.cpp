@@ -164,7 +164,20 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
         // and RCCL's workgroups (kern::plan_split).
         H2D_HIP(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
       }
-      H2D_HIP(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+      // The comm stream (bands, exchange) at the highest priority: when both
+      // streams' next launches become ready together (steady-state cycles),
+      // the band waves are dispatched before the interior's, as the lead
+      // order issues them in a cycle's first launch (HEAT2D_COMM_PRIORITY=0:
+      // default priority, A/B).
+      static const bool prio = [] {
+        const char* e = std::getenv("HEAT2D_COMM_PRIORITY");
+        return !e || std::atoi(e) != 0;
+      }();
+      int least = 0, greatest = 0;
+      if (prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least)
+        H2D_HIP(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking, greatest));
+      else
+        H2D_HIP(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
       own_streams_ = true;
     }
     H2D_HIP(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
@@ -467,6 +480,11 @@ const kern::SplitPlan& Solver::split_plan(int k) {
       const std::string o = env;
       if (o == "edge-first" && p.valid == 1) p.valid = 3;
       if (o == "concurrent" && p.valid == 3) p.valid = 1;
+      if (o == "concurrent") p.flags &= ~kern::kPlanLead;
+      if (o == "lead" && (p.valid == 1 || p.valid == 3) && tr_->exchanges()) {
+        p.valid = 1;
+        p.flags |= kern::kPlanLead;
+      }
       if (o == "fused" && fused_ok()) {
         bool top, bot;
         sent_sides(&top, &bot);
@@ -486,7 +504,14 @@ const kern::SplitPlan& Solver::split_plan(int k) {
     const char* env_bands = std::getenv("HEAT2D_BANDS");
     if (env_seg || env_bands) {
       const int64_t nseg = env_seg ? std::atoll(env_seg) : -std::atoll(env_bands);  // < 0: bands
-      if (nseg != 0 && p.valid) {
+      if (nseg < 0 && p.valid == 4) {  // fused: the interior re-cut into n bands (segments: not offered)
+        bool top, bot;
+        sent_sides(&top, &bot);
+        const kern::SplitPlan f = kern::plan_fused(dtype(), L_, k, k, top, bot, compute_cus_, spare, p.ring,
+                                                   cfg_.arith, -nseg);
+        if (f.valid) p = f;
+        p.k = k;
+      } else if (nseg != 0 && p.valid) {
         const int valid = p.valid, ring = p.ring;
         p = valid == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, -nseg, cfg_.arith)
                        : kern::plan_split(dtype(), L_, k, k, compute_cus_, spare, ring, -nseg, cfg_.arith);
@@ -594,6 +619,15 @@ static bool fused_candidates() {
   return on;
 }
 
+// Lead-order candidates on exchanging slabs (HEAT2D_LEAD=0 keeps them out).
+static bool lead_candidates() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_LEAD");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 // smallest steady-state cycle (ms) for which edge-first split plans are tried
 constexpr float kEdgeFirstMinCycleMs = 0.4f;
 
@@ -624,6 +658,13 @@ void Solver::trial_cycle(const kern::SplitPlan& c) {
   }
   H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
   H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
+  if (c.flags & kern::kPlanLead) {  // lead: the band launch issued first
+    kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_, cfg_.arith);
+    kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+    return;
+  }
   kern::launch_split(dtype(), src, dst, L_, c, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
   H2D_HIP(hipEventRecord(ev_int_, s_compute_));
   kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_, cfg_.arith);
@@ -664,7 +705,7 @@ static uint64_t plan_env_hash() {
                              "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
                              "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
                              "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN", "HEAT2D_EDGE_BANDS",
-                             "HEAT2D_FUSED_BALANCE"}) {
+                             "HEAT2D_FUSED_BALANCE", "HEAT2D_EDGE_MAIN", "HEAT2D_LEAD", "HEAT2D_COMM_PRIORITY"}) {
       const char* e = std::getenv(name);
       const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
       for (unsigned char c : kv) v = (v ^ c) * 1099511628211ull;
@@ -712,6 +753,7 @@ bool Solver::cached_split(int k) {
   if (c.valid == 4 && (!fused_ok() || !fused_candidates())) return false;
   if ((c.flags & kern::kPlanDynamic) && !dynamic_candidates()) return false;
   if (c.valid == 2 && tr_->exchanges()) return false;
+  if ((c.flags & kern::kPlanLead) && (c.valid != 1 || !tr_->exchanges() || !lead_candidates())) return false;
   synchronize();
   const float t = time_plan(c, 4);
   H2D_HIP(hipEventRecord(ev_int_, s_compute_));
@@ -741,6 +783,15 @@ static bool staged_tuning() {
 }
 constexpr float kLongCycleMs = 8.0f;
 
+// HEAT2D_TUNE_LOG=1: every screening stage's ranking on stderr (diagnostics)
+static bool tune_log() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_TUNE_LOG");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 // The trial cycles cannot run the halo exchange (it is collective, and the
 // ranks' candidate lists differ), so on an exchanging slab each candidate is
 // ranked by its trial time plus the part of the exchange its order cannot
@@ -756,7 +807,8 @@ float Solver::exchange_penalty(const kern::SplitPlan& c, float trial_ms) const {
   if (!tr_->exchanges()) return 0.f;
   const double bytes = (double)halo_msg_bytes(L_, c.k, dtype_size(dtype()));
   const float tx = (float)(bytes / 50e6 + 0.010);  // ms
-  if (c.valid == 3 || c.valid == 4) return std::max(0.f, tx - 0.8f * trial_ms);
+  if (c.valid == 3 || c.valid == 4 || (c.valid == 1 && (c.flags & kern::kPlanLead)))
+    return std::max(0.f, tx - 0.8f * trial_ms);
   return tx;
 }
 
@@ -778,7 +830,18 @@ void Solver::autotune_split(int k) {
   bool top = false, bot = false;
   sent_sides(&top, &bot);
   std::vector<kern::SplitPlan> cands{best};
-  auto add = [&](const kern::SplitPlan& c) {
+  auto add = [&](const kern::SplitPlan& c0) {
+    // exchanging slabs: each concurrent candidate also in the lead order
+    if (c0.valid == 1 && tr_->exchanges() && lead_candidates()) {
+      kern::SplitPlan l = c0;
+      l.flags |= kern::kPlanLead;
+      cands.push_back(l);
+      if (dynamic_candidates() && l.main_items > l.main_waves) {
+        l.flags |= kern::kPlanDynamic;
+        cands.push_back(l);
+      }
+    }
+    const kern::SplitPlan& c = c0;
     cands.push_back(c);
     // more items than waves: also with the dynamic item queue (faster waves
     // take more items; per-wave timelines of the 32768^2 fp64 interior showed
@@ -887,6 +950,11 @@ void Solver::autotune_split(int k) {
       t.score = t.ms + exchange_penalty(t.plan, t.ms);
     }
     std::stable_sort(timed.begin(), timed.end(), [](const Timed& x, const Timed& y) { return x.score < y.score; });
+    if (tune_log())
+      for (const auto& t : timed)
+        std::fprintf(stderr, "heat2d tune k=%d cycles=%d: order %d ring %d bands %lld items %lld waves %lld dyn %d ms %.4f score %.4f\n",
+                     k, st.first, t.plan.valid, t.plan.ring, (long long)t.plan.main.nb, (long long)t.plan.main_items,
+                     (long long)t.plan.main_waves, (t.plan.flags & kern::kPlanDynamic) ? 1 : 0, t.ms, t.score);
     timed.resize(std::min(timed.size(), st.second));
   }
   best = timed.front().plan;
@@ -969,7 +1037,14 @@ void Solver::launch_overlap(int k, int64_t B) {
   H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));  // edge part c-1 (record not yet replaced)
   H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));     // main part c-1
   if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
-  if (sp.valid) {
+  if (sp.valid && (sp.flags & kern::kPlanLead)) {
+    // lead: the band launch first (comm stream), then the interior beside it
+    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_, cfg_.arith);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
+    kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  } else if (sp.valid) {
     if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
     kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
@@ -1047,6 +1122,7 @@ void Solver::ensure_pair_graph() {
     const int saved_lx0 = last_x_[0], saved_lx1 = last_x_[1];
     if (tr_->exchanges()) last_x_[0] = last_x_[1] = (int)band_;  // whatever a replay follows
     if (!ovl) {
+      if (fused_ok()) ensure_sig();  // (no allocation inside a capture)
       H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
       for (int c = 0; c < 2; ++c) {
         cycle_launch(K);
@@ -1061,6 +1137,7 @@ void Solver::ensure_pair_graph() {
       hipEvent_t fork = nullptr, join = nullptr;
       H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
       H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+      if (fused_ok()) ensure_sig();  // (no allocation inside a capture)
       H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
       H2D_HIP(hipEventRecord(fork, s_compute_));
       H2D_HIP(hipStreamWaitEvent(s_comm_, fork, 0));
@@ -1405,6 +1482,7 @@ float Solver::time_trial_schedule(const std::vector<int>& sc) {
   H2D_HIP(hipEventCreate(&e0));
   H2D_HIP(hipEventCreate(&e1));
   hipGraph_t g = nullptr;
+  if (fused_ok()) ensure_sig();  // (no allocation inside a capture)
   H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
   H2D_HIP(hipEventRecord(fork, s_compute_));
   H2D_HIP(hipStreamWaitEvent(s_comm_, fork, 0));
@@ -1459,6 +1537,7 @@ void Solver::capture_schedule(int64_t n) {
   H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
   H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
   hipGraph_t g = nullptr;
+  if (fused_ok()) ensure_sig();  // (no allocation inside a capture)
   H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
   H2D_HIP(hipEventRecord(fork, s_compute_));
   H2D_HIP(hipStreamWaitEvent(s_comm_, fork, 0));

@@ -111,6 +111,7 @@ def test_gloo_hip_ranks_share_gpu(native, gpu, tmp_path, world, tb, overlap, n, 
 @pytest.mark.parametrize("world,tb,n,dtype,graph,order", [(3, 10, 1100, "fp64", False, "fused"),
                                                           (4, 8, 1500, "fp32", False, "fused"),
                                                           (3, 10, 1100, "fp64", True, "fused"),
+                                                          (3, 10, 1100, "fp64", True, "lead"),
                                                           (2, 6, 900, "fp64", True, None)])
 def test_ipc_ranks_share_gpu_bitwise(native, gpu, tmp_path, monkeypatch, world, tb, n, dtype, graph, order):
     """Rank PROCESSES on the one GPU exchanging halos through the IPC transport

@@ -62,13 +62,12 @@ def periodic_golden(p, steps, k, dtype=np.float64):
 
 
 @pytest.mark.parametrize("order,graph", [("auto", False), ("edge-first", False), ("edge-first", True),
-                                         ("concurrent", True), ("concurrent", False), ("fused", False)])
+                                         ("concurrent", True), ("concurrent", False), ("lead", False),
+                                         ("lead", True)])
 def test_rccl_loop_rehearsal(native, gpu, order, graph, monkeypatch):
     """The 1-GPU rehearsal of the multi-GPU schedule: bands + RCCL self
     send/recv on the comm stream beside the interior. Checked bitwise on ALL
-    rows against the periodic-in-x golden the self exchange implements. The
-    fused order: both bands as the interior launch's first items, the exchange
-    gated on their count, the interior's short bands last (plan_fused)."""
+    rows against the periodic-in-x golden the self exchange implements."""
     from heat2d.models.heat2d import HeatSolver
     from heat2d.parallel.transport import RcclLoopTransport
 
@@ -90,3 +89,48 @@ def test_rccl_loop_rehearsal(native, gpu, order, graph, monkeypatch):
     assert not np.array_equal(got[:5], R.owned(R.ftcs(p))[:5])  # the periodic exchange really moved rows
     s.close()
     tr.close()
+
+
+def periodic_slab_golden(T, r, steps):
+    """A middle slab exchanging with itself (bench.py --rehearse-comm): the
+    halo rows above receive its last rows and the rows below its first ones,
+    so its rows evolve periodically (period = its row count); the column
+    frame stays pinned. T: the slab's rows with both frame columns."""
+    for _ in range(steps):
+        pad = np.vstack([T[-1:], T, T[:1]])
+        T = R.ftcs_step(pad, r)[1:-1]
+    return T
+
+
+@pytest.mark.parametrize("kind", ["rccl", "ipc"])
+@pytest.mark.parametrize("order", ["fused", "edge-first", "lead", "auto"])
+def test_middle_slab_rehearsal(native, gpu, monkeypatch, kind, order):
+    """The bench's strong-scaling rehearsal geometry: a middle slab (rows
+    [200, 360) of a 600^2 grid, interior boundary bands) exchanging both
+    bands with itself, per split order (lead: the band launch issued before
+    the interior, no wait between them; fused: both sent bands as the
+    interior launch's first items, the exchange gated on their count, the
+    interior's short bands last), bitwise the periodic-slab golden on rough data."""
+    from heat2d.models.heat2d import HeatSolver
+    from heat2d.parallel.transport import IpcLoopTransport, RcclLoopTransport
+
+    if order != "auto":
+        monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
+    K, rows, row0 = 8, 160, 200
+    p = heat2d.make_problem(heat2d.InputDat(n=600, sigma=0.25, nu=0.05, dom_len=1.0, ntime=5 * K), "ghost", "sine")
+    full = R.initial_field(p)
+    full[1:-1, 1:-1] = 1.0 + np.random.default_rng(5).random((600, 600))
+    slab = full[1 + row0:1 + row0 + rows].copy()
+    tr = RcclLoopTransport(0) if kind == "rccl" else IpcLoopTransport(0)
+    s = HeatSolver(p, dtype="fp64", backend="hip", tb=K, transport=tr, device=0, rows=rows, slab_row0=row0,
+                   graph=kind == "ipc", autotune=1, arith="exact")
+    s.upload(slab[:, 1:-1])
+    s.step(p.ntime)
+    got = s.download()
+    assert s.cycle_hist() == {K: 5}
+    if order != "auto":
+        assert s.plan(K)["order"] == order
+    s.close()
+    tr.close()
+    ref = periodic_slab_golden(slab, p.r, p.ntime)[:, 1:-1]
+    assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
