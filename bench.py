@@ -38,6 +38,7 @@ derived reference ceiling of BASELINE.md — 50 Gpts/s per MI250X GCD for its
 kernel + per-step D2D copy (>= 32 B/pt/step at 1.6 TB/s) — times N ranks.
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -143,8 +144,10 @@ def main():
                          "error bound of exact); bench (default): jacobi when r == 1/4, else auto")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="replay the timed schedule from one hipGraph captured in prepare() (auto: whenever the "
-                         "transport's exchange captures: single-rank runs and IPC; RCCL exchanges stay eager)")
+                    help="replay the timed schedule from one hipGraph captured in prepare() (auto: single-rank "
+                         "runs without an exchange; exchanging runs stay eager — a graph launch starts the "
+                         "interior ~40 us after the band launch, eager ~12 us: 4096-row IPC slab rehearsal "
+                         "3362-3468 with the graph, 3768-3943 eager, profiles/r4/k/)")
     ap.add_argument("--comm-cus", type=int, default=0, help="CUs reserved for bands + RCCL (0: default, -1: none)")
     ap.add_argument("--check", action="store_true", help="print field statistics after the run")
     ap.add_argument("--phase-timers", action="store_true",
@@ -253,9 +256,11 @@ def main():
         return SelfTransport()
 
     def uses_graph(kind):
-        # graphs whenever the exchange captures: single-rank runs and the IPC transport (RCCL's does not)
-        capt = kind in ("self", "ipc", "ipc-loop")
-        return hip and (args.graph == "on" or (args.graph == "auto" and capt))
+        # auto: graphs for single-rank runs without an exchange (their short
+        # cycles are launch-bound: the small grid); "on": also IPC (RCCL's exchange does not capture)
+        if not hip or args.graph == "off":
+            return False
+        return kind == "self" or (args.graph == "on" and kind in ("ipc", "ipc-loop"))
 
     def build(kind, tr):
         return HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb, overlap=not args.no_overlap,
@@ -264,6 +269,8 @@ def main():
                           slab_row0=slab_row0)
 
     def timed(s):
+        gc.collect()
+        gc.disable()  # no collector pause inside a sub-ms timed region
         barrier()
         t0 = time.perf_counter()
         s.step(args.steps)
@@ -271,6 +278,7 @@ def main():
         sync()
         t1 = time.perf_counter()
         barrier()
+        gc.enable()
         return amax(t1 - t0)
 
     live = {}  # kind -> (transport, solver, prepare seconds)

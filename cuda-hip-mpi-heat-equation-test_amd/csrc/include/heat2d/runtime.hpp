@@ -418,6 +418,7 @@ class Solver {
   std::map<std::pair<int, int64_t>, kern::SplitPlan> banded_;  // split_plan_banded cache
   hipStream_t s_compute_ = nullptr, s_comm_ = nullptr;
   bool own_streams_ = false;
+  bool first_cycle_ = false;  // the next launch_overlap is a step() call's first cycle (lead_first)
   hipEvent_t ev_bnd_ = nullptr, ev_comm_ = nullptr, ev_int_ = nullptr;
   double* d_work_ = nullptr;   // stats workspace + 6 results
   bool timing_ = false;

@@ -619,10 +619,19 @@ static bool fused_candidates() {
   return on;
 }
 
-// Lead-order candidates on exchanging slabs (HEAT2D_LEAD=0 keeps them out).
-static bool lead_candidates() {
+// The first cycle of a step() call on an exchanging slab runs in the lead
+// order whatever its plan's split order (HEAT2D_LEAD_FIRST=0: the plan's
+// order): issued onto an idle GPU, the band launch gets its wave slots before
+// the interior's, which follows without waiting for it — the band launch (and
+// the exchange behind it) off the cycle's critical path. In steady-state
+// cycles both streams' launches become ready together and the band waves can
+// lose that race (then the bands end with the interior and the exchange
+// follows), so later cycles keep the autotuned order. A one-cycle step (the
+// 8-rank 20-step strong-scaling run) is all first cycle: 4096-row fp64 slab
+// rehearsal, kernel span 647 -> 610 us per cycle (profiles/r4/h/).
+static bool lead_first() {
   static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_LEAD");
+    const char* e = std::getenv("HEAT2D_LEAD_FIRST");
     return !e || std::atoi(e) != 0;
   }();
   return on;
@@ -705,7 +714,7 @@ static uint64_t plan_env_hash() {
                              "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
                              "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
                              "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN", "HEAT2D_EDGE_BANDS",
-                             "HEAT2D_FUSED_BALANCE", "HEAT2D_EDGE_MAIN", "HEAT2D_LEAD", "HEAT2D_COMM_PRIORITY"}) {
+                             "HEAT2D_FUSED_BALANCE", "HEAT2D_EDGE_MAIN", "HEAT2D_COMM_PRIORITY"}) {
       const char* e = std::getenv(name);
       const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
       for (unsigned char c : kv) v = (v ^ c) * 1099511628211ull;
@@ -753,7 +762,7 @@ bool Solver::cached_split(int k) {
   if (c.valid == 4 && (!fused_ok() || !fused_candidates())) return false;
   if ((c.flags & kern::kPlanDynamic) && !dynamic_candidates()) return false;
   if (c.valid == 2 && tr_->exchanges()) return false;
-  if ((c.flags & kern::kPlanLead) && (c.valid != 1 || !tr_->exchanges() || !lead_candidates())) return false;
+  if ((c.flags & kern::kPlanLead) && (c.valid != 1 || !tr_->exchanges())) return false;
   synchronize();
   const float t = time_plan(c, 4);
   H2D_HIP(hipEventRecord(ev_int_, s_compute_));
@@ -830,18 +839,7 @@ void Solver::autotune_split(int k) {
   bool top = false, bot = false;
   sent_sides(&top, &bot);
   std::vector<kern::SplitPlan> cands{best};
-  auto add = [&](const kern::SplitPlan& c0) {
-    // exchanging slabs: each concurrent candidate also in the lead order
-    if (c0.valid == 1 && tr_->exchanges() && lead_candidates()) {
-      kern::SplitPlan l = c0;
-      l.flags |= kern::kPlanLead;
-      cands.push_back(l);
-      if (dynamic_candidates() && l.main_items > l.main_waves) {
-        l.flags |= kern::kPlanDynamic;
-        cands.push_back(l);
-      }
-    }
-    const kern::SplitPlan& c = c0;
+  auto add = [&](const kern::SplitPlan& c) {
     cands.push_back(c);
     // more items than waves: also with the dynamic item queue (faster waves
     // take more items; per-wave timelines of the 32768^2 fp64 interior showed
@@ -1018,7 +1016,10 @@ void Solver::launch_overlap(int k, int64_t B) {
     pend_ = Pending::Fused;
     return;
   }
-  if (sp.valid == 3) {
+  const bool lead = (sp.valid == 1 || sp.valid == 3) &&
+                    ((sp.flags & kern::kPlanLead) || (first_cycle_ && tr_->exchanges() && lead_first()));
+  first_cycle_ = false;
+  if (sp.valid == 3 && !lead) {
     // edge-first: compute stream = [exchange c-1 landed] bands(c) -> interior(c);
     // comm stream (cycle_finish) = [bands(c) done] exchange(c), beside the interior.
     H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
@@ -1037,7 +1038,7 @@ void Solver::launch_overlap(int k, int64_t B) {
   H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));  // edge part c-1 (record not yet replaced)
   H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));     // main part c-1
   if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
-  if (sp.valid && (sp.flags & kern::kPlanLead)) {
+  if (lead) {
     // lead: the band launch first (comm stream), then the interior beside it
     kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_, cfg_.arith);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
@@ -1228,6 +1229,7 @@ void Solver::step(int64_t n) {
     return;
   }
   const std::vector<CycleRun> runs = step_runs(n, cur_);
+  first_cycle_ = true;
   // each cycle's exchange moves the rows the NEXT cycle reads; the last one
   // those of this call's first cycle (a repeated step(n) — bench, the CLI's
   // chunks — then never tops up)

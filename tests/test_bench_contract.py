@@ -124,18 +124,19 @@ def test_bench_reports_halo_traffic_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype,steps", [("fp64", 40), ("fp32", 37)])
-def test_bench_ipc_transport_share_gpu_matches_one_rank(dtype, steps):
+@pytest.mark.parametrize("dtype,steps,graph", [("fp64", 40, "on"), ("fp32", 37, "auto")])
+def test_bench_ipc_transport_share_gpu_matches_one_rank(dtype, steps, graph):
     """`bench.py --gpus 4 --share-gpu --transport peer`: four rank PROCESSES on the
     one GPU, fields mapped through hipIpc handles, halos pulled by device copies
-    ordered by stream-side counters (no RCCL), cycles replayed from hipGraphs —
-    the exact multi-process bench path on a 1-GPU box. The field statistics
+    ordered by stream-side counters (no RCCL), cycles replayed from hipGraphs
+    (--graph on) or eager (auto) — the exact multi-process bench path on a
+    1-GPU box. The field statistics
     equal the 1-rank run's exactly (sum, min, max; the sum is all-reduced, so
     compared to 1e-12)."""
     common = ["--grid", "8192", "--steps", str(steps), "--warmup", "5", "--check", "--dtype", dtype]
     one = run_plain("--gpus", "1", *common)
-    four = run_plain("--gpus", "4", "--share-gpu", "--transport", "peer", *common)
-    assert four["config"]["transport"] == "ipc" and four["config"]["graph"] is True
+    four = run_plain("--gpus", "4", "--share-gpu", "--transport", "peer", "--graph", graph, *common)
+    assert four["config"]["transport"] == "ipc" and four["config"]["graph"] is (graph == "on")
     assert four["config"]["parallelism"] == "slab4-shared-gpu"
     a, b = one["field_stats"], four["field_stats"]
     assert a["min"] == b["min"] and a["max"] == b["max"]
