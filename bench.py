@@ -269,8 +269,10 @@ def main():
                           slab_row0=slab_row0)
 
     def timed(s):
-        gc.collect()
-        gc.disable()  # no collector pause inside a sub-ms timed region
+        # no collector pause inside a sub-ms timed region (and no gc.collect()
+        # here: its pause idles the GPU, whose clocks then drop before a 3 ms
+        # timed run — 4096^2 fp32: 5008-5153 Gpts/s with it, profiles/r4/l/)
+        gc.disable()
         barrier()
         t0 = time.perf_counter()
         s.step(args.steps)

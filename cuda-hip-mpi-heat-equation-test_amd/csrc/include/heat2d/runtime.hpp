@@ -385,7 +385,7 @@ class Solver {
   void trial_cycle(const kern::SplitPlan& c);
   bool schedule_graphs() const;
   void capture_schedule(int64_t n);
-  float time_trial_schedule(const std::vector<int>& sc);  // ms of one graph replay of sc's trial cycles
+  float time_trial_schedule(const std::vector<int>& sc, int reps = 1);  // ms: the fastest of reps graph replays of sc
   void prepare_plans(int64_t n);  // prepare()'s planning / autotune / measured schedule (HIP split engine)
   float time_plan(const kern::SplitPlan& c, int kTimed);  // steady-state ms per trial cycle
   std::string cache_ctx() const;   // plan-cache key of this slab (plan_cache.hpp)
