@@ -52,9 +52,8 @@ typedef struct heat2d_split_plan {
   heat2d_rect main;
   heat2d_rect edge[4];
   int64_t main_waves, edge_waves, main_items, edge_items;
-  int32_t nfused, flags;  // flags & 2: dynamic item queue
-  heat2d_rect fused[6];
-  int64_t sig_items;
+  int32_t nrects, flags;  // flags & 2: dynamic item queue, & 4: lead order
+  heat2d_rect rects[6];
 } heat2d_split_plan;
 
 typedef int (*heat2d_exchange_fn)(void* ctx, void* send_lo, void* send_hi, void* recv_lo,

@@ -66,8 +66,8 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 struct TbRect {
   int64_t r0, r1, s0, s1, nb;
 };
-// rects of one launch (SplitPlan::fused, the kernel's TbArgs::rect)
-constexpr int kMaxFused = 6;
+// rects of one launch (SplitPlan::rects, the kernel's TbArgs::rect)
+constexpr int kMaxPlanRects = 6;
 constexpr int32_t kPlanDynamic = 2;  // SplitPlan::flags
 constexpr int32_t kPlanLead = 4;     // SplitPlan::flags (valid = 1)
 struct SplitPlan {
@@ -75,20 +75,16 @@ struct SplitPlan {
   TbRect main;
   TbRect edge[4];
   int64_t main_waves, edge_waves, main_items, edge_items;
-  // valid = 4 (fused, plan_fused): the MAIN launch's rects in item order —
-  // the exchanged bands first (sig_items items that signal their completion),
-  // then the interior — and `edge` holds only bands on the Dirichlet frame.
-  // valid = 1..3 with nfused > 0 (arith 2): `main` cut into frame-strip-
-  // weighted rects, launched instead of `main` (stencil_tb.hip weight_main).
+  // nrects > 0 (arith 2): `main` cut into frame-strip-weighted rects,
+  // launched instead of `main` (stencil_tb.hip weight_main).
   // flags & kPlanDynamic: the main launch takes its items from a dynamic
   // queue (more items than waves; TbArgs::queue). flags & kPlanLead (valid 1,
   // exchanging slabs): the concurrent order with the band launch issued
   // FIRST — its waves take their slots before the interior's, the interior's
   // last-dispatched waves (its one-item waves) start behind them, and the
   // exchange follows the bands on the comm stream.
-  int32_t nfused, flags;
-  TbRect fused[kMaxFused];
-  int64_t sig_items;
+  int32_t nrects, flags;
+  TbRect rects[kMaxPlanRects];
 };
 // The same plan with its boundary-band (EDGE) rects cut into `nb` row bands
 // each (valid = 1 / 3; default 1): more, shorter band items — nb x as many
@@ -104,29 +100,6 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
 // where the second launch costs more than it saves.
 SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int ring_override = 0, int64_t bands = 0,
                       int arith = 0);
-// Fused cycle (valid = 4) for slabs whose halo exchange can be gated on a
-// device counter (Transport::gates()): ONE interior-kernel launch whose first
-// items are the boundary bands the exchange sends (top if send_top, bottom if
-// send_bottom; taken by wave id as the first items of waves 0 .. Nb-1, their
-// rows republished at device scope, each item counted in a device counter
-// when its stores drain), then the interior as row bands (main_bands; 0:
-// chosen as for the split plan) from the dynamic item queue, so the waves
-// that marched a band item take less interior; bands on the Dirichlet frame
-// (a first / last rank) go to a small general launch beside it. The exchange starts as soon as the band count is
-// reached instead of after a separate band launch (the edge-first order's
-// serial phase: 77 of 879 us on the 8-rank fp64 slab, profiles/r3/thin/).
-// valid = 0 if the slab is too thin or has more band items than waves.
-SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool send_top, bool send_bottom, int cus = 0,
-                     int spare_waves = 0, int ring_override = 0, int arith = 0, int64_t main_bands = 0);
-// Launch the MAIN part of a fused plan, counting band items into *sig (queue:
-// the dynamic item queue's counters, used when the plan has more items than waves).
-void launch_fused_main(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, uint32_t* sig,
-                       double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr);
-// A one-wave kernel on `stream` that waits until *counter >= target (an
-// exchange gated on a fused cycle's band count); a wait longer than
-// timeout_ticks sets *err and returns.
-void launch_wait_counter(const uint32_t* counter, uint32_t target, uint64_t timeout_ticks, unsigned int* err,
-                         hipStream_t stream);
 // queue: 2 device counters (zeroed once) for plans with flags & kPlanDynamic (dynamic items)
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr);

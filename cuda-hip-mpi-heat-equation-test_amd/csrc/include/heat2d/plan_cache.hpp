@@ -15,7 +15,7 @@
 // cached plan (a drift of more than 10 % re-tunes).
 //
 // File: $HEAT2D_PLAN_CACHE (path; "off" disables), default
-// $XDG_CACHE_HOME/heat2d/plans-v3.txt or ~/.cache/heat2d/plans-v3.txt. One
+// $XDG_CACHE_HOME/heat2d/plans-v4.txt or ~/.cache/heat2d/plans-v4.txt. One
 // "key<TAB>value" line per entry, appended (O_APPEND: concurrent rank
 // processes add whole lines); the last line of a key wins.
 #pragma once

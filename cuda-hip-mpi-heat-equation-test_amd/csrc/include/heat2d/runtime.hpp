@@ -108,18 +108,6 @@ class Transport {
   // The solver's two field buffers (allocation bases, layout L): transports
   // that map their peers' fields once (IPC) do it here. Collective.
   virtual void attach(void* /*buf0*/, void* /*buf1*/, const SlabLayout& /*L*/, DType /*dt*/) {}
-  // Exchanges that can wait on a device-side gate (a kernel on the stream
-  // spinning on a counter): the fused cycle (kern::plan_fused), whose band
-  // rows are produced by the first items of the still-running interior launch.
-  struct Gate {
-    uint32_t* counter;       // device: band items done (the gate consumes it)
-    uint32_t target;
-    uint64_t timeout_ticks;
-    unsigned int* err;       // host-visible: the wait timed out
-  };
-  virtual bool gates() const { return false; }
-  virtual void exchange_gated(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
-                              const Gate& g);
 };
 
 // RAII bracket of Transport::io_phase.
@@ -392,12 +380,6 @@ class Solver {
   std::string sched_ctx() const;   // ... of the decomposition's schedules
   bool cached_split(int k);        // plan of depth k from the cache, re-validated
   bool cached_schedule(int64_t n); // measured schedule of n steps from the cache (collective)
-  // fused cycles (kern::plan_fused): the exchange gated on the interior
-  // launch's band items (HEAT2D_FUSED=0 disables)
-  bool fused_ok() const;
-  void sent_sides(bool* top, bool* bottom) const;
-  void ensure_err();
-  void ensure_sig();
   void run_schedule_graph(int64_t n);
   float depth_ms(int k);
   float prescan_ms(int k);  // default-plan cycle time of depth k, max over ranks (schedule prescan)
@@ -431,7 +413,7 @@ class Solver {
   double phase_acc_[5] = {};
   PhaseEvents* phase_begin(int kind);
   // the launched, not yet finished cycle (cycle_launch -> cycle_finish)
-  enum class Pending { None, Serial, Concurrent, EdgeFirst, Fused };
+  enum class Pending { None, Serial, Concurrent, EdgeFirst };
   Pending pend_ = Pending::None;
   int pend_k_ = 0;
   int64_t pend_pe_ = -1;  // index into phase_ev_ (timing) or -1
@@ -453,11 +435,7 @@ class Solver {
   int64_t plans_made_ = 0;
   int64_t plan_cache_hits_ = 0;
   int plan_origin_[kMaxTB + 1];           // plan_origin(), initialised to -1
-  unsigned int* h_err_ = nullptr;         // pinned, host-visible error word (exchange gates)
-  uint32_t* d_sig_ = nullptr;             // [0]: band items of the running fused cycle; [1]: trial scratch
   uint32_t* d_queue_ = nullptr;           // dynamic item queue of the main launches (SplitPlan::pair bit 1)
-  int64_t pend_sig_ = 0;                  // band items the pending fused cycle signals
-  uint64_t gate_timeout_ticks_ = 0;
   hipEvent_t ev_t0_ = nullptr, ev_t1_ = nullptr;  // time_plan
   hipGraphExec_t graph_exec_ = nullptr;  // two cycles (A->B->A) at depth K
   int graph_k_ = 0;

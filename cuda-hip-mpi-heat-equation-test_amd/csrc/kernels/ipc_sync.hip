@@ -61,34 +61,7 @@ __global__ __launch_bounds__(64) void ipc_depart_kernel(IpcSlot* slots, int me) 
   st_rel(&slots[me].done, c + 1);
 }
 
-// Gate of an exchange on a fused cycle's band count (the interior launch's
-// first items): wait until *c >= target, then consume the count (reset it to
-// 0 for the next cycle — no cycle number baked in, so a captured graph
-// replays it). The next cycle's launch starts only after the exchange that
-// follows this kernel, so the reset cannot race the next count.
-__global__ __launch_bounds__(64) void wait_counter_kernel(uint32_t* c, uint32_t target, uint64_t limit,
-                                                          unsigned int* err) {
-  if (threadIdx.x != 0) return;
-  const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    if (wall_clock64() - t0 > limit) {
-      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 }  // namespace
-
-void launch_wait_counter(const uint32_t* counter, uint32_t target, uint64_t timeout_ticks, unsigned int* err,
-                         hipStream_t stream) {
-  hipLaunchKernelGGL(wait_counter_kernel, dim3(1), dim3(64), 0, stream, const_cast<uint32_t*>(counter), target,
-                     timeout_ticks, err);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("wait_counter launch: ") + hipGetErrorString(e));
-}
 
 void launch_ipc_arrive(IpcSlot* slots, uint64_t* ctrl, int me, int p0, int p1, uint64_t timeout_ticks,
                        hipStream_t stream) {

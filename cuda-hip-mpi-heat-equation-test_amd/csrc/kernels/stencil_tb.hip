@@ -119,16 +119,6 @@ decltype(auto) with_ar(int arith, F&& f) {
   if (arith == 1) return f(std::integral_constant<int, 1>{});
   return f(std::integral_constant<int, 0>{});
 }
-// the fused cycle's interior kernel exists for arith 0..2 only (opt-in; not
-// instantiated for the scaled-level arithmetic 3)
-template <class F>
-decltype(auto) with_ar_fused(int arith, F&& f) {
-  HEAT2D_REQUIRE(arith >= 0 && arith <= 2, "fused cycles: arith 0, 1 or 2");
-  if (arith == 2) return f(std::integral_constant<int, 2>{});
-  if (arith == 1) return f(std::integral_constant<int, 1>{});
-  return f(std::integral_constant<int, 0>{});
-}
-
 template <typename T, int AR>
 int occupancy_t(int ring, bool main, int k) {
   if (ring == 4) return main ? occupancy_blocks<T, 4, true, AR>(k) : occupancy_blocks<T, 4, false, AR>(k);
@@ -263,8 +253,7 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t simds, int k, int64_t pri
 // partials != nullptr: the fused-statistics kernel (general, ring 4). Returns the waves launched.
 int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
                      const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith,
-                     double* partials = nullptr, int64_t sig_items = 0, uint32_t* sig = nullptr,
-                     uint32_t* queue = nullptr) {
+                     double* partials = nullptr, uint32_t* queue = nullptr) {
   HEAT2D_REQUIRE(nrect >= 1 && nrect <= (main ? kMainRects : kMaxRects), "bad rect count");
   TbArgs a{};
   a.pitch = L.pitch;
@@ -292,9 +281,6 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   a.nitems = items;
   a.nwaves = std::max<int64_t>(1, std::min<int64_t>(nwaves, items));
   a.partials = partials;
-  HEAT2D_REQUIRE(sig_items == 0 || (main && sig != nullptr && sig_items <= items), "bad band-signal items");
-  a.sig_items = sig_items;
-  a.sig = sig;
   a.wtimes = wave_times_buf(a.nwaves);
   if (arith == 3) {  // scaled levels (tb_impl.hpp AR 3): coefficients of this depth, in double
     HEAT2D_REQUIRE(r > 0.0, "arith 3 (fast) needs r > 0");
@@ -302,10 +288,8 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
     a.fu = std::pow(r, (double)k);
     a.fu1 = std::pow(r, (double)(k - 1));
   }
-  // the dynamic queue only pays with more items than waves (plain and fused
-  // interior kernels; a fused launch's band items are the first nwaves items,
-  // taken by wave id, so the queue hands out interior items only)
-  HEAT2D_REQUIRE(!sig || sig_items <= a.nwaves, "band-signal items must be first items of the waves");
+  // the dynamic queue only pays with more items than waves (interior and
+  // single launches; not the statistics kernel)
   a.queue = (queue && !partials && items > a.nwaves) ? queue : nullptr;
   const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
   const int64_t o = L.origin();
@@ -317,21 +301,6 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
       constexpr int AR = decltype(ar)::value;
       if (dt == DType::F32) dispatch_stats<float, AR>(k, nblocks, s32, static_cast<float*>(dst) + o, a, (float)r, stream);
       else dispatch_stats<double, AR>(k, nblocks, s64, static_cast<double*>(dst) + o, a, r, stream);
-    });
-  } else if (sig) {  // the fused cycle's interior kernel
-    const float* s32 = static_cast<const float*>(src) + o;
-    const double* s64 = static_cast<const double*>(src) + o;
-    float* d32 = static_cast<float*>(dst) + o;
-    double* d64 = static_cast<double*>(dst) + o;
-    with_ar_fused(arith, [&](auto ar) {
-      constexpr int AR = decltype(ar)::value;
-      if (dt == DType::F32) {
-        if (ring == 4) dispatch_fused<float, 4, AR>(k, nblocks, s32, d32, a, (float)r, stream);
-        else dispatch_fused<float, 6, AR>(k, nblocks, s32, d32, a, (float)r, stream);
-      } else {
-        if (ring == 4) dispatch_fused<double, 4, AR>(k, nblocks, s64, d64, a, r, stream);
-        else dispatch_fused<double, 6, AR>(k, nblocks, s64, d64, a, r, stream);
-      }
     });
   } else if (dt == DType::F32) {
     dispatch_t<float>(ring, main, arith, k, nblocks, static_cast<const float*>(src) + o, static_cast<float*>(dst) + o, a,
@@ -428,7 +397,7 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 // does, priming rows (2k per item) included: (Le + 2k) w = Li + 2k. A plan
 // whose segments tile every strip exactly keeps doing so (a segment crossing
 // a strip end pays a second priming), with as many interior segments per
-// strip as fit the original item count. plan.fused[] / plan.nfused hold the
+// strip as fit the original item count. plan.rects[] / plan.nrects hold the
 // rects; plan.main keeps the unweighted rect that describes the plan.
 //
 // Frame ROWS likewise: an item whose march reaches the global top / bottom row
@@ -462,7 +431,7 @@ double pinned_weight(DType dt, bool row, bool single, int ring) {
   return single ? 1.3 : 1.6;
 }
 
-int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect out[kMaxFused], bool single,
+int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect out[kMaxPlanRects], bool single,
                   int ring) {
   const int64_t ns = R.s1 - R.s0, rows = R.r1 - R.r0;
   if (ns < 3 || rows < 2) return 0;
@@ -534,14 +503,14 @@ int weighted_main(DType dt, int k, const TbRect& R, const SlabLayout& L, TbRect 
 
 int64_t rect_items(const TbRect& R) { return R.nb > 0 ? R.nb * (R.s1 - R.s0) : -R.nb; }
 
-// arith 2: put the weighted rects of p.main into p.fused (see weighted_main)
+// arith 2: put the weighted rects of p.main into p.rects (see weighted_main)
 void weight_main(DType dt, const SlabLayout& L, SplitPlan& p, int arith, int64_t slots, bool single) {
   if (arith != 2) return;
-  const int n = weighted_main(dt, p.k, p.main, L, p.fused, single, p.ring);
+  const int n = weighted_main(dt, p.k, p.main, L, p.rects, single, p.ring);
   if (n == 0) return;
-  p.nfused = n;
+  p.nrects = n;
   p.main_items = 0;
-  for (int i = 0; i < n; ++i) p.main_items += rect_items(p.fused[i]);
+  for (int i = 0; i < n; ++i) p.main_items += rect_items(p.rects[i]);
   p.main_waves = std::min<int64_t>(p.main_items, slots);
 }
 
@@ -595,89 +564,6 @@ SplitPlan with_edge_bands(DType dt, const SplitPlan& p, int64_t nb, int arith) {
   const int bpc_e = occupancy(dt, q.ring, false, q.k, arith);
   q.edge_waves = std::min<int64_t>(q.edge_items, (int64_t)cu_count() * bpc_e * 4);
   return q;
-}
-
-SplitPlan plan_fused(DType dt, const SlabLayout& L, int k, int64_t band, bool send_top, bool send_bottom, int cus,
-                     int spare_waves, int ring_override, int arith, int64_t main_bands) {
-  check_layout(dt, L, k);
-  SplitPlan p{};
-  p.k = k;
-  p.ring = ring_ok(dt, k, (ring_override == 4 || ring_override == 6) ? ring_override : default_ring(dt, k));
-  const int64_t n = L.nrows, B = std::max<int64_t>(band, k);
-  const int64_t U = useful_width(dt, k);
-  const int64_t ns = (L.ncols + U - 1) / U;
-  const int64_t rows_m = n - 2 * B;
-  if (rows_m < 4 * k) return p;
-  // a band whose march reaches the Dirichlet frame needs the general kernel
-  const bool frame_top = L.row0 < k, frame_bottom = L.row0 + n + k > L.nrows_global;
-  if ((send_top && frame_top) || (send_bottom && frame_bottom)) return p;
-  const int nsig = (send_top ? 1 : 0) + (send_bottom ? 1 : 0);
-  if (nsig == 0) return p;
-  if (arith == 3) return p;  // no fused kernel for the scaled-level arithmetic
-  const int bpc = with_ar_fused(arith, [&](auto ar) {
-    constexpr int AR = decltype(ar)::value;
-    if (dt == DType::F32) return p.ring == 4 ? occupancy_fused<float, 4, AR>(k) : occupancy_fused<float, 6, AR>(k);
-    return p.ring == 4 ? occupancy_fused<double, 4, AR>(k) : occupancy_fused<double, 6, AR>(k);
-  });
-  const int64_t slots = (int64_t)(cus > 0 ? cus : cu_count()) * bpc * 4;
-  const int64_t W = std::max<int64_t>(4, slots - std::max(0, spare_waves));
-  const int64_t Nb = nsig * ns;
-  if (Nb >= W) return p;  // every band item must be a wave's FIRST item (taken by wave id)
-  // item order: the sent bands first — waves 0 .. Nb-1 take them by wave id
-  // and the exchange is gated on their count — then the interior as row
-  // bands (the split plan's interior, the same locality: waves in flight on the
-  // same rows of adjacent strips share the strip halos in L2), handed out by
-  // the dynamic queue, so the waves that marched a band item take less of it
-  int64_t nb = choose_bands(rows_m, ns, dt == DType::F32 ? balance_units(dt, cus, bpc) : W, k,
-                            dt == DType::F32 ? std::max(1, k - 1) : -1);
-  if (main_bands > 0) nb = std::min<int64_t>(main_bands, std::max<int64_t>(1, rows_m / (2 * (int64_t)k)));
-  int nf = 0;
-  if (send_top) p.fused[nf++] = TbRect{0, B, 0, ns, 1};
-  if (send_bottom) p.fused[nf++] = TbRect{n - B, n, 0, ns, 1};
-  // The waves that marched a band item (B + P march rows, P the priming rows
-  // of an item) take their interior item last, from the queue: unless those
-  // items are shorter by B + P rows, the cycle ends a band item after the rest
-  // (the serial band launch of the edge-first order, moved into the waves).
-  // So the last nsig bands of every strip are short (S = L - B - P,
-  // (nb - nsig) L + nsig S = rows_m) and come last in item order.
-  // HEAT2D_FUSED_BALANCE=0: equal bands (A/B).
-  const int64_t P = dt == DType::F32 ? std::max(1, k - 1) : 2 * (int64_t)k;
-  const int64_t nbl = nb - nsig;
-  const int64_t Lr = nbl > 0 ? (rows_m + nsig * (B + P) + nb - 1) / nb : 0;
-  const int64_t S = nbl > 0 ? (rows_m - nbl * Lr) / nsig : 0;
-  static const bool balance = [] {
-    const char* e = std::getenv("HEAT2D_FUSED_BALANCE");
-    return !e || std::atoi(e) != 0;
-  }();
-  if (balance && nbl > 0 && S >= std::max<int64_t>(2 * P, 16)) {
-    p.fused[nf++] = TbRect{B, B + nbl * Lr, 0, ns, nbl};
-    p.fused[nf++] = TbRect{B + nbl * Lr, n - B, 0, ns, nsig};
-  } else {
-    p.fused[nf++] = TbRect{B, n - B, 0, ns, nb};
-  }
-  p.nfused = nf;
-  p.sig_items = Nb;
-  p.main = TbRect{B, n - B, 0, ns, nb};  // (the interior as a whole: its band count re-cuts it)
-  p.main_items = Nb + nb * ns;
-  p.main_waves = std::min<int64_t>(W, p.main_items);
-  if (p.main_items > p.main_waves) p.flags |= kPlanDynamic;
-  // bands on the frame (first / last rank): general kernel, beside the main launch
-  int ne = 0;
-  if (!send_top) p.edge[ne++] = TbRect{0, B, 0, ns, 1};
-  if (!send_bottom) p.edge[ne++] = TbRect{n - B, n, 0, ns, 1};
-  p.nedge = ne;
-  p.edge_items = ne * ns;
-  const int bpc_e = occupancy(dt, p.ring, false, k, arith);
-  p.edge_waves = std::min<int64_t>(std::max<int64_t>(p.edge_items, 1), (int64_t)cu_count() * bpc_e * 4);
-  p.valid = 4;
-  return p;
-}
-
-void launch_fused_main(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, uint32_t* sig,
-                       double r, hipStream_t stream, int arith, uint32_t* queue) {
-  HEAT2D_REQUIRE(p.valid == 4 && p.nfused >= 2 && p.nfused <= kMainRects, "not a fused plan");
-  launch_rects(dt, src, dst, L, p.k, p.ring, true, p.fused, p.nfused, p.main_waves, r, stream, arith, nullptr,
-               p.sig_items, sig, (p.flags & kPlanDynamic) ? queue : nullptr);
 }
 
 SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus, int ring_override, int64_t bands, int arith) {
@@ -748,18 +634,16 @@ void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, con
   // (SplitPlan::flags & kPlanDynamic: the main part takes its items from the dynamic queue)
   uint32_t* q = (p.flags & kPlanDynamic) ? queue : nullptr;
   HEAT2D_REQUIRE(p.valid, "invalid split plan");
-  HEAT2D_REQUIRE(p.valid != 4 || !main_part, "a fused plan's main part needs its band counter (launch_fused_main)");
-  if (p.valid == 4 && p.nedge == 0) return;  // no band on the frame
   // the main part: p.main, or its frame-strip-weighted rects (weight_main)
-  const TbRect* mr = p.nfused > 0 ? p.fused : &p.main;
-  const int nm = p.nfused > 0 ? p.nfused : 1;
+  const TbRect* mr = p.nrects > 0 ? p.rects : &p.main;
+  const int nm = p.nrects > 0 ? p.nrects : 1;
   if (p.valid == 2) {  // single general launch over the whole slab (no edge part)
     if (main_part)
-      launch_rects(dt, src, dst, L, p.k, p.ring, false, mr, nm, p.main_waves, r, stream, arith, nullptr, 0, nullptr, q);
+      launch_rects(dt, src, dst, L, p.k, p.ring, false, mr, nm, p.main_waves, r, stream, arith, nullptr, q);
     return;
   }
   if (main_part)
-    launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith, nullptr, 0, nullptr, q);
+    launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith, nullptr, q);
   else
     launch_rects(dt, src, dst, L, p.k, p.ring, edges_on_main(L, p.k, p.edge, p.nedge), p.edge, p.nedge, p.edge_waves,
                  r, stream, arith);

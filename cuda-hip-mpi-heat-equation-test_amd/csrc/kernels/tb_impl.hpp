@@ -82,8 +82,8 @@ __device__ __forceinline__ float sadd_from_lower(float a, float x) { return fenc
 // Kernel arguments: the work is up to kMaxRects rectangles (output rows x
 // strips), each cut into `nb` row bands; a work item is one (band, strip) of
 // one rectangle. item0 = index of the rectangle's first item.
-constexpr int kMaxRects = kMaxFused;
-constexpr int kMainRects = 4;  // interior (MAIN) kernels: frame-strip rects or a fused plan's
+constexpr int kMaxRects = kMaxPlanRects;
+constexpr int kMainRects = 4;  // interior (MAIN) kernels: frame-strip rects or the boundary bands
 struct TbRectArg {
   int64_t r0, r1;  // output rows [r0, r1)
   int64_t s0, s1;  // strips [s0, s1)
@@ -102,12 +102,6 @@ struct TbArgs {
   int32_t xcd_remap;  // 1: XCD-aware block -> wave-id mapping (tb_kernel)
   TbRectArg rect[kMaxRects];
   double* partials;   // ST kernels: per-wave statistics, partials[j * nwaves + wave] (kNStatFused = 6 values)
-  // Fused cycles (MAIN kernel): items [0, sig_items) are the boundary bands a
-  // halo exchange sends. Their rows are stored at device scope and each one
-  // counts itself done in *sig once its stores have drained, so the exchange
-  // (gated on the count) starts while the rest of the launch runs.
-  int64_t sig_items;
-  uint32_t* sig;
   // Diagnostics (HEAT2D_WAVE_TIMES, kern::wave_times): per launched wave
   // {start, end (wall clock, 100 MHz), first item, its edge kind}; nullptr off
   uint64_t* wtimes;
@@ -981,46 +975,13 @@ __device__ __forceinline__ bool tb_piece(const TbArgs& a, int64_t it, int32_t li
 // K = 12 on, so it has none.) The r = 1/4 (AR 2) fp64 interior kernel keeps 2
 // waves/SIMD at K = 18..19 under a floor; at K = 20 ring 4 a floor spills (its
 // ring-6 twin fits 241 VGPRs, which the autotuner weighs). The fp32 interior
-// kernels at K = 17..20 (ring 4) keep 2 waves/SIMD under a floor. The fused-cycle
-// variant (more state) takes no floor. Checked per build:
+// kernels at K = 17..20 (ring 4) keep 2 waves/SIMD under a floor. Checked per build:
 // ScratchSize = 0 in the ISA (tools/isa_report.py, tests/test_isa.py).
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
 constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K == 11) ? 4
                           : (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 2 && K >= 18 && K <= 19) ? 2
                           : (std::is_same<T, float>::value && MAIN && RING == 4 && K >= 17)                        ? 2
                                                                                                                   : 1;
-
-// Rows [t0, t1) of `strip` that this wave just stored: re-read (sc0: past the
-// CU's L1, from the XCD's L2 that holds them) and store again at device scope
-// (nt sc1: written through past the non-coherent L2), 8 rows in flight.
-template <typename T, int NV, int K>
-__device__ __forceinline__ void republish(T* dst, const TbArgs& a, int64_t strip, int64_t t0, int64_t t1, int lane) {
-  using S = TbShape<T, NV, K>;
-  using U4 = unsigned int __attribute__((ext_vector_type(4)));
-  static_assert(NV == 1, "16 B per lane");
-  constexpr int ES = (int)sizeof(T);
-  const int64_t u0 = strip * S::U;
-  const int64_t mycol = u0 - S::KA + (int64_t)lane * S::V;
-  const int64_t ustop = min(u0 + (int64_t)S::U, a.ncols);
-  const bool ok = mycol >= u0 && mycol < ustop && mycol >= a.col_lo && mycol + S::V <= a.col_hi;
-  const int32_t off = ok ? (int32_t)((mycol - a.col_lo) * ES) : kOob;
-  const char* base = reinterpret_cast<const char*>(dst + a.col_lo);
-  const int64_t pitch_b = a.pitch * ES;
-  constexpr int kChunk = 8;
-  for (int64_t r0 = t0; r0 < t1; r0 += kChunk) {
-    U4 v[kChunk];
-#pragma unroll
-    for (int i = 0; i < kChunk; ++i) {
-      const __amdgpu_buffer_rsrc_t rs = row_rsrc(base + (r0 + i) * pitch_b, r0 + i < t1 ? (uint32_t)pitch_b : 0u);
-      v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 1);
-    }
-#pragma unroll
-    for (int i = 0; i < kChunk; ++i) {
-      const __amdgpu_buffer_rsrc_t rs = row_rsrc(base + (r0 + i) * pitch_b, r0 + i < t1 ? (uint32_t)pitch_b : 0u);
-      __builtin_amdgcn_raw_buffer_store_b128(v[i], rs, off, 0, 16 | 2);
-    }
-  }
-}
 
 // wave-wide sum / min / max (fixed xor butterfly: every lane ends with the
 // same bits, lane 0's are written)
@@ -1059,21 +1020,18 @@ __device__ __forceinline__ void queue_exit(const TbArgs& a) {
 }
 
 // Kernel variants (VAR): 0 plain; 1 fused statistics (StatAcc; general kernel).
-// (A third, latency-oriented variant for the boundary-band launch — priming
-// skip + dependency chains — measured slower everywhere and was removed:
-// profiles/edge_kernel.md.)
-// 2: the interior kernel of a fused cycle (kern::plan_fused): device-scope
-// row stores, band items counted into TbArgs::sig.
-constexpr int kVarPlain = 0, kVarStats = 1, kVarFused = 2;
+// (A latency-oriented variant for the boundary-band launch — priming skip +
+// dependency chains — measured slower everywhere and was removed:
+// profiles/edge_kernel.md. So was the fused-cycle interior kernel, whose
+// first items were the bands the exchange sends: one such launch ran 720 us
+// where band launch + interior take 647 (edge-first) or 610 (lead order),
+// profiles/r4/lead/.)
+constexpr int kVarPlain = 0, kVarStats = 1;
 
-// (The fused interior variant's band-item code costs the fp64 K = 20 ring-4
-// kernel 2 VGPRs over 256 — 1 wave/SIMD; a 2-wave floor spilled 28 B to
-// scratch. Its ring-6 twin keeps 2 waves at 245: the autotuner weighs both.)
 template <typename T, int NV, int K, int RING, bool MAIN, int AR, int VAR = kVarPlain>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVarPlain ? kMinWaves<T, NV, K, RING, MAIN, AR> : 1))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
   constexpr bool ST = VAR == kVarStats;
   static_assert(VAR != kVarStats || !MAIN, "the statistics variant uses the general kernel");
-  static_assert(VAR != kVarFused || MAIN, "the fused variant is an interior kernel");
   using S = TbShape<T, NV, K>;
   const int lane = threadIdx.x & 63;
   // readfirstlane: make the wave id (and everything derived from it: strip, rows,
@@ -1104,12 +1062,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
   while (it < a.nitems) {
     int64_t strip, t0, t1;
     if (!tb_piece<NR>(a, it, lin, strip, t0, t1)) {
-      if constexpr (VAR == kVarFused) {
-        if (it < a.sig_items) {  // a band item of a fused cycle is complete: count it
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lane == 0) __hip_atomic_fetch_add(a.sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
       it = next_item(a, it);
       if (it < a.nitems) lin = tb_span<NR>(a, it).lin;
       continue;
@@ -1131,13 +1083,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
         march<T, NV, K, 2, RING, AR, false, PS>(src, dst, a, r, strip, t0, t1, lane);
       else
         march<T, NV, K, 0, RING, AR, false, PS>(src, dst, a, r, strip, t0, t1, lane);
-      if constexpr (VAR == kVarFused) {
-        // a band item (single piece): its rows again, written through to the
-        // device-coherent level, for the exchange that reads them while this
-        // launch still runs (storing every row at device scope cost the
-        // interior ~25 %, and a second march instance a wave per SIMD)
-        if (it < a.sig_items) republish<T, NV, K>(dst, a, strip, t0, t1, lane);
-      }
     } else {
       const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
                      (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
@@ -1194,11 +1139,6 @@ template <typename T, int RING, bool MAIN, int AR>
 void dispatch(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
 template <typename T, int RING, bool MAIN, int AR>
 int occupancy_blocks(int k);
-// fused-cycle interior kernels (VAR = kVarFused), instantiated beside the MAIN ones
-template <typename T, int RING, int AR>
-void dispatch_fused(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
-template <typename T, int RING, int AR>
-int occupancy_fused(int k);
 // fused-statistics kernels: general kernel, ring 4 (tb_<dtype>_stats.hip)
 template <typename T, int AR>
 void dispatch_stats(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
@@ -1248,36 +1188,6 @@ int occupancy_blocks_stats(int k);
         break;                                                                                          \
     }                                                                                                   \
     return 1;                                                                                           \
-  }
-#define H2D_FU_CASE(T, RING, MAIN, AR, KK)                                                                          \
-  case KK:                                                                                                          \
-    hipLaunchKernelGGL((tb_kernel<T, 1, KK, RING, true, AR, kVarFused>), dim3(nblocks), dim3(256), 0, s, src, dst, a, \
-                       r);                                                                                          \
-    return;
-#define H2D_FU_OCC_CASE(T, RING, MAIN, AR, KK) \
-  case KK:                                     \
-    return blocks_per_cu<T, 1, KK, RING, true, AR, kVarFused>();
-#define H2D_FU_UNIT(T, RING, AR, DEEP)                                                                     \
-  template <>                                                                                              \
-  void dispatch_fused<T, RING, AR>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r,    \
-                                   hipStream_t s) {                                                        \
-    switch (k) {                                                                                           \
-      H2D_TB_CASES(H2D_FU_CASE, T, RING, true, AR)                                                         \
-      DEEP(H2D_FU_CASE, T, RING, true, AR)                                                                 \
-      default:                                                                                             \
-        break;                                                                                             \
-    }                                                                                                      \
-    HEAT2D_REQUIRE(false, "temporal depth not instantiated for the fused interior kernel");                \
-  }                                                                                                        \
-  template <>                                                                                              \
-  int occupancy_fused<T, RING, AR>(int k) {                                                                \
-    switch (k) {                                                                                           \
-      H2D_TB_CASES(H2D_FU_OCC_CASE, T, RING, true, AR)                                                     \
-      DEEP(H2D_FU_OCC_CASE, T, RING, true, AR)                                                             \
-      default:                                                                                             \
-        break;                                                                                             \
-    }                                                                                                      \
-    return 1;                                                                                              \
   }
 #define H2D_TB_UNIT(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_NO_CASES)
 #define H2D_TB_UNIT_F64(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_DEEP)

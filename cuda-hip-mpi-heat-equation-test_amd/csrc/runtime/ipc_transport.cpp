@@ -103,13 +103,6 @@ class IpcTransport final : public Transport {
   bool aborted() const override { return aborted_.load(); }
   void io_phase(bool on) override { io_ += on ? 1 : -1; }
   void graph_launched(hipStream_t stream) override { track(stream, "graph replay"); }
-  bool gates() const override { return true; }
-  void exchange_gated(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
-                      const Gate& g) override {
-    if ((size_ == 1 && !loop_) || k <= 0) return;
-    kern::launch_wait_counter(g.counter, g.target, g.timeout_ticks, g.err, stream);
-    exchange(field, L, dt, k, stream, true);
-  }
 
   void attach(void* buf0, void* buf1, const SlabLayout& L, DType dt) override {
     if (size_ == 1 && !loop_) return;

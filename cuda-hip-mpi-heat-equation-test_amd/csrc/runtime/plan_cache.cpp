@@ -33,7 +33,7 @@ std::string default_path() {
   if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) base = x;
   else if (const char* h = std::getenv("HOME"); h && *h) base = std::string(h) + "/.cache";
   else return "";
-  return base + "/heat2d/plans-v3.txt";
+  return base + "/heat2d/plans-v4.txt";
 }
 
 void mkdirs(const std::string& file) {
@@ -132,18 +132,19 @@ bool get_plan(const std::string& ctx, int k, int64_t band, kern::SplitPlan* p, f
   q.edge_items = w[3];
   float t = 0.f;
   in >> t;
-  long long nf = 0, sig = 0;
-  in >> nf;
-  for (auto& e : q.fused) {
+  long long nr = 0;
+  in >> nr;
+  for (auto& e : q.rects) {
     for (auto& x : r) in >> x;
     e = kern::TbRect{r[0], r[1], r[2], r[3], r[4]};
   }
   long long pr = 0;
-  in >> sig >> pr;
-  q.nfused = (int32_t)nf;
-  q.sig_items = sig;
+  in >> pr;
+  q.nrects = (int32_t)nr;
   q.flags = (int32_t)pr;
-  if (!in || q.k != k || q.nedge < 0 || q.nedge > 4 || q.nfused < 0 || q.nfused > kern::kMaxFused || q.flags < 0 || q.flags > (kern::kPlanDynamic | kern::kPlanLead)) return false;
+  if (!in || q.k != k || q.valid < 1 || q.valid > 3 || q.nedge < 0 || q.nedge > 4 || q.nrects < 0 ||
+      q.nrects > kern::kMaxPlanRects || q.flags < 0 || q.flags > (kern::kPlanDynamic | kern::kPlanLead))
+    return false;
   *p = q;
   *ms = t;
   return true;
@@ -156,9 +157,9 @@ void put_plan(const std::string& ctx, int k, int64_t band, const kern::SplitPlan
   rect(p.main);
   for (const auto& e : p.edge) rect(e);
   o << ' ' << p.main_waves << ' ' << p.edge_waves << ' ' << p.main_items << ' ' << p.edge_items << ' ' << ms;
-  o << ' ' << p.nfused;
-  for (const auto& e : p.fused) rect(e);
-  o << ' ' << p.sig_items << ' ' << p.flags;
+  o << ' ' << p.nrects;
+  for (const auto& e : p.rects) rect(e);
+  o << ' ' << p.flags;
   store(plan_key(ctx, k, band), o.str());
 }
 

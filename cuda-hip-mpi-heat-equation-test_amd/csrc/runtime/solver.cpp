@@ -164,20 +164,9 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
         // and RCCL's workgroups (kern::plan_split).
         H2D_HIP(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
       }
-      // The comm stream (bands, exchange) at the highest priority: when both
-      // streams' next launches become ready together (steady-state cycles),
-      // the band waves are dispatched before the interior's, as the lead
-      // order issues them in a cycle's first launch (HEAT2D_COMM_PRIORITY=0:
-      // default priority, A/B).
-      static const bool prio = [] {
-        const char* e = std::getenv("HEAT2D_COMM_PRIORITY");
-        return !e || std::atoi(e) != 0;
-      }();
-      int least = 0, greatest = 0;
-      if (prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least)
-        H2D_HIP(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking, greatest));
-      else
-        H2D_HIP(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+      // (A high-priority comm stream did not get the band waves dispatched
+      // first in steady-state cycles, nor change the small grid: profiles/r4/lead/, r4/m/.)
+      H2D_HIP(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
       own_streams_ = true;
     }
     H2D_HIP(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
@@ -210,9 +199,7 @@ Solver::~Solver() {
       if (b) (void)hipFree(b);
     if (d_work_) (void)hipFree(d_work_);
     if (d_part_) (void)hipFree(d_part_);
-    if (d_sig_) (void)hipFree(d_sig_);
     if (d_queue_) (void)hipFree(d_queue_);
-    if (h_err_) (void)hipHostFree(h_err_);
     if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
     if (ev_int_) (void)hipEventDestroy(ev_int_);
@@ -362,15 +349,6 @@ void Solver::cycle_finish() {
   if (pend_ == Pending::Serial) {
     exchange_on(dst, pend_x_, s_compute_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
-  } else if (pend_ == Pending::Fused) {
-    if (tr_->exchanges()) {
-      HEAT2D_REQUIRE(pend_x_ >= 1 && pend_x_ <= band_, "halo exchange depth outside [1, band]");
-      tr_->exchange_gated(dst, L_, dtype(), pend_x_, s_comm_,
-                          Transport::Gate{d_sig_, (uint32_t)pend_sig_, gate_timeout_ticks_, h_err_});
-      halo_rows_ += pend_x_;
-    }
-    if (pe) H2D_HIP(hipEventRecord(pe->ev[5], s_comm_));
-    H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
   } else {
     // both split orders: the exchange of the new bands runs on the comm
     // stream (concurrent: right behind the EDGE launch there; edge-first:
@@ -485,13 +463,6 @@ const kern::SplitPlan& Solver::split_plan(int k) {
         p.valid = 1;
         p.flags |= kern::kPlanLead;
       }
-      if (o == "fused" && fused_ok()) {
-        bool top, bot;
-        sent_sides(&top, &bot);
-        const kern::SplitPlan f = kern::plan_fused(dtype(), L_, k, k, top, bot, compute_cus_, spare, 0, cfg_.arith);
-        if (f.valid) p = f;
-        p.k = k;
-      }
       if (o == "single" && !tr_->exchanges()) {
         p = kern::plan_single(dtype(), L_, k, compute_cus_, 0, 0, cfg_.arith);
         p.k = k;
@@ -504,14 +475,7 @@ const kern::SplitPlan& Solver::split_plan(int k) {
     const char* env_bands = std::getenv("HEAT2D_BANDS");
     if (env_seg || env_bands) {
       const int64_t nseg = env_seg ? std::atoll(env_seg) : -std::atoll(env_bands);  // < 0: bands
-      if (nseg < 0 && p.valid == 4) {  // fused: the interior re-cut into n bands (segments: not offered)
-        bool top, bot;
-        sent_sides(&top, &bot);
-        const kern::SplitPlan f = kern::plan_fused(dtype(), L_, k, k, top, bot, compute_cus_, spare, p.ring,
-                                                   cfg_.arith, -nseg);
-        if (f.valid) p = f;
-        p.k = k;
-      } else if (nseg != 0 && p.valid) {
+      if (nseg != 0 && p.valid) {
         const int valid = p.valid, ring = p.ring;
         p = valid == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, -nseg, cfg_.arith)
                        : kern::plan_split(dtype(), L_, k, k, compute_cus_, spare, ring, -nseg, cfg_.arith);
@@ -537,14 +501,6 @@ const kern::SplitPlan& Solver::split_plan_banded(int k, int64_t B) {
   if (B <= k || !base.valid || base.valid == 2) return base;
   auto it = banded_.find({k, B});
   if (it != banded_.end()) return it->second;
-  if (base.valid == 4) {  // fused: the same ring, the bands and the interior balance re-cut for B
-    bool top, bot;
-    sent_sides(&top, &bot);
-    kern::SplitPlan d = kern::plan_fused(dtype(), L_, k, B, top, bot, compute_cus_, spare_waves(), base.ring, cfg_.arith,
-                                         base.main.nb > 0 ? base.main.nb : 0);
-    d.k = k;
-    return banded_.emplace(std::make_pair(k, B), d).first->second;
-  }
   // the same choice (order, ring, interior bands / segments) over the interior
   // left between B-row bands; too thin for that: valid = 0 (serial cycle)
   kern::SplitPlan d = kern::plan_split(dtype(), L_, k, B, compute_cus_, spare_waves(), base.ring, base.main.nb,
@@ -607,18 +563,6 @@ static bool tune_segments() {
   return on;
 }
 
-// Fused plans among the autotuner's candidates: opt-in (HEAT2D_FUSED=1). The
-// trials cannot see the exchange, and end to end the fused cycle measured
-// level with or behind the edge-first order on the rehearsed slabs
-// (profiles/r3/fused_v2/README.md); HEAT2D_SPLIT_ORDER=fused forces it.
-static bool fused_candidates() {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_FUSED");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
-}
-
 // The first cycle of a step() call on an exchanging slab runs in the lead
 // order whatever its plan's split order (HEAT2D_LEAD_FIRST=0: the plan's
 // order): issued onto an idle GPU, the band launch gets its wave slots before
@@ -647,16 +591,6 @@ void Solver::trial_cycle(const kern::SplitPlan& c) {
   void* src = buf_[cur_];
   void* dst = buf_[cur_ ^ 1];
   last_k_ = 0;  // the other buffer no longer holds T_{n-1}: stats(residual) reports NaN
-  if (c.valid == 4) {  // fused: interior launch (its band items counted into the scratch counter) + frame bands
-    ensure_sig();
-    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
-    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
-    kern::launch_fused_main(dtype(), src, dst, L_, c, d_sig_ + 1, cfg_.r, s_compute_, cfg_.arith, d_queue_);
-    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-    kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_comm_, cfg_.arith);
-    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
-    return;
-  }
   if (c.valid == 3) {  // edge-first: both parts in order on the compute stream
     H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
     kern::launch_split(dtype(), src, dst, L_, c, false, cfg_.r, s_compute_, cfg_.arith);
@@ -714,7 +648,7 @@ static uint64_t plan_env_hash() {
                              "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
                              "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
                              "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN", "HEAT2D_EDGE_BANDS",
-                             "HEAT2D_FUSED_BALANCE", "HEAT2D_EDGE_MAIN", "HEAT2D_COMM_PRIORITY"}) {
+                             "HEAT2D_FUSED_BALANCE", "HEAT2D_EDGE_MAIN"}) {
       const char* e = std::getenv(name);
       const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
       for (unsigned char c : kv) v = (v ^ c) * 1099511628211ull;
@@ -738,10 +672,10 @@ std::string Solver::cache_ctx() const {
   }
   const int pos = (L_.row0 == 0 ? 1 : 0) | (L_.row0 + L_.nrows == L_.nrows_global ? 2 : 0);
   char b[640];
-  std::snprintf(b, sizeof(b), "%s|cu%d|%s|ar%d|%lldx%lld|p%lld|h%lld|pos%d|ccu%d|sp%d|x%d|tr=%s|g%d|env%016llx",
+  std::snprintf(b, sizeof(b), "%s|cu%d|%s|ar%d|%lldx%lld|p%lld|h%lld|pos%d|ccu%d|sp%d|x%d|tr=%s|env%016llx",
                 arch.c_str(), ncu, dtype_name(dtype()), cfg_.arith, (long long)L_.nrows, (long long)L_.ncols,
                 (long long)L_.pitch, (long long)L_.halo, pos, compute_cus_, spare_waves(), tr_->exchanges() ? 1 : 0,
-                tr_->name().c_str(), tr_->gates() ? 1 : 0, (unsigned long long)plan_env_hash());
+                tr_->name().c_str(), (unsigned long long)plan_env_hash());
   return b;
 }
 
@@ -759,7 +693,6 @@ bool Solver::cached_split(int k) {
   // semantic checks on top of the key: a plan kind this run may not use
   // (fused cycles need a gating transport and HEAT2D_FUSED; the dynamic queue
   // is off under HEAT2D_DYNAMIC=0; a single launch cannot exchange)
-  if (c.valid == 4 && (!fused_ok() || !fused_candidates())) return false;
   if ((c.flags & kern::kPlanDynamic) && !dynamic_candidates()) return false;
   if (c.valid == 2 && tr_->exchanges()) return false;
   if ((c.flags & kern::kPlanLead) && (c.valid != 1 || !tr_->exchanges())) return false;
@@ -816,7 +749,7 @@ float Solver::exchange_penalty(const kern::SplitPlan& c, float trial_ms) const {
   if (!tr_->exchanges()) return 0.f;
   const double bytes = (double)halo_msg_bytes(L_, c.k, dtype_size(dtype()));
   const float tx = (float)(bytes / 50e6 + 0.010);  // ms
-  if (c.valid == 3 || c.valid == 4 || (c.valid == 1 && (c.flags & kern::kPlanLead)))
+  if (c.valid == 3 || (c.valid == 1 && (c.flags & kern::kPlanLead)))
     return std::max(0.f, tx - 0.8f * trial_ms);
   return tx;
 }
@@ -836,8 +769,6 @@ void Solver::autotune_split(int k) {
   // (no exchange): one general launch; mode 3 (exchange): edge-first split —
   // the short band launch first on the whole chip, then the interior, with the
   // exchange of the bands running beside the interior (valid = 3)
-  bool top = false, bot = false;
-  sent_sides(&top, &bot);
   std::vector<kern::SplitPlan> cands{best};
   auto add = [&](const kern::SplitPlan& c) {
     cands.push_back(c);
@@ -857,21 +788,8 @@ void Solver::autotune_split(int k) {
   }
   const std::vector<double> factors = long_cycles ? std::vector<double>{1.0, 0.5, 2.0}
                                                   : std::vector<double>{1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 1.25, 1.5, 2.0};
-  for (int mode : {1, 2, 3, 4}) {
+  for (int mode : {1, 2, 3}) {
     if (mode == 2 && !single_ok) continue;
-    if (mode == 4) {
-      // fused (exchange gated on the interior launch's band items): like the
-      // edge-first order it needs an interior long enough to hide the exchange
-      if (!fused_candidates() || !fused_ok() || best.valid != 1 || base_ms < kEdgeFirstMinCycleMs) continue;
-      for (int ring : {4, 6})
-        for (double f : long_cycles ? std::vector<double>{1.0} : std::vector<double>{1.0, 0.5, 2.0}) {
-          const int64_t nb = std::max<int64_t>(1, (int64_t)(std::max<int64_t>(nb0, 1) * f + 0.5));
-          kern::SplitPlan c = kern::plan_fused(dtype(), L_, k, k, top, bot, compute_cus_, spare, ring, cfg_.arith,
-                                               f == 1.0 ? 0 : nb);
-          if (c.valid) cands.push_back(c);
-        }
-      continue;
-    }
     // the trials run without the exchange, which the edge-first order puts
     // beside the WHOLE interior: only where the interior is long enough to
     // hide it (measured on the 1-rank RCCL rehearsal, profiles/multi_gpu_rehearsal_v4.md:
@@ -995,27 +913,6 @@ void Solver::launch_overlap(int k, int64_t B) {
   roctxRangePushA("heat2d.cycle.split");
   PhaseEvents* pe = timing_ ? phase_begin(0) : nullptr;
   pend_pe_ = pe ? (int64_t)phase_ev_.size() - 1 : -1;
-  if (sp.valid == 4) {
-    // fused: compute stream = [exchange c-1 landed, frame bands c-1 done]
-    // interior launch c, its first items the bands the exchange sends;
-    // comm stream = [interior c-1 done] frame bands c, then (cycle_finish)
-    // the exchange, gated on the band items' count, beside the interior.
-    ensure_sig();
-    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_comm_, 0));
-    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
-    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));
-    if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
-    kern::launch_fused_main(dtype(), src, dst, L_, sp, d_sig_, cfg_.r, s_compute_, cfg_.arith, d_queue_);
-    if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
-    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-    if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
-    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_, cfg_.arith);
-    if (pe) H2D_HIP(hipEventRecord(pe->ev[3], s_comm_));
-    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
-    pend_sig_ = sp.sig_items;
-    pend_ = Pending::Fused;
-    return;
-  }
   const bool lead = (sp.valid == 1 || sp.valid == 3) &&
                     ((sp.flags & kern::kPlanLead) || (first_cycle_ && tr_->exchanges() && lead_first()));
   first_cycle_ = false;
@@ -1123,7 +1020,6 @@ void Solver::ensure_pair_graph() {
     const int saved_lx0 = last_x_[0], saved_lx1 = last_x_[1];
     if (tr_->exchanges()) last_x_[0] = last_x_[1] = (int)band_;  // whatever a replay follows
     if (!ovl) {
-      if (fused_ok()) ensure_sig();  // (no allocation inside a capture)
       H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
       for (int c = 0; c < 2; ++c) {
         cycle_launch(K);
@@ -1138,7 +1034,6 @@ void Solver::ensure_pair_graph() {
       hipEvent_t fork = nullptr, join = nullptr;
       H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
       H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-      if (fused_ok()) ensure_sig();  // (no allocation inside a capture)
       H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
       H2D_HIP(hipEventRecord(fork, s_compute_));
       H2D_HIP(hipStreamWaitEvent(s_comm_, fork, 0));
@@ -1484,7 +1379,6 @@ float Solver::time_trial_schedule(const std::vector<int>& sc, int reps) {
   H2D_HIP(hipEventCreate(&e0));
   H2D_HIP(hipEventCreate(&e1));
   hipGraph_t g = nullptr;
-  if (fused_ok()) ensure_sig();  // (no allocation inside a capture)
   H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
   H2D_HIP(hipEventRecord(fork, s_compute_));
   H2D_HIP(hipStreamWaitEvent(s_comm_, fork, 0));
@@ -1543,7 +1437,6 @@ void Solver::capture_schedule(int64_t n) {
   H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
   H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
   hipGraph_t g = nullptr;
-  if (fused_ok()) ensure_sig();  // (no allocation inside a capture)
   H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
   H2D_HIP(hipEventRecord(fork, s_compute_));
   H2D_HIP(hipStreamWaitEvent(s_comm_, fork, 0));
@@ -1719,40 +1612,6 @@ void Solver::prepare_plans(int64_t n) {
   }
 }
 
-bool Solver::fused_ok() const {
-  return hip_ && cfg_.overlap && !cfg_.copy_swap && !jit_ && tr_->exchanges() && tr_->gates() && s_comm_ != s_compute_ &&
-         cfg_.arith != 3;
-}
-
-
-// the bands this rank's exchange sends: toward rank - 1 (top) / rank + 1
-// (bottom); a 1-rank periodic rehearsal sends both
-void Solver::sent_sides(bool* top, bool* bottom) const {
-  const int P = tr_->size(), r = tr_->rank();
-  const bool loop = P == 1 && tr_->exchanges();
-  *top = loop || r > 0;
-  *bottom = loop || r < P - 1;
-}
-
-void Solver::ensure_err() {
-  if (h_err_) return;
-  H2D_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_err_), sizeof(unsigned int), hipHostMallocCoherent));
-  *h_err_ = 0;
-}
-
-void Solver::ensure_sig() {
-  if (d_sig_) return;
-  ensure_err();
-  H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_sig_), 2 * sizeof(uint32_t)));
-  H2D_HIP(hipMemsetAsync(d_sig_, 0, 2 * sizeof(uint32_t), s_compute_));
-  H2D_HIP(hipStreamSynchronize(s_compute_));
-  int khz = 0;
-  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg_.device) != hipSuccess || khz <= 0) khz = 100000;
-  // the watchdog (HEAT2D_COMM_TIMEOUT) normally fires first; this bounds the wave
-  const double to = Watchdog::env_timeout(600.0);
-  gate_timeout_ticks_ = (uint64_t)((to > 0 ? to * 1.5 + 5.0 : 3600.0) * 1e3 * (double)khz);
-}
-
 void Solver::synchronize() {
   if (!hip_) return;
   H2D_HIP(hipSetDevice(cfg_.device));
@@ -1773,9 +1632,6 @@ void Solver::synchronize() {
     }
     H2D_HIP(q);
   }
-  if (h_err_ && __atomic_load_n(h_err_, __ATOMIC_ACQUIRE) != 0)
-    fail(__FILE__, __LINE__, "rank " + std::to_string(tr_->rank()) +
-                                 ": an exchange gate timed out waiting for the interior launch's band items");
   tr_->check();
 }
 

@@ -40,10 +40,6 @@ namespace heat2d {
     if (r_ != ncclSuccess) fail(__FILE__, __LINE__, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
-void Transport::exchange_gated(void*, const SlabLayout&, DType, int64_t, hipStream_t, const Gate&) {
-  fail(__FILE__, __LINE__, "transport '" + name() + "' has no gated exchange (fused cycles need RCCL or IPC)");
-}
-
 namespace {
 
 // ------------------------------------------------------------------ self (P=1)
@@ -104,14 +100,6 @@ class RcclTransport final : public Transport {
   void graph_launched(hipStream_t stream) override { track(stream, "graph replay"); }
   bool exchanges() const override { return size_ > 1 || loop_; }
   bool aborted() const override { return aborted_.load(); }
-  // fused cycles: the send/recv kernels follow a one-wave wait for the
-  // interior launch's band items on the same stream
-  bool gates() const override { return true; }
-  void exchange_gated(void* field, const SlabLayout& L, DType dt, int64_t k, hipStream_t stream,
-                      const Gate& g) override {
-    kern::launch_wait_counter(g.counter, g.target, g.timeout_ticks, g.err, stream);
-    exchange(field, L, dt, k, stream, true);
-  }
   // collectives of an I/O phase wait on peers' host I/O: not tracked (a slow
   // output turn is not a hung fabric); exchanges are never issued inside one
   void io_phase(bool on) override { io_ += on ? 1 : -1; }

@@ -93,7 +93,7 @@ class SplitPlan(C.Structure):
         ("k", C.c_int32), ("ring", C.c_int32), ("valid", C.c_int32), ("nedge", C.c_int32),
         ("main", Rect), ("edge", Rect * 4),
         ("main_waves", C.c_int64), ("edge_waves", C.c_int64), ("main_items", C.c_int64), ("edge_items", C.c_int64),
-        ("nfused", C.c_int32), ("flags", C.c_int32), ("fused", Rect * 6), ("sig_items", C.c_int64),
+        ("nrects", C.c_int32), ("flags", C.c_int32), ("rects", Rect * 6),
     ]
 
 

@@ -108,18 +108,17 @@ def test_gloo_hip_ranks_share_gpu(native, gpu, tmp_path, world, tb, overlap, n, 
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,tb,n,dtype,graph,order", [(3, 10, 1100, "fp64", False, "fused"),
-                                                          (4, 8, 1500, "fp32", False, "fused"),
-                                                          (3, 10, 1100, "fp64", True, "fused"),
+@pytest.mark.parametrize("world,tb,n,dtype,graph,order", [(3, 10, 1100, "fp64", False, "lead"),
+                                                          (4, 8, 1500, "fp32", False, "edge-first"),
                                                           (3, 10, 1100, "fp64", True, "lead"),
+                                                          (3, 10, 1100, "fp64", True, "edge-first"),
                                                           (2, 6, 900, "fp64", True, None)])
 def test_ipc_ranks_share_gpu_bitwise(native, gpu, tmp_path, monkeypatch, world, tb, n, dtype, graph, order):
     """Rank PROCESSES on the one GPU exchanging halos through the IPC transport
     (neighbours' fields mapped via hipIpc handles, pulls ordered by stream-side
     counters), optionally replayed from hipGraphs (the IPC exchange captures),
-    and with the fused cycle forced: one interior launch whose first items are
-    the bands the exchange sends, the exchange gated on their device count
-    (middle ranks both bands, end ranks one band + a frame band launch).
+    per split order (lead: every cycle's band launch issued before the
+    interior, no wait between them; edge-first; the autotuner's).
     Random data, bitwise the single-rank golden, global statistics reduced."""
     if order:
         monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)

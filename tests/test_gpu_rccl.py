@@ -103,14 +103,13 @@ def periodic_slab_golden(T, r, steps):
 
 
 @pytest.mark.parametrize("kind", ["rccl", "ipc"])
-@pytest.mark.parametrize("order", ["fused", "edge-first", "lead", "auto"])
+@pytest.mark.parametrize("order", ["edge-first", "lead", "concurrent", "auto"])
 def test_middle_slab_rehearsal(native, gpu, monkeypatch, kind, order):
     """The bench's strong-scaling rehearsal geometry: a middle slab (rows
     [200, 360) of a 600^2 grid, interior boundary bands) exchanging both
     bands with itself, per split order (lead: the band launch issued before
-    the interior, no wait between them; fused: both sent bands as the
-    interior launch's first items, the exchange gated on their count, the
-    interior's short bands last), bitwise the periodic-slab golden on rough data."""
+    the interior, no wait between them), bitwise the periodic-slab golden on
+    rough data."""
     from heat2d.models.heat2d import HeatSolver
     from heat2d.parallel.transport import IpcLoopTransport, RcclLoopTransport
 

@@ -31,10 +31,10 @@ def tb():
     # main/gen x 4 arith x (ring 4: fp32 K 1..20 + fp64 K 1..24; ring 6: fp32
     # K 1..16 + fp64 K 1..24), the fp32 general ring-8 kernels of single
     # launches (4 arith x K 1..16), plus the fused-statistics variants
-    # (general, ring 4, 4 arith); the fused-cycle interior kernels (3 arith)
+    # (general, ring 4, 4 arith)
     assert sum(len(p) == 6 for p in ks) == 8 * (20 + 24) + 8 * (16 + 24) + 4 * 16, len(ks)
     assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 4 * (20 + 24), len(ks)
-    assert sum(len(p) == 7 and p[6] == "fused" for p in ks) == 3 * ((20 + 24) + (16 + 24)), len(ks)
+    assert len(ks) == 8 * (20 + 24) + 8 * (16 + 24) + 4 * 16 + 4 * (20 + 24), len(ks)
     return ks
 
 

@@ -78,7 +78,7 @@ def tb_params(mangled):
     p = ("fp64" if m.group(1) == "d" else "fp32", int(m.group(2)), int(m.group(3)), int(m.group(4)),
          m.group(5) == "1", int(m.group(6)))
     var = m.group(7) or "0"  # kernel variant (tb_impl.hpp): 1 fused statistics, 2 fused-cycle interior
-    return p + ({"1": "stats", "2": "fused"}[var],) if var in ("1", "2") else p
+    return p + ("stats",) if var == "1" else p
 
 
 def main():

@@ -1,14 +1,15 @@
 """Per-wave timeline of the interior launch of a middle-slab rehearsal cycle
 (diagnostics): the bench's strong-scaling slab (rows ROWS of an N x N grid,
 middle rank, RCCL self-exchange), CYCLES eager cycles of depth K with the plan
-the env selects (HEAT2D_SPLIT_ORDER / HEAT2D_BANDS / HEAT2D_TB_RING /
-HEAT2D_FUSED_BALANCE), then the per-wave {start, end} stamps of the LAST
-stencil launch (the interior; kern::wave_times, 100 MHz):
+the env selects (HEAT2D_SPLIT_ORDER=edge-first puts the interior last /
+HEAT2D_BANDS / HEAT2D_TB_RING), then the per-wave {start, end} stamps of the
+LAST stencil launch (kern::wave_times, 100 MHz):
 
     HEAT2D_WAVE_TIMES=1 python tools/wave_times_slab.py DTYPE N ROWS K [CYCLES]
 
-One JSON line: span, dispatch ramp, and end-time percentiles of the waves that
-marched a sent band first (fused plans: wave id < sig_items) vs the rest."""
+One JSON line: span, dispatch ramp, end-time and duration percentiles, and
+the mean duration of the waves with two static items vs one (grid stride).
+(Round 4 also timed the removed fused cycle with it: profiles/r4/lead/.)"""
 import json
 import os
 import sys
@@ -41,18 +42,19 @@ tr.close()
 t0 = w[:, 0].min()
 start, end = (w[:, 0] - t0) / 100.0, (w[:, 1] - t0) / 100.0  # us
 wid = w[:, 2]
-nsig = int(pl.get("sig_items", 0) or 0)
+items = int(pl["main_items"])
+two = wid < max(0, items - len(w))  # static grid stride: these waves take a second item
 
 
 def pct(x):
     return [round(float(v), 1) for v in np.percentile(x, [0, 50, 90, 100])] if len(x) else None
 
 
+dur = end - start
 print(json.dumps({"dtype": dtype, "rows": rows, "n": n, "k": k, "waves": int(len(w)),
                   "plan": {kk: pl.get(kk) for kk in ("order", "dynamic", "ring", "main_bands", "main_items",
-                                                     "main_waves", "sig_items", "main_rects")},
+                                                     "main_waves", "main_rects")},
                   "span_us": round(float(end.max()), 1), "start_p50_p90_max_us": pct(start)[1:],
-                  "end_band_waves_min_p50_p90_max": pct(end[wid < nsig]),
-                  "end_other_waves_min_p50_p90_max": pct(end[wid >= nsig]),
-                  "dur_band_waves_mean": round(float((end - start)[wid < nsig].mean()), 1) if nsig else None,
-                  "dur_other_waves_mean": round(float((end - start)[wid >= nsig].mean()), 1)}))
+                  "end_min_p50_p90_max_us": pct(end), "dur_min_p50_p90_max_us": pct(dur),
+                  "dur_two_item_waves_mean": round(float(dur[two].mean()), 1) if two.any() else None,
+                  "dur_one_item_waves_mean": round(float(dur[~two].mean()), 1) if (~two).any() else None}))
