@@ -644,11 +644,11 @@ float Solver::time_plan(const kern::SplitPlan& c, int kTimed) {
 static uint64_t plan_env_hash() {
   static const uint64_t h = [] {
     uint64_t v = 1469598103934665603ull;
-    for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_TUNE_SEGMENTS", "HEAT2D_FUSED", "HEAT2D_W_ROW", "HEAT2D_W_COL",
+    for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_TUNE_SEGMENTS", "HEAT2D_W_ROW", "HEAT2D_W_COL",
                              "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
                              "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
                              "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN", "HEAT2D_EDGE_BANDS",
-                             "HEAT2D_FUSED_BALANCE", "HEAT2D_EDGE_MAIN"}) {
+                             "HEAT2D_EDGE_MAIN"}) {
       const char* e = std::getenv(name);
       const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
       for (unsigned char c : kv) v = (v ^ c) * 1099511628211ull;
@@ -691,8 +691,8 @@ bool Solver::cached_split(int k) {
                                                  c.main.nb, cfg_.arith);
   if (!c.valid || (c.valid != 2 && !fresh.valid) || c.main.r1 > L_.nrows || c.nedge > 4) return false;
   // semantic checks on top of the key: a plan kind this run may not use
-  // (fused cycles need a gating transport and HEAT2D_FUSED; the dynamic queue
-  // is off under HEAT2D_DYNAMIC=0; a single launch cannot exchange)
+  // (the dynamic queue is off under HEAT2D_DYNAMIC=0; a single launch cannot
+  // exchange; the lead order is for exchanging slabs)
   if ((c.flags & kern::kPlanDynamic) && !dynamic_candidates()) return false;
   if (c.valid == 2 && tr_->exchanges()) return false;
   if ((c.flags & kern::kPlanLead) && (c.valid != 1 || !tr_->exchanges())) return false;
