@@ -573,12 +573,9 @@ static bool tune_segments() {
 // follows), so later cycles keep the autotuned order. A one-cycle step (the
 // 8-rank 20-step strong-scaling run) is all first cycle: 4096-row fp64 slab
 // rehearsal, kernel span 647 -> 610 us per cycle (profiles/r4/h/).
-static bool lead_first() {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_LEAD_FIRST");
-    return !e || std::atoi(e) != 0;
-  }();
-  return on;
+static bool lead_first() {  // (read per call: tests toggle it within one process)
+  const char* e = std::getenv("HEAT2D_LEAD_FIRST");
+  return !e || std::atoi(e) != 0;
 }
 
 // smallest steady-state cycle (ms) for which edge-first split plans are tried

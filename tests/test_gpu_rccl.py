@@ -103,16 +103,20 @@ def periodic_slab_golden(T, r, steps):
 
 
 @pytest.mark.parametrize("kind", ["rccl", "ipc"])
-@pytest.mark.parametrize("order", ["edge-first", "lead", "concurrent", "auto"])
+@pytest.mark.parametrize("order", ["edge-first", "lead", "concurrent", "auto", "edge-first-only"])
 def test_middle_slab_rehearsal(native, gpu, monkeypatch, kind, order):
     """The bench's strong-scaling rehearsal geometry: a middle slab (rows
     [200, 360) of a 600^2 grid, interior boundary bands) exchanging both
     bands with itself, per split order (lead: the band launch issued before
-    the interior, no wait between them), bitwise the periodic-slab golden on
-    rough data."""
+    the interior, no wait between them; every order's first cycle runs
+    lead-ordered unless HEAT2D_LEAD_FIRST=0), bitwise the periodic-slab golden
+    on rough data."""
     from heat2d.models.heat2d import HeatSolver
     from heat2d.parallel.transport import IpcLoopTransport, RcclLoopTransport
 
+    if order == "edge-first-only":  # no lead-ordered first cycle either
+        monkeypatch.setenv("HEAT2D_LEAD_FIRST", "0")
+        order = "edge-first"
     if order != "auto":
         monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
     K, rows, row0 = 8, 160, 200
