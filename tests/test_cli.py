@@ -74,6 +74,29 @@ def test_cli_flags_and_json(cli, tmp_path):
     assert "passes=" in out
 
 
+@pytest.mark.parametrize("dev", [pytest.param(["--cpu"], id="cpu"),
+                                 pytest.param(["--gpus", "1"], id="gpu", marks=pytest.mark.gpu)])
+def test_cli_time_transfers(cli, tmp_path, dev):
+    """--time-transfers: the whole-field H2D of the IC and D2H of the result
+    inside the timed region, as fortran/hip/heat.F90:284-295 times them. The
+    field round-trips unchanged (bitwise the golden), the JSON reports both
+    copy times, and they are part of the elapsed time."""
+    import json
+    (tmp_path / "input.dat").write_text("300 0.25 0.05 1.0 37 0\n")
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    ref = R.owned(R.ftcs(prob))
+    out = run_cli(tmp_path, *dev, "--tb", "8", "--time-transfers", "--json", "t.json", "--output", "npy")
+    assert "Average time:" in out
+    r = json.loads((tmp_path / "t.json").read_text())
+    assert r["time_transfers"] is True and r["h2d_s"] > 0 and r["d2h_s"] > 0
+    assert r["wall_s"] >= r["h2d_s"] + r["d2h_s"]
+    assert np.array_equal(np.load(tmp_path / "soln00000.npy"), ref)
+    run_cli(tmp_path, *dev, "--tb", "8", "--json", "n.json", "--output", "npy")
+    n = json.loads((tmp_path / "n.json").read_text())
+    assert n["time_transfers"] is False and n["h2d_s"] == 0 and n["d2h_s"] == 0
+    assert np.array_equal(np.load(tmp_path / "soln00000.npy"), ref)
+
+
 def test_cli_time_it_every_step_keeps_deep_cycles(cli, tmp_path):
     """--print-every 1: one time_it line per step, in order (the reference,
     fortran/hip/heat.F90:241), without cutting the run into depth-1 cycles:
