@@ -197,3 +197,36 @@ def test_bench_plan_cache_second_run(tmp_path):
     # one ~0.5 ms timed cycle per run: a cold first process (clocks) can be
     # 10 % off the second; the cache must not make it slower
     assert second["value"] >= 0.9 * first["value"], (first["value"], second["value"])
+
+
+@pytest.mark.gpu
+def test_bench_plan_cache_respects_knobs(tmp_path):
+    """A run with a plan-shaping knob neither reuses plans tuned without it
+    nor the other way round: HEAT2D_DYNAMIC=1 (queue forced) fills the cache,
+    a HEAT2D_DYNAMIC=0 run on the same cache file then tunes afresh and runs
+    the static plan (round 3 replayed the cached dynamic plan instead)."""
+    env_cache = str(tmp_path / "plans.txt")
+    saved = {k: os.environ.get(k) for k in ("HEAT2D_PLAN_CACHE", "HEAT2D_DYNAMIC")}
+    os.environ["HEAT2D_PLAN_CACHE"] = env_cache
+    try:
+        args = ["--gpus", "1", "--grid", "8192", "--steps", "20", "--warmup", "5", "--verify", "off"]
+        os.environ["HEAT2D_DYNAMIC"] = "1"
+        dyn = run_plain(*args)
+        os.environ["HEAT2D_DYNAMIC"] = "0"
+        static = run_plain(*args)
+        static2 = run_plain(*args)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    pd = dyn["config"]["launch_plans"]
+    ps = static["config"]["launch_plans"]
+    assert any(p["dynamic"] == 1 for p in pd.values()), pd
+    assert all(p["dynamic"] == 0 and p["origin"] != "cache" for p in ps.values()), ps
+    assert static["config"]["plan_cache"]["hits"] == 0
+    # the static run's own plans are cached under its key (a hit is re-timed:
+    # a drifted one is re-tuned, so hits, not every plan's origin, are checked)
+    assert static2["config"]["plan_cache"]["hits"] >= 1
+    assert all(p["dynamic"] == 0 for p in static2["config"]["launch_plans"].values())
