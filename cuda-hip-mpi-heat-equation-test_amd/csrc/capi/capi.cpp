@@ -493,6 +493,40 @@ int heat2d_solver_plan_cache_hits(void* s, int64_t* out) {
   return guarded([&] { *out = static_cast<Solver*>(s)->plan_cache_hits(); });
 }
 
+// The plan cache's own entry points (tests of its on-disk format): reload the
+// file named by $HEAT2D_PLAN_CACHE, put / get one plan and one schedule.
+int heat2d_plan_cache_reload() {
+  return guarded([&] { plancache::reset(); });
+}
+
+int heat2d_plan_cache_put(const char* ctx, int k, int64_t band, const heat2d_split_plan* p, float ms) {
+  return guarded([&] {
+    kern::SplitPlan q;
+    std::memcpy(&q, p, sizeof(q));
+    plancache::put_plan(ctx, k, band, q, ms);
+  });
+}
+
+int heat2d_plan_cache_get(const char* ctx, int k, int64_t band, heat2d_split_plan* p, float* ms, int32_t* found) {
+  return guarded([&] {
+    kern::SplitPlan q{};
+    *found = plancache::get_plan(ctx, k, band, &q, ms) ? 1 : 0;
+    if (*found) std::memcpy(p, &q, sizeof(q));
+  });
+}
+
+int heat2d_plan_cache_put_schedule(const char* ctx, int64_t n, const int32_t* depths, int64_t count) {
+  return guarded([&] { plancache::put_schedule(ctx, n, std::vector<int>(depths, depths + count)); });
+}
+
+int heat2d_plan_cache_get_schedule(const char* ctx, int64_t n, int32_t* depths, int64_t cap, int64_t* count) {
+  return guarded([&] {
+    std::vector<int> s;
+    *count = plancache::get_schedule(ctx, n, &s) ? (int64_t)s.size() : -1;
+    for (int64_t i = 0; i < std::min<int64_t>(cap, (int64_t)s.size()); ++i) depths[i] = s[(size_t)i];
+  });
+}
+
 int heat2d_plan_cache_path(char* buf, int64_t cap) {
   return guarded([&] {
     const std::string p = plancache::enabled() ? plancache::path() : std::string();

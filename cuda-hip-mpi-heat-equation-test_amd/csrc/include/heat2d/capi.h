@@ -187,6 +187,14 @@ int heat2d_solver_plan_cache_hits(void* s, int64_t* out);
 // Depths autotuned in this process and candidate plans screened for them.
 int heat2d_solver_tune_stats(void* s, int64_t* depths, int64_t* candidates);
 int heat2d_plan_cache_path(char* buf, int64_t cap);
+// The plan cache's own entry points (format tests): reload $HEAT2D_PLAN_CACHE,
+// put / get one plan (found = 0 on a miss or a refused entry) and one schedule
+// (count = -1 on a miss).
+int heat2d_plan_cache_reload(void);
+int heat2d_plan_cache_put(const char* ctx, int k, int64_t band, const heat2d_split_plan* p, float ms);
+int heat2d_plan_cache_get(const char* ctx, int k, int64_t band, heat2d_split_plan* p, float* ms, int32_t* found);
+int heat2d_plan_cache_put_schedule(const char* ctx, int64_t n, const int32_t* depths, int64_t count);
+int heat2d_plan_cache_get_schedule(const char* ctx, int64_t n, int32_t* depths, int64_t cap, int64_t* count);
 // Where the depth-k split plan came from: 0 planned (not autotuned), 1 autotuned in
 // this process, 2 the plan cache (re-validated), -1 not planned yet.
 int heat2d_solver_plan_origin(void* s, int k, int32_t* out);

@@ -7,7 +7,7 @@
 // winners on disk, keyed by everything the measurement depended on — GPU
 // architecture and CU count, dtype, arithmetic, the slab's rows / columns /
 // pitch / position in the domain, the depth and band, the compute stream's CU
-// budget, the exchange kind, the transport (name, gated exchanges), a hash of
+// budget, the exchange kind, the transport name, a hash of
 // the plan-shaping HEAT2D_* environment knobs, and the build (a hash of the
 // kernel and runtime sources, HEAT2D_BUILD_ID; a build without one, "dev",
 // disables the cache) — and a hit is checked semantically (a plan kind this

@@ -196,6 +196,13 @@ _SIGS = {
     "heat2d_solver_plan_cache_hits": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "heat2d_solver_tune_stats": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "heat2d_plan_cache_path": (C.c_int, [C.c_char_p, _I64]),
+    "heat2d_plan_cache_reload": (C.c_int, []),
+    "heat2d_plan_cache_put": (C.c_int, [C.c_char_p, C.c_int, _I64, C.c_void_p, C.c_float]),
+    "heat2d_plan_cache_get": (C.c_int, [C.c_char_p, C.c_int, _I64, C.c_void_p, C.POINTER(C.c_float),
+                                        C.POINTER(C.c_int32)]),
+    "heat2d_plan_cache_put_schedule": (C.c_int, [C.c_char_p, _I64, C.POINTER(C.c_int32), _I64]),
+    "heat2d_plan_cache_get_schedule": (C.c_int, [C.c_char_p, _I64, C.POINTER(C.c_int32), _I64,
+                                                 C.POINTER(C.c_int64)]),
     "heat2d_solver_plan_origin": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int32)]),
 }
 
