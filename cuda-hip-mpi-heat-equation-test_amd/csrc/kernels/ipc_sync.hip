@@ -47,7 +47,11 @@ __global__ __launch_bounds__(64) void ipc_arrive_kernel(IpcSlot* slots, uint64_t
     while (ld_acq(&slots[p].ready) < c + 1 || ld_acq(&slots[p].done) < c) {
       if (ld_acq(&ctrl[0]) != 0) return;  // aborted: drain
       if (wall_clock64() - t0 > timeout_ticks) {
-        st_rel(&ctrl[1], (uint64_t)me + 1);  // the host's check() reports it
+        // the host's check() reports it; the abort word makes every rank's
+        // waits return (their hosts then fail at their next synchronisation,
+        // before any result of these unsynchronised halos is handed out)
+        st_rel(&ctrl[1], (uint64_t)me + 1);
+        st_rel(&ctrl[0], (uint64_t)me + 1);
         return;
       }
       __builtin_amdgcn_s_sleep(4);

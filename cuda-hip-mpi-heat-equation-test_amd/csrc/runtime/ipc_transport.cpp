@@ -100,7 +100,13 @@ class IpcTransport final : public Transport {
   std::string name() const override { return loop_ ? "ipc-loop" : "ipc"; }
   bool capturable() const override { return true; }
   bool exchanges() const override { return size_ > 1 || loop_; }
-  bool aborted() const override { return aborted_.load(); }
+  // (also a device-side timeout or another rank's abort, seen in the shared
+  // control words: the solver's synchronize() then fails at once instead of
+  // waiting for the drained streams)
+  bool aborted() const override {
+    return aborted_.load() || (hctrl_ && (__atomic_load_n(&hctrl_[0], __ATOMIC_ACQUIRE) != 0 ||
+                                          __atomic_load_n(&hctrl_[1], __ATOMIC_ACQUIRE) != 0));
+  }
   void io_phase(bool on) override { io_ += on ? 1 : -1; }
   void graph_launched(hipStream_t stream) override { track(stream, "graph replay"); }
 
@@ -235,6 +241,10 @@ class IpcTransport final : public Transport {
       if (t != 0)
         fail(__FILE__, __LINE__, "IPC transport: rank " + std::to_string((long long)t - 1) +
                                      " timed out waiting for a neighbour's halo (rank " + std::to_string(rank_) + ")");
+      const uint64_t a = __atomic_load_n(&hctrl_[0], __ATOMIC_ACQUIRE);
+      if (a != 0)
+        fail(__FILE__, __LINE__, "IPC transport: rank " + std::to_string((long long)a - 1) +
+                                     " aborted the exchange (rank " + std::to_string(rank_) + ")");
     }
   }
 

@@ -128,3 +128,31 @@ def test_ipc_ranks_share_gpu_bitwise(native, gpu, tmp_path, monkeypatch, world, 
     ref = golden(args)
     assert np.array_equal(got, ref), np.abs(got.astype(np.float64) - ref).max()
     assert meta["info"]["transport"] == "ipc"
+
+
+@pytest.mark.gpu
+def test_ipc_dead_rank_survivor_fails_fast(native, gpu, tmp_path):
+    """IPC transport, two rank processes on the one GPU: rank 1 dies
+    (os._exit) after its first chunk while rank 0 keeps exchanging. Rank 0's
+    arrive kernel must not spin past the comm timeout: its watchdog (or the
+    kernel's own wall-clock limit) raises the shared abort word, the wait
+    returns, and the process exits non-zero within seconds."""
+    import time
+    port = free_port()
+    args = {"n": 1100, "steps": 40, "tb": 8, "backend": "hip", "transport": "ipc", "die_rank": 1, "die_after": 8}
+    env = dict(os.environ, OMP_NUM_THREADS="1", HEAT2D_COMM_TIMEOUT="5", MASTER_ADDR="127.0.0.1")
+    t0 = time.time()
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), "2", str(port),
+                               str(tmp_path), json.dumps(args)], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT) for r in range(2)]
+    try:
+        outs = [p.communicate(timeout=150)[0].decode(errors="replace") for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    elapsed = time.time() - t0
+    assert procs[1].returncode == 3, outs[1][-2000:]  # the injected death
+    assert procs[0].returncode != 0, outs[0][-2000:]  # the survivor fails instead of hanging
+    assert "abort" in outs[0] or "timed out" in outs[0] or "no halo exchange completed" in outs[0], outs[0][-2000:]
+    assert elapsed < 120, elapsed
