@@ -154,5 +154,6 @@ def test_ipc_dead_rank_survivor_fails_fast(native, gpu, tmp_path):
     elapsed = time.time() - t0
     assert procs[1].returncode == 3, outs[1][-2000:]  # the injected death
     assert procs[0].returncode != 0, outs[0][-2000:]  # the survivor fails instead of hanging
-    assert "abort" in outs[0] or "timed out" in outs[0] or "no halo exchange completed" in outs[0], outs[0][-2000:]
+    # (the IPC watchdog's abort normally; a gloo collective may notice the dead peer first)
+    assert any(w in outs[0] for w in ("abort", "timed out", "no halo exchange", "onnection", "peer")), outs[0][-2000:]
     assert elapsed < 120, elapsed
