@@ -50,7 +50,7 @@ constexpr int64_t kColPad = 32;
 // (a floor: tb_impl.hpp kMinWaves) — deeper passes for the HBM-bound big fp32
 // grids (one read + one write of the field per K steps).
 constexpr int kMaxTB = 24;
-constexpr int kMaxTBF32 = 20;
+constexpr int kMaxTBF32 = 24;
 inline int max_tb(DType dt) { return dt == DType::F64 ? kMaxTB : kMaxTBF32; }
 // Default halo depth (ghost rows per side). Must be >= temporal depth used.
 constexpr int64_t kDefaultHalo = kMaxTB;

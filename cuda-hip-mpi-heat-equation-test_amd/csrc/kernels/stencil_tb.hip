@@ -172,7 +172,7 @@ void dispatch_t(int ring, bool main, int arith, int k, unsigned nblocks, const T
 }
 
 void check_layout(DType dt, const SlabLayout& L, int k) {
-  HEAT2D_REQUIRE(k >= 1 && k <= max_tb(dt), "k must be in [1, max_tb(dtype)] (fp64 24, fp32 20)");
+  HEAT2D_REQUIRE(k >= 1 && k <= max_tb(dt), "k must be in [1, max_tb(dtype)] (24)");
   HEAT2D_REQUIRE(k <= L.halo, "temporal depth exceeds the halo depth");
   HEAT2D_REQUIRE(L.cpad >= (k + 1) / 2 * 2 + 4, "column padding too small for the strip halo");
   // the march keeps row indices in 32 bits (scalar compares)

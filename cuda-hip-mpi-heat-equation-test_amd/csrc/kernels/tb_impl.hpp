@@ -1161,7 +1161,8 @@ int occupancy_blocks_stats(int k);
 // fp32: K = 17..20 (kMaxTBF32, common.hpp): the big fp32 grids are HBM-bound
 // at K = 16, and the packed march fits K = 20 in 2 waves/SIMD
 #define H2D_TB_CASES_F32DEEP(M, T, RING, MAIN, AR)                                                     \
-  M(T, RING, MAIN, AR, 17) M(T, RING, MAIN, AR, 18) M(T, RING, MAIN, AR, 19) M(T, RING, MAIN, AR, 20)
+  M(T, RING, MAIN, AR, 17) M(T, RING, MAIN, AR, 18) M(T, RING, MAIN, AR, 19) M(T, RING, MAIN, AR, 20)   \
+  M(T, RING, MAIN, AR, 21) M(T, RING, MAIN, AR, 22) M(T, RING, MAIN, AR, 23) M(T, RING, MAIN, AR, 24)
 // fp64 only: K = 17..24 (kMaxTB)
 #define H2D_TB_CASES_DEEP(M, T, RING, MAIN, AR)                                                        \
   M(T, RING, MAIN, AR, 17) M(T, RING, MAIN, AR, 18) M(T, RING, MAIN, AR, 19) M(T, RING, MAIN, AR, 20)   \

@@ -384,13 +384,13 @@ def test_prepare_covers_warmup_parity(gpu, native, tb):
 def test_measured_schedule(gpu, native, dtype, n, steps):
     """prepare(n) on an autotuned slab picks step(n)'s cycle schedule from
     measured cycle times (balanced depths for the best cycle count, up to
-    max_tb: fp64 24, fp32 20); step(n) runs exactly that schedule, plans
+    max_tb: 24 for both dtypes); step(n) runs exactly that schedule, plans
     nothing new, and stays bitwise equal to the golden."""
     from collections import Counter
     p = prob(n, steps, "ghost", "sine")
     npdt = np.float64 if dtype == "fp64" else np.float32
     s = HeatSolver(p, dtype=dtype, backend="hip", device=0, autotune=1)
-    assert s.tb == (24 if dtype == "fp64" else 20)
+    assert s.tb == 24
     s.upload(R.owned(R.initial_field(p, npdt)))
     s.prepare(steps)
     sched = s.schedule(steps)

@@ -28,13 +28,13 @@ def tb():
         p = isa_report.tb_params(k["name"])
         if p:
             ks[p] = k
-    # main/gen x 4 arith x (ring 4: fp32 K 1..20 + fp64 K 1..24; ring 6: fp32
+    # main/gen x 4 arith x (ring 4: fp32 K 1..24 + fp64 K 1..24; ring 6: fp32
     # K 1..16 + fp64 K 1..24), the fp32 general ring-8 kernels of single
     # launches (4 arith x K 1..16), plus the fused-statistics variants
     # (general, ring 4, 4 arith)
-    assert sum(len(p) == 6 for p in ks) == 8 * (20 + 24) + 8 * (16 + 24) + 4 * 16, len(ks)
-    assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 4 * (20 + 24), len(ks)
-    assert len(ks) == 8 * (20 + 24) + 8 * (16 + 24) + 4 * 16 + 4 * (20 + 24), len(ks)
+    assert sum(len(p) == 6 for p in ks) == 8 * (24 + 24) + 8 * (16 + 24) + 4 * 16, len(ks)
+    assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 4 * (24 + 24), len(ks)
+    assert len(ks) == 8 * (24 + 24) + 8 * (16 + 24) + 4 * 16 + 4 * (24 + 24), len(ks)
     return ks
 
 
@@ -52,15 +52,16 @@ def test_occupancy_floors(tb):
 
 
 def test_deep_fp64_interior_two_waves(tb):
-    """fp64 K = 17..24 exist for one-pass short runs: the interior (MAIN) kernel
+    """fp64 K = 17..24 exist for one-pass short runs, fp32 K = 17..24 for the
+    HBM-bound big fp32 grids: the interior (MAIN) kernel
     must keep 2 waves/SIMD with ring 4 there (the general one may drop to 1;
     the r = 1/4 K = 20 kernel with ring 6)."""
     for k in range(17, 25):
         for ar in (0, 1, 2, 3):
             ring = 6 if (ar, k) == (2, 20) else 4  # r = 1/4, K = 20: ring 4 needs 258 VGPRs, ring 6 fits
             assert tb[("fp64", 1, k, ring, True, ar)]["waves_per_simd"] >= 2, (k, ar)
-    assert not any(p[0] == "fp32" and p[2] > 20 for p in tb)
-    for k in range(17, 21):  # fp32 K = 17..20: the interior kernel keeps 2 waves/SIMD at ring 4 (floor)
+    assert not any(p[0] == "fp32" and p[2] > 24 for p in tb)
+    for k in range(17, 25):  # fp32 K = 17..24: the interior kernel keeps 2 waves/SIMD at ring 4 (floor)
         for ar in (0, 1, 2, 3):
             assert tb[("fp32", 1, k, 4, True, ar)]["waves_per_simd"] >= 2, (k, ar)
 

@@ -89,7 +89,8 @@ def test_jacobi_needs_quarter_r(native):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype,tb", [("fp64", 1), ("fp64", 4), ("fp64", 12), ("fp64", 20), ("fp64", 24),
-                                      ("fp32", 1), ("fp32", 7), ("fp32", 16), ("fp32", 18), ("fp32", 20)])
+                                      ("fp32", 1), ("fp32", 7), ("fp32", 16), ("fp32", 18), ("fp32", 20),
+                                      ("fp32", 22), ("fp32", 24)])
 def test_hip_jacobi_equals_golden(gpu, native, dtype, tb):
     """Every edge kind (frame rows, frame columns, corners, interior) on a small
     odd grid, rough data: the scaled interior and the unscaled pinned kinds
@@ -104,7 +105,8 @@ def test_hip_jacobi_equals_golden(gpu, native, dtype, tb):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype,tb,n", [("fp64", 12, 1100), ("fp32", 10, 1100), ("fp64", 20, 1500),
-                                        ("fp32", 16, 1300), ("fp32", 20, 1300), ("fp32", 17, 1500)])
+                                        ("fp32", 16, 1300), ("fp32", 20, 1300), ("fp32", 17, 1500),
+                                        ("fp32", 24, 1300), ("fp32", 21, 1500)])
 def test_hip_jacobi_split_schedule(gpu, native, dtype, tb, n):
     """Split (MAIN + EDGE) schedule with the autotuner, rough data."""
     p = prob(n, 2 * tb + 3)

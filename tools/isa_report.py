@@ -59,8 +59,10 @@ def kernels(so_path):
                     f = re.search(r"\." + key + r":\s+(\d+)", block)
                     return int(f.group(1)) if f else default
                 vg, ag = field("vgpr_count"), field("agpr_count")
-                # unified register file: 512 per SIMD lane, 8-register granule
-                regs = ((vg + 7) // 8) * 8 + ((ag + 3) // 4) * 4
+                # unified register file: 512 per SIMD lane, 8-register granule;
+                # on gfx90a+ .vgpr_count is the TOTAL (arch VGPRs aligned to 4,
+                # then the AGPRs: fp64 K = 20 general kernel 374 = 256 + 118)
+                regs = ((vg + 7) // 8) * 8
                 out.append({"name": name, "triple": triple, "vgpr": vg, "agpr": ag,
                             "sgpr": field("sgpr_count"), "scratch": field("private_segment_fixed_size"),
                             "waves_per_simd": min(8, 512 // max(regs, 1))})
