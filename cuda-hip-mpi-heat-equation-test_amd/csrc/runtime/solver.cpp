@@ -758,6 +758,42 @@ void Solver::autotune_split(int k) {
   kern::SplitPlan best = split_[k];
   const float base_ms = time_plan(best, staged ? 2 : 4);
   const bool long_cycles = staged && base_ms > kLongCycleMs;
+  auto finish = [&](kern::SplitPlan b, float ms) {
+    synchronize();
+    b.k = k;
+    split_[k] = b;
+    tuned_ms_[k] = ms;
+    if (plancache::enabled()) plancache::put_plan(cache_ctx(), k, k, b, ms);
+    // restore the event protocol: both streams idle, events recorded
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+    synchronize();
+  };
+  // Long cycles (the full-HBM grids, ~50 ms per pass): a neighbouring depth
+  // (k -/+ 1) tuned in this process lends its choice — order, ring, interior
+  // bands / segments, queue, edge bands — re-planned for k and timed once: a
+  // balanced schedule mixes depths k and k + 1, and a second full screening
+  // costs ~10 s there (240 GB fp32 grid, 64 steps: depths 21 and 22 —
+  // prepare 21 s, profiles/r4/t/).
+  if (long_cycles) {
+    for (int nk : {k - 1, k + 1}) {
+      if (nk < 1 || nk > kMaxTB || (plan_origin_[nk] != 1 && plan_origin_[nk] != 2)) continue;
+      const kern::SplitPlan& q = split_[nk];
+      if (q.k != nk || !q.valid) continue;
+      kern::SplitPlan c = q.valid == 2
+                              ? kern::plan_single(dtype(), L_, k, compute_cus_, q.ring, q.main.nb, cfg_.arith)
+                              : kern::plan_split(dtype(), L_, k, k, compute_cus_, spare, q.ring, q.main.nb, cfg_.arith);
+      if (!c.valid) continue;
+      c.valid = q.valid;
+      c.flags = q.flags;
+      if ((c.valid == 1 || c.valid == 3) && q.nedge > 0 && q.edge[0].nb > 1)
+        c = kern::with_edge_bands(dtype(), c, q.edge[0].nb, cfg_.arith);
+      const float t = time_plan(c, 2);
+      ++tune_trials_;
+      finish(c, t);
+      return;
+    }
+  }
   const int64_t nb0 = best.main.nb;
   // without an exchange to hide, a single general launch per cycle competes too
   const bool single_ok = !tr_->exchanges();
@@ -891,15 +927,7 @@ void Solver::autotune_split(int k) {
     }
   }
   tune_trials_ += (int64_t)cands.size();
-  synchronize();
-  best.k = k;
-  split_[k] = best;
-  tuned_ms_[k] = best_ms;
-  if (plancache::enabled()) plancache::put_plan(cache_ctx(), k, k, best, best_ms);
-  // restore the event protocol: both streams idle, events recorded
-  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
-  H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
-  synchronize();
+  finish(best, best_ms);
 }
 
 void Solver::launch_overlap(int k, int64_t B) {
