@@ -133,8 +133,8 @@ def main():
                          "every rank keeps ~n^2 points (e.g. --dtype fp32 --n 173056: the full-HBM 240 GB per GPU)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--tb", type=int, default=0,
-                    help="largest time-step depth fused per HBM pass (0: every depth the kernels have, fp64 24 / "
-                         "fp32 20; prepare() picks the cycle schedule of the timed steps by measurement)")
+                    help="largest time-step depth fused per HBM pass (0: every depth the kernels have, 24; "
+                         "prepare() picks the cycle schedule of the timed steps by measurement)")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--arith", default="bench", choices=["bench", "auto", "exact", "fma", "jacobi", "fast"],
                     help="fma: contracted update (one op fewer per point); exact: every op rounded; auto: fma when "

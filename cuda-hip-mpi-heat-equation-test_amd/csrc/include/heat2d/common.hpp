@@ -44,11 +44,12 @@ struct Error : std::runtime_error {
 // temporal-block depth (rounded to the vector width) and keep rows aligned.
 constexpr int64_t kColPad = 32;
 // Largest supported temporal-block depth (time steps fused per HBM pass):
-// 24 for fp64, 20 for fp32 (max_tb). The fp64 interior kernel keeps 2
-// waves/SIMD up to K = 24 with ring 4, so a short run can take one HBM pass;
-// the packed fp32 interior kernel keeps 2 waves/SIMD up to K = 20 with ring 4
-// (a floor: tb_impl.hpp kMinWaves) — deeper passes for the HBM-bound big fp32
-// grids (one read + one write of the field per K steps).
+// 24 for both dtypes (max_tb). The fp64 interior kernel keeps 2 waves/SIMD up
+// to K = 24 with ring 4, so a short run can take one HBM pass; the packed fp32
+// interior kernel keeps 2 waves/SIMD up to K = 24 with ring 4 (a floor:
+// tb_impl.hpp kMinWaves) — deeper passes for the HBM-bound big fp32 grids (one
+// read + one write of the field per K steps: the 240 GB grid's 64 steps in 3
+// passes instead of 4, +13.8 %, profiles/r4/deep32/).
 constexpr int kMaxTB = 24;
 constexpr int kMaxTBF32 = 24;
 inline int max_tb(DType dt) { return dt == DType::F64 ? kMaxTB : kMaxTBF32; }

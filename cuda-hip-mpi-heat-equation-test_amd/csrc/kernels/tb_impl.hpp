@@ -1158,8 +1158,8 @@ int occupancy_blocks_stats(int k);
   M(T, RING, MAIN, AR, 5) M(T, RING, MAIN, AR, 6) M(T, RING, MAIN, AR, 7) M(T, RING, MAIN, AR, 8)       \
   M(T, RING, MAIN, AR, 9) M(T, RING, MAIN, AR, 10) M(T, RING, MAIN, AR, 11) M(T, RING, MAIN, AR, 12)    \
   M(T, RING, MAIN, AR, 13) M(T, RING, MAIN, AR, 14) M(T, RING, MAIN, AR, 15) M(T, RING, MAIN, AR, 16)
-// fp32: K = 17..20 (kMaxTBF32, common.hpp): the big fp32 grids are HBM-bound
-// at K = 16, and the packed march fits K = 20 in 2 waves/SIMD
+// fp32: K = 17..24 (kMaxTBF32, common.hpp): the big fp32 grids are HBM-bound
+// at K = 16-20, and the packed interior march fits K = 24 in 2 waves/SIMD
 #define H2D_TB_CASES_F32DEEP(M, T, RING, MAIN, AR)                                                     \
   M(T, RING, MAIN, AR, 17) M(T, RING, MAIN, AR, 18) M(T, RING, MAIN, AR, 19) M(T, RING, MAIN, AR, 20)   \
   M(T, RING, MAIN, AR, 21) M(T, RING, MAIN, AR, 22) M(T, RING, MAIN, AR, 23) M(T, RING, MAIN, AR, 24)
