@@ -145,7 +145,8 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="replay the timed schedule from one hipGraph captured in prepare() (auto: single-rank "
-                         "runs without an exchange; exchanging runs stay eager — a graph launch starts the "
+                         "runs without an exchange, schedules of cycles under 250 us — longer ones launch eager, "
+                         "HEAT2D_GRAPH_MAX_CYCLE_US; on: every schedule; exchanging runs stay eager — a graph launch starts the "
                          "interior ~40 us after the band launch, eager ~12 us: 4096-row IPC slab rehearsal "
                          "3362-3468 with the graph, 3768-3943 eager, profiles/r4/k/)")
     ap.add_argument("--comm-cus", type=int, default=0, help="CUs reserved for bands + RCCL (0: default, -1: none)")
@@ -176,6 +177,8 @@ def main():
     args = ap.parse_args()
     if args.transport == "peer":
         args.transport = "ipc"
+    if args.graph == "on":  # replay every measured schedule, long cycles too
+        os.environ.setdefault("HEAT2D_GRAPH_MAX_CYCLE_US", "1e30")
     if args.share_gpu and args.transport == "rccl":
         ap.error("--share-gpu needs --transport ipc or auto (RCCL refuses two ranks on one GPU)")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -394,6 +397,8 @@ def main():
     plan_cache = {"hits": s.plan_cache_hits, "path": N.plan_cache_path()} if hip else None
     tune = s.tune_stats if hip else None
     measured = s.schedule(args.steps) is not None
+    # a measured schedule of long cycles launches eagerly even with graph=True
+    replayed = bool(uses_graph(kind)) and (s.schedule_replayed(args.steps) if measured else True)
     s.close()
     tr.close()
     live.clear()
@@ -443,7 +448,7 @@ def main():
                 "arith": arith_name(prob.r, arith) + {"auto": " (auto)", "bench": " (r = 1/4)" if prob.r == 0.25
                                                       else " (auto)"}.get(args.arith, ""),
                 "overlap": not args.no_overlap,
-                "graph": bool(uses_graph(kind)),
+                "graph": replayed,
                 "launch_plans": plans or None,
                 "backend": args.backend,
             },

@@ -465,6 +465,10 @@ int heat2d_solver_schedule(void* s, int64_t n, int32_t* out, int64_t cap, int64_
   });
 }
 
+int heat2d_solver_schedule_replayed(void* s, int64_t n, int32_t* out) {
+  return guarded([&] { *out = static_cast<Solver*>(s)->schedule_replayed(n) ? 1 : 0; });
+}
+
 int heat2d_solver_step_cycles(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len) {
   return guarded([&] {
     const std::vector<int> v = static_cast<Solver*>(s)->step_cycles(n);

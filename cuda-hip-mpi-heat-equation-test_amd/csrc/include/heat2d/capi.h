@@ -176,6 +176,8 @@ int heat2d_solver_cycle_hist(void* s, int64_t* out, int n, int reset);
 /* the measured cycle schedule prepare(n) chose for step(n): depths in out[0..min(cap, len)); len = -1 if none
    (step(n) then runs balanced cycles of the preferred depth) */
 int heat2d_solver_schedule(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len);
+/* *out = 1 if step(n) replays its measured schedule as one captured hipGraph, else 0 (eager launches) */
+int heat2d_solver_schedule_replayed(void* s, int64_t n, int32_t* out);
 // Cycle depths step(n) runs from the solver's current state (len = count; out may be null).
 int heat2d_solver_step_cycles(void* s, int64_t n, int32_t* out, int64_t cap, int64_t* len);
 // Halo rows exchanged per side since the last reset (sum over cycles).

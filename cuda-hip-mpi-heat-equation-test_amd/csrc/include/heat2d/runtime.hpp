@@ -255,6 +255,12 @@ class Solver {
   // The measured schedule step(n) will run (nullptr: balanced cycles of
   // pref_depth()).
   const std::vector<int>* schedule(int64_t n) const;
+  // whether step(n) replays its schedule as one captured graph (prepare(n)
+  // decides: short-cycle schedules only, replay_schedule)
+  bool schedule_replayed(int64_t n) const {
+    auto it = sched_replay_.find(n);
+    return it != sched_replay_.end() && it->second;
+  }
   // depth of the balanced cycles when no measured schedule applies (the
   // steady-state best: fp64 14, fp32 16 unless --tb is given)
   int pref_depth() const { return k_pref_; }
@@ -372,6 +378,7 @@ class Solver {
   bool measured_schedules() const;
   void trial_cycle(const kern::SplitPlan& c);
   bool schedule_graphs() const;
+  bool replay_schedule(int64_t n);
   void capture_schedule(int64_t n);
   float time_trial_schedule(const std::vector<int>& sc, int reps = 1);  // ms: the fastest of reps graph replays of sc
   void prepare_plans(int64_t n);  // prepare()'s planning / autotune / measured schedule (HIP split engine)
@@ -423,6 +430,7 @@ class Solver {
   bool stats_next_ = false;   // the next cycle_launch is the fused-statistics cycle
   double* d_part_ = nullptr;  // fused statistics: per-wave partials
   std::map<int64_t, std::vector<int>> sched_;  // measured schedules by step count
+  std::map<int64_t, bool> sched_replay_;       // step(n) replays its schedule as a graph
   // use_graph + a capturable transport: each measured schedule captured whole
   // (both streams), keyed by (steps, starting buffer parity)
   std::map<std::pair<int64_t, int>, hipGraphExec_t> sched_graph_;

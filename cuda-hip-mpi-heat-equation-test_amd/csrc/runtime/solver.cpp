@@ -645,7 +645,7 @@ static uint64_t plan_env_hash() {
                              "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
                              "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
                              "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN", "HEAT2D_EDGE_BANDS",
-                             "HEAT2D_EDGE_MAIN"}) {
+                             "HEAT2D_EDGE_MAIN", "HEAT2D_GRAPH_MAX_CYCLE_US"}) {
       const char* e = std::getenv(name);
       const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
       for (unsigned char c : kv) v = (v ^ c) * 1099511628211ull;
@@ -1156,7 +1156,7 @@ void Solver::step(int64_t n) {
   // chunks — then never tops up)
   const int first = runs.front().k;
   topup(first);
-  if (schedule(n) && schedule_graphs()) {
+  if (schedule(n) && replay_schedule(n)) {
     run_schedule_graph(n);
     return;
   }
@@ -1442,6 +1442,33 @@ bool Solver::schedule_graphs() const {
   return cfg_.use_graph && hip_ && cfg_.overlap && (!tr_->exchanges() || tr_->capturable());
 }
 
+// Mean cycle time (us) from which step(n) launches its schedule eagerly
+// instead of replaying it as a graph (HEAT2D_GRAPH_MAX_CYCLE_US).
+static double graph_max_cycle_us() {
+  const char* e = std::getenv("HEAT2D_GRAPH_MAX_CYCLE_US");
+  return e ? std::atof(e) : 250.0;
+}
+
+// Whether step(n) replays its measured schedule as one captured graph. A
+// graph removes the host launches between cycles — what a short-cycle
+// schedule needs (4096^2 fp32: ~47 us cycles, the launch gaps a quarter of
+// one) — but a long-cycle schedule hides them anyway behind its kernels, and
+// there the replay measured slower than the eager launches: 32768^2 fp64
+// 20 steps (one 4.3 ms cycle), graph 4724 vs eager 4840 Gpts/s, means of 4
+// interleaved runs (profiles/r4/ge/). Decided from the tuned cycle times, max
+// over ranks (depth_ms), so every rank decides the same.
+bool Solver::replay_schedule(int64_t n) {
+  if (!schedule_graphs()) return false;
+  if (auto it = sched_replay_.find(n); it != sched_replay_.end()) return it->second;
+  const std::vector<int>* s = schedule(n);
+  if (!s || s->empty()) return false;
+  double est = 0.0;
+  for (int k : *s) est += std::max(0.0, (double)depth_ms(k));
+  const bool g = est * 1e3 < graph_max_cycle_us() * (double)s->size();
+  sched_replay_[n] = g;
+  return g;
+}
+
 // Capture the whole measured schedule of n steps, from the current buffer
 // parity, as one graph: both streams (the comm stream forked off the capture),
 // the cycles' event protocol as graph edges. Replayed by step(n) with no
@@ -1585,9 +1612,12 @@ void Solver::prepare_plans(int64_t n) {
     // candidates within 5 % and keep each one's fastest of 5 replays: one
     // replay each picked depths 16 / 17 (3.05 us per step) over 15 / 16 (3.01)
     // in two of three runs (profiles/r4/c/small_*.json).
-    if (!s.empty() && schedule_graphs() && !tr_->exchanges()) {
-      double est = 0.0;
-      for (int k : s) est += depth_ms(k);
+    // (replayed schedules only: long-cycle ones launch eagerly, replay_schedule)
+    double est = 0.0;
+    if (!s.empty() && schedule_graphs() && !tr_->exchanges())
+      for (int k : s) est += std::max(0.0, (double)depth_ms(k));
+    if (!s.empty() && schedule_graphs() && !tr_->exchanges() &&
+        est * 1e3 < graph_max_cycle_us() * (double)s.size()) {
       const bool tiny = est < 10.0;
       // (the near-tie scan autotunes every depth it visits: short runs only)
       const auto near = est < 50.0 ? cycle_schedule_near(n, cfg_.tb, [this](int k) { return (double)depth_ms(k); },
@@ -1609,7 +1639,7 @@ void Solver::prepare_plans(int64_t n) {
       sched_[n] = std::move(s);
     }
   }
-  if (schedule(n) && schedule_graphs()) {
+  if (schedule(n) && replay_schedule(n)) {
     // both buffer parities (a warmup between prepare and step(n) may flip it);
     // a capture only records the launches, so flipping cur_ around it is safe
     for (int p = 0; p < 2; ++p) {

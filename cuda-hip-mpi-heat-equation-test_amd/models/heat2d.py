@@ -225,6 +225,13 @@ class HeatSolver:
         N.call("heat2d_solver_schedule", self._h, int(n), out, ln.value, C.byref(ln))
         return [int(v) for v in out[:ln.value]]
 
+    def schedule_replayed(self, n: int) -> bool:
+        """Whether step(n) replays its measured schedule as one captured hipGraph
+        (graph=True and short cycles; long-cycle schedules launch eagerly)."""
+        out = C.c_int32()
+        N.call("heat2d_solver_schedule_replayed", self._h, int(n), C.byref(out))
+        return bool(out.value)
+
     def cycle_hist(self, reset: bool = False) -> dict:
         """{depth: cycles} that step() launched since the last reset (graph replays count 2 each)."""
         return _cycle_hist(self._h, reset)

@@ -187,6 +187,7 @@ _SIGS = {
     "heat2d_cycle_schedule_near": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.c_double, C.c_int,
                                              C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "heat2d_solver_schedule": (C.c_int, [_P, _I64, C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64)]),
+    "heat2d_solver_schedule_replayed": (C.c_int, [_P, _I64, C.POINTER(C.c_int32)]),
     "heat2d_write_xyz": (C.c_int, [C.c_char_p, C.c_int, _P, _I64, _I64, _I64, _P, _P, C.c_int]),
     "heat2d_write_npy": (C.c_int, [C.c_char_p, C.c_int, _P, _I64, _I64, _I64]),
     "heat2d_solver_step_cycles": (C.c_int, [_P, _I64, C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64)]),

@@ -420,12 +420,17 @@ def test_deep_fp64_bitwise(gpu, native, k):
         assert np.array_equal(got, R.owned(R.ftcs(p))), (k, overlap)
 
 
-@pytest.mark.parametrize("dtype,n,steps,warm", [("fp32", 1100, 61, 0), ("fp32", 1100, 61, 3), ("fp64", 900, 45, 5)])
-def test_measured_schedule_graph(gpu, native, dtype, n, steps, warm):
+@pytest.mark.parametrize("dtype,n,steps,warm,eager", [("fp32", 1100, 61, 0, False), ("fp32", 1100, 61, 3, False),
+                                                      ("fp64", 900, 45, 5, False), ("fp32", 1100, 61, 3, True)])
+def test_measured_schedule_graph(gpu, native, monkeypatch, dtype, n, steps, warm, eager):
     """graph=True + a measured schedule: prepare(n) captures the whole schedule
     (both streams, both buffer parities) as one hipGraph; step(n) replays it
     with nothing planned or captured inside; bitwise, also after a warmup
-    that flips the parity, and when replayed twice."""
+    that flips the parity, and when replayed twice. These short cycles replay;
+    with the eager threshold at 0 us (every schedule "long") the same steps
+    launch eagerly, still bitwise."""
+    if eager:
+        monkeypatch.setenv("HEAT2D_GRAPH_MAX_CYCLE_US", "0")
     p = prob(n, warm + 2 * steps, "ghost", "sine")
     npdt = np.float64 if dtype == "fp64" else np.float32
     s = HeatSolver(p, dtype=dtype, backend="hip", device=0, autotune=1, graph=True)
@@ -433,6 +438,7 @@ def test_measured_schedule_graph(gpu, native, dtype, n, steps, warm):
     s.step(warm)
     s.prepare(steps)
     assert s.schedule(steps)
+    assert s.schedule_replayed(steps) == (not eager)
     before = s.plans_made
     s.cycle_hist(reset=True)
     s.step(steps)
