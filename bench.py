@@ -145,7 +145,7 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="replay the timed schedule from one hipGraph captured in prepare() (auto: single-rank "
-                         "runs without an exchange, schedules of cycles under 250 us — longer ones launch eager, "
+                         "runs without an exchange, schedules of cycles under 400 us — longer ones launch eager, "
                          "HEAT2D_GRAPH_MAX_CYCLE_US; on: every schedule; exchanging runs stay eager — a graph launch starts the "
                          "interior ~40 us after the band launch, eager ~12 us: 4096-row IPC slab rehearsal "
                          "3362-3468 with the graph, 3768-3943 eager, profiles/r4/k/)")

@@ -1267,6 +1267,7 @@ float Solver::depth_ms(int k) {
     double v = tuned_ms_[k];
     tr_->allreduce(&v, 1, 1);
     depth_ms_[k] = v > 0 ? (float)v : -1.f;
+    if (tune_log()) std::fprintf(stderr, "heat2d sched depth k=%d tuned ms %.4f\n", k, depth_ms_[k]);
   }
   return depth_ms_[k];
 }
@@ -1316,6 +1317,9 @@ float Solver::prescan_ms(int k) {
 std::vector<int> Solver::choose_schedule(int64_t n) {
   if (!sched_prescan()) return cycle_schedule(n, cfg_.tb, [this](int k) { return (double)depth_ms(k); });
   const auto near = cycle_schedule_near(n, cfg_.tb, [this](int k) { return (double)prescan_ms(k); }, 0.20, 4);
+  if (tune_log())
+    for (int k = 1; k <= cfg_.tb; ++k)
+      if (pre_ms_[k] != 0.f) std::fprintf(stderr, "heat2d sched n=%lld prescan k=%d ms %.4f\n", (long long)n, k, pre_ms_[k]);
   std::vector<int> best;
   double best_cost = 1e300;
   for (const auto& sc : near) {  // the same order and depths on every rank: depth_ms is collective
@@ -1328,10 +1332,47 @@ std::vector<int> Solver::choose_schedule(int64_t n) {
       }
       cost += t;
     }
+    if (tune_log())
+      std::fprintf(stderr, "heat2d sched n=%lld candidate %zu cycles of %d..%d: tuned cost %.4f ms\n", (long long)n,
+                   sc.size(), sc.back(), sc.front(), cost);
     if (cost >= 0.0 && cost < best_cost) {
       best_cost = cost;
       best = sc;
     }
+  }
+  // The default plans the prescan times can miss a depth whose tuned plan is
+  // far better: 16384^2 fp64, 480 steps — default-plan cycles of depths 14..20
+  // all within 1.25..1.47 ms, so the 4 candidates were depths 17..20 (tuned
+  // cost 31.2-31.7 ms), while depth 16's tuned plan runs 0.94 ms (30 cycles:
+  // 28.2 ms; the fp64 general kernel holds 2 waves/SIMD up to K = 16, one from
+  // K = 17). Long runs (>= 8 cycles) therefore also try the next shallower base
+  // depths on tuned times, one at a time while the cost improves.
+  int lo = 0;
+  for (const auto& sc : near) lo = lo == 0 ? sc.back() : std::min(lo, sc.back());
+  while (!best.empty() && lo > 1) {
+    const int64_t c0 = n / lo + 1;  // fewest cycles with a shallower base depth
+    if (c0 < 8) break;
+    const int b = (int)(n / c0);
+    double bc = 1e300;
+    int64_t cb = 0;
+    for (int64_t c = c0; c <= n / b; ++c) {  // every cycle count with base b: depths b / b + 1
+      const int64_t rem = n % c;
+      const double tb = depth_ms(b), t1 = rem ? depth_ms(b + 1) : 0.0;
+      if (tb < 0 || t1 < 0) break;
+      const double cost = (double)(c - rem) * tb + (double)rem * t1;
+      if (cost < bc) {
+        bc = cost;
+        cb = c;
+      }
+    }
+    if (tune_log())
+      std::fprintf(stderr, "heat2d sched n=%lld shallower base %d: %lld cycles, tuned cost %.4f ms\n", (long long)n, b,
+                   (long long)cb, bc);
+    if (cb == 0 || bc >= best_cost) break;
+    best_cost = bc;
+    best.clear();
+    for (int64_t i = 0; i < cb; ++i) best.push_back(i < n % cb ? b + 1 : b);
+    lo = b;
   }
   return best;
 }
@@ -1446,17 +1487,19 @@ bool Solver::schedule_graphs() const {
 // instead of replaying it as a graph (HEAT2D_GRAPH_MAX_CYCLE_US).
 static double graph_max_cycle_us() {
   const char* e = std::getenv("HEAT2D_GRAPH_MAX_CYCLE_US");
-  return e ? std::atof(e) : 250.0;
+  return e ? std::atof(e) : 400.0;
 }
 
 // Whether step(n) replays its measured schedule as one captured graph. A
 // graph removes the host launches between cycles — what a short-cycle
 // schedule needs (4096^2 fp32: ~47 us cycles, the launch gaps a quarter of
 // one) — but a long-cycle schedule hides them anyway behind its kernels, and
-// there the replay measured slower than the eager launches: 32768^2 fp64
-// 20 steps (one 4.3 ms cycle), graph 4724 vs eager 4840 Gpts/s, means of 4
-// interleaved runs (profiles/r4/ge/). Decided from the tuned cycle times, max
-// over ranks (depth_ms), so every rank decides the same.
+// there the replay measured slower than the eager launches (interleaved on one
+// box, profiles/r4/gf/, r4/gg/): 32768^2 fp64 20 steps (one 4.3 ms cycle) 4735
+// vs 4861 Gpts/s, 100 steps 4797 vs 4917; 16384^2 fp32 480 steps (0.59 ms
+// cycles) 9129 vs 10579; 8192^2 fp64 (0.28 ms cycles) 3676 replayed vs 3638.
+// Decided from the tuned cycle times, max over ranks (depth_ms), so every rank
+// decides the same.
 bool Solver::replay_schedule(int64_t n) {
   if (!schedule_graphs()) return false;
   if (auto it = sched_replay_.find(n); it != sched_replay_.end()) return it->second;
