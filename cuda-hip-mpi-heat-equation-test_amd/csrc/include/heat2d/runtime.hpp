@@ -217,6 +217,13 @@ std::vector<int> cycle_schedule(int64_t n, int kmax, const std::function<double(
 // of the best, best first, at most m of them and one per base depth, as schedules.
 std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std::function<double(int)>& t,
                                                   double tol, int m);
+// Schedule `best` (cost best_cost; lo = the shallowest base depth already
+// costed) improved by trying the next shallower base depths on t, one base at
+// a time while the cost drops; only while that base needs >= min_cycles cycles
+// (prepare's prescan can miss a depth whose tuned plan is far better than its
+// default plan: solver.cpp, choose_schedule).
+std::vector<int> cycle_schedule_shallower(int64_t n, std::vector<int> best, double best_cost, int lo,
+                                          const std::function<double(int)>& t, int64_t min_cycles = 8);
 // Whether slabs of this decomposition get autotuned split plans and measured
 // cycle schedules (SolverConfig::autotune, -1 = auto). A function of the
 // GLOBAL problem only — the smallest slab (n_rows / P rows) decides — so every

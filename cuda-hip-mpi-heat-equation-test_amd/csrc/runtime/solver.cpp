@@ -1349,30 +1349,12 @@ std::vector<int> Solver::choose_schedule(int64_t n) {
   // depths on tuned times, one at a time while the cost improves.
   int lo = 0;
   for (const auto& sc : near) lo = lo == 0 ? sc.back() : std::min(lo, sc.back());
-  while (!best.empty() && lo > 1) {
-    const int64_t c0 = n / lo + 1;  // fewest cycles with a shallower base depth
-    if (c0 < 8) break;
-    const int b = (int)(n / c0);
-    double bc = 1e300;
-    int64_t cb = 0;
-    for (int64_t c = c0; c <= n / b; ++c) {  // every cycle count with base b: depths b / b + 1
-      const int64_t rem = n % c;
-      const double tb = depth_ms(b), t1 = rem ? depth_ms(b + 1) : 0.0;
-      if (tb < 0 || t1 < 0) break;
-      const double cost = (double)(c - rem) * tb + (double)rem * t1;
-      if (cost < bc) {
-        bc = cost;
-        cb = c;
-      }
-    }
-    if (tune_log())
-      std::fprintf(stderr, "heat2d sched n=%lld shallower base %d: %lld cycles, tuned cost %.4f ms\n", (long long)n, b,
-                   (long long)cb, bc);
-    if (cb == 0 || bc >= best_cost) break;
-    best_cost = bc;
-    best.clear();
-    for (int64_t i = 0; i < cb; ++i) best.push_back(i < n % cb ? b + 1 : b);
-    lo = b;
+  if (!best.empty()) {
+    std::vector<int> ext = cycle_schedule_shallower(n, best, best_cost, lo, [this](int k) { return (double)depth_ms(k); });
+    if (tune_log() && ext != best)
+      std::fprintf(stderr, "heat2d sched n=%lld shallower: %zu cycles of %d..%d\n", (long long)n, ext.size(), ext.back(),
+                   ext.front());
+    best = std::move(ext);
   }
   return best;
 }
@@ -1432,6 +1414,33 @@ std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std
     out.push_back(std::move(sched));
   }
   return out;
+}
+
+std::vector<int> cycle_schedule_shallower(int64_t n, std::vector<int> best, double best_cost, int lo,
+                                          const std::function<double(int)>& t, int64_t min_cycles) {
+  while (!best.empty() && lo > 1) {
+    const int64_t c0 = n / lo + 1;  // fewest cycles with a shallower base depth
+    if (c0 < min_cycles) break;
+    const int b = (int)(n / c0);
+    double bc = 1e300;
+    int64_t cb = 0;
+    for (int64_t c = c0; c <= n / b; ++c) {  // every cycle count with base b: depths b / b + 1
+      const int64_t rem = n % c;
+      const double tb = t(b), t1 = rem ? t(b + 1) : 0.0;
+      if (tb < 0 || t1 < 0) break;
+      const double cost = (double)(c - rem) * tb + (double)rem * t1;
+      if (cost < bc) {
+        bc = cost;
+        cb = c;
+      }
+    }
+    if (cb == 0 || bc >= best_cost) break;
+    best_cost = bc;
+    best.clear();
+    for (int64_t i = 0; i < cb; ++i) best.push_back(i < n % cb ? b + 1 : b);
+    lo = b;
+  }
+  return best;
 }
 
 // One timed replay of a graph of sc's TRIAL cycles (each reads the current

@@ -90,3 +90,45 @@ def test_schedule_near_candidates(native, curve, n, kmax):
         assert cost(s) <= cost(near[0]) * 1.03 + 1e-12
     assert len({min(s) for s in near}) == len(near)  # one candidate per base depth
     assert schedules_near(n, kmax, t, 0.0, 3)[0] == near[0]
+
+
+def shallower(n, kmax, t, best, lo):
+    tm = (C.c_double * (kmax + 1))(*([0.0] + [t(k) for k in range(1, kmax + 1)]))
+    b = (C.c_int32 * len(best))(*best)
+    out = (C.c_int32 * max(1, n))()
+    ln = C.c_int64()
+    N.call("heat2d_cycle_schedule_shallower", n, kmax, tm, b, len(best), sum(t(k) for k in best), lo, out, n,
+           C.byref(ln))
+    return [int(v) for v in out[:ln.value]]
+
+
+def cliff16(k):
+    """16384^2 fp64 tuned cycle ms (profiles/r4/gh, r4/gi): an occupancy cliff
+    makes depth 16 far cheaper per step than 17..20."""
+    return {15: 0.905, 16: 0.940, 17: 1.136, 18: 1.170, 19: 1.237, 20: 1.310}.get(k, 1.5 + 0.05 * k)
+
+
+def test_schedule_shallower_finds_cliff(native):
+    """The prescan's candidates (bases 17..20, the best 26 x 18/19) missed
+    depth 16: walking shallower from base 17 on tuned times finds 30 x 16
+    (28.2 ms) and stops at base 15 (29.0 ms). A step that does not beat the
+    best so far ends the walk: from base 18, base 17 (27 cycles, 31.4 ms) is
+    no cheaper, so 16 is never reached."""
+    best = [19] * 12 + [18] * 14  # 26 cycles of 18/19 (the candidates' best)
+    assert shallower(480, 24, cliff16, best, lo=17) == [16] * 30
+    # base 17 (the next after 18) is no cheaper than 18/19: the walk stops there
+    assert shallower(480, 24, cliff16, best, lo=18) == best
+
+
+def test_schedule_shallower_short_runs_untouched(native):
+    """Runs of few cycles (the headline's 20 steps) never pay for tuning more depths."""
+    assert shallower(20, 24, cliff16, [20], lo=10) == [20]
+    assert shallower(64, 24, lambda k: 0.1 * k, [22, 21, 21], lo=21) == [22, 21, 21]
+
+
+@pytest.mark.parametrize("curve", sorted(CURVES))
+def test_schedule_shallower_never_worse(native, curve):
+    t = CURVES[curve]
+    best = schedule(480, 24, t)
+    got = shallower(480, 24, t, best, lo=min(best))
+    assert sum(got) == 480 and sum(t(k) for k in got) <= sum(t(k) for k in best) * (1 + 1e-12)
