@@ -455,6 +455,17 @@ int heat2d_cycle_schedule_shallower(int64_t n, int kmax, const double* t_ms, con
   });
 }
 
+int heat2d_cycle_schedule_deeper(int64_t n, int kmax, const double* t_ms, const int32_t* best, int64_t nbest,
+                                 double best_cost, int hi, int32_t* out, int64_t cap, int64_t* len) {
+  return guarded([&] {
+    const std::vector<int> v =
+        cycle_schedule_deeper(n, kmax, std::vector<int>(best, best + nbest), best_cost, hi,
+                              [&](int k) { return k >= 1 && k <= kmax ? t_ms[k] : -1.0; });
+    *len = (int64_t)v.size();
+    for (int64_t i = 0; i < std::min<int64_t>(cap, *len); ++i) out[i] = v[(size_t)i];
+  });
+}
+
 int heat2d_transport_abort(void* t, const char* reason) {
   return guarded([&] { static_cast<TransportHandle*>(t)->t->abort(reason ? reason : "aborted by the caller"); });
 }

@@ -210,6 +210,9 @@ int heat2d_cycle_schedule_near(int64_t n, int kmax, const double* t_ms, double t
 // cycle_schedule_shallower (runtime.hpp): `best` (nbest depths, cost best_cost) tried against shallower base depths
 int heat2d_cycle_schedule_shallower(int64_t n, int kmax, const double* t_ms, const int32_t* best, int64_t nbest,
                                     double best_cost, int lo, int32_t* out, int64_t cap, int64_t* len);
+// cycle_schedule_deeper (runtime.hpp): the same walk toward deeper base depths (above hi, up to kmax)
+int heat2d_cycle_schedule_deeper(int64_t n, int kmax, const double* t_ms, const int32_t* best, int64_t nbest,
+                                 double best_cost, int hi, int32_t* out, int64_t cap, int64_t* len);
 
 /* I/O (io.cpp). */
 int heat2d_write_xyz(const char* path, int dtype, const void* host, int64_t nrows, int64_t ncols,

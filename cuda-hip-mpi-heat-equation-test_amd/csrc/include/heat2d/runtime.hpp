@@ -224,6 +224,10 @@ std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std
 // default plan: solver.cpp, choose_schedule).
 std::vector<int> cycle_schedule_shallower(int64_t n, std::vector<int> best, double best_cost, int lo,
                                           const std::function<double(int)>& t, int64_t min_cycles = 8);
+// The same walk toward deeper base depths (above hi, the deepest base already
+// costed; depths <= kmax), while the base still needs >= min_cycles cycles.
+std::vector<int> cycle_schedule_deeper(int64_t n, int kmax, std::vector<int> best, double best_cost, int hi,
+                                       const std::function<double(int)>& t, int64_t min_cycles = 8);
 // Whether slabs of this decomposition get autotuned split plans and measured
 // cycle schedules (SolverConfig::autotune, -1 = auto). A function of the
 // GLOBAL problem only — the smallest slab (n_rows / P rows) decides — so every

@@ -1347,12 +1347,21 @@ std::vector<int> Solver::choose_schedule(int64_t n) {
   // 28.2 ms; the fp64 general kernel holds 2 waves/SIMD up to K = 16, one from
   // K = 17). Long runs (>= 8 cycles) therefore also try the next shallower base
   // depths on tuned times, one at a time while the cost improves.
-  int lo = 0;
-  for (const auto& sc : near) lo = lo == 0 ? sc.back() : std::min(lo, sc.back());
+  int lo = 0, hi = 0;
+  for (const auto& sc : near) {
+    lo = lo == 0 ? sc.back() : std::min(lo, sc.back());
+    hi = std::max(hi, sc.back());
+  }
   if (!best.empty()) {
-    std::vector<int> ext = cycle_schedule_shallower(n, best, best_cost, lo, [this](int k) { return (double)depth_ms(k); });
+    const auto t = [this](int k) { return (double)depth_ms(k); };
+    std::vector<int> ext = cycle_schedule_shallower(n, best, best_cost, lo, t);
+    double ext_cost = 0.0;
+    for (int k : ext) ext_cost += t(k);
+    // ... and deeper (the same miss one way up: 32768^2 fp32 480 steps picked
+    // 25 cycles of 19/20 on one box, 11335 Gpts/s, vs 20 x 24 at 12503)
+    ext = cycle_schedule_deeper(n, cfg_.tb, ext, ext_cost, hi, t);
     if (tune_log() && ext != best)
-      std::fprintf(stderr, "heat2d sched n=%lld shallower: %zu cycles of %d..%d\n", (long long)n, ext.size(), ext.back(),
+      std::fprintf(stderr, "heat2d sched n=%lld walk: %zu cycles of %d..%d\n", (long long)n, ext.size(), ext.back(),
                    ext.front());
     best = std::move(ext);
   }
@@ -1439,6 +1448,35 @@ std::vector<int> cycle_schedule_shallower(int64_t n, std::vector<int> best, doub
     best.clear();
     for (int64_t i = 0; i < cb; ++i) best.push_back(i < n % cb ? b + 1 : b);
     lo = b;
+  }
+  return best;
+}
+
+std::vector<int> cycle_schedule_deeper(int64_t n, int kmax, std::vector<int> best, double best_cost, int hi,
+                                       const std::function<double(int)>& t, int64_t min_cycles) {
+  while (!best.empty() && hi < kmax) {
+    const int64_t c1 = n / (hi + 1);  // most cycles with a deeper base depth
+    if (c1 < std::max<int64_t>(1, min_cycles)) break;
+    const int b = (int)(n / c1);
+    if (b > kmax) break;
+    double bc = 1e300;
+    int64_t cb = 0;
+    for (int64_t c = n / (b + 1) + 1; c <= c1; ++c) {  // every cycle count with base b: depths b / b + 1
+      const int64_t rem = n % c;
+      if (rem && b + 1 > kmax) continue;
+      const double tb = t(b), t1 = rem ? t(b + 1) : 0.0;
+      if (tb < 0 || t1 < 0) continue;
+      const double cost = (double)(c - rem) * tb + (double)rem * t1;
+      if (cost < bc) {
+        bc = cost;
+        cb = c;
+      }
+    }
+    if (cb == 0 || bc >= best_cost) break;
+    best_cost = bc;
+    best.clear();
+    for (int64_t i = 0; i < cb; ++i) best.push_back(i < n % cb ? b + 1 : b);
+    hi = b;
   }
   return best;
 }

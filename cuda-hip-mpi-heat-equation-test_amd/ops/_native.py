@@ -187,6 +187,8 @@ _SIGS = {
     "heat2d_cycle_schedule_shallower": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int32), _I64,
                                                   C.c_double, C.c_int, C.POINTER(C.c_int32), _I64,
                                                   C.POINTER(C.c_int64)]),
+    "heat2d_cycle_schedule_deeper": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int32), _I64,
+                                               C.c_double, C.c_int, C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64)]),
     "heat2d_cycle_schedule_near": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.c_double, C.c_int,
                                              C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "heat2d_solver_schedule": (C.c_int, [_P, _I64, C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64)]),

@@ -132,3 +132,41 @@ def test_schedule_shallower_never_worse(native, curve):
     best = schedule(480, 24, t)
     got = shallower(480, 24, t, best, lo=min(best))
     assert sum(got) == 480 and sum(t(k) for k in got) <= sum(t(k) for k in best) * (1 + 1e-12)
+
+
+def deeper(n, kmax, t, best, hi):
+    tm = (C.c_double * (kmax + 1))(*([0.0] + [t(k) for k in range(1, kmax + 1)]))
+    b = (C.c_int32 * len(best))(*best)
+    out = (C.c_int32 * max(1, n))()
+    ln = C.c_int64()
+    N.call("heat2d_cycle_schedule_deeper", n, kmax, tm, b, len(best), sum(t(k) for k in best), hi, out, n,
+           C.byref(ln))
+    return [int(v) for v in out[:ln.value]]
+
+
+def hbm_bound(k):
+    """fp32 32768^2-like: a pass costs about the same at any depth (HBM-bound),
+    so the deepest cut is cheapest."""
+    return 2.0 + 0.01 * k
+
+
+def test_schedule_deeper_walks_to_kmax(native):
+    """Candidates that stopped at base 20 (25 cycles of 19/20) walk up to 20 x 24."""
+    best = [20] * 5 + [19] * 20
+    assert deeper(480, 24, hbm_bound, best, hi=19) == [24] * 20
+    assert deeper(480, 22, hbm_bound, best, hi=19)[0] <= 22  # never past kmax
+    # a per-step cost that rises with depth (VALU-bound) keeps the candidates' choice
+    assert deeper(480, 24, lambda k: 0.3 * k + 0.01 * k * k, best, hi=19) == best
+
+
+def test_schedule_deeper_short_runs_untouched(native):
+    assert deeper(20, 24, hbm_bound, [10, 10], hi=10) == [10, 10]  # 1 cycle < 8: no extra tuning
+    assert deeper(64, 24, hbm_bound, [16] * 4, hi=16) == [16] * 4
+
+
+@pytest.mark.parametrize("curve", sorted(CURVES))
+def test_schedule_deeper_never_worse(native, curve):
+    t = CURVES[curve]
+    best = [16] * 30
+    got = deeper(480, 24, t, best, hi=16)
+    assert sum(got) == 480 and max(got) <= 24 and sum(t(k) for k in got) <= sum(t(k) for k in best) * (1 + 1e-12)
