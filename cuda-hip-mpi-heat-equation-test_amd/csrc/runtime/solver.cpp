@@ -1357,9 +1357,12 @@ std::vector<int> Solver::choose_schedule(int64_t n) {
     std::vector<int> ext = cycle_schedule_shallower(n, best, best_cost, lo, t);
     double ext_cost = 0.0;
     for (int k : ext) ext_cost += t(k);
-    // ... and deeper (the same miss one way up: 32768^2 fp32 480 steps picked
-    // 25 cycles of 19/20 on one box, 11335 Gpts/s, vs 20 x 24 at 12503)
-    ext = cycle_schedule_deeper(n, cfg_.tb, ext, ext_cost, hi, t);
+    // ... and deeper when the best candidate is the deepest one (the same
+    // miss one way up: 32768^2 fp32 480 steps picked 25 cycles of 19/20 on one
+    // box, 11335 Gpts/s, vs 20 x 24 at 12503). Only then: each deeper fp64
+    // 32768^2 depth costs ~2.5 s of autotuning (prepare 9.4 -> 14.6 s for a
+    // walk that found nothing, profiles/r4/gn/).
+    if (!best.empty() && best.back() == hi) ext = cycle_schedule_deeper(n, cfg_.tb, ext, ext_cost, hi, t);
     if (tune_log() && ext != best)
       std::fprintf(stderr, "heat2d sched n=%lld walk: %zu cycles of %d..%d\n", (long long)n, ext.size(), ext.back(),
                    ext.front());
