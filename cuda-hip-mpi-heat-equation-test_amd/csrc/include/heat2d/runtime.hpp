@@ -219,7 +219,8 @@ std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std
                                                   double tol, int m);
 // Schedule `best` (cost best_cost; lo = the shallowest base depth already
 // costed) improved by trying the next shallower base depths on t, one base at
-// a time while the cost drops; only while that base needs >= min_cycles cycles
+// a time until two in a row do not beat the best; only while that base needs
+// >= min_cycles cycles
 // (prepare's prescan can miss a depth whose tuned plan is far better than its
 // default plan: solver.cpp, choose_schedule).
 std::vector<int> cycle_schedule_shallower(int64_t n, std::vector<int> best, double best_cost, int lo,
@@ -392,6 +393,9 @@ class Solver {
   bool replay_schedule(int64_t n);
   void capture_schedule(int64_t n);
   float time_trial_schedule(const std::vector<int>& sc, int reps = 1);  // ms: the fastest of reps graph replays of sc
+  float time_trial_eager(const std::vector<int>& sc, int reps);  // ms: the fastest of reps eager launches of sc
+  // the last choose_schedule's costed candidates: (tuned cost ms, schedule)
+  std::vector<std::pair<double, std::vector<int>>> sched_cands_;
   void prepare_plans(int64_t n);  // prepare()'s planning / autotune / measured schedule (HIP split engine)
   float time_plan(const kern::SplitPlan& c, int kTimed);  // steady-state ms per trial cycle
   std::string cache_ctx() const;   // plan-cache key of this slab (plan_cache.hpp)

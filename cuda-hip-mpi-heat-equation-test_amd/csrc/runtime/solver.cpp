@@ -1315,6 +1315,7 @@ float Solver::prescan_ms(int k) {
 }
 
 std::vector<int> Solver::choose_schedule(int64_t n) {
+  sched_cands_.clear();
   if (!sched_prescan()) return cycle_schedule(n, cfg_.tb, [this](int k) { return (double)depth_ms(k); });
   const auto near = cycle_schedule_near(n, cfg_.tb, [this](int k) { return (double)prescan_ms(k); }, 0.20, 4);
   if (tune_log())
@@ -1335,6 +1336,7 @@ std::vector<int> Solver::choose_schedule(int64_t n) {
     if (tune_log())
       std::fprintf(stderr, "heat2d sched n=%lld candidate %zu cycles of %d..%d: tuned cost %.4f ms\n", (long long)n,
                    sc.size(), sc.back(), sc.front(), cost);
+    if (cost >= 0.0) sched_cands_.emplace_back(cost, sc);
     if (cost >= 0.0 && cost < best_cost) {
       best_cost = cost;
       best = sc;
@@ -1346,7 +1348,8 @@ std::vector<int> Solver::choose_schedule(int64_t n) {
   // cost 31.2-31.7 ms), while depth 16's tuned plan runs 0.94 ms (30 cycles:
   // 28.2 ms; the fp64 general kernel holds 2 waves/SIMD up to K = 16, one from
   // K = 17). Long runs (>= 8 cycles) therefore also try the next shallower base
-  // depths on tuned times, one at a time while the cost improves.
+  // depths on tuned times, one at a time until two in a row do not beat the
+  // best (candidates 18..24 on one box: base 17 is no cheaper, 16 is).
   int lo = 0, hi = 0;
   for (const auto& sc : near) {
     lo = lo == 0 ? sc.back() : std::min(lo, sc.back());
@@ -1366,6 +1369,11 @@ std::vector<int> Solver::choose_schedule(int64_t n) {
     if (tune_log() && ext != best)
       std::fprintf(stderr, "heat2d sched n=%lld walk: %zu cycles of %d..%d\n", (long long)n, ext.size(), ext.back(),
                    ext.front());
+    if (ext != best) {
+      double c = 0.0;
+      for (int k : ext) c += t(k);
+      sched_cands_.emplace_back(c, ext);
+    }
     best = std::move(ext);
   }
   return best;
@@ -1430,6 +1438,7 @@ std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std
 
 std::vector<int> cycle_schedule_shallower(int64_t n, std::vector<int> best, double best_cost, int lo,
                                           const std::function<double(int)>& t, int64_t min_cycles) {
+  int misses = 0;  // bases in a row that did not beat the best: the walk ends at 2
   while (!best.empty() && lo > 1) {
     const int64_t c0 = n / lo + 1;  // fewest cycles with a shallower base depth
     if (c0 < min_cycles) break;
@@ -1446,11 +1455,16 @@ std::vector<int> cycle_schedule_shallower(int64_t n, std::vector<int> best, doub
         cb = c;
       }
     }
-    if (cb == 0 || bc >= best_cost) break;
+    if (cb == 0) break;
+    lo = b;
+    if (bc >= best_cost) {
+      if (++misses >= 2) break;
+      continue;
+    }
+    misses = 0;
     best_cost = bc;
     best.clear();
     for (int64_t i = 0; i < cb; ++i) best.push_back(i < n % cb ? b + 1 : b);
-    lo = b;
   }
   return best;
 }
@@ -1487,6 +1501,36 @@ std::vector<int> cycle_schedule_deeper(int64_t n, int kmax, std::vector<int> bes
 // One timed replay of a graph of sc's TRIAL cycles (each reads the current
 // buffer and writes the other one: the solution is untouched), captured like
 // capture_schedule's graph: what step(n) would replay, minus the data flow.
+// The fastest of reps eager launches of sc's TRIAL cycles (as time_plan, over
+// a schedule; the solution is untouched), after one untimed pass.
+float Solver::time_trial_eager(const std::vector<int>& sc, int reps) {
+  for (int k : sc) (void)split_plan(k);
+  synchronize();
+  if (!ev_t0_) {
+    H2D_HIP(hipEventCreate(&ev_t0_));
+    H2D_HIP(hipEventCreate(&ev_t1_));
+  }
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+  for (int k : sc) trial_cycle(split_plan(k));  // warm
+  float best = 1e30f;
+  for (int r = 0; r < std::max(1, reps); ++r) {
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+    H2D_HIP(hipEventRecord(ev_t0_, s_compute_));
+    for (int k : sc) trial_cycle(split_plan(k));
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));
+    H2D_HIP(hipEventRecord(ev_t1_, s_compute_));
+    H2D_HIP(hipEventSynchronize(ev_t1_));
+    float ms = 0.f;
+    H2D_HIP(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));
+    best = std::min(best, ms);
+  }
+  H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+  H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+  synchronize();
+  return best;
+}
+
 float Solver::time_trial_schedule(const std::vector<int>& sc, int reps) {
   for (int k : sc) (void)split_plan(k);
   synchronize();
@@ -1720,6 +1764,33 @@ void Solver::prepare_plans(int64_t n) {
         float best = 1e30f;
         for (auto& c : near) {
           const float ms = time_trial_schedule(c, tiny ? 5 : 1);
+          if (ms < best) {
+            best = ms;
+            s = c;
+          }
+        }
+      }
+    }
+    // Eager (long-cycle) single-rank runs: the tuned costs of near-tied
+    // candidates mispredict their run by a few % too (32768^2 fp32 480 steps:
+    // 22/23-deep cycles estimated 0.5 % cheaper than 20 x 24, ran 2-2.5 %
+    // slower: profiles/r4/gn/, r4/gi/), so time the candidates within 3 % of
+    // the best as eager trial schedules (best of 2) — runs of >= 8 cycles
+    // estimated under 50 ms; candidates already tuned, no extra autotuning.
+    if (!s.empty() && !tr_->exchanges() && s.size() >= 8 &&
+        !(schedule_graphs() && est * 1e3 < graph_max_cycle_us() * (double)s.size())) {
+      double e = 0.0;
+      for (int k : s) e += std::max(0.0, (double)depth_ms(k));
+      std::vector<std::vector<int>> near;
+      for (const auto& c : sched_cands_)
+        if (c.first <= e * 1.03 && std::find(near.begin(), near.end(), c.second) == near.end()) near.push_back(c.second);
+      if (e < 50.0 && near.size() > 1) {
+        float best = 1e30f;
+        for (const auto& c : near) {
+          const float ms = time_trial_eager(c, 2);
+          if (tune_log())
+            std::fprintf(stderr, "heat2d sched n=%lld eager trial %zu cycles of %d..%d: %.4f ms\n", (long long)n,
+                         c.size(), c.back(), c.front(), ms);
           if (ms < best) {
             best = ms;
             s = c;

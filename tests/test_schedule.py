@@ -109,15 +109,15 @@ def cliff16(k):
 
 
 def test_schedule_shallower_finds_cliff(native):
-    """The prescan's candidates (bases 17..20, the best 26 x 18/19) missed
-    depth 16: walking shallower from base 17 on tuned times finds 30 x 16
-    (28.2 ms) and stops at base 15 (29.0 ms). A step that does not beat the
-    best so far ends the walk: from base 18, base 17 (27 cycles, 31.4 ms) is
-    no cheaper, so 16 is never reached."""
+    """The prescan's candidates (bases 17..20 or 18..24, the best 26 x 18/19)
+    missed depth 16: walking shallower on tuned times finds 30 x 16 (28.2 ms)
+    and stops after two bases in a row that do not beat it (15, 14). From base
+    18 the first step (17: 27 cycles, 31.4 ms) is no cheaper, the next is."""
     best = [19] * 12 + [18] * 14  # 26 cycles of 18/19 (the candidates' best)
     assert shallower(480, 24, cliff16, best, lo=17) == [16] * 30
-    # base 17 (the next after 18) is no cheaper than 18/19: the walk stops there
-    assert shallower(480, 24, cliff16, best, lo=18) == best
+    assert shallower(480, 24, cliff16, best, lo=18) == [16] * 30
+    # a cost that only rises toward shallow depths keeps the candidates' choice
+    assert shallower(480, 24, lambda k: 1.0 + 0.01 * k, best, lo=18) == best
 
 
 def test_schedule_shallower_short_runs_untouched(native):
