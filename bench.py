@@ -171,6 +171,11 @@ def main():
     ap.add_argument("--verify", default="on", choices=["on", "off"],
                     help="after the timed run: a small uneven rough-data problem on the same transport kind and "
                          "rank layout, gathered and compared bitwise with the NumPy golden (JSON 'verified')")
+    ap.add_argument("--field-check", default="auto", choices=["auto", "full", "windows", "off"],
+                    help="after the timed run (untimed): its field checked against the run-time compiled one-step "
+                         "kernel in the reference arithmetic from the same IC (JSON 'timed_field_check'); auto: the "
+                         "whole slab when a second copy fits, else row windows at the slab boundaries and middle")
+    ap.add_argument("--window-rows", type=int, default=64, help="rows per checked window (--field-check windows)")
     ap.add_argument("--rehearse-comm", action="store_true",
                     help="1 GPU only: run the multi-GPU schedule (bands + RCCL self-exchange beside a CU-masked "
                          "interior) to measure its per-rank cost; not the headline (periodic halo)")
@@ -358,6 +363,64 @@ def main():
         kind = ("torch-dist" if world > 1 else
                 (("ipc-loop" if args.transport == "ipc" else "rccl-loop") if (args.rehearse_comm and hip) else "self"))
         setup(kind)
+    def timed_field_check(s, kind):
+        """The timed field itself (IC + warmup + steps, the state the timed run
+        left), checked against an independent engine started from the same IC:
+        the run-time compiled one-step kernel (hipRTC, ops/jit.py) in the
+        reference arithmetic, run for warmup + steps steps on the same rank
+        layout through a fresh transport of the same kind, compared on the
+        device (max |diff| and differing bit patterns, reduced over ranks).
+        When a second copy of the slab does not fit (the full-HBM grids), row
+        windows at both slab boundaries and the middle of every slab are
+        checked by single-rank reference runs instead (select.field_windows).
+        Outside the timed region. Skipped for the self-exchange rehearsals
+        (their periodic halo is not the problem's physics)."""
+        if kind in ("rccl-loop", "ipc-loop"):
+            return {"skipped": "self-exchange rehearsal: not the problem's physics"}
+        total = args.warmup + args.steps
+        es = 8 if args.dtype == "fp64" else 4
+        if hip:
+            need = 2.0 * (s.nrows + 2 * s.layout.halo) * s.layout.pitch * es + (256 << 20)
+            free = torch.cuda.mem_get_info(device)[0] / (world if args.share_gpu else 1)
+            fits = args.field_check == "full" or (args.field_check == "auto" and free >= 1.05 * need)
+        else:
+            fits = args.field_check != "windows"
+        full = amin(1.0 if fits else 0.0) >= 1.0
+
+        def make_ref(full_run, rows=None, slab_row0=None, arith="exact"):
+            if full_run:
+                vkind = kind
+                tr_ref = make_transport(vkind)
+                rr, r0 = (s.nrows, slab_row0_run) if rows_run else (None, None)
+            else:
+                tr_ref = SelfTransport()
+                rr, r0 = rows, slab_row0
+            try:
+                ref = HeatSolver(prob, dtype=args.dtype, backend=args.backend, transport=tr_ref,
+                                 device=device if hip else None, rows=rr, slab_row0=r0, arith=arith,
+                                 engine="jit" if hip else "tb", tb=1, overlap=False, graph=False, autotune=0)
+            except Exception:
+                tr_ref.close()
+                raise
+            close = ref.close
+
+            def close_both():
+                close()
+                tr_ref.close()
+            ref.close = close_both
+            return ref
+
+        rows_run = rows
+        slab_row0_run = slab_row0
+        t0 = time.perf_counter()
+        out = select.check_timed_field(s, make_ref, total, arith=arith_name(prob.r, arith), r=prob.r,
+                                       dtype=args.dtype, t0_absmax=2.0, full=full, amax=amax,
+                                       asum=lambda v: reduce(v, dist.ReduceOp.SUM), window=args.window_rows)
+        out["seconds"] = round(time.perf_counter() - t0, 2)
+        if not hip:
+            out["engine"] = out["engine"].replace("jit", "cpu")
+        return out
+
     tr, s, prepare_s = live[kind]
     s.cycle_hist(reset=True)
     s.halo_rows_exchanged(reset=True)
@@ -399,6 +462,9 @@ def main():
     measured = s.schedule(args.steps) is not None
     # a measured schedule of long cycles launches eagerly even with graph=True
     replayed = bool(uses_graph(kind)) and (s.schedule_replayed(args.steps) if measured else True)
+    field_check = None
+    if args.field_check != "off":
+        field_check = timed_field_check(s, kind)
     s.close()
     tr.close()
     live.clear()
@@ -458,6 +524,7 @@ def main():
             "halo_bytes_per_cycle": round(halo_bytes / max(1, sum(hist.values())), 1),
             "verified": None if verify is None else verify["verified"],
             "verify": verify,
+            "timed_field_check": field_check,
             "baseline_basis": "BASELINE.md derived ceiling 50 Gpts/s per MI250X GCD x n_gpus",
         }
         if stats:

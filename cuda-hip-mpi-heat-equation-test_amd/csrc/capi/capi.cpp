@@ -266,6 +266,10 @@ int heat2d_solver_download(void* s, void* host, int64_t ld) {
   return guarded([&] { static_cast<Solver*>(s)->download(host, ld); });
 }
 
+int heat2d_solver_compare(void* s, void* other, int64_t r0, int64_t nrows, int64_t other_r0, double* out2) {
+  return guarded([&] { static_cast<Solver*>(s)->compare(*static_cast<Solver*>(other), r0, nrows, other_r0, out2); });
+}
+
 int heat2d_solver_upload(void* s, const void* host, int64_t ld) {
   return guarded([&] { static_cast<Solver*>(s)->upload(host, ld); });
 }

@@ -3,8 +3,10 @@
 // `heat2d [input.dat] [flags]` reproduces the run behaviour of every
 // reference program (reads ./input.dat by default, prints the same progress /
 // completion / timing lines, writes int.dat / soln.dat / soln%05d.dat):
-//   --variant mpi     fortran/hip + fortran/mpi+cuda (6-field input; ghost frame,
-//                     uniform IC, per-rank soln%05d.dat, "Average time:")
+//   --variant mpi     fortran/hip (6-field input; ghost frame, uniform IC,
+//                     per-rank soln%05d.dat, "Average time:")
+//   --variant mpicuda fortran/mpi+cuda (as mpi, but "Sum of Temperature:" — here
+//                     the real all-reduced sum — and a per-iteration "total time:")
 //   --variant serial  fortran/serial (5-field input; boundary-inclusive grid,
 //                     hat IC, int.dat + soln.dat, "total time:")
 //   --variant cuda    fortran/cuda_cuf + fortran/cuda_kernel (hat on y in [0.5,1.0])
@@ -12,14 +14,17 @@
 //   --cpu             native CPU path (replaces the gfortran serial build)
 //   --engine jit      run-time specialised hipRTC kernel (python/cuda/cuda.py's JIT)
 // Multi-GPU is one host thread per GPU (hipSetDevice(rank), the reference's
-// node-local rank -> device binding, fortran/hip/heat.F90:119-125) with RCCL
-// communicators; the halo exchange is RCCL send/recv over xGMI.
+// node-local rank -> device binding, fortran/hip/heat.F90:119-125); the halo
+// exchange is RCCL send/recv over xGMI, or — `--transport auto` (default) when
+// RCCL cannot build its communicators on every rank, or `--transport peer` —
+// device copies out of the neighbours' fields (peer access over xGMI).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -67,20 +72,22 @@ struct Args {
   std::string checkpoint;       // --checkpoint DIR (utils/checkpoint.py format)
   int64_t checkpoint_every = 0;
   std::string restart;          // --restart DIR (any writer rank count)
-  std::string transport = "rccl";  // GPU ranks: rccl | peer (device copies between the ranks' fields, no RCCL)
+  // GPU ranks: auto (RCCL if its communicators build on every rank, else
+  // peer) | rccl | peer (device copies between the ranks' fields, no RCCL)
+  std::string transport = "auto";
   bool share_gpu = false;          // --share-gpu: every rank on device 0 (peer transport; tests / rehearsals)
   int autotune = -1;               // --autotune auto|on|off (SolverConfig::autotune)
 };
 
 void usage() {
   std::printf(
-      "usage: heat2d [input.dat] [--variant mpi|serial|cuda] [--gpus N | --cpu] [--dtype fp64|fp32]\n"
+      "usage: heat2d [input.dat] [--variant mpi|mpicuda|serial|cuda] [--gpus N | --cpu] [--dtype fp64|fp32]\n"
       "              [--tb K] [--no-overlap] [--copy-swap] [--managed] [--graph] [--ic NAME]\n"
       "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
       "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith auto|exact|fma|jacobi|fast]\n"
       "              [--time-transfers]\n"
       "              [--checkpoint DIR [--checkpoint-every N]] [--restart DIR]\n"
-      "              [--transport rccl|peer] [--share-gpu] [--autotune auto|on|off]\n");
+      "              [--transport auto|rccl|peer] [--share-gpu] [--autotune auto|on|off]\n");
 }
 
 Args parse_args(int argc, char** argv) {
@@ -147,7 +154,10 @@ struct Shared {
   std::string err;
   std::vector<std::shared_ptr<Transport>> trs;  // every rank's transport (fail-fast abort)
   std::vector<std::shared_ptr<Transport>> cpu_trs;  // --cpu with P > 1: the host-thread transports
-  std::vector<std::shared_ptr<Transport>> peer_trs;  // --transport peer with P > 1
+  std::vector<std::shared_ptr<Transport>> peer_trs;  // --transport peer (or auto's fallback) with P > 1
+  std::vector<std::shared_ptr<Transport>> rccl_trs;  // --transport auto: the communicators built up front
+  std::string transport_used = "self";               // self | rccl | peer | host
+  std::string transport_note;                        // why auto fell back (empty: no fallback)
   double final_stats[6] = {0};
   int tb_used = 1;  // largest temporal depth the solver may run (jit / copy-swap force 1)
   int64_t hist[kMaxTB + 1] = {0};  // cycles per depth of the timed loop (rank 0)
@@ -185,6 +195,16 @@ void save_checkpoint(Shared& sh, Solver& s, Transport& tr, int rank, int64_t ste
   tr.barrier();
 }
 
+std::string json_str(const std::string& v) {
+  std::string o = "\"";
+  for (char c : v) {
+    if (c == '"' || c == '\\') o += '\\';
+    if ((unsigned char)c < 0x20) c = ' ';
+    o += c;
+  }
+  return o + "\"";
+}
+
 std::string rank_file(int rank) {
   char b[32];
   std::snprintf(b, sizeof(b), "soln%05d.dat", rank);
@@ -217,7 +237,8 @@ void run_rank(Shared& sh, int rank) {
     }
     if (P == 1) tr = make_self_transport();
     else if (a.cpu) tr = sh.cpu_trs[(size_t)rank];  // host threads (the reference's `make mpi`)
-    else if (a.transport == "peer") tr = sh.peer_trs[(size_t)rank];
+    else if (!sh.peer_trs.empty()) tr = sh.peer_trs[(size_t)rank];
+    else if (!sh.rccl_trs.empty()) tr = sh.rccl_trs[(size_t)rank];
     else tr = make_rccl_transport(sh.uid, rank, P, device);
     {
       std::lock_guard<std::mutex> g(sh.mu);
@@ -283,6 +304,7 @@ void run_rank(Shared& sh, int rank) {
       }
     }
     if (root && !a.quiet) {
+      // (fortran/hip prints the decomposition line; fortran/mpi+cuda only nx / ny)
       if (P > 1 || sh.args.variant == "mpi") std::printf(" Automatic MPI decomposition: %12d  x 1\n", P);
       std::printf(" nx: %12lld\n", (long long)s.layout().nrows);
       std::printf(" ny: %12lld\n", (long long)s.layout().ncols);
@@ -453,6 +475,68 @@ void run_rank(Shared& sh, int rank) {
   }
 }
 
+// --transport auto: build every rank's RCCL communicator up front (one thread
+// per rank: ncclCommInitRank is collective) and keep them only if EVERY rank
+// got one; otherwise release the ones that did and run on the peer transport
+// (device copies out of the neighbours' fields), so a node whose RCCL cannot
+// initialise — or ranks sharing a GPU, which RCCL refuses — still runs. The
+// reference has one fabric and fails with it (mpirun, fortran/hip/heat.F90:115-125).
+// An init that neither returns nor fails within HEAT2D_RCCL_INIT_TIMEOUT
+// seconds (default 120) ends the program with an error instead of a hang.
+void choose_gpu_transport(Shared& sh) {
+  const Args& a = sh.args;
+  const int P = sh.nranks;
+  std::vector<std::shared_ptr<Transport>> trs((size_t)P);
+  std::vector<std::string> errs((size_t)P);
+  if (const char* f = std::getenv("HEAT2D_FORCE_RCCL_FAIL"); f && std::atoi(f) != 0) {
+    errs[0] = "HEAT2D_FORCE_RCCL_FAIL set (fallback test)";
+  } else {
+    rccl_unique_id(sh.uid);
+    std::mutex mu;
+    std::condition_variable cv;
+    int finished = 0;
+    std::vector<std::thread> th;
+    for (int r = 0; r < P; ++r)
+      th.emplace_back([&, r] {
+        try {
+          const int device = a.share_gpu ? 0 : r;
+          trs[(size_t)r] = make_rccl_transport(sh.uid, r, P, device);
+        } catch (const std::exception& e) {
+          errs[(size_t)r] = e.what();
+        }
+        std::lock_guard<std::mutex> g(mu);
+        ++finished;
+        cv.notify_all();
+      });
+    const char* tv = std::getenv("HEAT2D_RCCL_INIT_TIMEOUT");
+    const double limit = tv ? std::atof(tv) : 120.0;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      if (!cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return finished == P; })) {
+        std::fprintf(stderr, "heat2d: RCCL communicator init did not finish within %.0f s on every rank\n", limit);
+        std::fflush(stderr);
+        std::_Exit(1);  // threads stuck inside RCCL's bootstrap cannot be joined
+      }
+    }
+    for (auto& t : th) t.join();
+  }
+  std::string why;
+  for (int r = 0; r < P; ++r)
+    if (!errs[(size_t)r].empty() && why.empty()) why = "rank " + std::to_string(r) + ": " + errs[(size_t)r];
+  if (why.empty()) {
+    sh.rccl_trs = std::move(trs);
+    sh.transport_used = "rccl";
+    return;
+  }
+  for (auto& t : trs)
+    if (t) t->abort("RCCL unavailable on another rank: falling back to the peer transport");
+  trs.clear();
+  sh.peer_trs = make_peer_transports(P);
+  sh.transport_used = "peer";
+  sh.transport_note = "RCCL unavailable (" + why + ")";
+  if (!a.quiet) std::fprintf(stderr, "heat2d: %s: falling back to the peer transport\n", sh.transport_note.c_str());
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -464,8 +548,11 @@ int main(int argc, char** argv) {
     if (a.n > 0) sh.in.n = a.n;
     if (a.ntime >= 0) sh.in.ntime = a.ntime;
     if (a.variant.empty()) a.variant = sh.in.nfields >= 6 ? "mpi" : "serial";
-    Convention conv = a.variant == "mpi" ? Convention::Ghost : Convention::Inclusive;
-    std::string ic = a.ic.empty() ? (a.variant == "mpi" ? "uniform" : a.variant == "cuda" ? "hat-cuda" : "hat") : a.ic;
+    if (a.variant != "mpi" && a.variant != "mpicuda" && a.variant != "serial" && a.variant != "cuda")
+      fail(__FILE__, __LINE__, "--variant must be mpi, mpicuda, serial or cuda");
+    const bool ghost = a.variant == "mpi" || a.variant == "mpicuda";
+    Convention conv = ghost ? Convention::Ghost : Convention::Inclusive;
+    std::string ic = a.ic.empty() ? (ghost ? "uniform" : a.variant == "cuda" ? "hat-cuda" : "hat") : a.ic;
     sh.prob = make_problem(sh.in, conv, ic);
     if (sh.prob.r > 0.25 + 1e-12 && !a.quiet)
       std::fprintf(stderr, "warning: r = %.6g > 0.25: FTCS is unstable in 2-D\n", sh.prob.r);
@@ -476,13 +563,23 @@ int main(int argc, char** argv) {
       a.cpu = true;
     }
     sh.nranks = a.cpu ? std::max(1, a.gpus) : (a.gpus > 0 ? a.gpus : 1);
-    if (a.transport != "rccl" && a.transport != "peer") fail(__FILE__, __LINE__, "--transport must be rccl or peer");
-    if (a.share_gpu && a.transport != "peer")
-      fail(__FILE__, __LINE__, "--share-gpu needs --transport peer (RCCL refuses two ranks on one GPU)");
+    if (a.transport != "auto" && a.transport != "rccl" && a.transport != "peer")
+      fail(__FILE__, __LINE__, "--transport must be auto, rccl or peer");
+    if (a.share_gpu && a.transport == "rccl")
+      fail(__FILE__, __LINE__, "--share-gpu needs --transport peer or auto (RCCL refuses two ranks on one GPU)");
     if (!a.cpu && !a.share_gpu && sh.nranks > ndev) fail(__FILE__, __LINE__, "more GPUs requested than present");
-    if (a.cpu && sh.nranks > 1) sh.cpu_trs = make_thread_transports(sh.nranks);
-    else if (sh.nranks > 1 && a.transport == "peer") sh.peer_trs = make_peer_transports(sh.nranks);
-    else if (sh.nranks > 1) rccl_unique_id(sh.uid);
+    if (a.cpu && sh.nranks > 1) {
+      sh.cpu_trs = make_thread_transports(sh.nranks);
+      sh.transport_used = "host";
+    } else if (sh.nranks > 1 && a.transport == "peer") {
+      sh.peer_trs = make_peer_transports(sh.nranks);
+      sh.transport_used = "peer";
+    } else if (sh.nranks > 1 && a.transport == "auto") {
+      choose_gpu_transport(sh);
+    } else if (sh.nranks > 1) {
+      rccl_unique_id(sh.uid);
+      sh.transport_used = "rccl";
+    }
   } catch (const std::exception& e) {
     std::fprintf(stderr, "heat2d: %s\n", e.what());
     return 1;
@@ -518,13 +615,21 @@ int main(int argc, char** argv) {
   // model bytes/pt/step: one read + one write of the field per HBM pass; copy mode adds the copy
   const double bpp = a.copy_swap ? 4.0 * es
                                  : (passes > 0 && ntime > 0 ? 2.0 * es * (double)passes / (double)ntime : 2.0 * es / K);
+  // fortran/mpi+cuda/heat.F90:275 prints gsum, whose reduction is commented
+  // out (an uninitialised value); here it is the real all-reduced sum of T
+  if (a.variant == "mpicuda") std::printf(" Sum of Temperature: %24.16g\n", sh.final_stats[0]);
   std::printf(" simulation completed!!!!\n");
   if (a.time_transfers && !a.quiet)
     std::printf(" heat2d: timed region includes the whole-field H2D (%.6f s) and D2H (%.6f s)\n", sh.t_h2d, sh.t_d2h);
   if (a.variant == "mpi")
     std::printf(" Average time: %24.16g\n", ntime > 0 ? tmax / (double)ntime : 0.0);
+  else if (a.variant == "mpicuda")  // per iteration, fortran/mpi+cuda/heat.F90:292
+    std::printf(" total time: %24.16g\n", ntime > 0 ? tmax / (double)ntime : 0.0);
   else
     std::printf(" total time: %24.16g\n", tmax);
+  if (!a.quiet && sh.nranks > 1)
+    std::printf(" heat2d: halo transport %s%s%s\n", sh.transport_used.c_str(), sh.transport_note.empty() ? "" : ": ",
+                sh.transport_note.c_str());
   if (!a.quiet)
     std::printf(" heat2d: n=%lld P=%d %s K<=%d passes=%lld steps=%lld wall=%.6f s  %.3f Gpts/s  %.1f GB/s(model)  "
                 "sum(T)=%.17g\n",
@@ -550,12 +655,14 @@ int main(int argc, char** argv) {
                    "\"gpts_per_s\": %.9g, \"model_gb_per_s\": %.9g, \"sum\": %.17g, \"min\": %.17g, \"max\": %.17g, "
                    "\"backend\": \"%s\", \"variant\": \"%s\", \"arith\": \"%s\", \"cycles_per_rank\": [%s], "
                    "\"halo_rows_per_rank\": [%s], \"schedule\": \"%s\", \"arith_used\": \"%s\", "
-                   "\"time_transfers\": %s, \"h2d_s\": %.9g, \"d2h_s\": %.9g}\n",
+                   "\"time_transfers\": %s, \"h2d_s\": %.9g, \"d2h_s\": %.9g, \"transport\": \"%s\", "
+                   "\"transport_fallback\": %s}\n",
                    (long long)sh.prob.n_owned, sh.nranks, a.dtype.c_str(), K, depths.c_str(), (long long)ntime, tmax,
                    gpts, gpts * bpp,
                    sh.final_stats[0], sh.final_stats[2], sh.final_stats[3], a.cpu ? "cpu" : "hip", a.variant.c_str(),
                    a.arith.c_str(), per_rank.c_str(), halo.c_str(), sh.measured ? "measured" : "balanced",
-                   sh.arith_used.c_str(), a.time_transfers ? "true" : "false", sh.t_h2d, sh.t_d2h);
+                   sh.arith_used.c_str(), a.time_transfers ? "true" : "false", sh.t_h2d, sh.t_d2h,
+                   sh.transport_used.c_str(), sh.transport_note.empty() ? "null" : json_str(sh.transport_note).c_str());
       std::fclose(f);
     }
   }

@@ -141,6 +141,9 @@ int heat2d_solver_pref_depth(void* s, int32_t* out);
 int heat2d_solver_sync(void* s);
 int heat2d_solver_stats(void* s, double* out6, int residual);
 int heat2d_solver_download(void* s, void* host, int64_t ld);
+// s's current field, local rows [r0, r0 + nrows), against other's, rows
+// [other_r0, ...): out2 = {max |a - b| (NaN if any), differing bit patterns}
+int heat2d_solver_compare(void* s, void* other, int64_t r0, int64_t nrows, int64_t other_r0, double* out2);
 int heat2d_solver_upload(void* s, const void* host, int64_t ld);
 int heat2d_solver_layout(void* s, heat2d_layout* out);
 /* run-time specialised FTCS step (hipRTC; python/cuda/cuda.py parity) */

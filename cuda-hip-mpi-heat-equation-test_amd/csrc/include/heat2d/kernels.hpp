@@ -152,6 +152,15 @@ void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, 
                      double* out6, hipStream_t stream, int arith = 0);
 void launch_reduce_partials(const double* partials, int64_t nparts, double* out6, hipStream_t stream);
 
+// Field comparison (the bench's check of its timed field against an
+// independent engine): rows [ra, ra + nrows) of `a` (layout La) against rows
+// [rb, rb + nrows) of `b` (layout Lb), owned columns (La.ncols == Lb.ncols).
+// out2 (device) = {max |a - b|, number of elements whose bit patterns differ}
+// (NaN anywhere: max = NaN). `work` >= 2 * compare_work_blocks() doubles.
+int64_t compare_work_blocks();
+void launch_compare(DType dt, const void* a, const SlabLayout& La, int64_t ra, const void* b, const SlabLayout& Lb,
+                    int64_t rb, int64_t nrows, double* work, double* out2, hipStream_t stream);
+
 // Vectorised streaming copy / read (bandwidth roof probes; copy-swap mode).
 void launch_copy(void* dst, const void* src, int64_t bytes, hipStream_t stream, int blocks = 0);
 void launch_read(const void* src, int64_t bytes, unsigned* sink, hipStream_t stream, int blocks = 0);

@@ -293,6 +293,12 @@ class Solver {
   // Any rectangle of the current buffer (local rows [r0,r1), cols [c0,c1),
   // ghost/frame included) -> host.
   void download_region(int64_t r0, int64_t r1, int64_t c0, int64_t c1, void* host, int64_t ld);
+  // This rank's current field, local rows [r0, r0 + nrows), against `other`'s
+  // current field, local rows [other_r0, other_r0 + nrows) (same device, same
+  // dtype and width; e.g. an independent engine's run of the same problem):
+  // out = {max |a - b| (NaN if any), elements whose bit patterns differ}.
+  // Local to this rank (callers reduce over ranks); synchronises both solvers.
+  void compare(Solver& other, int64_t r0, int64_t nrows, int64_t other_r0, double out[2]);
 
   // Phase API. One cycle of depth k = cycle_launch(k, x) (kernels, the event
   // that marks the bands written, Transport::post) then cycle_finish() (halo

@@ -6,8 +6,10 @@
 // replacement for the strided K2-K4 gather/scatter, fortran/hip/heat_kernel.cpp:63-150).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <type_traits>
 
 #include "heat2d/kernels.hpp"
 
@@ -142,6 +144,72 @@ __global__ __launch_bounds__(kStatsThreads) void stats_pass2(const double* __res
   if (threadIdx.x < kNStat) out[threadIdx.x] = red[threadIdx.x][0];
 }
 
+// Field comparison, pass 1: a block per group of rows, a lane per column
+// (fully coalesced rows), per-block {max |a - b|, differing bit patterns};
+// pass 2 reduces the block partials in a fixed order. NaN propagates into the
+// max (fmax would drop it), so a NaN anywhere is never reported as a match.
+constexpr int kCmpBlocks = 2048;
+
+template <typename T>
+__global__ __launch_bounds__(256) void compare_pass1(const T* __restrict__ a, SlabLayout La, int64_t ra,
+                                                     const T* __restrict__ b, SlabLayout Lb, int64_t rb,
+                                                     int64_t nrows, double* __restrict__ work) {
+  using Bits = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned int>::type;
+  double mx = 0.0, cnt = 0.0;
+  for (int64_t i = blockIdx.x; i < nrows; i += gridDim.x) {
+    const T* pa = a + La.offset(ra + i, 0);
+    const T* pb = b + Lb.offset(rb + i, 0);
+    for (int64_t j = threadIdx.x; j < La.ncols; j += blockDim.x) {
+      const T x = pa[j], y = pb[j];
+      const double d = fabs((double)x - (double)y);
+      mx = (d > mx || d != d) ? d : mx;  // keeps a NaN
+      cnt += (__builtin_bit_cast(Bits, x) != __builtin_bit_cast(Bits, y)) ? 1.0 : 0.0;
+    }
+  }
+  __shared__ double sm[2][256];
+  sm[0][threadIdx.x] = mx;
+  sm[1][threadIdx.x] = cnt;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const double o = sm[0][threadIdx.x + w];
+      sm[0][threadIdx.x] = (o > sm[0][threadIdx.x] || o != o) ? o : sm[0][threadIdx.x];
+      sm[1][threadIdx.x] += sm[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    work[blockIdx.x] = sm[0][0];
+    work[kCmpBlocks + blockIdx.x] = sm[1][0];
+  }
+}
+
+__global__ __launch_bounds__(256) void compare_pass2(const double* __restrict__ work, int nblocks,
+                                                     double* __restrict__ out) {
+  __shared__ double sm[2][256];
+  double mx = 0.0, cnt = 0.0;
+  for (int i = threadIdx.x; i < nblocks; i += blockDim.x) {
+    const double v = work[i];
+    mx = (v > mx || v != v) ? v : mx;
+    cnt += work[kCmpBlocks + i];
+  }
+  sm[0][threadIdx.x] = mx;
+  sm[1][threadIdx.x] = cnt;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const double o = sm[0][threadIdx.x + w];
+      sm[0][threadIdx.x] = (o > sm[0][threadIdx.x] || o != o) ? o : sm[0][threadIdx.x];
+      sm[1][threadIdx.x] += sm[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = sm[0][0];
+    out[1] = sm[1][0];
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ f, SlabLayout L,
                                                         int64_t row, int64_t nrows,
@@ -237,6 +305,26 @@ void launch_reduce_partials(const double* partials, int64_t nparts, double* out,
   HEAT2D_REQUIRE(nparts >= 1, "no partials to reduce");
   hipLaunchKernelGGL(stats_pass2, dim3(1), dim3(kStatsThreads), 0, stream, partials, nparts, out);
   check_launch("stats_pass2 (fused partials)");
+}
+
+int64_t compare_work_blocks() { return kCmpBlocks; }
+
+void launch_compare(DType dt, const void* a, const SlabLayout& La, int64_t ra, const void* b, const SlabLayout& Lb,
+                    int64_t rb, int64_t nrows, double* work, double* out2, hipStream_t stream) {
+  HEAT2D_REQUIRE(La.ncols == Lb.ncols, "compared fields differ in width");
+  HEAT2D_REQUIRE(nrows >= 0 && ra >= -La.halo && ra + nrows <= La.nrows + La.halo && rb >= -Lb.halo &&
+                     rb + nrows <= Lb.nrows + Lb.halo,
+                 "compared rows outside the allocations");
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(kCmpBlocks, nrows));
+  if (dt == DType::F32)
+    hipLaunchKernelGGL(compare_pass1<float>, dim3(nb), dim3(256), 0, stream, static_cast<const float*>(a), La, ra,
+                       static_cast<const float*>(b), Lb, rb, nrows, work);
+  else
+    hipLaunchKernelGGL(compare_pass1<double>, dim3(nb), dim3(256), 0, stream, static_cast<const double*>(a), La, ra,
+                       static_cast<const double*>(b), Lb, rb, nrows, work);
+  check_launch("compare_pass1");
+  hipLaunchKernelGGL(compare_pass2, dim3(1), dim3(256), 0, stream, work, nb, out2);
+  check_launch("compare_pass2");
 }
 
 void launch_copy(void* dst, const void* src, int64_t bytes, hipStream_t stream, int blocks) {

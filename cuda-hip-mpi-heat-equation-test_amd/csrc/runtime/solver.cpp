@@ -1952,6 +1952,44 @@ void Solver::download_region(int64_t r0, int64_t r1, int64_t c0, int64_t c1, voi
   }
 }
 
+void Solver::compare(Solver& other, int64_t r0, int64_t nrows, int64_t other_r0, double out[2]) {
+  const SlabLayout& Lo = other.layout();
+  HEAT2D_REQUIRE(other.dtype() == dtype() && other.hip_ == hip_, "compared solvers differ in dtype or backend");
+  HEAT2D_REQUIRE(Lo.ncols == L_.ncols, "compared solvers differ in width");
+  HEAT2D_REQUIRE(nrows >= 0 && r0 >= 0 && r0 + nrows <= L_.nrows && other_r0 >= 0 && other_r0 + nrows <= Lo.nrows,
+                 "compared rows outside the owned slabs");
+  out[0] = out[1] = 0.0;
+  if (nrows == 0) return;
+  if (hip_) {
+    HEAT2D_REQUIRE(other.cfg_.device == cfg_.device, "compared solvers live on different devices");
+    other.synchronize();
+    synchronize();
+    double* res = d_work_ + kern::stats_work_elems();
+    kern::launch_compare(dtype(), buf_[cur_], L_, r0, other.field(), Lo, other_r0, nrows, d_work_, res, s_compute_);
+    H2D_HIP(hipMemcpyAsync(out, res, 2 * sizeof(double), hipMemcpyDeviceToHost, s_compute_));
+    H2D_HIP(hipStreamSynchronize(s_compute_));
+    return;
+  }
+  const size_t es = dtype_size(dtype());
+  for (int64_t i = 0; i < nrows; ++i) {
+    const char* pa = static_cast<const char*>(buf_[cur_]) + (size_t)L_.offset(r0 + i, 0) * es;
+    const char* pb = static_cast<const char*>(other.field()) + (size_t)Lo.offset(other_r0 + i, 0) * es;
+    for (int64_t j = 0; j < L_.ncols; ++j) {
+      double x, y;
+      if (dtype() == DType::F32) {
+        x = reinterpret_cast<const float*>(pa)[j];
+        y = reinterpret_cast<const float*>(pb)[j];
+      } else {
+        x = reinterpret_cast<const double*>(pa)[j];
+        y = reinterpret_cast<const double*>(pb)[j];
+      }
+      const double d = std::fabs(x - y);
+      if (d > out[0] || d != d) out[0] = std::isnan(out[0]) ? out[0] : d;
+      out[1] += std::memcmp(pa + (size_t)j * es, pb + (size_t)j * es, es) != 0 ? 1.0 : 0.0;
+    }
+  }
+}
+
 void Solver::upload(const void* host, int64_t ld) {
   upload_owned(host, ld);
   exchange_post();

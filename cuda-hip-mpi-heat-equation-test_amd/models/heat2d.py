@@ -349,6 +349,18 @@ class HeatSolver:
             raise ValueError(f"expected {(self.nrows, self.ncols)}, got {a.shape}")
         N.call("heat2d_solver_upload", self._h, a.ctypes.data_as(C.c_void_p), self.ncols)
 
+    def compare(self, other: "HeatSolver", r0: int = 0, nrows: Optional[int] = None, other_r0: Optional[int] = None
+                ) -> dict:
+        """This rank's current field, local rows [r0, r0 + nrows), against
+        ``other``'s current field, local rows [other_r0, other_r0 + nrows)
+        (default: the same rows), on the device (same GPU, dtype and width):
+        {"max_abs_diff": max |a - b| (NaN if either holds one), "mismatches":
+        elements whose bit patterns differ}. Local to this rank."""
+        n = self.nrows - r0 if nrows is None else int(nrows)
+        out = (C.c_double * 2)()
+        N.call("heat2d_solver_compare", self._h, other._h, int(r0), n, int(r0 if other_r0 is None else other_r0), out)
+        return {"max_abs_diff": float(out[0]), "mismatches": int(out[1])}
+
     def gather(self) -> Optional[np.ndarray]:
         """Whole owned grid on rank 0 (None elsewhere). Uses torch.distributed when size > 1."""
         local = self.download()

@@ -19,18 +19,25 @@ class Variant:
     convention: str         # GHOST (n owned + ghost frame) or INCLUSIVE (n incl. boundary)
     ic: str                 # IC name (utils.config.make_ic)
     outputs: str            # "serial": int.dat + soln.dat; "mpi": soln%05d.dat if soln == 1
-    timing_line: str        # "total time:" (whole run) or "Average time:" (per iteration)
+    timing_line: str        # "total time:" or "Average time:"
     managed: bool = False
+    per_step: bool = False    # the timing line is seconds per iteration (V7 / V8), not the whole run
+    sum_line: bool = False    # "Sum of Temperature:" before the completion line (V7)
     extra_step: bool = False  # python variants run nt+1 steps (python/serial/heat.py:48)
     default_input: Optional[InputDat] = None
     notes: str = ""
 
 
 VARIANTS = {
-    "mpi": Variant("mpi", "fortran/hip/heat.F90 + heat_kernel.cpp (V8), fortran/mpi+cuda/heat.F90 (V7)",
-                   GHOST, "uniform", "mpi", "Average time:",
+    "mpi": Variant("mpi", "fortran/hip/heat.F90 + heat_kernel.cpp (V8)",
+                   GHOST, "uniform", "mpi", "Average time:", per_step=True,
                    default_input=InputDat(32768, 0.25, 0.05, 1.0, 25000, 0, 6),
                    notes="slab decomposition along x, Dirichlet T=1 ghost frame, T=2 inside; soln%05d.dat per rank"),
+    "mpicuda": Variant("mpicuda", "fortran/mpi+cuda/heat.F90 (V7)", GHOST, "uniform", "mpi", "total time:",
+                       per_step=True, sum_line=True, default_input=InputDat(100, 0.25, 0.05, 2.0, 10, 1, 6),
+                       notes="as mpi; prints \"Sum of Temperature:\" (the reference's gsum is uninitialised, its "
+                             "reduction commented out, heat.F90:266-275; here the all-reduced sum) and a "
+                             "per-iteration \"total time:\" (heat.F90:292)"),
     "serial": Variant("serial", "fortran/serial/heat.f90 (V3)", INCLUSIVE, "hat", "serial", "total time:",
                       default_input=InputDat(1024, 0.25, 0.05, 2.0, 30, 0, 5),
                       notes="n points incl. boundary, hat T=2 on [0.5,1.5]^2, int.dat + soln.dat"),

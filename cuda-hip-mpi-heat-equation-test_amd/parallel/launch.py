@@ -12,6 +12,10 @@ native engine. One process per GPU:
 
     torchrun --nproc-per-node 2 -m heat2d input.dat --transport peer --share-gpu  # 2 ranks, 1 GPU, hipIpc
 
+GPU ranks exchange halos over RCCL (--transport auto, the default: RCCL when
+its communicator builds on every rank, else the peer transport — hipIpc
+mappings of the neighbours' fields — on every rank alike; parallel/select.py).
+
 Extras: --tb K, --dtype, --check-every N (global sum / residual, NaN abort),
 --checkpoint DIR --checkpoint-every N, --restart DIR, --json FILE, --output npy.
 """
@@ -28,7 +32,7 @@ import numpy as np
 def build_parser():
     ap = argparse.ArgumentParser(prog="python -m heat2d", description=__doc__.split("\n")[0])
     ap.add_argument("input", nargs="?", default="input.dat")
-    ap.add_argument("--variant", default=None, help="mpi | serial | cuda | managed | python | pycuda")
+    ap.add_argument("--variant", default=None, help="mpi | mpicuda | serial | cuda | managed | python | pycuda")
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "cpu"])
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--ic", default=None)
@@ -53,16 +57,17 @@ def build_parser():
     ap.add_argument("--checkpoint-every", type=int, default=0)
     ap.add_argument("--restart", default=None)
     ap.add_argument("--quiet", action="store_true")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "peer"],
-                    help="halo exchange between GPU rank processes: rccl (RCCL send/recv) or peer (hipIpc "
-                         "mappings of the neighbours' fields, stream-ordered by host-shared counters; host "
-                         "collectives over gloo)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "peer"],
+                    help="halo exchange between GPU rank processes: rccl (RCCL send/recv), peer (hipIpc "
+                         "mappings of the neighbours' fields, stream-ordered by host-shared counters), or auto "
+                         "(default): rccl if its communicator and solver build on every rank, else peer on every "
+                         "rank; host collectives over gloo")
     ap.add_argument("--share-gpu", action="store_true",
-                    help="every rank on GPU 0 (needs --transport peer): the multi-process path on one GPU")
+                    help="every rank on GPU 0 (--transport peer or auto): the multi-process path on one GPU")
     return ap
 
 
-def _dist_setup(backend: str, peer: bool = False, share_gpu: bool = False):
+def _dist_setup(backend: str, share_gpu: bool = False):
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -73,11 +78,39 @@ def _dist_setup(backend: str, peer: bool = False, share_gpu: bool = False):
     if world > 1 and not dist.is_initialized():
         from datetime import timedelta
         to = timedelta(seconds=float(os.environ.get("HEAT2D_COMM_TIMEOUT", "600")))  # dead peer -> error, not hang
-        if backend == "hip" and not peer:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=to)
-        else:
-            dist.init_process_group("gloo", timeout=to)
+        # host collectives over gloo whatever the halo fabric (the RCCL unique
+        # id, barriers, the timing MAX, the transport choice)
+        dist.init_process_group("gloo", timeout=to)
     return rank, world, local
+
+
+def _make_solver(kinds, make_transport, make_solver, world):
+    """The first transport kind whose transport AND solver build on every rank
+    (parallel/select.try_collective: a failure on any rank skips the kind on
+    every rank — e.g. RCCL refusing ranks that share a GPU, or a node whose RCCL
+    cannot initialise). Returns (transport, solver, kind, {kind: error})."""
+    from heat2d.parallel import select
+
+    def amin(v):
+        if world == 1:
+            return float(v)
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return float(t.item())
+
+    errors = {}
+    for kind in kinds:
+        tr, why = select.try_collective(lambda: make_transport(kind), amin,
+                                        cleanup=lambda t: (t.abort("another rank failed to initialise"), t.close()))
+        if why is None:
+            s, why = select.try_collective(lambda: make_solver(tr), amin, cleanup=lambda x: x.close())
+            if why is None:
+                return tr, s, kind, errors
+            tr.close()
+        errors[kind] = why
+    raise SystemExit(f"heat2d: no halo transport works on every rank: {errors}")
 
 
 def run(argv=None) -> int:
@@ -90,10 +123,9 @@ def run(argv=None) -> int:
     from heat2d.utils.config import make_problem, read_input
 
     backend = resolve_backend(a.backend)
-    if a.share_gpu and a.transport != "peer":
-        raise SystemExit("--share-gpu needs --transport peer (RCCL refuses two ranks on one GPU)")
-    peer = a.transport == "peer" and backend == "hip"
-    rank, world, local = _dist_setup(backend, peer, a.share_gpu)
+    if a.share_gpu and a.transport == "rccl":
+        raise SystemExit("--share-gpu needs --transport peer or auto (RCCL refuses two ranks on one GPU)")
+    rank, world, local = _dist_setup(backend, a.share_gpu)
     root = rank == 0
     inp = read_input(a.input)
     if a.n:
@@ -115,20 +147,30 @@ def run(argv=None) -> int:
         lim = N.device_limits(local)
         print(lim["MAX_THREADS_PER_BLOCK"])
         print(" device limits: " + " ".join(f"{k}={v}" for k, v in lim.items()), flush=True)
-    if world > 1:
-        if backend != "hip":
-            tr = T.TorchDistTransport()
-        else:
-            tr = T.IpcTransport(local) if peer else T.RcclTransport(rank, world, local)
-    else:
-        tr = T.SelfTransport()
     engine = a.engine or ("jit" if var.name == "pycuda" and backend == "hip" else "tb")
     arith = a.arith
     if arith == "auto" and prob.r == 0.25 and prob.ic.sterbenz_safe() and not a.restart and engine == "tb":
         arith = "jacobi"  # bitwise the reference rounding on this IC (the CLI's auto does the same)
-    s = HeatSolver(prob, dtype=a.dtype, backend=backend, tb=a.tb, overlap=not a.no_overlap, copy_swap=a.copy_swap,
-                   managed=a.managed or var.managed, graph=a.graph, transport=tr,
-                   device=local if backend == "hip" else None, engine=engine, arith=arith)
+
+    def make_transport(kind):
+        return {"torch-dist": T.TorchDistTransport, "self": T.SelfTransport,
+                "rccl": lambda: T.RcclTransport(rank, world, local), "peer": lambda: T.IpcTransport(local)}[kind]()
+
+    def make_solver(tr):
+        return HeatSolver(prob, dtype=a.dtype, backend=backend, tb=a.tb, overlap=not a.no_overlap,
+                          copy_swap=a.copy_swap, managed=a.managed or var.managed, graph=a.graph, transport=tr,
+                          device=local if backend == "hip" else None, engine=engine, arith=arith)
+
+    if world == 1:
+        kinds = ["self"]
+    elif backend != "hip":
+        kinds = ["torch-dist"]
+    else:
+        kinds = {"auto": ["rccl", "peer"], "rccl": ["rccl"], "peer": ["peer"]}[a.transport]
+    tr, s, kind, fallback = _make_solver(kinds, make_transport, make_solver, world)
+    if fallback and root and not a.quiet:
+        print(f"heat2d: halo transport {kind} ({'; '.join(f'{k} failed: {v}' for k, v in fallback.items())})",
+              file=sys.stderr, flush=True)
     if root and not a.quiet:
         if world > 1 or var.outputs == "mpi":
             print(f" Automatic MPI decomposition: {world:12d}  x 1")
@@ -187,7 +229,7 @@ def run(argv=None) -> int:
     s.synchronize()
     _barrier(world)
     elapsed = time.perf_counter() - t0
-    elapsed = _max_over_ranks(elapsed, world, "hip" if backend == "hip" and not peer else "cpu")
+    elapsed = _max_over_ranks(elapsed, world, "cpu")
     ran = nsteps - start_step
     cycles = s.cycle_hist()
 
@@ -209,13 +251,14 @@ def run(argv=None) -> int:
                 io.write_xyz(f"soln{rank:05d}.dat", local_T, x[1 + s.row0:1 + s.row0 + s.nrows], x[1:-1])
     st = s.stats()
     if root:
+        if var.sum_line:  # fortran/mpi+cuda/heat.F90:275 (there an uninitialised gsum; here the all-reduced sum)
+            print(f" Sum of Temperature: {st['sum']:24.16g}")
         print(" simulation completed!!!!")
-        if var.timing_line == "Average time:":
-            print(f" Average time: {elapsed / max(ran, 1):24.16g}")
-        else:
-            print(f" total time: {elapsed:24.16g}")
+        per = elapsed / max(ran, 1) if var.per_step else elapsed
+        print(f" {var.timing_line} {per:24.16g}")
         rec = metrics.record(prob.n_owned, ran, elapsed, world, a.dtype, s.tb, backend, a.copy_swap,
-                             {"variant": var.name, "arith": arith, "sum": st["sum"], "min": st["min"], "max": st["max"]},
+                             {"variant": var.name, "arith": arith, "sum": st["sum"], "min": st["min"], "max": st["max"],
+                              "transport": kind, "transport_fallback": fallback or None},
                              cycles=cycles)
         if not a.quiet:
             print(f" heat2d: n={prob.n_owned} P={world} {a.dtype} K<={s.tb} passes={sum(cycles.values())} "

@@ -39,6 +39,10 @@ def test_bench_json_line_multi_rank(nproc, dtype):
     # the self-check after the timed run: an uneven rough-data problem over the
     # same ranks and transport kind, gathered and compared bitwise to the golden
     assert d["verified"] is True and d["verify"]["n"] == 256 * nproc + 5 and d["verify"]["max_abs_diff"] == 0.0
+    # the timed field itself, against the one-step reference run from the same IC
+    fc = d["timed_field_check"]
+    assert fc["ok"] is True and fc["mode"] == "full" and fc["mismatches"] == 0 and fc["max_abs_diff"] == 0.0, fc
+    assert fc["rows_checked"] == 100 and fc["steps"] == 28
 
 
 def test_bench_multi_rank_times_the_same_state_as_one_rank():
@@ -230,3 +234,30 @@ def test_bench_plan_cache_respects_knobs(tmp_path):
     # a drifted one is re-tuned, so hits, not every plan's origin, are checked)
     assert static2["config"]["plan_cache"]["hits"] >= 1
     assert all(p["dynamic"] == 0 for p in static2["config"]["launch_plans"].values())
+
+
+@pytest.mark.parametrize("nproc", [1, 2])
+def test_bench_timed_field_check_windows_cpu(nproc):
+    """--field-check windows (what a grid too big for a second copy gets): row
+    windows at both slab boundaries and the middle of every slab, each run by a
+    single-rank reference solver with steps + 1 rows of margin, bitwise."""
+    args = ["--backend", "cpu", "--gpus", str(nproc), "--grid", "150", "--steps", "12", "--warmup", "3", "--tb", "4",
+            "--field-check", "windows", "--window-rows", "16", "--verify", "off"]
+    d = run_plain(*args)
+    fc = d["timed_field_check"]
+    assert fc["mode"] == "windows" and fc["ok"] is True and fc["mismatches"] == 0, fc
+    assert fc["rows_checked"] == nproc * 3 * 16 and fc["steps"] == 15
+
+
+def test_bench_timed_field_check_sigma_fast_cpu():
+    """A non-reference arithmetic is checked within its stated bound (fast form,
+    sigma 0.2); the contracted form at that sigma is checked bitwise against the
+    contracted one-step reference."""
+    fast = run_plain("--backend", "cpu", "--grid", "96", "--steps", "10", "--warmup", "2", "--tb", "5", "--sigma", "0.2",
+                     "--arith", "fast", "--verify", "off")
+    fc = fast["timed_field_check"]
+    assert fc["ok"] is True and "bound" in fc and fc["max_abs_diff"] <= fc["bound"], fc
+    fma = run_plain("--backend", "cpu", "--grid", "96", "--steps", "10", "--warmup", "2", "--tb", "5", "--sigma", "0.2",
+                    "--arith", "fma")
+    assert fma["timed_field_check"]["ok"] is True and fma["timed_field_check"]["mismatches"] == 0
+    assert fma["verified"] is True and "bound" in fma["verify"], fma["verify"]

@@ -225,9 +225,51 @@ def test_cli_peer_transport_fails_fast(cli, gpu, tmp_path):
 
 def test_cli_share_gpu_needs_peer(cli, tmp_path):
     (tmp_path / "input.dat").write_text("64 0.25 0.05 1.0 5 0\n")
-    p = subprocess.run([N.CLI_PATH, "--gpus", "2", "--share-gpu"], cwd=tmp_path, capture_output=True, text=True,
-                       timeout=120)
-    assert p.returncode != 0 and "--share-gpu needs --transport peer" in p.stderr
+    p = subprocess.run([N.CLI_PATH, "--gpus", "2", "--share-gpu", "--transport", "rccl"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "--share-gpu needs --transport peer or auto" in p.stderr
+
+
+def test_cli_mpicuda_variant_cpu(cli, tmp_path):
+    """--variant mpicuda (fortran/mpi+cuda, V7): its stdout lines — nx / ny,
+    "Sum of Temperature:" (there an uninitialised gsum, heat.F90:266-275; here
+    the all-reduced sum of the field), "simulation completed!!!!" and a
+    per-iteration "total time:" (heat.F90:292) — on 3 host-thread ranks."""
+    (tmp_path / "input.dat").write_text("100 0.25 0.05 2.0 10 1\n")
+    out = run_cli(tmp_path, "--cpu", "--variant", "mpicuda", "--gpus", "3", "--json", "m.json")
+    lines = out.splitlines()
+    i_sum = next(i for i, l in enumerate(lines) if "Sum of Temperature:" in l)
+    i_done = next(i for i, l in enumerate(lines) if "simulation completed!!!!" in l)
+    i_time = next(i for i, l in enumerate(lines) if l.strip().startswith("total time:"))
+    assert i_sum < i_done < i_time and "Average time:" not in out
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    ref = float(np.sum(R.owned(R.ftcs(prob))))
+    assert float(lines[i_sum].split(":")[1]) == pytest.approx(ref, rel=1e-15)
+    import json
+    d = json.loads((tmp_path / "m.json").read_text())
+    per_step = float(lines[i_time].split(":")[1])
+    assert per_step == pytest.approx(d["wall_s"] / 10, rel=1e-6)
+    assert d["transport"] == "host" and d["transport_fallback"] is None
+    got = np.concatenate([read_xyz(tmp_path / f"soln{r:05d}.dat")[:, 2] for r in range(3)])
+    assert np.array_equal(got, R.owned(R.ftcs(prob)).ravel())
+
+
+@pytest.mark.gpu
+def test_cli_auto_transport_falls_back_to_peer(cli, gpu, tmp_path):
+    """--transport auto (the default) with ranks sharing one GPU: RCCL refuses
+    to build the communicators, every rank falls back to the peer transport
+    (reported on stderr and in the JSON), and the run is bitwise the golden."""
+    (tmp_path / "input.dat").write_text("1100 0.25 0.05 1.0 31 0\n")
+    p = subprocess.run([N.CLI_PATH, "--gpus", "3", "--share-gpu", "--output", "npy", "--json", "m.json"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "falling back to the peer transport" in p.stderr
+    import json
+    d = json.loads((tmp_path / "m.json").read_text())
+    assert d["transport"] == "peer" and "RCCL unavailable" in d["transport_fallback"], d
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    got = np.concatenate([np.load(tmp_path / f"soln{r:05d}.npy") for r in range(3)])
+    assert np.array_equal(got, R.owned(R.ftcs(prob)))
 
 
 @pytest.mark.gpu

@@ -62,6 +62,28 @@ def test_cli_multi_gpu_bitwise(tmp_path, transport, P, extra):
     assert np.array_equal(got, R.owned(R.ftcs(prob, dtype=npdt)))
 
 
+@pytest.mark.parametrize("force_fail", [False, True])
+def test_cli_multi_gpu_auto_transport(tmp_path, force_fail):
+    """--transport auto (the CLI default) on P distinct GPUs: RCCL when its
+    communicators build on every rank; with HEAT2D_FORCE_RCCL_FAIL=1 (a node
+    whose RCCL cannot initialise) every rank falls back to the peer transport.
+    Both bitwise the golden."""
+    P = SIZES[-1]
+    (tmp_path / "input.dat").write_text("2051 0.25 0.05 1.0 57 0\n")
+    env = dict(os.environ)
+    if force_fail:
+        env["HEAT2D_FORCE_RCCL_FAIL"] = "1"
+    p = subprocess.run([N.CLI_PATH, "--gpus", str(P), "--output", "npy", "--json", "m.json"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    d = json.loads((tmp_path / "m.json").read_text())
+    assert d["transport"] == ("peer" if force_fail else "rccl"), d
+    assert (d["transport_fallback"] is not None) == force_fail
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    got = np.concatenate([np.load(tmp_path / f"soln{r:05d}.npy") for r in range(P)])
+    assert np.array_equal(got, R.owned(R.ftcs(prob)))
+
+
 def run_bench(*args, timeout=900):
     env = dict(os.environ, OMP_NUM_THREADS="1")
     env.pop("WORLD_SIZE", None)
@@ -90,6 +112,8 @@ def test_bench_multi_gpu_matches_one_gpu(one_gpu_stats, transport, P):
     else:
         assert set(ch) >= {"rccl", "ipc"}
     assert d["verified"] is True, d["verify"]
+    fc = d["timed_field_check"]
+    assert fc["ok"] is True and fc["mode"] == "full" and fc["mismatches"] == 0, fc
     b = d["field_stats"]
     assert one_gpu_stats["min"] == b["min"] and one_gpu_stats["max"] == b["max"]
     assert b["sum"] == pytest.approx(one_gpu_stats["sum"], rel=1e-12, abs=0)

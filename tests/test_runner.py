@@ -247,9 +247,41 @@ def test_checkpoint_resave_same_step_never_overwrites(native, tmp_path, writer):
 def test_share_gpu_needs_peer_transport(native, tmp_path):
     (tmp_path / "input.dat").write_text("20 0.25 0.05 1.0 3 0\n")
     env = dict(os.environ, PYTHONPATH=ROOT)
-    out = subprocess.run([sys.executable, "-m", "heat2d", "--backend", "cpu", "--share-gpu"], cwd=tmp_path, env=env,
-                         capture_output=True, text=True, timeout=120)
-    assert out.returncode != 0 and "--share-gpu needs --transport peer" in out.stderr
+    out = subprocess.run([sys.executable, "-m", "heat2d", "--backend", "cpu", "--share-gpu", "--transport", "rccl"],
+                         cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "--share-gpu needs --transport peer or auto" in out.stderr
+
+
+def test_torchrun_mpicuda_variant_cpu(native, tmp_path):
+    """--variant mpicuda (fortran/mpi+cuda, V7) on 2 gloo ranks: "Sum of
+    Temperature:" with the all-reduced sum, then the completion line and a
+    per-iteration "total time:"; per-rank soln%05d.dat files."""
+    (tmp_path / "input.dat").write_text("60 0.25 0.05 2.0 9 1\n")
+    out = py(tmp_path, "--backend", "cpu", "--variant", "mpicuda", "--json", "m.json", nproc=2)
+    lines = [l.strip() for l in out.splitlines()]
+    i_sum = next(i for i, l in enumerate(lines) if l.startswith("Sum of Temperature:"))
+    i_done = lines.index("simulation completed!!!!")
+    i_time = next(i for i, l in enumerate(lines) if l.startswith("total time:"))
+    assert i_sum < i_done < i_time
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    ref = R.owned(R.ftcs(prob))
+    assert float(lines[i_sum].split(":")[1]) == pytest.approx(float(ref.sum()), rel=1e-15)
+    T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    assert np.array_equal(T, ref)
+
+
+@pytest.mark.gpu
+def test_torchrun_auto_transport_falls_back_share_gpu(native, gpu, tmp_path):
+    """`python -m heat2d --share-gpu` with the default --transport auto under
+    torchrun: RCCL refuses two ranks on one GPU on every rank, every rank takes
+    the peer (hipIpc) transport, and the result is bitwise the golden."""
+    (tmp_path / "input.dat").write_text("300 0.25 0.05 1.0 23 1\n")
+    out = py(tmp_path, "--backend", "hip", "--share-gpu", "--arith", "exact", "--json", "m.json", nproc=2)
+    d = json.loads((tmp_path / "m.json").read_text())
+    assert d["transport"] == "peer" and "rccl" in d["transport_fallback"], d
+    T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
 
 
 @pytest.mark.gpu
