@@ -40,6 +40,7 @@ kernel + per-step D2D copy (>= 32 B/pt/step at 1.6 TB/s) — times N ranks.
 import argparse
 import gc
 import json
+import math
 import os
 import sys
 import time
@@ -124,8 +125,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=480)
     ap.add_argument("--warmup", type=int, default=48)
-    ap.add_argument("--n", "--grid", dest="n", type=int, default=32768,
-                    help="grid edge (use --grid under torchrun: its parser takes --n as an abbreviation)")
+    ap.add_argument("--n", "--grid", dest="n", default="32768",
+                    help="grid edge (use --grid under torchrun: its parser takes --n as an abbreviation), or 'max': "
+                         "the memory-fit planner's largest grid (utils/memplan.py: free device memory minus a "
+                         "reserve; --weak: the largest global grid on N GPUs, else the largest 1-GPU grid)")
     ap.add_argument("--sigma", type=float, default=0.25,
                     help="input.dat sigma (= r, the FTCS coefficient); the reference's inputs all use 0.25")
     ap.add_argument("--weak", action="store_true",
@@ -238,10 +241,26 @@ def main():
     from heat2d.parallel.transport import (IpcLoopTransport, IpcTransport, RcclLoopTransport, RcclTransport,
                                            SelfTransport, TorchDistTransport)
 
-    n_glob = args.n
-    if args.weak:
-        import math
-        n_glob = int(round(args.n * math.sqrt(world)))
+    mem_plan = None
+    if args.n == "max":
+        # the largest grid the free device memory holds (rank 0's slab is the
+        # largest): over `world` ranks for weak scaling, one GPU's for strong
+        # scaling (a fixed total problem); min free memory over the ranks
+        from heat2d.utils import memplan
+        if hip:
+            free = memplan.mem_info(device)[0] / (world if args.share_gpu else 1)
+        else:
+            free = 64 << 20  # CPU rehearsal of the planner: a 64 MiB "device"
+        free = int(amin(free))
+        mem_plan = memplan.plan_max_grid(args.dtype, world if args.weak else 1, free_bytes=free,
+                                         reserve=memplan.reserve_bytes(free) if hip else 0)
+        n_glob = mem_plan["n"]
+        n_per_gpu = n_glob if not args.weak else int(round(n_glob / math.sqrt(world)))
+    else:
+        n_per_gpu = int(args.n)
+        n_glob = n_per_gpu
+        if args.weak:
+            n_glob = int(round(n_per_gpu * math.sqrt(world)))
     inp = heat2d.InputDat(n=n_glob, sigma=args.sigma, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     arith = args.arith if args.arith != "bench" else ("jacobi" if prob.r == 0.25 else "auto")
@@ -491,7 +510,8 @@ def main():
             "dtype": args.dtype,
             "data": "synthetic (reference benchmark IC: T=2 interior, Dirichlet T=1 frame)",
             "config": {
-                "model": (f"heat2d FTCS 5-point, weak scaling: {args.n}^2 points per GPU (global {n_glob}^2)" if args.weak
+                "model": (f"heat2d FTCS 5-point, weak scaling: {n_per_gpu}^2 points per GPU (global {n_glob}^2)"
+                          + (" — the memory-fit planner's largest grid" if mem_plan else "") if args.weak
                           else "heat2d FTCS 5-point, fortran/hip/input.dat (32768 0.25 0.05 1.0 25000 0)"
                           if n_glob == 32768 and args.sigma == 0.25
                           else f"heat2d FTCS 5-point, {n_glob}^2 (sigma {args.sigma:g}, nu 0.05, L 1.0)"),
@@ -525,6 +545,7 @@ def main():
             "verified": None if verify is None else verify["verified"],
             "verify": verify,
             "timed_field_check": field_check,
+            "memory_plan": mem_plan,
             "baseline_basis": "BASELINE.md derived ceiling 50 Gpts/s per MI250X GCD x n_gpus",
         }
         if stats:

@@ -242,6 +242,29 @@ int heat2d_solver_create(const heat2d_config* cfg, void* transport, void** out) 
   });
 }
 
+int heat2d_solver_footprint(const heat2d_config* cfg, int rank, int nranks, int64_t* out3) {
+  return guarded([&] {
+    const Footprint f = solver_footprint(to_cfg(cfg), rank, nranks);
+    out3[0] = f.field_bytes;
+    out3[1] = f.work_bytes;
+    out3[2] = f.total_bytes;
+  });
+}
+
+int heat2d_plan_max_grid(int dtype, int nranks, int64_t budget_bytes, int64_t* n) {
+  return guarded([&] { *n = plan_max_grid(dtype, nranks, budget_bytes); });
+}
+
+int heat2d_mem_info(int device, int64_t* free_bytes, int64_t* total_bytes) {
+  return guarded([&] {
+    if (hipSetDevice(device) != hipSuccess) fail(__FILE__, __LINE__, "hipSetDevice failed");
+    size_t f = 0, t = 0;
+    if (hipMemGetInfo(&f, &t) != hipSuccess) fail(__FILE__, __LINE__, "hipMemGetInfo failed");
+    *free_bytes = (int64_t)f;
+    *total_bytes = (int64_t)t;
+  });
+}
+
 int heat2d_solver_free(void* s) {
   return guarded([&] { delete static_cast<Solver*>(s); });
 }

@@ -60,6 +60,7 @@ struct Args {
   int64_t check_every = 0;
   int64_t ntime = -1;  // override
   int64_t n = -1;      // override
+  bool n_max = false;  // --n max: the largest grid the GPUs' free memory holds (memory-fit planner)
   bool quiet = false;
   bool timers = false;
   std::string engine = "tb";
@@ -84,7 +85,7 @@ void usage() {
       "usage: heat2d [input.dat] [--variant mpi|mpicuda|serial|cuda] [--gpus N | --cpu] [--dtype fp64|fp32]\n"
       "              [--tb K] [--no-overlap] [--copy-swap] [--managed] [--graph] [--ic NAME]\n"
       "              [--print-every N] [--check-every N] [--output ascii|npy|none] [--json FILE]\n"
-      "              [--n N] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith auto|exact|fma|jacobi|fast]\n"
+      "              [--n N|max] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith auto|exact|fma|jacobi|fast]\n"
       "              [--time-transfers]\n"
       "              [--checkpoint DIR [--checkpoint-every N]] [--restart DIR]\n"
       "              [--transport auto|rccl|peer] [--share-gpu] [--autotune auto|on|off]\n");
@@ -120,7 +121,11 @@ Args parse_args(int argc, char** argv) {
     else if (s == "--print-every") a.print_every = std::atoll(need("--print-every").c_str());
     else if (s == "--check-every") a.check_every = std::atoll(need("--check-every").c_str());
     else if (s == "--ntime") a.ntime = std::atoll(need("--ntime").c_str());
-    else if (s == "--n") a.n = std::atoll(need("--n").c_str());
+    else if (s == "--n") {
+      const std::string v = need("--n");
+      if (v == "max") a.n_max = true;
+      else a.n = std::atoll(v.c_str());
+    }
     else if (s == "--quiet") a.quiet = true;
     else if (s == "--timers") a.timers = true;
     else if (s == "--checkpoint") a.checkpoint = need("--checkpoint");
@@ -475,6 +480,39 @@ void run_rank(Shared& sh, int rank) {
   }
 }
 
+// --n max: the memory-fit planner (runtime.hpp plan_max_grid) on the smallest
+// free memory of the GPUs the ranks use (hipMemGetInfo; shared by the ranks
+// with --share-gpu), minus a reserve for what the solver does not own
+// (2 GiB + 1 %: runtime growth, RCCL buffers; utils/memplan.py uses the same).
+// The reference's grid is whatever input.dat says, plus a whole-field host
+// mirror (fortran/hip/heat.F90:161-176); here nothing mirrors the field.
+void plan_n_max(Shared& sh, int ndev, Convention conv) {
+  const Args& a = sh.args;
+  HEAT2D_REQUIRE(!a.cpu, "--n max plans device memory: it needs a GPU");
+  const int P = sh.nranks;
+  int64_t free_min = INT64_MAX, total = 0;
+  for (int d = 0; d < (a.share_gpu ? 1 : std::min(P, ndev)); ++d) {
+    size_t f = 0, t = 0;
+    if (hipSetDevice(d) != hipSuccess || hipMemGetInfo(&f, &t) != hipSuccess)
+      fail(__FILE__, __LINE__, "hipMemGetInfo failed");
+    free_min = std::min<int64_t>(free_min, (int64_t)f);
+    total = (int64_t)t;
+  }
+  if (a.share_gpu) free_min /= P;
+  const int64_t reserve = (int64_t(2) << 30) + free_min / 100;
+  const int dt = a.dtype == "fp32" ? 0 : 1;
+  const int64_t n_owned = plan_max_grid(dt, P, free_min - reserve);
+  sh.in.n = conv == Convention::Inclusive ? n_owned + 2 : n_owned;  // input.dat's n
+  SolverConfig c{};
+  c.n_rows = c.n_cols = n_owned;
+  c.dtype = dt;
+  const Footprint fp = solver_footprint(c, 0, P);
+  if (!a.quiet)
+    std::printf(" heat2d: --n max: n = %lld (%d rank%s, %s): %.2f GB per GPU of %.2f GB free (%.1f %%), %.2f GB total\n",
+                (long long)sh.in.n, P, P > 1 ? "s" : "", a.dtype.c_str(), fp.total_bytes / 1e9, free_min / 1e9,
+                100.0 * fp.total_bytes / free_min, total / 1e9);
+}
+
 // --transport auto: build every rank's RCCL communicator up front (one thread
 // per rank: ncclCommInitRank is collective) and keep them only if EVERY rank
 // got one; otherwise release the ones that did and run on the peer transport
@@ -553,9 +591,6 @@ int main(int argc, char** argv) {
     const bool ghost = a.variant == "mpi" || a.variant == "mpicuda";
     Convention conv = ghost ? Convention::Ghost : Convention::Inclusive;
     std::string ic = a.ic.empty() ? (ghost ? "uniform" : a.variant == "cuda" ? "hat-cuda" : "hat") : a.ic;
-    sh.prob = make_problem(sh.in, conv, ic);
-    if (sh.prob.r > 0.25 + 1e-12 && !a.quiet)
-      std::fprintf(stderr, "warning: r = %.6g > 0.25: FTCS is unstable in 2-D\n", sh.prob.r);
     int ndev = 0;
     if (!a.cpu && hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
     if (!a.cpu && ndev == 0) {
@@ -563,6 +598,10 @@ int main(int argc, char** argv) {
       a.cpu = true;
     }
     sh.nranks = a.cpu ? std::max(1, a.gpus) : (a.gpus > 0 ? a.gpus : 1);
+    if (a.n_max) plan_n_max(sh, ndev, conv);
+    sh.prob = make_problem(sh.in, conv, ic);
+    if (sh.prob.r > 0.25 + 1e-12 && !a.quiet)
+      std::fprintf(stderr, "warning: r = %.6g > 0.25: FTCS is unstable in 2-D\n", sh.prob.r);
     if (a.transport != "auto" && a.transport != "rccl" && a.transport != "peer")
       fail(__FILE__, __LINE__, "--transport must be auto, rccl or peer");
     if (a.share_gpu && a.transport == "rccl")

@@ -141,6 +141,13 @@ int heat2d_solver_pref_depth(void* s, int32_t* out);
 int heat2d_solver_sync(void* s);
 int heat2d_solver_stats(void* s, double* out6, int residual);
 int heat2d_solver_download(void* s, void* host, int64_t ld);
+// memory-fit planner (runtime.hpp solver_footprint / plan_max_grid): out3 =
+// {field bytes, workspace bytes, total} of a Solver of cfg on rank of nranks
+int heat2d_solver_footprint(const heat2d_config* cfg, int rank, int nranks, int64_t* out3);
+// the largest n x n grid of dtype on nranks ranks whose largest slab fits budget_bytes
+int heat2d_plan_max_grid(int dtype, int nranks, int64_t budget_bytes, int64_t* n);
+// hipMemGetInfo of device
+int heat2d_mem_info(int device, int64_t* free_bytes, int64_t* total_bytes);
 // s's current field, local rows [r0, r0 + nrows), against other's, rows
 // [other_r0, ...): out2 = {max |a - b| (NaN if any), differing bit patterns}
 int heat2d_solver_compare(void* s, void* other, int64_t r0, int64_t nrows, int64_t other_r0, double* out2);

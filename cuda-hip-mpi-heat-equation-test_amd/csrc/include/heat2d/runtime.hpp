@@ -244,6 +244,26 @@ inline int exchange_depth(const std::vector<int>& seq, size_t i, int next) {
   return i + 1 < seq.size() ? seq[i + 1] : next;
 }
 
+// The slab layout a Solver of config `cfg` uses on `rank` of `nranks` (uneven
+// decompose() slabs, or the 1-rank middle-slab rehearsal), ghost bands of
+// cfg.halo (0: kDefaultHalo) rows, pitched columns.
+SlabLayout solver_layout(const SolverConfig& cfg, int rank, int nranks);
+// Device bytes that Solver allocates for its state: both pitched fields with
+// their ghost bands (field_bytes) plus the statistics / partials / item-queue
+// workspaces (work_bytes; HIP backend) — exactly the constructor's hipMallocs
+// (tests/test_memory_plan.py compares them with hipMemGetInfo). Not counted:
+// the transport's own buffers and the runtime (the planner's reserve).
+struct Footprint {
+  int64_t field_bytes, work_bytes, total_bytes;
+};
+Footprint solver_footprint(const SolverConfig& cfg, int rank, int nranks);
+// Memory-fit planner: the largest n such that an n x n grid of `dtype` on
+// `nranks` ranks fits budget_bytes per GPU (the largest slab, rank 0's,
+// decides). The reference sizes nothing: its grid is input.dat's n, with a
+// whole-field host mirror (fortran/hip/heat.F90:161-176); here the IC is made
+// on the device, so only the two device fields count.
+int64_t plan_max_grid(int dtype, int nranks, int64_t budget_bytes, int64_t halo = 0);
+
 class Solver {
  public:
   Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream_t external_stream = nullptr);

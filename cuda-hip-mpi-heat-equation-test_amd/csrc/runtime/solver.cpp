@@ -59,6 +59,48 @@ void* host_alloc(size_t bytes) {
 }
 }  // namespace
 
+SlabLayout solver_layout(const SolverConfig& cfg, int rank, int nranks) {
+  const int64_t halo = cfg.halo > 0 ? cfg.halo : kDefaultHalo;
+  if (cfg.slab_rows_global > 0) {  // 1-rank rehearsal of a middle slab of a bigger grid
+    HEAT2D_REQUIRE(nranks == 1, "slab_rows_global: single-rank rehearsal only");
+    HEAT2D_REQUIRE(cfg.slab_row0 >= 0 && cfg.slab_row0 + cfg.n_rows <= cfg.slab_rows_global, "slab outside the grid");
+    return make_layout(cfg.n_rows, cfg.n_cols, halo, cfg.slab_row0, cfg.slab_rows_global);
+  }
+  const SlabRange sr = decompose(cfg.n_rows, nranks, rank);
+  return make_layout(sr.nrows, cfg.n_cols, halo, sr.row0, cfg.n_rows);
+}
+
+Footprint solver_footprint(const SolverConfig& cfg, int rank, int nranks) {
+  const SlabLayout L = solver_layout(cfg, rank, nranks);
+  Footprint f{};
+  f.field_bytes = 2 * L.elems() * (int64_t)dtype_size((DType)cfg.dtype);
+  if (cfg.backend == (int32_t)Backend::Hip)
+    f.work_bytes = (kern::stats_work_elems() + 8) * 8 + 6 * kern::max_stats_waves() * 8 + 2 * 4;
+  f.total_bytes = f.field_bytes + f.work_bytes;
+  return f;
+}
+
+int64_t plan_max_grid(int dtype, int nranks, int64_t budget_bytes, int64_t halo) {
+  HEAT2D_REQUIRE(nranks >= 1 && budget_bytes > 0, "plan_max_grid needs nranks >= 1 and a positive budget");
+  SolverConfig c{};
+  c.dtype = dtype;
+  c.backend = (int32_t)Backend::Hip;
+  c.halo = halo;
+  // the largest slab is rank 0's (decompose() gives the remainder to the first ranks)
+  auto fits = [&](int64_t n) {
+    c.n_rows = c.n_cols = n;
+    return solver_footprint(c, 0, nranks).total_bytes <= budget_bytes;
+  };
+  int64_t lo = 0, hi = 1;
+  while (fits(hi) && hi < (int64_t(1) << 31)) hi *= 2;  // the footprint grows with n
+  while (hi - lo > 1) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    (fits(mid) ? lo : hi) = mid;
+  }
+  HEAT2D_REQUIRE(lo >= nranks, "no grid of at least one row per rank fits the budget");
+  return lo;
+}
+
 Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream_t external_stream)
     : cfg_(cfg), tr_(std::move(tr)) {
   HEAT2D_REQUIRE(tr_ != nullptr, "transport required");
@@ -110,17 +152,8 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
   cfg_.tb = K;
   band_ = K;
   k_pref_ = tb_given ? K : std::min(K, tb_pref);
-  const int64_t halo = cfg_.halo > 0 ? cfg_.halo : kDefaultHalo;
-  HEAT2D_REQUIRE(halo >= K, "halo must be >= temporal depth");
-  const SlabRange sr = decompose(cfg_.n_rows, P, rank);
-  if (cfg_.slab_rows_global > 0) {  // 1-rank rehearsal of a middle slab of a bigger grid
-    HEAT2D_REQUIRE(P == 1, "slab_rows_global: single-rank rehearsal only");
-    HEAT2D_REQUIRE(cfg_.slab_row0 >= 0 && cfg_.slab_row0 + cfg_.n_rows <= cfg_.slab_rows_global,
-                   "slab outside the grid");
-    L_ = make_layout(cfg_.n_rows, cfg_.n_cols, halo, cfg_.slab_row0, cfg_.slab_rows_global);
-  } else {
-    L_ = make_layout(sr.nrows, cfg_.n_cols, halo, sr.row0, cfg_.n_rows);
-  }
+  HEAT2D_REQUIRE((cfg_.halo > 0 ? cfg_.halo : kDefaultHalo) >= K, "halo must be >= temporal depth");
+  L_ = solver_layout(cfg_, rank, P);
 
   const size_t bytes = (size_t)L_.elems() * dtype_size(dtype());
   if (hip_) {
@@ -130,6 +163,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
       if (cfg_.managed) H2D_HIP(hipMallocManaged(&buf_[b], bytes));
       else H2D_HIP(hipMalloc(&buf_[b], bytes));
     }
+    // (solver_footprint() counts exactly these allocations: keep them in step)
     H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_work_), (size_t)(kern::stats_work_elems() + 8) * sizeof(double)));
     H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_part_), (size_t)(6 * kern::max_stats_waves()) * sizeof(double)));
     H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_queue_), 2 * sizeof(uint32_t)));

@@ -166,6 +166,9 @@ _SIGS = {
     "heat2d_solver_stats": (C.c_int, [_P, _P, C.c_int]),
     "heat2d_solver_download": (C.c_int, [_P, _P, _I64]),
     "heat2d_solver_compare": (C.c_int, [_P, _P, _I64, _I64, _I64, _P]),
+    "heat2d_solver_footprint": (C.c_int, [C.POINTER(Config), C.c_int, C.c_int, C.POINTER(_I64)]),
+    "heat2d_plan_max_grid": (C.c_int, [C.c_int, C.c_int, _I64, C.POINTER(_I64)]),
+    "heat2d_mem_info": (C.c_int, [C.c_int, C.POINTER(_I64), C.POINTER(_I64)]),
     "heat2d_solver_upload": (C.c_int, [_P, _P, _I64]),
     "heat2d_solver_layout": (C.c_int, [_P, _LP]),
     "heat2d_solver_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(_I64), C.POINTER(_I64),
