@@ -9,6 +9,7 @@
 // restart at all (its int.dat / soln*.dat dumps are never read back;
 // SURVEY.md §5).
 #include <algorithm>
+#include <cctype>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -163,24 +164,38 @@ NpyInfo npy_header(FILE* f, const std::string& path) {
 
 }  // namespace
 
-// A name no earlier save of this step used, sorting after all of them (and
-// before the next step): `base` for the first save, then base-000001,
-// base-000002, ... one past the highest generation present — never a gap a
-// pruned generation left, so name order stays write order for pruning.
+// (step, generation) of a step directory name "step-<12 digits>[-<digits>]"
+// (generation 0: the bare name; any all-digit suffix counts, the legacy -N
+// too); false for anything else. Pruning orders saves by this key, not by
+// name: a legacy step-X-7 and a new step-X-000008 compare by their numbers.
+static bool step_key(const std::string& n, long long* step, long long* gen) {
+  if (n.compare(0, 5, "step-") != 0 || n.size() < 5 + 12) return false;
+  for (size_t i = 5; i < 17; ++i)
+    if (!std::isdigit((unsigned char)n[i])) return false;
+  *step = std::atoll(n.c_str() + 5);
+  *gen = 0;
+  if (n.size() == 17) return true;
+  if (n[17] != '-' || n.size() == 18) return false;
+  for (size_t i = 18; i < n.size(); ++i)
+    if (!std::isdigit((unsigned char)n[i])) return false;
+  *gen = std::atoll(n.c_str() + 18);
+  return true;
+}
+
+// A name no earlier save of this step used, ordered after all of them (and
+// before the next step) by step_key: `base` for the first save, then
+// base-000001, base-000002, ... one past the highest generation present
+// (legacy -N suffixes included) — never a gap a pruned generation left.
 std::string step_dir_name(const std::string& dir, int64_t step) {
   const std::string base = step_name(step);
   bool any = false;
   long long gmax = 0;
   if (DIR* d = ::opendir(dir.c_str())) {
     while (dirent* e = ::readdir(d)) {
-      const std::string n = e->d_name;
-      if (n.compare(0, base.size(), base) != 0) continue;
-      if (n.size() == base.size()) {
-        any = true;
-      } else if (n.size() == base.size() + 7 && n[base.size()] == '-') {
-        any = true;
-        gmax = std::max(gmax, std::atoll(n.c_str() + base.size() + 1));
-      }
+      long long st = 0, g = 0;
+      if (!step_key(e->d_name, &st, &g) || st != (long long)step) continue;
+      any = true;
+      gmax = std::max(gmax, g);
     }
     ::closedir(d);
   }
@@ -213,14 +228,20 @@ void write_meta(const std::string& dir, const std::string& name, const Meta& m) 
                 (long long)m.n_input, m.convention.c_str(), m.sigma, m.nu, m.dom_len, m.r);
   write_atomic(join(join(dir, name), "meta.json"), buf);  // + fsync of the step directory (rank files' entries)
   write_atomic(join(dir, "latest"), name + "\n");  // the commit point
-  // prune: keep the two newest complete steps (names sort by step)
+  // prune: keep the two newest complete saves, ordered by (step, generation)
   std::vector<std::string> steps;
   if (DIR* d = ::opendir(dir.c_str())) {
+    long long st = 0, g = 0;
     while (dirent* e = ::readdir(d))
-      if (std::strncmp(e->d_name, "step-", 5) == 0) steps.push_back(e->d_name);
+      if (step_key(e->d_name, &st, &g)) steps.push_back(e->d_name);
     ::closedir(d);
   }
-  std::sort(steps.begin(), steps.end());
+  std::sort(steps.begin(), steps.end(), [](const std::string& a, const std::string& b) {
+    long long sa = 0, ga = 0, sb = 0, gb = 0;
+    step_key(a, &sa, &ga);
+    step_key(b, &sb, &gb);
+    return sa != sb ? sa < sb : ga < gb;
+  });
   const auto cur = std::find(steps.begin(), steps.end(), name);
   for (auto it = steps.begin(); cur != steps.end() && it + 1 < cur; ++it) {
     const std::string sd = join(dir, *it);

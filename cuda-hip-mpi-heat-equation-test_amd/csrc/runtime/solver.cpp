@@ -344,7 +344,10 @@ void Solver::cycle_launch(int k, int x) {
   HEAT2D_REQUIRE(!tr_->exchanges() || ghost_ >= k,
                  "cycle of depth " + std::to_string(k) + " on " + std::to_string(ghost_) +
                      " valid ghost rows (rank " + std::to_string(tr_->rank()) + "): topup() first");
-  if (stats_next_ && hip_ && !jit_) launch_stats_cycle(k);
+  if (stats_next_ && hip_ && !jit_) {
+    first_cycle_ = false;
+    launch_stats_cycle(k);
+  }
   // Boundary bands: the rows the exchange sends (x) must be written by the
   // band launch, and MAIN must not touch rows a receiver-driven transport
   // (loopback, peer, IPC pulls) may still be reading: the previous exchange
@@ -824,8 +827,13 @@ void Solver::autotune_split(int k) {
         c = kern::with_edge_bands(dtype(), c, q.edge[0].nb, cfg_.arith);
       const float t = time_plan(c, 2);
       ++tune_trials_;
-      finish(c, t);
-      return;
+      // kept only if it beats this depth's default plan on the same score
+      // (trial + the exchange its order cannot hide); else the screening runs
+      if (t + exchange_penalty(c, t) <= base_ms + exchange_penalty(best, base_ms)) {
+        finish(c, t);
+        return;
+      }
+      break;
     }
   }
   const int64_t nb0 = best.main.nb;
@@ -1037,6 +1045,7 @@ void Solver::cycle_copy_swap() {
 
 void Solver::run_graph_cycles(int64_t npairs) {
   ensure_pair_graph();
+  first_cycle_ = false;  // the replay is this call's first cycle: any eager cycle after it is not
   const int K = k_pref_;
   const bool ovl = cfg_.overlap != 0;
   if (ovl) {  // the graph starts only when the eager work on both streams is done
@@ -1078,6 +1087,7 @@ void Solver::ensure_pair_graph() {
     ghost_ = (int)band_;  // replays start after step()'s top-up
     const int saved_lx0 = last_x_[0], saved_lx1 = last_x_[1];
     if (tr_->exchanges()) last_x_[0] = last_x_[1] = (int)band_;  // whatever a replay follows
+    first_cycle_ = false;  // captured cycles keep their plans' order, whatever ran before
     if (!ovl) {
       H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
       for (int c = 0; c < 2; ++c) {
@@ -1657,6 +1667,7 @@ void Solver::capture_schedule(int64_t n) {
   if (tr_->exchanges()) last_x_[0] = last_x_[1] = (int)band_;  // whatever a replay follows
   int64_t saved_hist[kMaxTB + 1];
   std::copy(hist_, hist_ + kMaxTB + 1, saved_hist);
+  first_cycle_ = false;  // captured cycles keep their plans' order, whatever ran before
   hipEvent_t fork = nullptr, join = nullptr;
   H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
   H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
@@ -1702,6 +1713,7 @@ void Solver::capture_schedule(int64_t n) {
 }
 
 void Solver::run_schedule_graph(int64_t n) {
+  first_cycle_ = false;
   auto it = sched_graph_.find({n, cur_});
   if (it == sched_graph_.end()) {
     capture_schedule(n);

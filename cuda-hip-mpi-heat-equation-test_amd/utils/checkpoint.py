@@ -37,23 +37,35 @@ def step_dir(directory: str, step: int) -> str:
     return os.path.join(directory, f"step-{int(step):012d}")
 
 
+def step_key(name: str):
+    """(step, generation) of a step directory name "step-<12 digits>[-<digits>]"
+    (generation 0: the bare name; any all-digit suffix, the legacy -N too), or
+    None. Saves are ordered by this key, not by name (csrc twin: checkpoint.cpp
+    step_key)."""
+    if not name.startswith("step-") or len(name) < 17 or not name[5:17].isdigit():
+        return None
+    if len(name) == 17:
+        return int(name[5:17]), 0
+    if name[17] != "-" or not name[18:].isdigit():
+        return None
+    return int(name[5:17]), int(name[18:])
+
+
 def fresh_step_dir(directory: str, step: int) -> str:
-    """A step directory name no earlier save used, sorting after all of them
-    (and before the next step): the bare name first, then -000001, -000002,
-    ... one past the highest generation present (a pruned generation's name
-    is never reused, so name order stays write order; csrc twin:
+    """A step directory name no earlier save used, ordered after all of them
+    (and before the next step) by step_key: the bare name first, then -000001,
+    -000002, ... one past the highest generation present, legacy -N suffixes
+    included (a pruned generation's number is never reused; csrc twin:
     checkpoint.cpp step_dir_name)."""
     base = step_dir(directory, step)
-    name = os.path.basename(base)
     try:
         entries = os.listdir(directory)
     except FileNotFoundError:
         entries = []
-    gens = [int(e[len(name) + 1:]) for e in entries
-            if e.startswith(name + "-") and len(e) == len(name) + 7 and e[len(name) + 1:].isdigit()]
-    if name not in entries and not gens:
+    keys = [k for k in map(step_key, entries) if k is not None and k[0] == int(step)]
+    if not keys:
         return base
-    return f"{base}-{max(gens, default=0) + 1:06d}"
+    return f"{base}-{max(g for _, g in keys) + 1:06d}"
 
 
 def _fsync_dir(path: str) -> None:
@@ -103,7 +115,7 @@ def save(solver, directory: str, step: Optional[int] = None, extra: Optional[dic
         meta.update(extra or {})
         _write_atomic(os.path.join(sd, "meta.json"), json.dumps(meta, indent=1))
         _write_atomic(os.path.join(directory, "latest"), os.path.basename(sd) + "\n")  # the commit point
-        steps = sorted(d for d in os.listdir(directory) if d.startswith("step-") and not d.endswith(".tmp"))
+        steps = sorted((d for d in os.listdir(directory) if step_key(d) is not None), key=step_key)
         for d in steps[:max(0, steps.index(os.path.basename(sd)) - 1)]:  # keep the two newest
             shutil.rmtree(os.path.join(directory, d), ignore_errors=True)
     _barrier(solver)

@@ -298,3 +298,39 @@ def test_torchrun_peer_transport_share_gpu_checkpoint(native, gpu, tmp_path):
     T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
     prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
     assert np.array_equal(T, R.owned(R.ftcs(prob)))
+
+
+@pytest.mark.parametrize("writer", ["python", "native"])
+def test_checkpoint_legacy_generation_names(native, tmp_path, writer):
+    """Saves are ordered by (step, generation) parsed from the names, legacy
+    unpadded -N generations included: a new save of step 9 after a legacy
+    step-...9-7 becomes -000008 (never a lexically-earlier name), and pruning
+    keeps the two newest by that order."""
+    from heat2d.models.heat2d import HeatSolver
+    from heat2d.utils import checkpoint
+    (tmp_path / "input.dat").write_text("44 0.25 0.05 1.0 9 1\n")
+    ck = tmp_path / "ck"
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+
+    def save():
+        if writer == "native":
+            subprocess.run([N.CLI_PATH, "--cpu", "--quiet", "--tb", "3", "--checkpoint", "ck", "--output", "none"],
+                           cwd=tmp_path, check=True, capture_output=True)
+        else:
+            s = HeatSolver(prob, dtype="fp64", backend="cpu", tb=3)
+            s.step(9)
+            checkpoint.save(s, str(ck))
+            s.close()
+
+    save()
+    save()  # step-...9 and step-...9-000001
+    os.rename(ck / "step-000000000009-000001", ck / "step-000000000009-7")  # a legacy generation name
+    (ck / "latest").write_text("step-000000000009-7\n")
+    assert checkpoint.fresh_step_dir(str(ck), 9).endswith("step-000000000009-000008")
+    save()
+    names = sorted((d.name for d in ck.iterdir() if d.name.startswith("step-")), key=checkpoint.step_key)
+    assert names == ["step-000000000009-7", "step-000000000009-000008"]
+    assert (ck / "latest").read_text().strip() == "step-000000000009-000008"
+    s = HeatSolver(prob, dtype="fp64", backend="cpu", tb=3)
+    checkpoint.load(s, str(ck))
+    assert np.array_equal(s.download(), R.owned(R.ftcs(prob)))
