@@ -179,6 +179,12 @@ def main():
                          "kernel in the reference arithmetic from the same IC (JSON 'timed_field_check'); auto: the "
                          "whole slab when a second copy fits, else row windows at the slab boundaries and middle")
     ap.add_argument("--window-rows", type=int, default=64, help="rows per checked window (--field-check windows)")
+    ap.add_argument("--measure-hbm", action="store_true",
+                    help="1 rank: after the run, re-run the timed region twice under rocprofv3 --pmc (FETCH_SIZE, "
+                         "then WRITE_SIZE; child processes, the same plans and schedule through the plan cache) and "
+                         "report the DRAM bytes of its stencil dispatches over this run's timed seconds "
+                         "(JSON 'hbm_gb_per_s_measured')")
+    ap.add_argument("--hbm-child", default="", help=argparse.SUPPRESS)
     ap.add_argument("--rehearse-comm", action="store_true",
                     help="1 GPU only: run the multi-GPU schedule (bands + RCCL self-exchange beside a CU-masked "
                          "interior) to measure its per-rank cost; not the headline (periodic halo)")
@@ -191,6 +197,11 @@ def main():
         ap.error("--share-gpu needs --transport ipc or auto (RCCL refuses two ranks on one GPU)")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_launch_ranks(args.gpus, args.backend, args.share_gpu))
+    if args.measure_hbm and os.environ.get("HEAT2D_PLAN_CACHE", "") in ("", "off") and not args.hbm_child:
+        # the profiled re-runs take this run's plans from a cache file (their
+        # own trials would be timed under counter collection)
+        import tempfile
+        os.environ["HEAT2D_PLAN_CACHE"] = os.path.join(tempfile.mkdtemp(prefix="heat2d_hbm_"), "plans.txt")
     out_fd = _claim_stdout()
 
     import torch
@@ -382,6 +393,68 @@ def main():
         kind = ("torch-dist" if world > 1 else
                 (("ipc-loop" if args.transport == "ipc" else "rccl-loop") if (args.rehearse_comm and hip) else "self"))
         setup(kind)
+    def hbm_marker():
+        """A 16-byte read kernel: brackets the timed region's dispatches in the profile."""
+        buf = torch.zeros(64, dtype=torch.uint8, device=f"cuda:{device}")
+        sink = torch.zeros(16, dtype=torch.uint8, device=f"cuda:{device}")
+        torch.cuda.synchronize()
+        N.call("heat2d_read", buf.data_ptr(), 16, sink.data_ptr(), None, 1)
+        torch.cuda.synchronize()
+
+    def measure_hbm(elapsed):
+        """DRAM bytes of the timed region: two child processes re-run this
+        bench (same flags, this run's plans and schedule from the plan cache,
+        HEAT2D_PLAN_CACHE_TRUST: no re-timing under the profiler) under
+        rocprofv3 --pmc, one counter set each (FETCH_SIZE needs 3 of the 4
+        TCC counters, WRITE_SIZE 2), the program right after `--`. The
+        stencil dispatches between the child's two marker dispatches are its
+        timed region; FETCH_SIZE is doubled (gfx950 counts wide streaming
+        reads at half: MI355X_MICROARCH.md §HBM, profiles/r4/c/). The rate is
+        over THIS run's timed seconds."""
+        import csv
+        import glob
+        import shutil
+        import subprocess
+        import tempfile
+        rocprof = shutil.which("rocprofv3")
+        if not rocprof:
+            return {"error": "rocprofv3 not found"}
+        argv = [a for a in sys.argv[1:] if a != "--measure-hbm"]
+        out = {"method": "rocprofv3 --pmc FETCH_SIZE (x2) / WRITE_SIZE over the stencil dispatches of two "
+                         "profiled re-runs of the timed region (same plans); rate over this run's timed seconds"}
+        tot = {}
+        work = tempfile.mkdtemp(prefix="heat2d_hbm_prof_")
+        env = dict(os.environ, HEAT2D_PLAN_CACHE=N.plan_cache_path(), HEAT2D_PLAN_CACHE_TRUST="1")
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(work, ctr)
+            info = os.path.join(work, ctr + ".json")
+            cmd = ["timeout", "-s", "KILL", "300", rocprof, "--pmc", ctr, "--output-format", "csv", "-d", d, "--",
+                   sys.executable, os.path.abspath(__file__), *argv, "--hbm-child", info, "--verify", "off",
+                   "--field-check", "off"]
+            p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=work)
+            if p.returncode != 0 or not os.path.exists(info):
+                return dict(out, error=f"{ctr} pass failed (rc {p.returncode}): {p.stderr[-400:]}")
+            rows_ = []
+            for fcsv in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                rows_ += list(csv.DictReader(open(fcsv)))
+            marks = sorted(int(r["Dispatch_Id"]) for r in rows_ if "read16_kernel" in r["Kernel_Name"])
+            if len(marks) < 2:
+                return dict(out, error=f"{ctr}: timed-region markers not found in the profile")
+            lo, hi = marks[-2], marks[-1]
+            sel = [r for r in rows_ if lo < int(r["Dispatch_Id"]) < hi and "tb_kernel" in r["Kernel_Name"]
+                   and r["Counter_Name"] == ctr]
+            tot[ctr] = sum(float(r["Counter_Value"]) for r in sel) * 1024.0  # KiB
+            out[ctr.lower() + "_dispatches"] = len({r["Dispatch_Id"] for r in sel})
+            out["child_cycles"] = json.load(open(info))["cycles"]
+        shutil.rmtree(work, ignore_errors=True)
+        rd, wr = 2.0 * tot["FETCH_SIZE"], tot["WRITE_SIZE"]
+        es = 8 if args.dtype == "fp64" else 4
+        field = float(s.nrows) * s.ncols * es
+        out.update({"read_bytes": rd, "write_bytes": wr, "read_over_field_per_cycle":
+                    round(rd / field / max(1, sum(out["child_cycles"].values())), 4),
+                    "gb_per_s": round((rd + wr) / elapsed / 1e9, 1)})
+        return out
+
     def timed_field_check(s, kind):
         """The timed field itself (IC + warmup + steps, the state the timed run
         left), checked against an independent engine started from the same IC:
@@ -445,6 +518,17 @@ def main():
     s.halo_rows_exchanged(reset=True)
     if args.phase_timers:
         s.set_timing(True)
+    if args.hbm_child:
+        # --measure-hbm's profiled re-run: the timed region between two marker
+        # dispatches (read16_kernel), nothing after it
+        hbm_marker()
+        elapsed = timed(s)
+        hbm_marker()
+        with open(args.hbm_child, "w") as f:
+            json.dump({"elapsed": elapsed, "cycles": {str(k): c for k, c in s.cycle_hist().items()}}, f)
+        s.close()
+        tr.close()
+        return
     elapsed = timed(s)
 
     pts = float(prob.n_owned) * float(rows or prob.n_owned)
@@ -484,6 +568,10 @@ def main():
     field_check = None
     if args.field_check != "off":
         field_check = timed_field_check(s, kind)
+    hbm = None
+    if args.measure_hbm:
+        hbm = (measure_hbm(elapsed) if hip and world == 1
+               else {"error": "--measure-hbm profiles single-rank GPU runs"})
     s.close()
     tr.close()
     live.clear()
@@ -539,6 +627,8 @@ def main():
                 "backend": args.backend,
             },
             "hbm_gb_per_s_plan": round(traffic / elapsed / 1e9, 1),
+            "hbm_gb_per_s_measured": (hbm or {}).get("gb_per_s"),
+            "hbm_measured": hbm,
             # halo bytes moved by all ranks in the timed region, and per cycle (whole node)
             "halo_bytes": halo_bytes,
             "halo_bytes_per_cycle": round(halo_bytes / max(1, sum(hist.values())), 1),

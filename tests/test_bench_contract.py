@@ -160,7 +160,12 @@ def test_bench_auto_transport_falls_back_to_ipc_share_gpu():
     assert four["config"]["transport"] == "ipc" and ch["chosen"] == "ipc" and ch["requested"] == "auto", ch
     assert "error" in ch["rccl"] and ch["ipc"]["ms"] > 0, ch
     assert four["verified"] is True and four["verify"]["max_abs_diff"] == 0.0, four["verify"]
+    # the timed field itself: 4 rank slabs vs the one-step JIT engine on the same layout and transport
+    fc = four["timed_field_check"]
+    assert fc["ok"] is True and fc["mode"] == "full" and fc["engine"] == "jit-exact", fc
+    assert fc["mismatches"] == 0 and fc["max_abs_diff"] == 0.0 and fc["rows_checked"] == 8192 and fc["steps"] == 25
     one = run_plain("--gpus", "1", *common)
+    assert one["timed_field_check"]["ok"] is True and one["timed_field_check"]["mismatches"] == 0
     assert one["verified"] is True and one["config"]["transport_choice"] is None
     a, b = one["field_stats"], four["field_stats"]
     assert a["min"] == b["min"] and a["max"] == b["max"]
@@ -261,3 +266,36 @@ def test_bench_timed_field_check_sigma_fast_cpu():
                     "--arith", "fma")
     assert fma["timed_field_check"]["ok"] is True and fma["timed_field_check"]["mismatches"] == 0
     assert fma["verified"] is True and "bound" in fma["verify"], fma["verify"]
+
+
+@pytest.mark.gpu
+def test_bench_timed_field_check_windows_gpu():
+    """The full-HBM grids' check (row windows at the slab boundaries and middle,
+    single-rank JIT reference runs) on a 4-rank shared-GPU run, and the fast
+    arithmetic within its bound."""
+    d = run_plain("--gpus", "4", "--share-gpu", "--grid", "4099", "--steps", "23", "--warmup", "3",
+                  "--field-check", "windows", "--verify", "off")
+    fc = d["timed_field_check"]
+    assert fc["mode"] == "windows" and fc["ok"] is True and fc["mismatches"] == 0, fc
+    assert fc["rows_checked"] == 4 * 3 * 64
+    f = run_plain("--grid", "4096", "--steps", "20", "--warmup", "3", "--sigma", "0.2", "--arith", "fast",
+                  "--verify", "off")
+    fc = f["timed_field_check"]
+    assert fc["ok"] is True and fc["max_abs_diff"] <= fc["bound"] and fc["mode"] == "full", fc
+
+
+@pytest.mark.gpu
+def test_bench_measure_hbm():
+    """--measure-hbm: the timed region's stencil dispatches re-run under
+    rocprofv3 --pmc (two child processes, the same plans): DRAM bytes close to
+    one read + one write of the field per pass, reported beside the plan model."""
+    d = run_plain("--grid", "8192", "--steps", "20", "--warmup", "5", "--measure-hbm", "--verify", "off",
+                  "--field-check", "off", timeout=900)
+    h = d["hbm_measured"]
+    assert "error" not in h, h
+    assert h["child_cycles"] == d["config"]["cycles"]
+    assert 0.9 < h["read_over_field_per_cycle"] < 2.0, h
+    field = 8192 * 8192 * 8
+    passes = sum(d["config"]["cycles"].values())
+    assert 0.95 * field * passes < h["write_bytes"] < 1.2 * field * passes, h
+    assert d["hbm_gb_per_s_measured"] == h["gb_per_s"] > 0
