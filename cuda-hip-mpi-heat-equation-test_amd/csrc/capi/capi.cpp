@@ -447,23 +447,25 @@ int heat2d_watchdog_selftest(double timeout_s, int mode, int progress_polls, dou
   });
 }
 
-int heat2d_cycle_schedule(int64_t n, int kmax, const double* t_ms, int32_t* out, int64_t cap, int64_t* len) {
+int heat2d_dp_schedule(int64_t n, int kmax, const double* t_ms, int32_t* out, int64_t cap, int64_t* len,
+                       double* total) {
   return guarded([&] {
-    const std::vector<int> v = cycle_schedule(n, kmax, [&](int k) { return k >= 1 && k <= kmax ? t_ms[k] : -1.0; });
+    const std::vector<int> v = dp_schedule(n, kmax, [&](int k) { return k >= 1 && k <= kmax ? t_ms[k] : -1.0; }, total);
     *len = (int64_t)v.size();
     for (int64_t i = 0; i < std::min<int64_t>(cap, *len); ++i) out[i] = v[(size_t)i];
   });
 }
 
-int heat2d_cycle_schedule_near(int64_t n, int kmax, const double* t_ms, double tol, int m, int32_t* out, int64_t cap,
-                               int64_t* lens, int32_t* count) {
+int heat2d_near_schedules(int64_t n, int kmax, const double* t_ms, double tol, int m, int32_t* out, int64_t cap,
+                          int64_t* lens, double* costs, int32_t* count) {
   return guarded([&] {
-    const auto v = cycle_schedule_near(n, kmax, [&](int k) { return k >= 1 && k <= kmax ? t_ms[k] : -1.0; }, tol, m);
+    const auto v = near_schedules(n, kmax, [&](int k) { return k >= 1 && k <= kmax ? t_ms[k] : -1.0; }, tol, m);
     *count = (int32_t)v.size();
     int64_t pos = 0;
     for (size_t i = 0; i < v.size(); ++i) {
-      lens[i] = (int64_t)v[i].size();
-      for (int d : v[i]) {
+      lens[i] = (int64_t)v[i].second.size();
+      costs[i] = v[i].first;
+      for (int d : v[i].second) {
         HEAT2D_REQUIRE(pos < cap, "schedule output buffer too small");
         out[pos++] = d;
       }
@@ -471,25 +473,19 @@ int heat2d_cycle_schedule_near(int64_t n, int kmax, const double* t_ms, double t
   });
 }
 
-int heat2d_cycle_schedule_shallower(int64_t n, int kmax, const double* t_ms, const int32_t* best, int64_t nbest,
-                                    double best_cost, int lo, int32_t* out, int64_t cap, int64_t* len) {
+int heat2d_search_schedule(int64_t n, int kmax, const double* pre_ms, const double* tuned_ms, int32_t* out,
+                           int64_t cap, int64_t* len, double* cost, int32_t* prescanned, int32_t* nprescanned,
+                           int32_t* tuned, int32_t* ntuned) {
   return guarded([&] {
-    const std::vector<int> v =
-        cycle_schedule_shallower(n, std::vector<int>(best, best + nbest), best_cost, lo,
-                                 [&](int k) { return k >= 1 && k <= kmax ? t_ms[k] : -1.0; });
-    *len = (int64_t)v.size();
-    for (int64_t i = 0; i < std::min<int64_t>(cap, *len); ++i) out[i] = v[(size_t)i];
-  });
-}
-
-int heat2d_cycle_schedule_deeper(int64_t n, int kmax, const double* t_ms, const int32_t* best, int64_t nbest,
-                                 double best_cost, int hi, int32_t* out, int64_t cap, int64_t* len) {
-  return guarded([&] {
-    const std::vector<int> v =
-        cycle_schedule_deeper(n, kmax, std::vector<int>(best, best + nbest), best_cost, hi,
-                              [&](int k) { return k >= 1 && k <= kmax ? t_ms[k] : -1.0; });
-    *len = (int64_t)v.size();
-    for (int64_t i = 0; i < std::min<int64_t>(cap, *len); ++i) out[i] = v[(size_t)i];
+    const ScheduleSearch r = search_schedule(
+        n, kmax, [&](int k) { return pre_ms[k]; }, [&](int k) { return tuned_ms[k]; });
+    *len = (int64_t)r.best.size();
+    for (int64_t i = 0; i < std::min<int64_t>(cap, *len); ++i) out[i] = r.best[(size_t)i];
+    *cost = r.cost;
+    *nprescanned = (int32_t)r.prescanned.size();
+    for (size_t i = 0; i < r.prescanned.size(); ++i) prescanned[i] = r.prescanned[i];
+    *ntuned = (int32_t)r.tuned.size();
+    for (size_t i = 0; i < r.tuned.size(); ++i) tuned[i] = r.tuned[i];
   });
 }
 

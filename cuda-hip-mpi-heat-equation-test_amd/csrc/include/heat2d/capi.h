@@ -213,16 +213,18 @@ int heat2d_solver_plan_origin(void* s, int k, int32_t* out);
 // Autotune / measured-schedule eligibility of a decomposition (the same on every rank).
 int heat2d_autotune_slabs(int64_t n_rows, int64_t n_cols, int nranks, int autotune, int32_t* out);
 /* the schedule search itself on given cycle times t_ms[k] (k = 1..kmax; t_ms[0] unused): depths in out */
-int heat2d_cycle_schedule(int64_t n, int kmax, const double* t_ms, int32_t* out, int64_t cap, int64_t* len);
-// cycle_schedule_near: up to m schedules within tol of the best estimate, concatenated in out, lengths in lens
-int heat2d_cycle_schedule_near(int64_t n, int kmax, const double* t_ms, double tol, int m, int32_t* out, int64_t cap,
-                               int64_t* lens, int32_t* count);
-// cycle_schedule_shallower (runtime.hpp): `best` (nbest depths, cost best_cost) tried against shallower base depths
-int heat2d_cycle_schedule_shallower(int64_t n, int kmax, const double* t_ms, const int32_t* best, int64_t nbest,
-                                    double best_cost, int lo, int32_t* out, int64_t cap, int64_t* len);
-// cycle_schedule_deeper (runtime.hpp): the same walk toward deeper base depths (above hi, up to kmax)
-int heat2d_cycle_schedule_deeper(int64_t n, int kmax, const double* t_ms, const int32_t* best, int64_t nbest,
-                                 double best_cost, int hi, int32_t* out, int64_t cap, int64_t* len);
+// schedule search (runtime.hpp, schedule.cpp), on per-depth cost arrays t_ms[0..kmax] (< 0: unusable):
+// dp_schedule: the exact least-cost schedule of n steps (*total its cost)
+int heat2d_dp_schedule(int64_t n, int kmax, const double* t_ms, int32_t* out, int64_t cap, int64_t* len,
+                       double* total);
+// near_schedules: balanced candidates within tol of the best, concatenated in out, lengths / costs per candidate
+int heat2d_near_schedules(int64_t n, int kmax, const double* t_ms, double tol, int m, int32_t* out, int64_t cap,
+                          int64_t* lens, double* costs, int32_t* count);
+// search_schedule with prescan(k) = pre_ms[k] and tune(k) = tuned_ms[k] (arrays of kmax + 1): the
+// chosen schedule, its cost and the depths prescanned / tuned, in order (each array >= kmax entries)
+int heat2d_search_schedule(int64_t n, int kmax, const double* pre_ms, const double* tuned_ms, int32_t* out,
+                           int64_t cap, int64_t* len, double* cost, int32_t* prescanned, int32_t* nprescanned,
+                           int32_t* tuned, int32_t* ntuned);
 
 /* I/O (io.cpp). */
 int heat2d_write_xyz(const char* path, int dtype, const void* host, int64_t nrows, int64_t ncols,

@@ -207,28 +207,37 @@ int num_threads();
 
 // ---------------------------------------------------------------- solver
 
-// Cycle schedule of n steps from per-depth cycle times t(k), k <= kmax (the
-// search of Solver::prepare, exposed for tests): balanced depths for the
-// cycle count c with the smallest sum of t over its cycles, c scanned upward
-// from ceil(n / kmax) until the base depth's per-step time is 25 % above the
-// best seen. Empty if t(k) < 0 for a depth it needs.
-std::vector<int> cycle_schedule(int64_t n, int kmax, const std::function<double(int)>& t);
-// The same scan's cycle counts whose estimated cost is within `tol` (relative)
-// of the best, best first, at most m of them and one per base depth, as schedules.
-std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std::function<double(int)>& t,
-                                                  double tol, int m);
-// Schedule `best` (cost best_cost; lo = the shallowest base depth already
-// costed) improved by trying the next shallower base depths on t, one base at
-// a time until two in a row do not beat the best; only while that base needs
-// >= min_cycles cycles
-// (prepare's prescan can miss a depth whose tuned plan is far better than its
-// default plan: solver.cpp, choose_schedule).
-std::vector<int> cycle_schedule_shallower(int64_t n, std::vector<int> best, double best_cost, int lo,
-                                          const std::function<double(int)>& t, int64_t min_cycles = 8);
-// The same walk toward deeper base depths (above hi, the deepest base already
-// costed; depths <= kmax), while the base still needs >= min_cycles cycles.
-std::vector<int> cycle_schedule_deeper(int64_t n, int kmax, std::vector<int> best, double best_cost, int hi,
-                                       const std::function<double(int)>& t, int64_t min_cycles = 8);
+// Cycle schedules (runtime/schedule.cpp): how n steps are cut into HBM passes
+// of depth <= kmax from per-depth cycle costs (ms; < 0: unusable depth).
+// The exact schedule minimising the summed cost (unbounded-knapsack DP;
+// ties: fewer cycles, deeper first), deepest cycles first; empty if n cannot be
+// reached. *total = its cost (or -1).
+std::vector<int> dp_schedule(int64_t n, int kmax, const std::function<double(int)>& cost, double* total = nullptr);
+// Balanced candidates (depths b and b + 1), one per base depth b, whose cost is
+// within tol (relative) of the best of them, best first, at most m: (cost, schedule).
+std::vector<std::pair<double, std::vector<int>>> near_schedules(int64_t n, int kmax, const std::function<double(int)>& cost,
+                                                                 double tol, int m);
+struct ScheduleSearchOptions {
+  double stop_ratio = 1.25;    // prescan stops once the per-step cost is this much worse than the best
+  double prescan_tol = 0.20;   // depths of the prescan schedules within this of the best are tuned ...
+  int prescan_bases = 4;       // ... at most this many base depths
+  int64_t walk_min_cycles = 8;  // runs of at least this many cycles walk beyond the tuned depths
+  int walk_patience = 2;       // a walk ends after this many tunings in a row that did not lower the cost
+  double near_tol = 0.03;      // near ties returned for timing
+  int near_max = 3;
+};
+struct ScheduleSearch {
+  std::vector<int> best;   // the chosen schedule (deepest cycles first), empty if none
+  double cost = -1.0;      // its summed tuned cost (ms)
+  std::vector<std::pair<double, std::vector<int>>> near;  // best first, then tuned near ties
+  std::vector<int> prescanned, tuned;                     // depths measured, in order
+};
+// The measured-schedule search of Solver::prepare (stages in schedule.cpp):
+// prescan(k) = default-plan cycle time, tune(k) = autotuned cycle time, each
+// called at most once per depth, in a deterministic order given their values
+// (the solver passes max-over-ranks measurements: every rank searches alike).
+ScheduleSearch search_schedule(int64_t n, int kmax, const std::function<double(int)>& prescan,
+                               const std::function<double(int)>& tune, const ScheduleSearchOptions& o = {});
 // Whether slabs of this decomposition get autotuned split plans and measured
 // cycle schedules (SolverConfig::autotune, -1 = auto). A function of the
 // GLOBAL problem only — the smallest slab (n_rows / P rows) decides — so every
@@ -420,8 +429,6 @@ class Solver {
   void capture_schedule(int64_t n);
   float time_trial_schedule(const std::vector<int>& sc, int reps = 1);  // ms: the fastest of reps graph replays of sc
   float time_trial_eager(const std::vector<int>& sc, int reps);  // ms: the fastest of reps eager launches of sc
-  // the last choose_schedule's costed candidates: (tuned cost ms, schedule)
-  std::vector<std::pair<double, std::vector<int>>> sched_cands_;
   void prepare_plans(int64_t n);  // prepare()'s planning / autotune / measured schedule (HIP split engine)
   float time_plan(const kern::SplitPlan& c, int kTimed);  // steady-state ms per trial cycle
   std::string cache_ctx() const;   // plan-cache key of this slab (plan_cache.hpp)
@@ -431,7 +438,7 @@ class Solver {
   void run_schedule_graph(int64_t n);
   float depth_ms(int k);
   float prescan_ms(int k);  // default-plan cycle time of depth k, max over ranks (schedule prescan)
-  std::vector<int> choose_schedule(int64_t n);
+  ScheduleSearch choose_schedule(int64_t n);
 
   SolverConfig cfg_;
   std::shared_ptr<Transport> tr_;

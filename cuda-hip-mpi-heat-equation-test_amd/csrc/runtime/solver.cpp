@@ -681,7 +681,7 @@ static uint64_t plan_env_hash() {
     for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_TUNE_SEGMENTS", "HEAT2D_W_ROW", "HEAT2D_W_COL",
                              "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
                              "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
-                             "HEAT2D_TUNE_STAGED", "HEAT2D_SCHED_PRESCAN", "HEAT2D_EDGE_BANDS",
+                             "HEAT2D_TUNE_STAGED", "HEAT2D_EDGE_BANDS",
                              "HEAT2D_EDGE_MAIN", "HEAT2D_GRAPH_MAX_CYCLE_US"}) {
       const char* e = std::getenv(name);
       const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
@@ -1326,27 +1326,6 @@ float Solver::depth_ms(int k) {
   return depth_ms_[k];
 }
 
-// Cycle schedule of n steps from measured cycle times. The cycle time t(k) is
-// flat while a pass is HBM-bound and grows ~linearly once it is VALU-bound
-// (profiles/depth_schedule.md), i.e. convex, so for c cycles the balanced
-// depths (n/c, rounded) are the best split; scan c upward from ceil(n/Kmax)
-// and stop once the base depth's per-step cost is 25 % worse than the best
-// seen (deeper into the HBM-bound region it only gets worse).
-// Prescan (HEAT2D_SCHED_PRESCAN=0 disables): the scan above needs the cycle
-// time of every depth it visits — ~15 depths for 480 steps, each autotuned
-// (~30 trial cycles of ~100 candidates: 44 s at 32768^2 fp64 in round 3).
-// Instead the scan runs on each depth's DEFAULT plan (1 warm-up + 2 timed
-// cycles, max over ranks), keeps the schedules within 20 % of its best (up to
-// 4, one per base depth), and only their depths are autotuned; the schedule
-// with the smallest autotuned cost wins.
-static bool sched_prescan() {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_SCHED_PRESCAN");
-    return !e || std::atoi(e) != 0;
-  }();
-  return on;
-}
-
 float Solver::prescan_ms(int k) {
   if (pre_ms_[k] == 0.f) {
     double v = 0.0;
@@ -1364,192 +1343,32 @@ float Solver::prescan_ms(int k) {
     }
     tr_->allreduce(&v, 1, 1);
     pre_ms_[k] = v > 0 ? (float)v : -1.f;
+    if (tune_log()) std::fprintf(stderr, "heat2d sched prescan k=%d ms %.4f\n", k, pre_ms_[k]);
   }
   return pre_ms_[k];
 }
 
-std::vector<int> Solver::choose_schedule(int64_t n) {
-  sched_cands_.clear();
-  if (!sched_prescan()) return cycle_schedule(n, cfg_.tb, [this](int k) { return (double)depth_ms(k); });
-  const auto near = cycle_schedule_near(n, cfg_.tb, [this](int k) { return (double)prescan_ms(k); }, 0.20, 4);
-  if (tune_log())
-    for (int k = 1; k <= cfg_.tb; ++k)
-      if (pre_ms_[k] != 0.f) std::fprintf(stderr, "heat2d sched n=%lld prescan k=%d ms %.4f\n", (long long)n, k, pre_ms_[k]);
-  std::vector<int> best;
-  double best_cost = 1e300;
-  for (const auto& sc : near) {  // the same order and depths on every rank: depth_ms is collective
-    double cost = 0.0;
-    for (int k : sc) {
-      const double t = depth_ms(k);
-      if (t < 0) {
-        cost = -1.0;
-        break;
-      }
-      cost += t;
-    }
-    if (tune_log())
-      std::fprintf(stderr, "heat2d sched n=%lld candidate %zu cycles of %d..%d: tuned cost %.4f ms\n", (long long)n,
-                   sc.size(), sc.back(), sc.front(), cost);
-    if (cost >= 0.0) sched_cands_.emplace_back(cost, sc);
-    if (cost >= 0.0 && cost < best_cost) {
-      best_cost = cost;
-      best = sc;
-    }
+// The measured schedule of n steps (schedule.cpp search_schedule): the default
+// plans of the deep depths prescanned (1 warm-up + 2 trial cycles each), the
+// near-best ones autotuned, the exact DP over the tuned cycle times, walks past
+// the tuned range on long runs. Both measurements are max-over-ranks all-reduces
+// issued in the same order on every rank (the search is a function of their
+// values), so the ranks agree without exchanging the schedule.
+ScheduleSearch Solver::choose_schedule(int64_t n) {
+  ScheduleSearchOptions o;
+  o.near_tol = 0.05;  // prepare_plans keeps 5 % (tiny graph runs) or 3 % of them
+  o.near_max = 4;
+  ScheduleSearch r = search_schedule(
+      n, cfg_.tb, [this](int k) { return (double)prescan_ms(k); }, [this](int k) { return (double)depth_ms(k); }, o);
+  if (tune_log()) {
+    std::fprintf(stderr, "heat2d sched n=%lld: %zu cycles of %d..%d, tuned cost %.4f ms (prescanned %zu, tuned %zu)\n",
+                 (long long)n, r.best.size(), r.best.empty() ? 0 : r.best.back(), r.best.empty() ? 0 : r.best.front(),
+                 r.cost, r.prescanned.size(), r.tuned.size());
+    for (const auto& c : r.near)
+      std::fprintf(stderr, "heat2d sched n=%lld near: %zu cycles of %d..%d, %.4f ms\n", (long long)n, c.second.size(),
+                   c.second.back(), c.second.front(), c.first);
   }
-  // The default plans the prescan times can miss a depth whose tuned plan is
-  // far better: 16384^2 fp64, 480 steps — default-plan cycles of depths 14..20
-  // all within 1.25..1.47 ms, so the 4 candidates were depths 17..20 (tuned
-  // cost 31.2-31.7 ms), while depth 16's tuned plan runs 0.94 ms (30 cycles:
-  // 28.2 ms; the fp64 general kernel holds 2 waves/SIMD up to K = 16, one from
-  // K = 17). Long runs (>= 8 cycles) therefore also try the next shallower base
-  // depths on tuned times, one at a time until two in a row do not beat the
-  // best (candidates 18..24 on one box: base 17 is no cheaper, 16 is).
-  int lo = 0, hi = 0;
-  for (const auto& sc : near) {
-    lo = lo == 0 ? sc.back() : std::min(lo, sc.back());
-    hi = std::max(hi, sc.back());
-  }
-  if (!best.empty()) {
-    const auto t = [this](int k) { return (double)depth_ms(k); };
-    std::vector<int> ext = cycle_schedule_shallower(n, best, best_cost, lo, t);
-    double ext_cost = 0.0;
-    for (int k : ext) ext_cost += t(k);
-    // ... and deeper when the best candidate is the deepest one (the same
-    // miss one way up: 32768^2 fp32 480 steps picked 25 cycles of 19/20 on one
-    // box, 11335 Gpts/s, vs 20 x 24 at 12503). Only then: each deeper fp64
-    // 32768^2 depth costs ~2.5 s of autotuning (prepare 9.4 -> 14.6 s for a
-    // walk that found nothing, profiles/r4/gn/).
-    if (!best.empty() && best.back() == hi) ext = cycle_schedule_deeper(n, cfg_.tb, ext, ext_cost, hi, t);
-    if (tune_log() && ext != best)
-      std::fprintf(stderr, "heat2d sched n=%lld walk: %zu cycles of %d..%d\n", (long long)n, ext.size(), ext.back(),
-                   ext.front());
-    if (ext != best) {
-      double c = 0.0;
-      for (int k : ext) c += t(k);
-      sched_cands_.emplace_back(c, ext);
-    }
-    best = std::move(ext);
-  }
-  return best;
-}
-
-std::vector<int> cycle_schedule(int64_t n, int kmax, const std::function<double(int)>& t) {
-  HEAT2D_REQUIRE(n >= 1 && kmax >= 1, "cycle_schedule needs n >= 1, kmax >= 1");
-  double best = 1e300, best_step = 1e300;
-  int64_t best_c = 0;
-  for (int64_t c = (n + kmax - 1) / kmax; c <= n; ++c) {
-    const int kb = (int)(n / c);
-    const int64_t rem = n % c;
-    const double tb = t(kb);
-    const double t1 = rem ? t(kb + 1) : 0.0;
-    if (tb < 0 || t1 < 0) return {};
-    const double cost = (double)(c - rem) * tb + (double)rem * t1;
-    if (cost < best) {
-      best = cost;
-      best_c = c;
-    }
-    best_step = std::min(best_step, tb / kb);
-    if (kb <= 1 || tb / kb > 1.25 * best_step) break;
-  }
-  std::vector<int> sched;
-  const int kb = (int)(n / best_c);
-  const int64_t rem = n % best_c;
-  for (int64_t i = 0; i < best_c; ++i) sched.push_back(i < rem ? kb + 1 : kb);
-  return sched;
-}
-
-std::vector<std::vector<int>> cycle_schedule_near(int64_t n, int kmax, const std::function<double(int)>& t,
-                                                  double tol, int m) {
-  HEAT2D_REQUIRE(n >= 1 && kmax >= 1, "cycle_schedule needs n >= 1, kmax >= 1");
-  std::vector<std::pair<double, int64_t>> cost;  // (estimated cost, cycle count)
-  double best_step = 1e300;
-  for (int64_t c = (n + kmax - 1) / kmax; c <= n; ++c) {
-    const int kb = (int)(n / c);
-    const int64_t rem = n % c;
-    const double tb = t(kb);
-    const double t1 = rem ? t(kb + 1) : 0.0;
-    if (tb < 0 || t1 < 0) return {};
-    cost.emplace_back((double)(c - rem) * tb + (double)rem * t1, c);
-    best_step = std::min(best_step, tb / kb);
-    if (kb <= 1 || tb / kb > 1.25 * best_step) break;
-  }
-  std::sort(cost.begin(), cost.end());
-  std::vector<std::vector<int>> out;
-  std::vector<int> bases;  // one candidate per base depth: neighbouring cycle counts are near-duplicates
-  for (const auto& e : cost) {
-    if ((int)out.size() >= m || e.first > cost.front().first * (1.0 + tol)) break;
-    const int base = (int)(n / e.second);
-    if (std::find(bases.begin(), bases.end(), base) != bases.end()) continue;
-    bases.push_back(base);
-    std::vector<int> sched;
-    const int kb = (int)(n / e.second);
-    const int64_t rem = n % e.second;
-    for (int64_t i = 0; i < e.second; ++i) sched.push_back(i < rem ? kb + 1 : kb);
-    out.push_back(std::move(sched));
-  }
-  return out;
-}
-
-std::vector<int> cycle_schedule_shallower(int64_t n, std::vector<int> best, double best_cost, int lo,
-                                          const std::function<double(int)>& t, int64_t min_cycles) {
-  int misses = 0;  // bases in a row that did not beat the best: the walk ends at 2
-  while (!best.empty() && lo > 1) {
-    const int64_t c0 = n / lo + 1;  // fewest cycles with a shallower base depth
-    if (c0 < min_cycles) break;
-    const int b = (int)(n / c0);
-    double bc = 1e300;
-    int64_t cb = 0;
-    for (int64_t c = c0; c <= n / b; ++c) {  // every cycle count with base b: depths b / b + 1
-      const int64_t rem = n % c;
-      const double tb = t(b), t1 = rem ? t(b + 1) : 0.0;
-      if (tb < 0 || t1 < 0) break;
-      const double cost = (double)(c - rem) * tb + (double)rem * t1;
-      if (cost < bc) {
-        bc = cost;
-        cb = c;
-      }
-    }
-    if (cb == 0) break;
-    lo = b;
-    if (bc >= best_cost) {
-      if (++misses >= 2) break;
-      continue;
-    }
-    misses = 0;
-    best_cost = bc;
-    best.clear();
-    for (int64_t i = 0; i < cb; ++i) best.push_back(i < n % cb ? b + 1 : b);
-  }
-  return best;
-}
-
-std::vector<int> cycle_schedule_deeper(int64_t n, int kmax, std::vector<int> best, double best_cost, int hi,
-                                       const std::function<double(int)>& t, int64_t min_cycles) {
-  while (!best.empty() && hi < kmax) {
-    const int64_t c1 = n / (hi + 1);  // most cycles with a deeper base depth
-    if (c1 < std::max<int64_t>(1, min_cycles)) break;
-    const int b = (int)(n / c1);
-    if (b > kmax) break;
-    double bc = 1e300;
-    int64_t cb = 0;
-    for (int64_t c = n / (b + 1) + 1; c <= c1; ++c) {  // every cycle count with base b: depths b / b + 1
-      const int64_t rem = n % c;
-      if (rem && b + 1 > kmax) continue;
-      const double tb = t(b), t1 = rem ? t(b + 1) : 0.0;
-      if (tb < 0 || t1 < 0) continue;
-      const double cost = (double)(c - rem) * tb + (double)rem * t1;
-      if (cost < bc) {
-        bc = cost;
-        cb = c;
-      }
-    }
-    if (cb == 0 || bc >= best_cost) break;
-    best_cost = bc;
-    best.clear();
-    for (int64_t i = 0; i < cb; ++i) best.push_back(i < n % cb ? b + 1 : b);
-    hi = b;
-  }
-  return best;
+  return r;
 }
 
 // One timed replay of a graph of sc's TRIAL cycles (each reads the current
@@ -1794,59 +1613,34 @@ void Solver::prepare_plans(int64_t n) {
     for (int k : sched_.at(n)) (void)split_plan(k);
   }
   if (measured_schedules() && !sched_.count(n)) {
-    std::vector<int> s = choose_schedule(n);
-    // Short graph-replayed runs: the per-depth estimates of near-tied
-    // schedules (within 3 %) mispredict their replay by up to ~5 % (4096^2
-    // fp64: depth 10 estimated 0.4 % faster, replayed 5 % slower than depth
-    // 12, profiles/r2_s3/sched_small/), so time the near-tied candidates as
-    // captured graphs of trial cycles and keep the fastest. Single-rank only
-    // (no collective needed to agree), runs estimated under 50 ms. Runs
-    // under 10 ms (the 4096^2 fp32 1000-step grid: ~3 ms) widen the scan to 4
-    // candidates within 5 % and keep each one's fastest of 5 replays: one
-    // replay each picked depths 16 / 17 (3.05 us per step) over 15 / 16 (3.01)
-    // in two of three runs (profiles/r4/c/small_*.json).
-    // (replayed schedules only: long-cycle ones launch eagerly, replay_schedule)
+    const ScheduleSearch r = choose_schedule(n);
+    std::vector<int> s = r.best;
+    // Near ties are timed as step(n) will run them: the summed per-depth
+    // estimates mispredict a whole schedule by a few % (4096^2 fp64: depth 10
+    // estimated 0.4 % faster, replayed 5 % slower than 12, profiles/r2_s3/
+    // sched_small/; 32768^2 fp32 480 steps: 22/23-deep cycles estimated 0.5 %
+    // cheaper than 20 x 24, ran 2-2.5 % slower eagerly, profiles/r4/gn/).
+    // Graph-replayed schedules: captured graphs of trial cycles (runs under
+    // 10 ms — the 4096^2 fp32 grid — widen to 4 within 5 %, the fastest of 5
+    // replays each: profiles/r4/c/small_*.json); eager ones of >= 8 cycles:
+    // eager trial schedules, best of 2. Single-rank runs estimated under 50 ms
+    // (no collective needed to agree; candidates are tuned already).
     double est = 0.0;
-    if (!s.empty() && schedule_graphs() && !tr_->exchanges())
-      for (int k : s) est += std::max(0.0, (double)depth_ms(k));
-    if (!s.empty() && schedule_graphs() && !tr_->exchanges() &&
-        est * 1e3 < graph_max_cycle_us() * (double)s.size()) {
-      const bool tiny = est < 10.0;
-      // (the near-tie scan autotunes every depth it visits: short runs only)
-      const auto near = est < 50.0 ? cycle_schedule_near(n, cfg_.tb, [this](int k) { return (double)depth_ms(k); },
-                                                         tiny ? 0.05 : 0.03, tiny ? 4 : 3)
-                                   : std::vector<std::vector<int>>{};
+    for (int k : s) est += std::max(0.0, (double)depth_ms(k));
+    const bool replay = schedule_graphs() && est * 1e3 < graph_max_cycle_us() * (double)s.size();
+    if (!s.empty() && !tr_->exchanges() && est < 50.0 && (replay || s.size() >= 8)) {
+      const bool tiny = replay && est < 10.0;
+      const double tol = tiny ? 0.05 : 0.03;
+      std::vector<std::vector<int>> near;
+      for (const auto& c : r.near)
+        if (c.first <= r.cost * (1.0 + tol) && (int)near.size() < (tiny ? 4 : 3)) near.push_back(c.second);
       if (near.size() > 1) {
         float best = 1e30f;
-        for (auto& c : near) {
-          const float ms = time_trial_schedule(c, tiny ? 5 : 1);
-          if (ms < best) {
-            best = ms;
-            s = c;
-          }
-        }
-      }
-    }
-    // Eager (long-cycle) single-rank runs: the tuned costs of near-tied
-    // candidates mispredict their run by a few % too (32768^2 fp32 480 steps:
-    // 22/23-deep cycles estimated 0.5 % cheaper than 20 x 24, ran 2-2.5 %
-    // slower: profiles/r4/gn/, r4/gi/), so time the candidates within 3 % of
-    // the best as eager trial schedules (best of 2) — runs of >= 8 cycles
-    // estimated under 50 ms; candidates already tuned, no extra autotuning.
-    if (!s.empty() && !tr_->exchanges() && s.size() >= 8 &&
-        !(schedule_graphs() && est * 1e3 < graph_max_cycle_us() * (double)s.size())) {
-      double e = 0.0;
-      for (int k : s) e += std::max(0.0, (double)depth_ms(k));
-      std::vector<std::vector<int>> near;
-      for (const auto& c : sched_cands_)
-        if (c.first <= e * 1.03 && std::find(near.begin(), near.end(), c.second) == near.end()) near.push_back(c.second);
-      if (e < 50.0 && near.size() > 1) {
-        float best = 1e30f;
         for (const auto& c : near) {
-          const float ms = time_trial_eager(c, 2);
+          const float ms = replay ? time_trial_schedule(c, tiny ? 5 : 1) : time_trial_eager(c, 2);
           if (tune_log())
-            std::fprintf(stderr, "heat2d sched n=%lld eager trial %zu cycles of %d..%d: %.4f ms\n", (long long)n,
-                         c.size(), c.back(), c.front(), ms);
+            std::fprintf(stderr, "heat2d sched n=%lld %s trial %zu cycles of %d..%d: %.4f ms\n", (long long)n,
+                         replay ? "graph" : "eager", c.size(), c.back(), c.front(), ms);
           if (ms < best) {
             best = ms;
             s = c;

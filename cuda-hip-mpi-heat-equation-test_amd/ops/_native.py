@@ -186,15 +186,15 @@ _SIGS = {
                                            C.c_char_p, _I64]),
     "heat2d_solver_pref_depth": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "heat2d_solver_step_stats": (C.c_int, [_P, _I64, C.POINTER(C.c_double)]),
-    "heat2d_cycle_schedule": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int32), _I64,
-                                        C.POINTER(C.c_int64)]),
-    "heat2d_cycle_schedule_shallower": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int32), _I64,
-                                                  C.c_double, C.c_int, C.POINTER(C.c_int32), _I64,
-                                                  C.POINTER(C.c_int64)]),
-    "heat2d_cycle_schedule_deeper": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int32), _I64,
-                                               C.c_double, C.c_int, C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64)]),
-    "heat2d_cycle_schedule_near": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.c_double, C.c_int,
-                                             C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    "heat2d_dp_schedule": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int32), _I64,
+                                     C.POINTER(_I64), C.POINTER(C.c_double)]),
+    "heat2d_near_schedules": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.c_double, C.c_int,
+                                        C.POINTER(C.c_int32), _I64, C.POINTER(_I64), C.POINTER(C.c_double),
+                                        C.POINTER(C.c_int32)]),
+    "heat2d_search_schedule": (C.c_int, [_I64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                         C.POINTER(C.c_int32), _I64, C.POINTER(_I64), C.POINTER(C.c_double),
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_int32)]),
     "heat2d_solver_schedule": (C.c_int, [_P, _I64, C.POINTER(C.c_int32), _I64, C.POINTER(C.c_int64)]),
     "heat2d_solver_schedule_replayed": (C.c_int, [_P, _I64, C.POINTER(C.c_int32)]),
     "heat2d_write_xyz": (C.c_int, [C.c_char_p, C.c_int, _P, _I64, _I64, _I64, _P, _P, C.c_int]),

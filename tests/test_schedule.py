@@ -1,8 +1,16 @@
-"""The measured-schedule search (Solver::prepare -> cycle_schedule), on CPU with
-synthetic cycle-time curves: it must find the cheapest cut of n steps into
-cycles of at most kmax steps among balanced splits, which for the convex t(k)
-the hardware shows (flat while a pass is HBM-bound, then linear in k) is the
-global optimum — checked against brute force over all compositions."""
+"""The measured-schedule search of Solver::prepare (csrc/runtime/schedule.cpp),
+on CPU with synthetic cycle-time curves:
+
+* dp_schedule — the exact least-cost cut of n steps into cycles of at most
+  kmax steps (checked against brute force over all compositions, and against
+  every balanced split);
+* near_schedules — one balanced candidate per base depth within a tolerance;
+* search_schedule — prescan (default plans) -> tune the near-best depths ->
+  DP over tuned costs -> walks past the tuned range on long runs, with the
+  measurements as callbacks: the known cases of the hardware (the 16384^2 fp64
+  occupancy cliff at depth 16, the HBM-bound fp32 grid that wants kmax, the
+  one-pass headline) and what it measures on the way.
+"""
 import ctypes as C
 
 import pytest
@@ -10,16 +18,43 @@ import pytest
 from heat2d.ops import _native as N
 
 
-def schedule(n, kmax, t):
-    tm = (C.c_double * (kmax + 1))(*([0.0] + [t(k) for k in range(1, kmax + 1)]))
+def _costs(kmax, t):
+    return (C.c_double * (kmax + 1))(*([0.0] + [float(t(k)) for k in range(1, kmax + 1)]))
+
+
+def dp(n, kmax, t):
     out = (C.c_int32 * max(1, n))()
-    ln = C.c_int64()
-    N.call("heat2d_cycle_schedule", n, kmax, tm, out, n, C.byref(ln))
-    return [int(v) for v in out[:ln.value]]
+    ln, tot = C.c_int64(), C.c_double()
+    N.call("heat2d_dp_schedule", n, kmax, _costs(kmax, t), out, n, C.byref(ln), C.byref(tot))
+    return [int(v) for v in out[:ln.value]], tot.value
+
+
+def near(n, kmax, t, tol, m):
+    out = (C.c_int32 * (m * n + 1))()
+    lens = (C.c_int64 * (m + 1))()
+    costs = (C.c_double * (m + 1))()
+    cnt = C.c_int32()
+    N.call("heat2d_near_schedules", n, kmax, _costs(kmax, t), tol, m, out, m * n, lens, costs, C.byref(cnt))
+    res, pos = [], 0
+    for i in range(cnt.value):
+        res.append((costs[i], [int(v) for v in out[pos:pos + lens[i]]]))
+        pos += lens[i]
+    return res
+
+
+def search(n, kmax, pre, tuned):
+    out = (C.c_int32 * max(1, n))()
+    ln, cost = C.c_int64(), C.c_double()
+    ps, ts = (C.c_int32 * (kmax + 1))(), (C.c_int32 * (kmax + 1))()
+    nps, nts = C.c_int32(), C.c_int32()
+    N.call("heat2d_search_schedule", n, kmax, _costs(kmax, pre), _costs(kmax, tuned), out, n, C.byref(ln),
+           C.byref(cost), ps, C.byref(nps), ts, C.byref(nts))
+    return ([int(v) for v in out[:ln.value]], cost.value, [int(v) for v in ps[:nps.value]],
+            [int(v) for v in ts[:nts.value]])
 
 
 def brute(n, kmax, t):
-    """Cheapest cut of n steps into cycles of <= kmax steps, over ALL compositions (DP)."""
+    """Cheapest cut of n steps into cycles of <= kmax steps over ALL compositions."""
     best = [0.0] + [float("inf")] * n
     for m in range(1, n + 1):
         best[m] = min(t(k) + best[m - k] for k in range(1, min(kmax, m) + 1))
@@ -30,143 +65,123 @@ def mi355x_fp64(k):  # measured shape at 32768^2 fp64 (profiles/depth_schedule.m
     return max(3.61, 0.30 * k - 0.05) + 0.02
 
 
+def cliff16(k):
+    """16384^2 fp64 TUNED cycle ms (profiles/r4/gh, r4/gi): an occupancy cliff
+    makes depth 16 far cheaper per step than 17..20."""
+    return {15: 0.905, 16: 0.940, 17: 1.136, 18: 1.170, 19: 1.237, 20: 1.310}.get(k, 1.5 + 0.05 * k)
+
+
+def cliff16_default(k):
+    """... and its DEFAULT plans (what the prescan sees): depth 16's default
+    plan is no better than its neighbours', so the prescan ranks 17..20 first."""
+    return {14: 1.40, 15: 1.42, 16: 1.38, 17: 1.25, 18: 1.29, 19: 1.36, 20: 1.47}.get(k, 2.0 + 0.05 * k)
+
+
+def hbm_bound(k):
+    """fp32 32768^2-like: a pass costs about the same at any depth (HBM-bound)."""
+    return 2.0 + 0.01 * k
+
+
 CURVES = {
     "measured-fp64": mi355x_fp64,
     "hbm-flat-then-linear": lambda k: max(1.0, 0.12 * k),
     "pure-linear": lambda k: 0.2 * k + 0.05,
     "launch-bound": lambda k: 0.05 + 0.004 * k,
+    "cliff16": cliff16,
+    "hbm-bound": hbm_bound,
+    "bumpy": lambda k: 1.0 + 0.07 * k + (0.3 if k % 3 == 0 else 0.0),
 }
 
 
 @pytest.mark.parametrize("curve", sorted(CURVES))
-@pytest.mark.parametrize("n,kmax", [(20, 24), (480, 24), (37, 16), (7, 24), (1, 24), (100, 14), (25000, 24)])
-def test_schedule_optimal(native, curve, n, kmax):
+@pytest.mark.parametrize("n,kmax", [(20, 24), (480, 24), (37, 16), (7, 24), (1, 24), (100, 14), (1000, 20)])
+def test_dp_is_optimal(native, curve, n, kmax):
     t = CURVES[curve]
-    s = schedule(n, kmax, t)
-    assert sum(s) == n and max(s) <= kmax and max(s) - min(s) <= 1
-    cost = sum(t(k) for k in s)
-    if n <= 30000:
-        assert cost <= brute(n, kmax, t) * (1 + 1e-9)
+    s, tot = dp(n, kmax, t)
+    assert sum(s) == n and max(s) <= kmax and s == sorted(s, reverse=True)
+    assert tot == pytest.approx(sum(t(k) for k in s), rel=1e-12)
+    assert tot <= brute(n, kmax, t) * (1 + 1e-12)
+    # never worse than any balanced split
+    for c in range(-(-n // kmax), n + 1):
+        b, rem = n // c, n % c
+        assert tot <= (c - rem) * t(b) + rem * (t(b + 1) if rem else 0) + 1e-9
 
 
-def test_schedule_examples(native):
-    assert schedule(20, 24, mi355x_fp64) == [20]  # one pass beats 2 x 10 (profiles/depth_schedule.md)
-    assert schedule(20, 14, mi355x_fp64) == [10, 10]
-    s = schedule(480, 24, mi355x_fp64)
-    assert set(s) <= {13, 14, 15, 16} and sum(s) == 480
+def test_dp_large_n_and_unusable_depths(native):
+    s, tot = dp(25000, 24, mi355x_fp64)  # the reference's literal 25000-step run
+    assert sum(s) == 25000 and tot > 0
+    # depths with a negative cost are never used; an unreachable n gives nothing
+    s, _ = dp(40, 24, lambda k: 1.0 if k in (8, 12) else -1.0)
+    assert sum(s) == 40 and set(s) <= {8, 12}
+    assert dp(7, 24, lambda k: 1.0 if k in (4,) else -1.0) == ([], -1.0)
 
 
-def test_schedule_missing_depth(native):
-    """A depth without a tuned time (t < 0, e.g. a slab too thin to split) aborts the search."""
-    assert schedule(20, 24, lambda k: -1.0 if k == 20 else 1.0) == []
+def test_dp_ties_fewer_cycles_deeper_first(native):
+    s, _ = dp(20, 24, lambda k: 1.0)  # every cycle costs the same: one cycle
+    assert s == [20]
+    s, _ = dp(30, 16, lambda k: 1.0 + 0.0 * k)
+    assert s == [16, 14]
 
 
-def schedules_near(n, kmax, t, tol, m):
-    tm = (C.c_double * (kmax + 1))(*([0.0] + [t(k) for k in range(1, kmax + 1)]))
-    out = (C.c_int32 * (m * n))()
-    lens = (C.c_int64 * m)()
-    cnt = C.c_int32()
-    N.call("heat2d_cycle_schedule_near", n, kmax, tm, tol, m, out, m * n, lens, C.byref(cnt))
-    res, pos = [], 0
-    for i in range(cnt.value):
-        res.append([int(v) for v in out[pos:pos + lens[i]]])
-        pos += lens[i]
-    return res
+def test_dp_mixes_depths_around_a_cliff(native):
+    """Balanced splits miss what the exact DP sees: 500 steps with the cheap
+    depth 16 and an expensive 17+ -> mostly 16s plus a 20 where 500 % 16 != 0."""
+    s, tot = dp(500, 24, cliff16)
+    assert sum(s) == 500 and s.count(16) >= 28
+    assert tot <= brute(500, 24, cliff16) * (1 + 1e-12)
+
+
+def test_near_candidates(native):
+    cand = near(480, 24, mi355x_fp64, 0.05, 4)
+    assert 1 <= len(cand) <= 4
+    costs = [c for c, _ in cand]
+    assert costs == sorted(costs) and costs[-1] <= costs[0] * 1.05
+    bases = [min(s) for _, s in cand]
+    assert len(set(bases)) == len(bases)  # one per base depth
+    for c, s in cand:
+        assert sum(s) == 480 and max(s) - min(s) <= 1 and c == pytest.approx(sum(mi355x_fp64(k) for k in s))
+
+
+def test_search_headline_one_pass(native):
+    """20 steps (the driver's headline): one depth-20 pass, only a handful of
+    depths prescanned and one or two tuned (prepare() stays ~2 s)."""
+    s, cost, pre, tun = search(20, 24, mi355x_fp64, lambda k: 0.97 * mi355x_fp64(k))
+    assert s == [20]
+    assert pre[0] == 20 and len(pre) <= 12
+    assert 20 in tun and len(tun) <= 3
+
+
+def test_search_finds_the_cliff(native):
+    """16384^2 fp64 480 steps: the prescan (default plans) ranks 17..20, their
+    tuned costs are tuned, and the downward walk from the lowest tuned depth
+    finds 16 (30 x 16, 28.2 ms) — round 4's 19/20 schedule ran 4055 Gpts/s,
+    30 x 16 4550 (profiles/r4/gh, r4/gi)."""
+    s, cost, pre, tun = search(480, 24, cliff16_default, cliff16)
+    assert s == [16] * 30 and cost == pytest.approx(30 * 0.94)
+    assert 16 in tun and 17 in tun
+    assert len(tun) <= 9
+
+
+def test_search_walks_up_when_the_deepest_wins(native):
+    """HBM-bound fp32: the deepest tuned depth wins, so the walk goes up to kmax."""
+    s, cost, pre, tun = search(480, 24, lambda k: 1.05 * hbm_bound(k), hbm_bound)
+    assert s == [24] * 20
+
+
+def test_search_short_runs_do_not_walk(native):
+    s, cost, pre, tun = search(40, 24, cliff16_default, cliff16)
+    assert sum(s) == 40
+    assert all(40 // k >= 1 for k in tun) and len(tun) <= 5
 
 
 @pytest.mark.parametrize("curve", sorted(CURVES))
-@pytest.mark.parametrize("n,kmax", [(20, 24), (1000, 16), (1000, 24), (480, 24), (37, 5)])
-def test_schedule_near_candidates(native, curve, n, kmax):
-    """prepare()'s graph-timed choice among near-tied schedules starts from
-    cycle_schedule_near: the best estimate first (= cycle_schedule), then other
-    balanced cycle counts within tol of it, at most m."""
+@pytest.mark.parametrize("n", [20, 64, 480, 1000])
+def test_search_matches_dp_over_what_it_tuned(native, curve, n):
+    """Whatever it measured, the result is the exact optimum over the tuned
+    costs (and no worse than the DP over the default plans it prescanned)."""
     t = CURVES[curve]
-    cost = lambda s: sum(t(k) for k in s)
-    near = schedules_near(n, kmax, t, 0.03, 3)
-    assert 1 <= len(near) <= 3
-    assert near[0] == schedule(n, kmax, t)
-    for s in near:
-        assert sum(s) == n and max(s) <= kmax and max(s) - min(s) <= 1
-        assert cost(s) <= cost(near[0]) * 1.03 + 1e-12
-    assert len({min(s) for s in near}) == len(near)  # one candidate per base depth
-    assert schedules_near(n, kmax, t, 0.0, 3)[0] == near[0]
-
-
-def shallower(n, kmax, t, best, lo):
-    tm = (C.c_double * (kmax + 1))(*([0.0] + [t(k) for k in range(1, kmax + 1)]))
-    b = (C.c_int32 * len(best))(*best)
-    out = (C.c_int32 * max(1, n))()
-    ln = C.c_int64()
-    N.call("heat2d_cycle_schedule_shallower", n, kmax, tm, b, len(best), sum(t(k) for k in best), lo, out, n,
-           C.byref(ln))
-    return [int(v) for v in out[:ln.value]]
-
-
-def cliff16(k):
-    """16384^2 fp64 tuned cycle ms (profiles/r4/gh, r4/gi): an occupancy cliff
-    makes depth 16 far cheaper per step than 17..20."""
-    return {15: 0.905, 16: 0.940, 17: 1.136, 18: 1.170, 19: 1.237, 20: 1.310}.get(k, 1.5 + 0.05 * k)
-
-
-def test_schedule_shallower_finds_cliff(native):
-    """The prescan's candidates (bases 17..20 or 18..24, the best 26 x 18/19)
-    missed depth 16: walking shallower on tuned times finds 30 x 16 (28.2 ms)
-    and stops after two bases in a row that do not beat it (15, 14). From base
-    18 the first step (17: 27 cycles, 31.4 ms) is no cheaper, the next is."""
-    best = [19] * 12 + [18] * 14  # 26 cycles of 18/19 (the candidates' best)
-    assert shallower(480, 24, cliff16, best, lo=17) == [16] * 30
-    assert shallower(480, 24, cliff16, best, lo=18) == [16] * 30
-    # a cost that only rises toward shallow depths keeps the candidates' choice
-    assert shallower(480, 24, lambda k: 1.0 + 0.01 * k, best, lo=18) == best
-
-
-def test_schedule_shallower_short_runs_untouched(native):
-    """Runs of few cycles (the headline's 20 steps) never pay for tuning more depths."""
-    assert shallower(20, 24, cliff16, [20], lo=10) == [20]
-    assert shallower(64, 24, lambda k: 0.1 * k, [22, 21, 21], lo=21) == [22, 21, 21]
-
-
-@pytest.mark.parametrize("curve", sorted(CURVES))
-def test_schedule_shallower_never_worse(native, curve):
-    t = CURVES[curve]
-    best = schedule(480, 24, t)
-    got = shallower(480, 24, t, best, lo=min(best))
-    assert sum(got) == 480 and sum(t(k) for k in got) <= sum(t(k) for k in best) * (1 + 1e-12)
-
-
-def deeper(n, kmax, t, best, hi):
-    tm = (C.c_double * (kmax + 1))(*([0.0] + [t(k) for k in range(1, kmax + 1)]))
-    b = (C.c_int32 * len(best))(*best)
-    out = (C.c_int32 * max(1, n))()
-    ln = C.c_int64()
-    N.call("heat2d_cycle_schedule_deeper", n, kmax, tm, b, len(best), sum(t(k) for k in best), hi, out, n,
-           C.byref(ln))
-    return [int(v) for v in out[:ln.value]]
-
-
-def hbm_bound(k):
-    """fp32 32768^2-like: a pass costs about the same at any depth (HBM-bound),
-    so the deepest cut is cheapest."""
-    return 2.0 + 0.01 * k
-
-
-def test_schedule_deeper_walks_to_kmax(native):
-    """Candidates that stopped at base 20 (25 cycles of 19/20) walk up to 20 x 24."""
-    best = [20] * 5 + [19] * 20
-    assert deeper(480, 24, hbm_bound, best, hi=19) == [24] * 20
-    assert deeper(480, 22, hbm_bound, best, hi=19)[0] <= 22  # never past kmax
-    # a per-step cost that rises with depth (VALU-bound) keeps the candidates' choice
-    assert deeper(480, 24, lambda k: 0.3 * k + 0.01 * k * k, best, hi=19) == best
-
-
-def test_schedule_deeper_short_runs_untouched(native):
-    assert deeper(20, 24, hbm_bound, [10, 10], hi=10) == [10, 10]  # 1 cycle < 8: no extra tuning
-    assert deeper(64, 24, hbm_bound, [16] * 4, hi=16) == [16] * 4
-
-
-@pytest.mark.parametrize("curve", sorted(CURVES))
-def test_schedule_deeper_never_worse(native, curve):
-    t = CURVES[curve]
-    best = [16] * 30
-    got = deeper(480, 24, t, best, hi=16)
-    assert sum(got) == 480 and max(got) <= 24 and sum(t(k) for k in got) <= sum(t(k) for k in best) * (1 + 1e-12)
+    s, cost, pre, tun = search(n, 24, lambda k: 1.1 * t(k), t)
+    assert sum(s) == n and set(s) <= set(tun)
+    best_over_tuned, _ = dp(n, 24, lambda k: t(k) if k in tun else -1.0)
+    assert cost == pytest.approx(sum(t(k) for k in best_over_tuned), rel=1e-12)
+    assert len(set(pre)) == len(pre) and len(set(tun)) == len(tun)  # each measured once
