@@ -62,18 +62,6 @@ int cu_count() {
 
 int vec_elems(DType dt) { return dt == DType::F32 ? 4 : 2; }
 
-// XCD-aware wave numbering in tb_kernel (TbArgs::xcd_remap). Measured on
-// MI355X (profiles/README.md §8): it cuts the strip-halo over-fetch from 1.14x
-// to 1.07x of the field but costs 6 % (fp64) / 3 % (fp32) — the round-robin
-// numbering, where the waves in flight cover each row evenly from every XCD,
-// streams HBM better. Off by default; HEAT2D_XCD_REMAP=1 enables it.
-int xcd_remap() {
-  static const int v = [] {
-    const char* env = std::getenv("HEAT2D_XCD_REMAP");
-    return env ? (std::atoi(env) != 0 ? 1 : 0) : 0;
-  }();
-  return v;
-}
 // halo columns per strip side (whole lanes) and useful strip width; must match TbShape
 int halo_cols(DType dt, int k) {
   const int v = vec_elems(dt);
@@ -277,7 +265,7 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   }
   if (q == 0) return 0;
   a.nrect = q;
-  a.xcd_remap = xcd_remap();
+  a.pad0 = 0;
   a.nitems = items;
   a.nwaves = std::max<int64_t>(1, std::min<int64_t>(nwaves, items));
   a.partials = partials;
@@ -408,10 +396,7 @@ void launch_tb2(DType dt, const void* src, void* dst, const SlabLayout& L, int64
 // the first and last item of every strip. When the rect's marches reach a
 // frame row, the interior strips get a top / bottom rect of one short band
 // each, (h + 2k) w1 = Li + 2k, and the segments / bands in between: 5 rects.
-// Weights: HEAT2D_W_ROW / HEAT2D_W_COL override (A/B).
 double pinned_weight(DType dt, bool row, bool single, int ring) {
-  const char* env = std::getenv(row ? "HEAT2D_W_ROW" : "HEAT2D_W_COL");
-  if (env && std::atof(env) >= 1.0) return std::atof(env);
   // Measured: fp32 columns 1.4 best over 1.0-2.3 (4096^2 K = 16, 1007
   // segments: 58.7-59.1 us per cycle against 60.1 at 1.5 and 60.7 at 1.75,
   // profiles/r3/sweep5/); rows from per-wave timelines (tools/wave_times.py,
@@ -616,14 +601,10 @@ void launch_tb_stats(DType dt, const void* src, void* dst, const SlabLayout& L, 
 // Boundary-band rects of a slab whose bands stay clear of the global frame
 // rows (every middle rank of a row decomposition): the interior kernel marches
 // them (item kinds 0 / 2 only), at its 2 waves per SIMD instead of the general
-// kernel's 1 (fp64 K = 20: 249 vs 374 + 118 acc VGPRs). HEAT2D_EDGE_MAIN=0: the
-// general kernel always (A/B).
+// kernel's 1 (fp64 K = 20: 249 vs 374 + 118 acc VGPRs; fp32 480-step slab
+// rehearsal 8838 -> 9233 Gpts/s, profiles/r4/lead/).
 bool edges_on_main(const SlabLayout& L, int k, const TbRect* R, int n) {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_EDGE_MAIN");
-    return !e || std::atoi(e) != 0;
-  }();
-  if (!on || n < 1 || n > kMainRects) return false;
+  if (n < 1 || n > kMainRects) return false;
   for (int i = 0; i < n; ++i)
     if (R[i].r1 > R[i].r0 && (R[i].r0 - k < -L.row0 || R[i].r1 + k > L.nrows_global - L.row0)) return false;
   return true;

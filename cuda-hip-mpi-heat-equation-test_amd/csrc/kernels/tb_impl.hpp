@@ -99,7 +99,7 @@ struct TbArgs {
   int64_t nwaves;  // launched waves (grid-stride over items)
   int64_t fixed_lo, fixed_hi;  // local rows outside [fixed_lo, fixed_hi) are Dirichlet
   int32_t nrect;
-  int32_t xcd_remap;  // 1: XCD-aware block -> wave-id mapping (tb_kernel)
+  int32_t pad0;
   TbRectArg rect[kMaxRects];
   double* partials;   // ST kernels: per-wave statistics, partials[j * nwaves + wave] (kNStatFused = 6 values)
   // Diagnostics (HEAT2D_WAVE_TIMES, kern::wave_times): per launched wave
@@ -1036,18 +1036,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
   const int lane = threadIdx.x & 63;
   // readfirstlane: make the wave id (and everything derived from it: strip, rows,
   // row addresses) provably wave-uniform -> SGPRs and scalar buffer descriptors
-  //
-  // XCD-aware numbering (a.xcd_remap): blocks are dealt round-robin over the 8
-  // XCDs (b and b + 8 share an L2), so consecutive block ids would put
-  // neighbouring strips — which re-read each other's K halo columns of every
-  // row — on different XCDs. Renumber so that each XCD's blocks own one
-  // contiguous run of strips: the halo re-reads hit the XCD's L2.
-  int blk = (int)blockIdx.x;
-  if (a.xcd_remap) {
-    const int nb = (int)gridDim.x, q = nb >> 3, rem = nb & 7, x = blk & 7;
-    blk = x * q + min(x, rem) + (blk >> 3);
-  }
-  const int64_t wid = (int64_t)blk * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  // (Blocks are dealt round-robin over the 8 XCDs; numbering them so that each
+  // XCD owns a contiguous run of strips cut the strip-halo re-fetch from 1.14x
+  // to 1.07x of the field but cost 6 % fp64 / 3 % fp32 — the round-robin
+  // numbering streams HBM better: profiles/README.md §8. Removed in round 5.)
+  const int64_t wid = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (wid >= a.nwaves) return;  // whole wave exits; no barriers in this kernel
   if (a.wtimes && lane_id_is0()) a.wtimes[wid * 4] = wall_clock64();
   // Band items are band-major within a rect: consecutive waves take adjacent

@@ -174,10 +174,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     } else {
       int ncu = 0;
       H2D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg_.device));
-      int want = cfg_.comm_cus;
-      if (want == 0) {
-        if (const char* env = std::getenv("HEAT2D_COMM_CUS")) want = std::atoi(env);
-      }
+      const int want = cfg_.comm_cus;
       const bool ovl = tr_->exchanges() && cfg_.overlap;
       if (ovl && want > 0 && want < ncu) {
         // Hard reservation: `want` CUs, spread over the XCDs, out of the
@@ -564,10 +561,10 @@ const kern::SplitPlan& Solver::split_plan_banded(int k, int64_t B) {
 // rule captured; a single isolated cycle mispredicts the loop, hence the
 // steady-state measurement (profiles/autotune.md).
 // Wave slots the interior grid leaves free for RCCL's kernels when the slab
-// exchanges halos (HEAT2D_SPARE_WAVES overrides; A/B in profiles/).
+// exchanges halos (8: more cost the interior more than the bands gain,
+// profiles/thin_slab.md §2).
 int Solver::spare_waves() const {
   if (!tr_->exchanges()) return 0;
-  if (const char* env = std::getenv("HEAT2D_SPARE_WAVES")) return std::max(0, std::atoi(env));
   return 8;
 }
 
@@ -587,14 +584,6 @@ static int device_cus_of(int device) {
 static bool dynamic_candidates() {
   static const bool on = [] {
     const char* e = std::getenv("HEAT2D_DYNAMIC");
-    return !e || std::atoi(e) != 0;
-  }();
-  return on;
-}
-
-static bool tune_segments() {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_TUNE_SEGMENTS");
     return !e || std::atoi(e) != 0;
   }();
   return on;
@@ -678,11 +667,9 @@ float Solver::time_plan(const kern::SplitPlan& c, int kTimed) {
 static uint64_t plan_env_hash() {
   static const uint64_t h = [] {
     uint64_t v = 1469598103934665603ull;
-    for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_TUNE_SEGMENTS", "HEAT2D_W_ROW", "HEAT2D_W_COL",
-                             "HEAT2D_TB_RING", "HEAT2D_XCD_REMAP", "HEAT2D_COMM_CUS", "HEAT2D_SPARE_WAVES",
+    for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_TB_RING",
                              "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
-                             "HEAT2D_TUNE_STAGED", "HEAT2D_EDGE_BANDS",
-                             "HEAT2D_EDGE_MAIN", "HEAT2D_GRAPH_MAX_CYCLE_US"}) {
+                             "HEAT2D_EDGE_BANDS", "HEAT2D_GRAPH_MAX_CYCLE_US"}) {
       const char* e = std::getenv(name);
       const std::string kv = std::string(name) + "=" + (e ? e : "<unset>") + ";";
       for (unsigned char c : kv) v = (v ^ c) * 1099511628211ull;
@@ -753,20 +740,13 @@ bool Solver::cached_split(int k) {
   return true;
 }
 
-// Staged screening (HEAT2D_TUNE_STAGED=0: every candidate over 4 cycles, the 4
-// best over 12, as round 3): stage A times every candidate over ONE cycle
+// Staged screening (round 3 timed every candidate over 4 cycles and the 4
+// best over 12, twice the trial cycles): stage A times every candidate over ONE cycle
 // (after one warm-up cycle; up to 4 for cycles under 1 ms, where one sample is
 // noisy and cheap), stage B the 6 best of A over 4, stage C the 3 best
 // of B over 12 — about half the trial cycles at the same winner (the leaders
 // are 1-2 % apart, which stage C resolves). Cycles longer than kLongCycleMs
 // (the full-HBM grids: ~50 ms per pass) screen a reduced candidate family.
-static bool staged_tuning() {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_TUNE_STAGED");
-    return !e || std::atoi(e) != 0;
-  }();
-  return on;
-}
 constexpr float kLongCycleMs = 8.0f;
 
 // HEAT2D_TUNE_LOG=1: every screening stage's ranking on stderr (diagnostics)
@@ -801,10 +781,9 @@ float Solver::exchange_penalty(const kern::SplitPlan& c, float trial_ms) const {
 void Solver::autotune_split(int k) {
   const int spare = spare_waves();
   synchronize();
-  const bool staged = staged_tuning();
   kern::SplitPlan best = split_[k];
-  const float base_ms = time_plan(best, staged ? 2 : 4);
-  const bool long_cycles = staged && base_ms > kLongCycleMs;
+  const float base_ms = time_plan(best, 2);
+  const bool long_cycles = base_ms > kLongCycleMs;
   auto finish = [&](kern::SplitPlan b, float ms) {
     synchronize();
     b.k = k;
@@ -899,11 +878,11 @@ void Solver::autotune_split(int k) {
       }
       // segment work items (TbRect nb < 0): the interior cut into equal runs of
       // strip rows, 1/2 .. 2 per persistent wave — balanced whatever the strip
-      // count (thin slabs: profiles/thin_slab.md); HEAT2D_TUNE_SEGMENTS=0 skips them.
+      // count (thin slabs: profiles/thin_slab.md).
       // fp32: single launches only — split plans over segments won 4-cycle trials
       // by noise and then ran 1.7 % slower than bands on 32768^2 (interleaved A/B,
       // profiles/thin_slab.md §4), while single launches over segments win 4096^2
-      if (!tune_segments() || (dtype() == DType::F32 && mode != 2)) continue;
+      if (dtype() == DType::F32 && mode != 2) continue;
       const int64_t w0 = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, 0, cfg_.arith).main_waves
                                    : best.main_waves;
       std::vector<int64_t> segs;
@@ -937,8 +916,7 @@ void Solver::autotune_split(int k) {
   // short cycles over up to 4 (a single ~50 us cycle is noisy; they are cheap)
   using Stage = std::pair<int, size_t>;
   const int a_cycles = std::max(1, std::min(4, (int)std::ceil(1.0f / std::max(base_ms, 1e-3f))));
-  const std::vector<Stage> stages = staged ? std::vector<Stage>{{a_cycles, 6}, {4, 3}, {12, 1}}
-                                           : std::vector<Stage>{{4, 4}, {12, 1}};
+  const std::vector<Stage> stages{{a_cycles, 6}, {4, 3}, {12, 1}};
   struct Timed {
     float score, ms;  // ranking score (trial + exposed exchange), trial ms per cycle
     kern::SplitPlan plan;

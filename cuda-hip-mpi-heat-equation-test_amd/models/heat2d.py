@@ -84,8 +84,8 @@ class HeatSolver:
         transport: a :class:`parallel.transport.Transport`; default picks self / RCCL / gloo.
         device: HIP device ordinal (default: torch's current device).
         comm_cus: room for the bands + RCCL beside the interior kernel when
-            overlapping: >0 CUs masked off the compute stream; 0 (default, or
-            $HEAT2D_COMM_CUS) interior planned for all CUs but 2, no mask; -1 none.
+            overlapping: >0 CUs masked off the compute stream; 0 (default): the
+            interior planned for all wave slots but 8 spare ones, no mask; -1 none.
         engine: "tb" — the temporal-blocked gfx950 kernels; "jit" — a kernel
             rendered for this slab and r and compiled at run time with hipRTC
             (one step per launch; the reference's PyCUDA program, ops/jit.py).
