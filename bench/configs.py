@@ -2,14 +2,15 @@
 """The BASELINE.json configuration list, measured on one MI355X (plus the CPU
 serial case). Prints one JSON line per configuration.
 
-    python bench/configs.py [--only NAME ...] [--max-gb 240]
+    python bench/configs.py [--only NAME ...] [--max-gb GB]
 
   cpu-256-fp64      256x256 fp64, native CPU path (python/serial + fortran/serial scale)
   gpu-4096-fp32     4096x4096 fp32, 1000 steps (fields live in the 256 MiB Infinity Cache)
   gpu-16384-fp64    16384x16384 fp64 (HBM-bound regime)
   gpu-32768-fp64    32768x32768 fp64 — the reference's benchmark input (fortran/hip/input.dat)
   gpu-32768-fp32    32768x32768 fp32 (the 8-GPU config of BASELINE.json, here on 1 GPU)
-  gpu-max-fp32      the largest fp32 grid two fields fit in --max-gb of HBM (weak-scaling unit)
+  gpu-max-fp32      the largest fp32 grid the free device memory holds (utils/memplan.py, the
+                    memory-fit planner; --max-gb GB: two fields of at most GB instead)
   gpu-32768-fp64-s0.2  the reference input with sigma = 0.2 (r != 1/4): the scaled-level
                        "fast" arithmetic (any r) and the exact reference rounding, 20 steps
 """
@@ -76,7 +77,8 @@ def run(name, n, dtype, steps, warmup, backend, tb, graph=False, arith="bench", 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", nargs="*", default=None)
-    ap.add_argument("--max-gb", type=float, default=240.0)
+    ap.add_argument("--max-gb", type=float, default=0.0,
+                    help="gpu-max-fp32: two fields of at most this many GB (default 0: the memory-fit planner)")
     ap.add_argument("--arith", default="bench", choices=["bench", "auto", "exact", "fma", "jacobi", "fast"],
                     help="update form (bench.py --arith): bench = jacobi where r == 1/4")
     a = ap.parse_args()
@@ -85,8 +87,13 @@ def main():
     if have_gpu:
         torch.cuda.set_device(0)
     es32 = 4
-    nmax = int(math.sqrt(a.max_gb * 1e9 / (2 * es32)))
-    nmax = nmax // 1024 * 1024
+    if a.max_gb > 0:
+        nmax = int(math.sqrt(a.max_gb * 1e9 / (2 * es32))) // 1024 * 1024
+    elif have_gpu:
+        from heat2d.utils import memplan
+        nmax = memplan.plan_max_grid("fp32", 1, device=0)["n"]
+    else:
+        nmax = 0
     plan = [
         # tb 0: depths up to the dtype's maximum, chosen per run by measurement
         ("cpu-256-fp64", 256, "fp64", 200, 8, "cpu", 8, False),
