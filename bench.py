@@ -433,7 +433,12 @@ def main():
                    "--field-check", "off"]
             p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=work)
             if p.returncode != 0 or not os.path.exists(info):
-                return dict(out, error=f"{ctr} pass failed (rc {p.returncode}): {p.stderr[-400:]}")
+                # the child's own lines (rocprofv3 logs with a glog prefix: [IWE]yyyymmdd ...)
+                own = [ln for ln in p.stderr.splitlines() if not (len(ln) > 9 and ln[0] in "IWE" and ln[1:9].isdigit())]
+                with open(os.path.join(work, ctr + ".stderr"), "w") as f:
+                    f.write(p.stderr)
+                return dict(out, error=f"{ctr} pass failed (rc {p.returncode}); stderr kept in {work}: "
+                                       + "\n".join(own[-25:]))
             rows_ = []
             for fcsv in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 rows_ += list(csv.DictReader(open(fcsv)))
