@@ -395,10 +395,11 @@ def main():
         setup(kind)
     def hbm_marker():
         """A 16-byte read kernel: brackets the timed region's dispatches in the profile."""
+        from heat2d.ops import _native as native
         buf = torch.zeros(64, dtype=torch.uint8, device=f"cuda:{device}")
         sink = torch.zeros(16, dtype=torch.uint8, device=f"cuda:{device}")
         torch.cuda.synchronize()
-        N.call("heat2d_read", buf.data_ptr(), 16, sink.data_ptr(), None, 1)
+        native.call("heat2d_read", buf.data_ptr(), 16, sink.data_ptr(), None, 1)
         torch.cuda.synchronize()
 
     def measure_hbm(elapsed):
@@ -424,7 +425,8 @@ def main():
                          "profiled re-runs of the timed region (same plans); rate over this run's timed seconds"}
         tot = {}
         work = tempfile.mkdtemp(prefix="heat2d_hbm_prof_")
-        env = dict(os.environ, HEAT2D_PLAN_CACHE=N.plan_cache_path(), HEAT2D_PLAN_CACHE_TRUST="1")
+        from heat2d.ops import _native as native
+        env = dict(os.environ, HEAT2D_PLAN_CACHE=native.plan_cache_path(), HEAT2D_PLAN_CACHE_TRUST="1")
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(work, ctr)
             info = os.path.join(work, ctr + ".json")
