@@ -14,9 +14,9 @@
 //   2. tune     — every depth of the near-best prescan schedules (one per base
 //                 depth, within prescan_tol, at most prescan_bases of them);
 //   3. DP       — the exact schedule of n steps minimising the sum of the best
-//                 known cycle times (tuned, else prescan); depths it picks that
-//                 are not tuned yet are tuned and the DP re-run, until its
-//                 choice is all tuned;
+//                 known cycle times (tuned, else prescan); a depth it picks that
+//                 is not tuned yet is tuned and the DP re-run, until its choice
+//                 is all tuned;
 //   4. walks    — runs of >= walk_min_cycles cycles also tune the depths below
 //                 the lowest tuned one (and above the highest, when the best
 //                 uses it), one at a time, until walk_patience in a row do not
@@ -148,16 +148,23 @@ ScheduleSearch search_schedule(int64_t n, int kmax, const std::function<double(i
   for (const auto& c : near_schedules(n, K, [&](int k) { return est(k); }, o.prescan_tol, o.prescan_bases))
     for (int k : c.second) (void)tun(k);
   // 3. + 4. DP over the best known costs; tune what it picks; walks
+  // (one depth at a time — the one the DP uses most, then the deeper — and the
+  // DP re-run: a tuned depth often makes another pick unnecessary)
   auto settle = [&] {
     for (;;) {
       r.best = dp_schedule(n, K, est, &r.cost);
-      bool more = false;
-      for (int k : r.best)
-        if (!tuned(k)) {
-          (void)tun(k);
-          more = true;
+      int pick = 0;
+      int64_t uses = 0;
+      for (int k : r.best) {
+        if (tuned(k)) continue;
+        const int64_t u = std::count(r.best.begin(), r.best.end(), k);
+        if (u > uses || (u == uses && k > pick)) {
+          uses = u;
+          pick = k;
         }
-      if (!more) return;
+      }
+      if (pick == 0) return;
+      (void)tun(pick);
     }
   };
   settle();

@@ -817,12 +817,11 @@ void Solver::autotune_split(int k) {
       const float t = time_plan(c, 2);
       ++tune_trials_;
       // kept only if it beats this depth's default plan on the same score
-      // (trial + the exchange its order cannot hide); else the screening runs
-      if (t + exchange_penalty(c, t) <= base_ms + exchange_penalty(best, base_ms)) {
-        finish(c, t);
-        return;
-      }
-      break;
+      // (trial + the exchange its order cannot hide); else the default plan
+      // stays — no second screening of ~50 ms cycles either way
+      if (t + exchange_penalty(c, t) <= base_ms + exchange_penalty(best, base_ms)) finish(c, t);
+      else finish(best, base_ms);
+      return;
     }
   }
   const int64_t nb0 = best.main.nb;
