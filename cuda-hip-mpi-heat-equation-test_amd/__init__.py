@@ -23,4 +23,7 @@ def __getattr__(name):
     if name in ("HeatSolver", "LoopbackGroup"):
         from .models import heat2d as _m
         return getattr(_m, name)
+    if name in ("plan_max_grid", "footprint"):  # the memory-fit planner (utils/memplan.py)
+        from .utils import memplan as _p
+        return getattr(_p, name)
     raise AttributeError(name)
