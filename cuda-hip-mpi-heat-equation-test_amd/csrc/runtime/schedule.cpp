@@ -190,6 +190,23 @@ ScheduleSearch search_schedule(int64_t n, int kmax, const std::function<double(i
     // upward only when the best already runs the deepest tuned depth (each
     // deeper fp64 32768^2 depth costs ~2.5 s of tuning, profiles/r4/gn/)
     if (std::find(r.best.begin(), r.best.end(), hi) != r.best.end()) walk(hi, +1);
+    // neighbours: the untuned depths next to the ones the best runs, until all
+    // are tuned — the walks leave gaps INSIDE the tuned range (16384^2 fp64:
+    // tuned 12..15 and 18..20 around the cliff, 16 never, so 32 x 15 at 29.9 ms
+    // instead of 30 x 16 at 28.2, profiles/r5/g/)
+    for (bool more = true; more;) {
+      more = false;
+      std::vector<int> uses(r.best);
+      std::sort(uses.begin(), uses.end());
+      uses.erase(std::unique(uses.begin(), uses.end()), uses.end());
+      for (int k : uses)
+        for (int nk : {k - 1, k + 1})
+          if (!more && nk >= 1 && nk <= K && !tuned(nk) && n / nk >= o.walk_min_cycles) {
+            (void)tun(nk);
+            settle();
+            more = true;
+          }
+    }
   }
   // 5. near ties among tuned depths (the caller times them as they would run)
   r.near = near_schedules(n, K, [&](int k) { return tuned(k) ? T[(size_t)k] : -1.0; }, o.near_tol, o.near_max);

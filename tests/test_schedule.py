@@ -162,6 +162,21 @@ def test_search_finds_the_cliff(native):
     assert len(tun) <= 9
 
 
+def test_search_fills_gaps_next_to_the_best(native):
+    """The prescan of profiles/r5/g (16384^2 fp64, 480 steps) put depth 16's
+    default plan behind 15's and 14's: the tuned depths became 12..15 and
+    18..20, the walks (below 12, above 20) never reach 16, and the DP took
+    32 x 15 (29.9 ms, 4314 Gpts/s). The neighbours of the best's depths are
+    tuned too: 16 joins and wins (30 x 16)."""
+    pre = {24: 1.7821, 23: 1.6835, 22: 1.8589, 21: 1.7732, 20: 1.4719, 19: 1.3863, 18: 1.3331, 17: 1.2580,
+           16: 1.3059, 15: 1.2669, 14: 1.0108, 13: 1.2365}
+    tuned = {20: 1.3236, 19: 1.2327, 18: 1.1801, 17: 1.136, 16: 0.940, 15: 0.9351, 14: 1.0108, 13: 0.9987,
+             12: 0.8982, 11: 0.85, 10: 0.80}
+    s, cost, _, tun = search(480, 24, lambda k: pre.get(k, 2.0 + 0.05 * k), lambda k: tuned.get(k, 1.5))
+    assert s == [16] * 30 and cost == pytest.approx(28.2)
+    assert 16 in tun and 17 in tun and len(tun) <= 11
+
+
 def test_search_walks_up_when_the_deepest_wins(native):
     """HBM-bound fp32: the deepest tuned depth wins, so the walk goes up to kmax."""
     s, cost, pre, tun = search(480, 24, lambda k: 1.05 * hbm_bound(k), hbm_bound)
