@@ -223,6 +223,7 @@ struct ScheduleSearchOptions {
   int prescan_bases = 4;       // ... at most this many base depths
   int64_t walk_min_cycles = 8;  // runs of at least this many cycles walk beyond the tuned depths
   int walk_patience = 2;       // a walk ends after this many tunings in a row that did not lower the cost
+  double walk_tol = 0.08;      // ... and whose per-step cost was more than this much above the best's
   double near_tol = 0.03;      // near ties returned for timing
   int near_max = 3;
 };

@@ -517,9 +517,11 @@ struct March {
   // descriptor). The trip count is rounded up to whole L-row bodies (the
   // extra rows' stores are dropped too): a loop body with a single exit, so
   // no load can be sunk past a mid-body exit (which would serialise the ring).
-  // PS: skip the levels the first march rows do not need (priming). Only the
-  // fp32 interior kernel uses it: the guarded priming body costs the fp64 and
-  // general kernels an occupancy level (profiles/priming_skip.md).
+  // PS: skip the levels the first march rows do not need (priming). The
+  // interior kernels use it (fp64 too since round 5: +5-8 % per pass at
+  // depths 13..20 although it costs some of them an occupancy level,
+  // profiles/r5/i/, r5/j/); the general kernels do not (4-5 % slower for the
+  // 1-wave/SIMD fp32 small grid, profiles/priming_skip.md).
   template <bool PS = false>
   __device__ __forceinline__ void run() {
     mload = t0 - K;
@@ -780,9 +782,11 @@ struct MarchF32 {
     (step<I, true>(m - I, Ch::levels_at(i + I)), ...);
   }
 
-  // PS: skip the levels the first march rows do not need (priming). Only the
-  // fp32 interior kernel uses it: the guarded priming body costs the fp64 and
-  // general kernels an occupancy level (profiles/priming_skip.md).
+  // PS: skip the levels the first march rows do not need (priming). The
+  // interior kernels use it (fp64 too since round 5: +5-8 % per pass at
+  // depths 13..20 although it costs some of them an occupancy level,
+  // profiles/r5/i/, r5/j/); the general kernels do not (4-5 % slower for the
+  // 1-wave/SIMD fp32 small grid, profiles/priming_skip.md).
   template <bool PS = false>
   __device__ __forceinline__ void run() {
     mload = t0 - K;
@@ -967,19 +971,17 @@ __device__ __forceinline__ bool tb_piece(const TbArgs& a, int64_t it, int32_t li
 // frame-column strips — two code paths, fewer registers than the general
 // kernel (no per-level row tests, no corner selects). MAIN = false: the general
 // kernel classifies each item (edge kinds 0..3, see March).
-// Occupancy floor handed to the register allocator: the fp64 fma interior
-// kernel at K = 11 lands at 129 VGPRs and fits 128 (4 waves/SIMD instead of 3)
-// without spilling (K = 12 did until the dynamic item queue's code; now it
-// would spill 32 B); its exact-arithmetic twin would spill. (The packed
-// fp32 march with the single across-lane adds spills under a 3-wave floor from
-// K = 12 on, so it has none.) The r = 1/4 (AR 2) fp64 interior kernel keeps 2
-// waves/SIMD at K = 18..19 under a floor; at K = 20 ring 4 a floor spills (its
-// ring-6 twin fits 241 VGPRs, which the autotuner weighs). The fp32 interior
-// kernels at K = 17..20 (ring 4) keep 2 waves/SIMD under a floor. Checked per build:
-// ScratchSize = 0 in the ISA (tools/isa_report.py, tests/test_isa.py).
+// Occupancy floor handed to the register allocator: the fp64 interior kernels
+// with ring 4 keep 2 waves/SIMD at K = 17 and 21..24 under a floor; at K =
+// 18..20 a floor spills since the priming skip (their ring-6 twins fit 226-247
+// VGPRs, which the autotuner weighs; round 4's fma K = 11 floor of 4 waves
+// spills with the skip too). (The packed fp32 march with the single
+// across-lane adds spills under a 3-wave floor from K = 12 on, so it has none.)
+// The fp32 interior kernels at K = 17..20 (ring 4) keep 2 waves/SIMD under a
+// floor. Checked per build: ScratchSize = 0 in the ISA (tools/isa_report.py,
+// tests/test_isa.py).
 template <typename T, int NV, int K, int RING, bool MAIN, int AR>
-constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 1 && K == 11) ? 4
-                          : (std::is_same<T, double>::value && MAIN && RING == 4 && AR == 2 && K >= 18 && K <= 19) ? 2
+constexpr int kMinWaves = (std::is_same<T, double>::value && MAIN && RING == 4 && (K == 17 || K >= 21))   ? 2
                           : (std::is_same<T, float>::value && MAIN && RING == 4 && K >= 17)                        ? 2
                                                                                                                   : 1;
 
@@ -1071,11 +1073,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
         default: march<T, NV, K, 3, RING, AR, true>(src, dst, a, r, strip, t0, t1, lane, &acc); break;
       }
     } else if constexpr (MAIN) {
-      constexpr bool PS = std::is_same<T, float>::value;  // priming skip: fp32 interior kernel only
       if ((c0 < 0) || (c0 + S::W > a.ncols))
-        march<T, NV, K, 2, RING, AR, false, PS>(src, dst, a, r, strip, t0, t1, lane);
+        march<T, NV, K, 2, RING, AR, false, true>(src, dst, a, r, strip, t0, t1, lane);
       else
-        march<T, NV, K, 0, RING, AR, false, PS>(src, dst, a, r, strip, t0, t1, lane);
+        march<T, NV, K, 0, RING, AR, false, true>(src, dst, a, r, strip, t0, t1, lane);
     } else {
       const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
                      (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);

@@ -20,7 +20,8 @@
 //   4. walks    — runs of >= walk_min_cycles cycles also tune the depths below
 //                 the lowest tuned one (and above the highest, when the best
 //                 uses it), one at a time, until walk_patience in a row do not
-//                 lower the DP cost (a default plan far worse than its tuned
+//                 lower the DP cost and cost more than walk_tol per step above
+//                 the best (a default plan far worse than its tuned
 //                 plan hides such a depth from the prescan: 16384^2 fp64 480
 //                 steps, depth 16 tuned 0.94 ms vs 17..20 at 1.14-1.31);
 //   5. near     — the tuned-cost schedules within near_tol of the best (one per
@@ -144,6 +145,14 @@ ScheduleSearch search_schedule(int64_t n, int kmax, const std::function<double(i
     best_step = std::min(best_step, v / k);
     if (v / k > o.stop_ratio * best_step) break;
   }
+  // ... and on, until some schedule of exactly n steps exists over the known
+  // depths (n = 25 with only 19..24 prescanned has none: 8 thin slabs of
+  // 525 rows, profiles/r5/k/)
+  for (int k = K; k >= 1; --k) {
+    double c = -1.0;
+    if (!dp_schedule(n, K, est, &c).empty()) break;
+    (void)pre(k);
+  }
   // 2. tune the depths of the near-best prescan schedules
   for (const auto& c : near_schedules(n, K, [&](int k) { return est(k); }, o.prescan_tol, o.prescan_bases))
     for (int k : c.second) (void)tun(k);
@@ -175,9 +184,12 @@ ScheduleSearch search_schedule(int64_t n, int kmax, const std::function<double(i
         if (n / k < o.walk_min_cycles) break;  // a base needing fewer cycles: not a long run's depth
         if (tuned(k)) continue;
         const double before = r.cost;
-        (void)tun(k);
+        const double v = tun(k);
         settle();
-        misses = (r.cost >= 0 && r.cost < before * (1.0 - 1e-9)) ? 0 : misses + 1;
+        // a depth within walk_tol of the best per step does not count as a
+        // miss: the walk goes on past near misses to a cliff's far side
+        const bool near_best = v > 0 && r.cost > 0 && v / k <= (1.0 + o.walk_tol) * r.cost / (double)n;
+        misses = (r.cost >= 0 && r.cost < before * (1.0 - 1e-9)) ? 0 : (near_best ? misses : misses + 1);
       }
     };
     int lo = K, hi = 1;

@@ -177,6 +177,31 @@ def test_search_fills_gaps_next_to_the_best(native):
     assert 16 in tun and 17 in tun and len(tun) <= 11
 
 
+def test_search_prescans_until_n_is_reachable(native):
+    """A flat cycle cost stops the prescan at depth 19 (per step 25 % worse
+    than depth 24's), and no schedule of exactly 25 steps uses only depths
+    19..24: the prescan goes on until one exists (round 5: 8 ranks of 525
+    rows, 25-step chunks, ran the balanced fallback)."""
+    s, cost, pre, tun = search(25, 24, lambda k: 1.0, lambda k: 1.0)
+    assert sum(s) == 25 and len(s) == 2 and cost == pytest.approx(2.0)
+    assert min(pre) <= 12 and len(pre) <= 13
+
+
+def test_search_walks_past_near_misses(native):
+    """profiles/r5/i (priming skip in the fp64 interior, 16384^2, 480 steps):
+    the prescan ranked depths 20..24 first and depth 20 won the DP; the walk
+    down met 19 and 18, each a little worse per step than 20 — two misses, so
+    it stopped and 24 x 20 ran (4336 Gpts/s) instead of 30 x 16 (4797). Depths
+    within walk_tol (8 %) per step of the best are not misses: the walk goes on
+    through 17 to 16."""
+    pre = {24: 1.45, 23: 1.40, 22: 1.36, 21: 1.30, 20: 1.25, 19: 1.30, 18: 1.28, 17: 1.26, 16: 1.40, 15: 1.30}
+    tuned = {24: 1.508, 23: 1.480, 22: 1.5015, 21: 1.33, 20: 1.2296, 19: 1.19, 18: 1.15, 17: 1.1158, 16: 0.8977,
+             15: 0.9246, 14: 0.9662, 13: 0.9605}
+    s, cost, _, tun = search(480, 24, lambda k: pre.get(k, 2.0 + 0.05 * k), lambda k: tuned.get(k, 1.5))
+    assert s == [16] * 30 and cost == pytest.approx(30 * 0.8977)
+    assert 16 in tun and len(tun) <= 12
+
+
 def test_search_walks_up_when_the_deepest_wins(native):
     """HBM-bound fp32: the deepest tuned depth wins, so the walk goes up to kmax."""
     s, cost, pre, tun = search(480, 24, lambda k: 1.05 * hbm_bound(k), hbm_bound)

@@ -74,6 +74,7 @@ def main():
         out.setdefault("wall_us", {})[variant] = {"median": statistics.median(walls), "min": min(walls),
                                                   "max": max(walls)}
         out.setdefault("enqueue_us", {})[variant] = statistics.median(enq)
+        out.setdefault("first_us", walls[0])  # the first step() after prepare()
     s.set_timing(True)
     spans = []
     for _ in range(args.reps):
