@@ -1570,10 +1570,13 @@ void Solver::prepare(int64_t n) {
     // or an idle gap runs at lower clocks (32768^2 fp64, one depth-20 pass:
     // 6.4 ms after a compute-bound cycle, 6.8 ms after a depth-5 one, 7.5 ms
     // after 0.5 s idle; profiles/depth_schedule.md). Trial cycles of its first
-    // depths (>= 3 cycles and ~20 ms), state untouched.
+    // depths, state untouched.
     synchronize();
+    // (>= 3 cycles, until ~100 ms or 64 cycles: the 8-rank slab's one 0.6 ms
+    // cycle ran 4252 Gpts/s after 33 of them (20 ms), 4348 after 64 — means of
+    // 4 and 10 interleaved runs, profiles/r5/m/, r5/n/)
     float ms = 0.f;
-    for (size_t i = 0; i < 64 && (i < 3 || ms < 20.f); ++i) {
+    for (size_t i = 0; i < 64 && (i < 3 || ms < 100.f); ++i) {
       const int k = (*s)[i % s->size()];
       trial_cycle(split_plan(k));
       ms += tuned_ms_[k] > 0.f ? tuned_ms_[k] : 1.f;  // local estimate: no collective here
