@@ -8,7 +8,7 @@ showed that first step 17-56 us slower than the median of back-to-back ones
 GPU span of the cycle from the solver's phase timers (hipEvents), for
 `--reps` steps right after prepare(), optionally after an idle pause.
 
-    python tools/first_step.py [--transport rccl|self] [--rows 4096] [--idle-ms 0] [--json out.json]
+    python tools/first_step.py [--transport rccl|self] [--rows 4096] [--idle-ms 0] [--spin-ms 0] [--json out.json]
 """
 import argparse
 import json
@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--idle-ms", type=float, default=0.0, help="sleep between prepare() and the first rep")
     ap.add_argument("--timers", type=int, default=1, help="phase timers on (GPU spans) or off (wall only)")
+    ap.add_argument("--spin-ms", type=float, default=0.0,
+                    help="busy-wait the host this long right before the first rep (CPU out of its idle state)")
     ap.add_argument("--json", default="")
     args = ap.parse_args()
     import torch
@@ -50,8 +52,12 @@ def main():
     if args.idle_ms > 0:
         time.sleep(args.idle_ms / 1e3)
     reps = []
-    for _ in range(args.reps):
+    for i in range(args.reps):
         torch.cuda.synchronize()
+        if i == 0 and args.spin_ms > 0:
+            te = time.perf_counter() + args.spin_ms / 1e3
+            while time.perf_counter() < te:
+                pass
         t0 = time.perf_counter()
         s.step(args.steps)
         te = time.perf_counter()
@@ -65,7 +71,8 @@ def main():
         reps.append(r)
     s.close()
     tr.close()
-    out = {"transport": args.transport, "rows": args.rows, "idle_ms": args.idle_ms, "timers": args.timers, "reps": reps}
+    out = {"transport": args.transport, "rows": args.rows, "idle_ms": args.idle_ms, "spin_ms": args.spin_ms,
+           "timers": args.timers, "reps": reps}
     line = json.dumps(out)
     print(line)
     if args.json:
