@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--timers", type=int, default=1, help="phase timers on (GPU spans) or off (wall only)")
     ap.add_argument("--spin-ms", type=float, default=0.0,
                     help="busy-wait the host this long right before the first rep (CPU out of its idle state)")
+    ap.add_argument("--pre-launch", type=int, default=0,
+                    help="launch N tiny torch kernels (and synchronise) right before the first rep")
     ap.add_argument("--json", default="")
     args = ap.parse_args()
     import torch
@@ -54,6 +56,11 @@ def main():
     reps = []
     for i in range(args.reps):
         torch.cuda.synchronize()
+        if i == 0 and args.pre_launch > 0:
+            x = torch.zeros(16, device="cuda:0")
+            for _ in range(args.pre_launch):
+                x.add_(1.0)
+            torch.cuda.synchronize()
         if i == 0 and args.spin_ms > 0:
             te = time.perf_counter() + args.spin_ms / 1e3
             while time.perf_counter() < te:
