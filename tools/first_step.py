@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rows", type=int, default=4096)
     ap.add_argument("--n", type=int, default=32768)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--row0", type=int, default=-1, help="the slab's first global row (default: the middle slab)")
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--idle-ms", type=float, default=0.0, help="sleep between prepare() and the first rep")
     ap.add_argument("--timers", type=int, default=1, help="phase timers on (GPU spans) or off (wall only)")
@@ -45,7 +46,8 @@ def main():
     tr = {"rccl": lambda: RcclLoopTransport(0), "ipc": lambda: IpcLoopTransport(0), "self": SelfTransport}[args.transport]()
     rows = args.rows if args.rows < args.n else None
     s = HeatSolver(prob, dtype="fp64", backend="hip", transport=tr, device=0, rows=rows,
-                   slab_row0=(args.n - rows) // 2 if rows else None, arith="jacobi", graph=False)
+                   slab_row0=(args.row0 if args.row0 >= 0 else (args.n - rows) // 2) if rows else None,
+                   arith="jacobi", graph=False)
     s.step(5)
     s.synchronize()
     s.prepare(args.steps)
