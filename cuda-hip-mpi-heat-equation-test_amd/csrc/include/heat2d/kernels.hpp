@@ -100,6 +100,10 @@ SplitPlan plan_split(DType dt, const SlabLayout& L, int k, int64_t band, int cus
 // where the second launch costs more than it saves.
 SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int ring_override = 0, int64_t bands = 0,
                       int arith = 0);
+// Whether the plan's boundary-band launch runs on the interior kernel (its
+// bands clear of the global frame rows: every middle rank) rather than the
+// general one (1 wave/SIMD at deep fp64 depths).
+bool edges_on_main(const SlabLayout& L, const SplitPlan& p);
 // queue: 2 device counters (zeroed once) for plans with flags & kPlanDynamic (dynamic items)
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr);

@@ -610,6 +610,10 @@ bool edges_on_main(const SlabLayout& L, int k, const TbRect* R, int n) {
   return true;
 }
 
+bool edges_on_main(const SlabLayout& L, const SplitPlan& p) {
+  return (p.valid == 1 || p.valid == 3) && edges_on_main(L, p.k, p.edge, p.nedge);
+}
+
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith, uint32_t* queue) {
   // (SplitPlan::flags & kPlanDynamic: the main part takes its items from the dynamic queue)

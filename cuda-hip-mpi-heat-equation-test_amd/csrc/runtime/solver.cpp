@@ -967,8 +967,14 @@ void Solver::launch_overlap(int k, int64_t B) {
   roctxRangePushA("heat2d.cycle.split");
   PhaseEvents* pe = timing_ ? phase_begin(0) : nullptr;
   pend_pe_ = pe ? (int64_t)phase_ev_.size() - 1 : -1;
+  // (the first cycle leads only where the band launch runs on the interior
+  // kernel: a slab at the global frame (the first / last rank) bands on the
+  // general kernel, whose 1-wave/SIMD waves issued first hold the register
+  // files of ~750 SIMDs against the interior — 850 us instead of 615 for its
+  // one-cycle step, edge-first 640: profiles/r5/ad/)
   const bool lead = (sp.valid == 1 || sp.valid == 3) &&
-                    ((sp.flags & kern::kPlanLead) || (first_cycle_ && tr_->exchanges() && lead_first()));
+                    ((sp.flags & kern::kPlanLead) ||
+                     (first_cycle_ && tr_->exchanges() && lead_first() && kern::edges_on_main(L_, sp)));
   first_cycle_ = false;
   if (sp.valid == 3 && !lead) {
     // edge-first: compute stream = [exchange c-1 landed] bands(c) -> interior(c);
