@@ -104,6 +104,11 @@ SplitPlan plan_single(DType dt, const SlabLayout& L, int k, int cus = 0, int rin
 // bands clear of the global frame rows: every middle rank) rather than the
 // general one (1 wave/SIMD at deep fp64 depths).
 bool edges_on_main(const SlabLayout& L, const SplitPlan& p);
+// One boundary-band rect of the plan alone, on the interior kernel where it
+// stays clear of the global frame rows, else the general one (edge ranks).
+bool edge_rect_on_main(const SlabLayout& L, const SplitPlan& p, int i);
+void launch_edge_rect(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, int i, double r,
+                      hipStream_t stream, int arith = 0);
 // queue: 2 device counters (zeroed once) for plans with flags & kPlanDynamic (dynamic items)
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr);

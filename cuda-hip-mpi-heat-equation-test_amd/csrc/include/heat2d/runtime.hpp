@@ -471,6 +471,8 @@ class Solver {
   // the launched, not yet finished cycle (cycle_launch -> cycle_finish)
   enum class Pending { None, Serial, Concurrent, EdgeFirst };
   Pending pend_ = Pending::None;
+  int pend_frame_ = -1;  // edge-rank lead cycle: the frame-side band rect cycle_finish launches after the exchange
+  int64_t pend_frame_b_ = 0;  // ... of the plan split_plan_banded(pend_k_, pend_frame_b_)
   int pend_k_ = 0;
   int64_t pend_pe_ = -1;  // index into phase_ev_ (timing) or -1
   int64_t hist_[kMaxTB + 1] = {};

@@ -614,6 +614,20 @@ bool edges_on_main(const SlabLayout& L, const SplitPlan& p) {
   return (p.valid == 1 || p.valid == 3) && edges_on_main(L, p.k, p.edge, p.nedge);
 }
 
+bool edge_rect_on_main(const SlabLayout& L, const SplitPlan& p, int i) {
+  return i >= 0 && i < p.nedge && edges_on_main(L, p.k, &p.edge[i], 1);
+}
+
+void launch_edge_rect(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, int i, double r,
+                      hipStream_t stream, int arith) {
+  HEAT2D_REQUIRE(i >= 0 && i < p.nedge, "edge rect index");
+  const TbRect& R = p.edge[i];
+  const bool on_main = edges_on_main(L, p.k, &R, 1);
+  const int64_t items = R.nb > 0 ? R.nb * (R.s1 - R.s0) : -R.nb;
+  const int64_t slots = (int64_t)cu_count() * occupancy(dt, p.ring, on_main, p.k, arith) * 4;
+  launch_rects(dt, src, dst, L, p.k, p.ring, on_main, &R, 1, std::min<int64_t>(items, slots), r, stream, arith);
+}
+
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith, uint32_t* queue) {
   // (SplitPlan::flags & kPlanDynamic: the main part takes its items from the dynamic queue)

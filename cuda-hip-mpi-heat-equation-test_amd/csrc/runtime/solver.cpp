@@ -390,6 +390,12 @@ void Solver::cycle_finish() {
     if (pend_ == Pending::EdgeFirst) H2D_HIP(hipStreamWaitEvent(s_comm_, ev_bnd_, 0));
     exchange_on(dst, pend_x_, s_comm_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[5], s_comm_));
+    if (pend_frame_ >= 0) {  // the edge rank's frame-side band (launch_overlap), after the exchange
+      kern::launch_edge_rect(dtype(), buf_[cur_], dst, L_, split_plan_banded(pend_k_, pend_frame_b_), pend_frame_, cfg_.r,
+                             s_comm_, cfg_.arith);
+      H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));  // the next cycle's interior waits for both bands
+      pend_frame_ = -1;
+    }
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
   }
   roctxRangePop();
@@ -975,7 +981,34 @@ void Solver::launch_overlap(int k, int64_t B) {
   const bool lead = (sp.valid == 1 || sp.valid == 3) &&
                     ((sp.flags & kern::kPlanLead) ||
                      (first_cycle_ && tr_->exchanges() && lead_first() && kern::edges_on_main(L_, sp)));
+  // An edge rank's first cycle: its two bands apart. The far band (the one
+  // the exchange sends, clear of the global frame) leads on the interior
+  // kernel as on a middle rank; the frame-side band — which no exchange
+  // reads — goes on the general kernel behind the exchange on the comm
+  // stream (cycle_finish), into the wave slots the interior's last round of
+  // items leaves free.
+  int frame_rect = -1;
+  if (!lead && (sp.valid == 1 || sp.valid == 3) && first_cycle_ && tr_->exchanges() && lead_first() &&
+      sp.nedge == 2 && kern::edge_rect_on_main(L_, sp, 0) != kern::edge_rect_on_main(L_, sp, 1))
+    frame_rect = kern::edge_rect_on_main(L_, sp, 0) ? 1 : 0;
   first_cycle_ = false;
+  if (frame_rect >= 0) {
+    H2D_HIP(hipStreamWaitEvent(s_compute_, ev_bnd_, 0));  // edge part c-1
+    H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));     // main part c-1
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
+    kern::launch_edge_rect(dtype(), src, dst, L_, sp, 1 - frame_rect, cfg_.r, s_comm_, cfg_.arith);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
+    kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
+    H2D_HIP(hipEventRecord(ev_int_, s_compute_));
+    if (pe) H2D_HIP(hipEventRecord(pe->ev[3], s_comm_));
+    H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
+    if (tr_->exchanges()) tr_->post(dst, L_, ev_bnd_);
+    pend_ = Pending::Concurrent;
+    pend_frame_ = frame_rect;
+    pend_frame_b_ = B;
+    return;
+  }
   if (sp.valid == 3 && !lead) {
     // edge-first: compute stream = [exchange c-1 landed] bands(c) -> interior(c);
     // comm stream (cycle_finish) = [bands(c) done] exchange(c), beside the interior.

@@ -1,10 +1,8 @@
 #!/bin/bash
-# r5 run AF/AG: the first cycle leads only where the band launch runs on the
-# interior kernel — edge-rank slabs (general-kernel bands) now edge-first:
-# run AD's probe again, the middle-slab bench, then the whole GPU suite.
+# r5 run AG: edge ranks' first cycle with the bands apart (far band led on the interior kernel, frame-side band behind the exchange) — probe, bench, the whole GPU suite.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r5af
+O=gpurun_out/r5ag
 mkdir -p $O
 export PYTHONUNBUFFERED=1 HEAT2D_PLAN_CACHE=off
 fatal() { case $1 in 124|134|137|139) echo "fatal rc $1: stopping"; exit $1;; esac; }
