@@ -31,7 +31,16 @@ this benchmark's IC (T = 2 inside, 1 on the frame) every value stays in
 [1, 2], so sum - 4c is exact (Sterbenz) and the field is bitwise identical to
 --arith exact (GPU-checked: tests/test_jacobi.py::
 test_hip_jacobi_equals_exact_on_reference_ic). --arith auto (fma, also bitwise
-identical here) and exact remain available.
+identical here) and exact remain available. The timed field is checked
+bitwise against the run-time compiled r * sum form and against the reference
+rounding: bitwise on this IC, within the stated bound on data where sum - 4c
+rounds (--ic hotspot, the zero + hot-spot data BASELINE.json names).
+
+Multi-rank runs (--transport auto): RCCL, and the IPC transport only where
+RCCL cannot be built on every rank. Transport and solver construction are
+bounded (HEAT2D_INIT_TIMEOUT); the JSON proves the decomposition per rank:
+what RCCL reports (ncclCommCount / ncclCommUserRank / ncclCommCuDevice), the
+PCI bus id of each rank's device, its slab rows and its own timed ms.
 
 vs_baseline: the reference publishes no numbers. We divide by the
 derived reference ceiling of BASELINE.md — 50 Gpts/s per MI250X GCD for its
@@ -129,6 +138,11 @@ def main():
                     help="grid edge (use --grid under torchrun: its parser takes --n as an abbreviation), or 'max': "
                          "the memory-fit planner's largest grid (utils/memplan.py: free device memory minus a "
                          "reserve; --weak: the largest global grid on N GPUs, else the largest 1-GPU grid)")
+    ap.add_argument("--ic", default="uniform", choices=["uniform", "hotspot", "hat"],
+                    help="initial data: uniform (default) — the reference benchmark's own IC, T = 2 inside a "
+                         "Dirichlet T = 1 frame (fortran/hip/heat.F90:274-282); hotspot — the zero field with a "
+                         "unit hot spot BASELINE.json names (utils/config.make_ic); hat — the serial solver's "
+                         "T = 2 box in T = 1 (fortran/serial/heat.f90:40-48)")
     ap.add_argument("--sigma", type=float, default=0.25,
                     help="input.dat sigma (= r, the FTCS coefficient); the reference's inputs all use 0.25")
     ap.add_argument("--weak", action="store_true",
@@ -158,15 +172,19 @@ def main():
                     help="record hipEvent phase timers in the timed region and report them (adds event records)")
     ap.add_argument("--rows", type=int, default=0,
                     help="with --rehearse-comm: rows of the slab (e.g. 4096 = one of 8 ranks of 32768)")
+    ap.add_argument("--slab-pos", default="middle", choices=["first", "middle", "last"],
+                    help="with --rehearse-comm --rows R: which rank's slab of the grid the rehearsal owns — the "
+                         "first / last (the global frame row on one side, rank 0 / N-1) or a middle one")
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"],
                     help="cpu: the same harness on the native CPU twin over gloo (CI rehearsal of the "
                          "multi-process path: tests/test_bench_contract.py); not a performance number")
-    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "ipc", "peer"],
+    ap.add_argument("--transport", default="auto", choices=["auto", "best", "rccl", "ipc", "peer"],
                     help="halo exchange between rank processes: rccl (RCCL send/recv over xGMI), ipc (alias peer: "
                          "no RCCL, the neighbours' fields mapped through hipIpc handles, halos pulled by device "
-                         "copies ordered by stream-side counters; capturable into hipGraphs), or auto (default): "
-                         "build both, time the real timed loop with each (MAX over ranks) and keep the faster; a "
-                         "transport that fails to initialise on any rank is skipped on every rank")
+                         "copies ordered by stream-side counters; capturable into hipGraphs), auto (default): RCCL, "
+                         "and IPC only where RCCL cannot be built on every rank (a transport that fails to "
+                         "initialise on any rank is skipped on every rank), or best: build both, time the real "
+                         "timed loop with each (MAX over ranks) and keep the faster")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank on GPU 0: the exact multi-process path on a 1-GPU box (RCCL refuses two ranks "
                          "on one GPU, so auto falls back to ipc); a correctness / overhead rehearsal, not a node "
@@ -189,6 +207,8 @@ def main():
                     help="1 GPU only: run the multi-GPU schedule (bands + RCCL self-exchange beside a CU-masked "
                          "interior) to measure its per-rank cost; not the headline (periodic halo)")
     args = ap.parse_args()
+    import faulthandler
+    faulthandler.enable()  # Python stacks on a fatal signal (the native library adds its backtrace)
     if args.transport == "peer":
         args.transport = "ipc"
     if args.graph == "on":  # replay every measured schedule, long cycles too
@@ -273,12 +293,14 @@ def main():
         if args.weak:
             n_glob = int(round(n_per_gpu * math.sqrt(world)))
     inp = heat2d.InputDat(n=n_glob, sigma=args.sigma, nu=0.05, dom_len=1.0, ntime=args.steps, soln=0, nfields=6)
-    prob = heat2d.make_problem(inp, "ghost", "uniform")
+    prob = heat2d.make_problem(inp, "ghost", args.ic)
     arith = args.arith if args.arith != "bench" else ("jacobi" if prob.r == 0.25 else "auto")
     rows = args.rows if (args.rows and world == 1) else None
     # a rehearsal of one rank's slab is a MIDDLE slab of the grid (interior
     # boundary bands, as on rank 3 of 8); --rows alone is a standalone rows x n grid
-    slab_row0 = (prob.n_owned - rows) // 2 if (rows and args.rehearse_comm) else None
+    slab_row0 = None
+    if rows and args.rehearse_comm:
+        slab_row0 = {"first": 0, "middle": (prob.n_owned - rows) // 2, "last": prob.n_owned - rows}[args.slab_pos]
 
     def make_transport(kind):
         if kind == "rccl":
@@ -306,6 +328,8 @@ def main():
                           device=device if hip else None, rows=rows, comm_cus=args.comm_cus, arith=arith,
                           slab_row0=slab_row0)
 
+    own_s = [0.0]  # this rank's own seconds of the last timed run (the JSON's per-rank proof)
+
     def timed(s):
         # no collector pause inside a sub-ms timed region (and no gc.collect()
         # here: its pause idles the GPU, whose clocks then drop before a 3 ms
@@ -319,19 +343,28 @@ def main():
         t1 = time.perf_counter()
         barrier()
         gc.enable()
+        own_s[0] = t1 - t0
         return amax(t1 - t0)
 
     live = {}  # kind -> (transport, solver, prepare seconds)
     warm_s = {}  # kind -> warm-up seconds
 
+    init_timeout = float(os.environ.get("HEAT2D_INIT_TIMEOUT", "300"))
+
     def setup(kind):
         """Transport + solver + warm-up + prepare(steps), each phase collective:
-        a failure on any rank raises Skip on every rank."""
-        tr, why = select.try_collective(lambda: make_transport(kind), amin,
-                                        cleanup=lambda t: (t.abort("another rank failed to initialise"), t.close()))
+        a failure on any rank raises Skip on every rank. Construction is
+        bounded (select.deadline, HEAT2D_INIT_TIMEOUT, default 300 s): a rank
+        blocked inside a native init call (RCCL bootstrap, an IPC import) exits
+        non-zero and the launcher stops the others — no hang."""
+        with select.deadline(init_timeout, f"{kind} transport construction", rank):
+            tr, why = select.try_collective(lambda: make_transport(kind), amin,
+                                            cleanup=lambda t: (t.abort("another rank failed to initialise"),
+                                                               t.close()))
         if why is not None:
             raise select.Skip(why)
-        s, why = select.try_collective(lambda: build(kind, tr), amin, cleanup=lambda x: x.close())
+        with select.deadline(init_timeout, f"{kind} solver construction (field allocation, peer attach)", rank):
+            s, why = select.try_collective(lambda: build(kind, tr), amin, cleanup=lambda x: x.close())
         if why is not None:
             tr.close()
             raise select.Skip(why)
@@ -367,9 +400,13 @@ def main():
                     release(kind)
             return ms
 
-        chosen, choice_report = select.choose_transport(cands, trial, amin, amax)
+        chosen, choice_report = select.choose_transport(cands, trial, amin, amax,
+                                                        first_working=args.transport != "best")
         if chosen is None:
-            raise SystemExit(f"bench.py: no transport works on every rank: {choice_report}")
+            # exit without interpreter teardown: a candidate's native init may
+            # still be blocked on a helper thread (the bounded IPC attach)
+            print(f"bench.py: no transport works on every rank: {choice_report}", file=sys.stderr, flush=True)
+            os._exit(3)
         for k in list(live):
             if k != chosen:
                 release(k)
@@ -402,7 +439,7 @@ def main():
         native.call("heat2d_read", buf.data_ptr(), 16, sink.data_ptr(), None, 1)
         torch.cuda.synchronize()
 
-    def measure_hbm(elapsed):
+    def measure_hbm(elapsed, nrows, ncols):
         """DRAM bytes of the timed region: two child processes re-run this
         bench (same flags, this run's plans and schedule from the plan cache,
         HEAT2D_PLAN_CACHE_TRUST: no re-timing under the profiler) under
@@ -420,7 +457,20 @@ def main():
         rocprof = shutil.which("rocprofv3")
         if not rocprof:
             return {"error": "rocprofv3 not found"}
-        argv = [a for a in sys.argv[1:] if a != "--measure-hbm"]
+        # the parent's resolved grid (a child planning --grid max itself would see
+        # less free memory), everything else as given
+        argv, skip = [], False
+        for a in sys.argv[1:]:
+            if skip:
+                skip = False
+                continue
+            if a in ("--n", "--grid"):
+                skip = True
+                continue
+            if a == "--measure-hbm" or a == "--weak" or a.startswith(("--n=", "--grid=")):
+                continue
+            argv.append(a)
+        argv += ["--grid", str(n_glob)]
         out = {"method": "rocprofv3 --pmc FETCH_SIZE (x2) / WRITE_SIZE over the stencil dispatches of two "
                          "profiled re-runs of the timed region (same plans); rate over this run's timed seconds"}
         tot = {}
@@ -452,11 +502,15 @@ def main():
                    and r["Counter_Name"] == ctr]
             tot[ctr] = sum(float(r["Counter_Value"]) for r in sel) * 1024.0  # KiB
             out[ctr.lower() + "_dispatches"] = len({r["Dispatch_Id"] for r in sel})
-            out["child_cycles"] = json.load(open(info))["cycles"]
+            child = json.load(open(info))
+            if (child.get("n"), child.get("nrows")) != (n_glob, nrows):
+                return dict(out, error=f"{ctr}: the profiled child ran n={child.get('n')} nrows={child.get('nrows')}, "
+                                       f"not this run's n={n_glob} nrows={nrows}")
+            out["child_cycles"] = child["cycles"]
         shutil.rmtree(work, ignore_errors=True)
         rd, wr = 2.0 * tot["FETCH_SIZE"], tot["WRITE_SIZE"]
         es = 8 if args.dtype == "fp64" else 4
-        field = float(s.nrows) * s.ncols * es
+        field = float(nrows) * ncols * es
         out.update({"read_bytes": rd, "write_bytes": wr, "read_over_field_per_cycle":
                     round(rd / field / max(1, sum(out["child_cycles"].values())), 4),
                     "gb_per_s": round((rd + wr) / elapsed / 1e9, 1)})
@@ -513,11 +567,13 @@ def main():
         slab_row0_run = slab_row0
         t0 = time.perf_counter()
         out = select.check_timed_field(s, make_ref, total, arith=arith_name(prob.r, arith), r=prob.r,
-                                       dtype=args.dtype, t0_absmax=2.0, full=full, amax=amax,
-                                       asum=lambda v: reduce(v, dist.ReduceOp.SUM), window=args.window_rows)
+                                       dtype=args.dtype, t0_absmax=prob.ic.absmax(), full=full, amax=amax,
+                                       asum=lambda v: reduce(v, dist.ReduceOp.SUM), window=args.window_rows,
+                                       sterbenz=prob.ic.sterbenz_safe())
         out["seconds"] = round(time.perf_counter() - t0, 2)
         if not hip:
-            out["engine"] = out["engine"].replace("jit", "cpu")
+            for d in [out] + [v for k, v in out.items() if k.startswith("vs_")]:
+                d["engine"] = d["engine"].replace("jit", "cpu")
         return out
 
     tr, s, prepare_s = live[kind]
@@ -532,7 +588,8 @@ def main():
         elapsed = timed(s)
         hbm_marker()
         with open(args.hbm_child, "w") as f:
-            json.dump({"elapsed": elapsed, "cycles": {str(k): c for k, c in s.cycle_hist().items()}}, f)
+            json.dump({"elapsed": elapsed, "cycles": {str(k): c for k, c in s.cycle_hist().items()}, "n": n_glob,
+                       "nrows": s.nrows}, f)
         s.close()
         tr.close()
         return
@@ -572,16 +629,23 @@ def main():
     measured = s.schedule(args.steps) is not None
     # a measured schedule of long cycles launches eagerly even with graph=True
     replayed = bool(uses_graph(kind)) and (s.schedule_replayed(args.steps) if measured else True)
+    # per-rank proof of the decomposition (what the fabric reports, devices, own timings)
+    gather = ((lambda me: (lambda out: (dist.all_gather_object(out, me), out)[1])([None] * world))
+              if world > 1 else (lambda me: [me]))
+    proof = select.rank_report(gather, rank=rank, device=device if hip else None, transport=tr, rows=s.nrows,
+                               row0=s.row0, timed_s=own_s[0], extra={"transport": tr.name})
     field_check = None
     if args.field_check != "off":
         field_check = timed_field_check(s, kind)
-    hbm = None
-    if args.measure_hbm:
-        hbm = (measure_hbm(elapsed) if hip and world == 1
-               else {"error": "--measure-hbm profiles single-rank GPU runs"})
+    nrows_run, ncols_run = s.nrows, s.ncols
     s.close()
     tr.close()
     live.clear()
+    hbm = None
+    if args.measure_hbm:
+        # (after this run's solver is gone: the profiled children get the whole GPU)
+        hbm = (measure_hbm(elapsed, nrows_run, ncols_run) if hip and world == 1
+               else {"error": "--measure-hbm profiles single-rank GPU runs"})
     verify = None
     if args.verify == "on":
         # the chosen transport kind and rank layout on a small uneven problem
@@ -603,18 +667,21 @@ def main():
             "scaling": "weak" if args.weak else "strong",
             "vs_baseline": round(gpts / (REF_GPTS_PER_RANK * world), 3),
             "dtype": args.dtype,
-            "data": "synthetic (reference benchmark IC: T=2 interior, Dirichlet T=1 frame)",
+            "data": {"uniform": "synthetic (reference benchmark IC: T=2 interior, Dirichlet T=1 frame)",
+                     "hotspot": "synthetic (zero field + unit hot spot on [0.4, 0.6]^2 L, zero Dirichlet frame)",
+                     "hat": "synthetic (fortran/serial IC: T=2 on [0.5, 1.5]^2, T=1 elsewhere)"}[args.ic],
             "config": {
                 "model": (f"heat2d FTCS 5-point, weak scaling: {n_per_gpu}^2 points per GPU (global {n_glob}^2)"
                           + (" — the memory-fit planner's largest grid" if mem_plan else "") if args.weak
                           else "heat2d FTCS 5-point, fortran/hip/input.dat (32768 0.25 0.05 1.0 25000 0)"
-                          if n_glob == 32768 and args.sigma == 0.25
-                          else f"heat2d FTCS 5-point, {n_glob}^2 (sigma {args.sigma:g}, nu 0.05, L 1.0)"),
+                          if n_glob == 32768 and args.sigma == 0.25 and args.ic == "uniform"
+                          else f"heat2d FTCS 5-point, {n_glob}^2 (sigma {args.sigma:g}, nu 0.05, L 1.0, IC {args.ic})"),
                 "grid": [rows or prob.n_owned, prob.n_owned],
                 "global_batch": 1,
                 "seq_len": prob.n_owned,
                 "sigma": args.sigma,
-                "parallelism": f"slab{world}" + ("-rehearsal" if args.rehearse_comm and world == 1 else "")
+                "ic": args.ic,
+                "parallelism": f"slab{world}" + (f"-rehearsal-{args.slab_pos}" if args.rehearse_comm and world == 1 else "")
                                + ("-shared-gpu" if args.share_gpu and world > 1 else ""),
                 "transport": tr.name,
                 "transport_choice": (dict(choice_report, chosen=kind, requested=args.transport)
@@ -642,6 +709,14 @@ def main():
             "verified": None if verify is None else verify["verified"],
             "verify": verify,
             "timed_field_check": field_check,
+            # proof of the decomposition: what the fabric reports per rank
+            # (RCCL: ncclCommCount / ncclCommUserRank / ncclCommCuDevice), the
+            # devices' PCI bus ids, slab rows and each rank's own timed ms
+            "rccl_nranks": proof["fabric_nranks"] if proof["fabric_kind"] == "rccl" else None,
+            "fabric": {"kind": proof["fabric_kind"], "nranks": proof["fabric_nranks"]},
+            "distinct_devices": proof["distinct_devices"],
+            "rank_timed_ms": proof["timed_ms"],
+            "per_rank": proof["ranks"],
             "memory_plan": mem_plan,
             "baseline_basis": "BASELINE.md derived ceiling 50 Gpts/s per MI250X GCD x n_gpus",
         }

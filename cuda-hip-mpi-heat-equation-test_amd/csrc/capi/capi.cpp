@@ -4,6 +4,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -67,6 +71,41 @@ struct TransportHandle {
 extern "C" {
 
 const char* heat2d_last_error(void) { return g_err.c_str(); }
+
+// Native backtrace on a fatal signal (SIGABRT from glibc's heap checks such
+// as "free(): invalid pointer", SIGSEGV, SIGBUS, SIGFPE, SIGILL): the frames
+// name the library that called free(), which Python's faulthandler (Python
+// frames only) cannot. Then the previous handler runs (faulthandler, or the
+// default action), so the exit status stays the signal's.
+namespace {
+struct sigaction g_prev_sig[65];
+void crash_handler(int sig, siginfo_t*, void*) {
+  static const char head[] = "\nheat2d: fatal signal, native backtrace:\n";
+  (void)!::write(2, head, sizeof(head) - 1);
+  void* frames[64];
+  const int n = ::backtrace(frames, 64);
+  ::backtrace_symbols_fd(frames, n, 2);
+  ::sigaction(sig, &g_prev_sig[sig], nullptr);
+  ::raise(sig);
+}
+}  // namespace
+
+int heat2d_install_crash_handler(void) {
+  return guarded([&] {
+    static std::once_flag once;
+    std::call_once(once, [] {
+      void* warm[2];
+      (void)::backtrace(warm, 2);  // load libgcc's unwinder now, not inside the handler
+      for (int sig : {SIGABRT, SIGSEGV, SIGBUS, SIGFPE, SIGILL}) {
+        struct sigaction sa {};
+        sa.sa_sigaction = crash_handler;
+        sa.sa_flags = SA_SIGINFO | SA_NODEFER;
+        sigemptyset(&sa.sa_mask);
+        ::sigaction(sig, &sa, &g_prev_sig[sig]);
+      }
+    });
+  });
+}
 int heat2d_version(void) { return 100; }
 int heat2d_max_tb(void) { return kMaxTB; }
 
@@ -232,6 +271,24 @@ int heat2d_transport_ipc_loop(int device, void** out) {
 
 int heat2d_transport_free(void* t) {
   return guarded([&] { delete static_cast<TransportHandle*>(t); });
+}
+
+int heat2d_transport_info(void* t, int32_t* out4) {
+  return guarded([&] {
+    const Transport::FabricInfo f = static_cast<TransportHandle*>(t)->t->fabric_info();
+    out4[0] = f.kind;
+    out4[1] = f.nranks;
+    out4[2] = f.rank;
+    out4[3] = f.device;
+  });
+}
+
+int heat2d_device_pci_bus_id(int device, char* out, int64_t cap) {
+  return guarded([&] {
+    HEAT2D_REQUIRE(cap >= 16, "PCI bus id buffer too small");
+    const hipError_t e = hipDeviceGetPCIBusId(out, (int)cap, device);
+    if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("hipDeviceGetPCIBusId: ") + hipGetErrorString(e));
+  });
 }
 
 int heat2d_solver_create(const heat2d_config* cfg, void* transport, void** out) {

@@ -62,6 +62,9 @@ typedef int (*heat2d_allreduce_fn)(void* ctx, double* vals, int32_t n, int32_t o
 typedef int (*heat2d_barrier_fn)(void* ctx);
 
 const char* heat2d_last_error(void);
+/* print a native backtrace to stderr on SIGABRT / SIGSEGV / SIGBUS / SIGFPE / SIGILL, then chain to the
+   previous handler (idempotent) */
+int heat2d_install_crash_handler(void);
 int heat2d_version(void);
 int heat2d_max_tb(void);
 int heat2d_device_count(int* n);
@@ -121,6 +124,11 @@ int heat2d_transport_ipc(heat2d_allgather_fn ag, heat2d_allreduce_fn ar, heat2d_
                          int size, int device, void** out);
 int heat2d_transport_ipc_loop(int device, void** out);
 int heat2d_transport_free(void* t);
+/* what the fabric reports for this rank: {kind (0 host/self, 1 RCCL, 2 IPC), nranks, rank, device}
+   (RCCL: ncclCommCount / ncclCommUserRank / ncclCommCuDevice) */
+int heat2d_transport_info(void* t, int32_t* out4);
+/* hipDeviceGetPCIBusId of a device ordinal ("dddd:bb:dd.f") */
+int heat2d_device_pci_bus_id(int device, char* out, int64_t cap);
 /* fail fast: abort the transport's fabric (RCCL: ncclCommAbort); its solver's next synchronisation raises */
 int heat2d_transport_abort(void* t, const char* reason);
 /* watchdog mechanism self-test (no GPU): mode 0 = progress for progress_polls polls then a hang,

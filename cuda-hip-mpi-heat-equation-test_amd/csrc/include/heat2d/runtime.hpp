@@ -108,6 +108,15 @@ class Transport {
   // The solver's two field buffers (allocation bases, layout L): transports
   // that map their peers' fields once (IPC) do it here. Collective.
   virtual void attach(void* /*buf0*/, void* /*buf1*/, const SlabLayout& /*L*/, DType /*dt*/) {}
+  // What the fabric itself reports about this rank — the proof that a
+  // multi-GPU run really put N ranks on N devices (the reference prints
+  // "MPI rank r using GPU d", fortran/hip/heat.F90:125). kind: 0 host / self,
+  // 1 RCCL (ncclCommCount / ncclCommUserRank / ncclCommCuDevice), 2 IPC (its
+  // rank / size and the device it mapped its peers on); device -1: none.
+  struct FabricInfo {
+    int32_t kind, nranks, rank, device;
+  };
+  virtual FabricInfo fabric_info() { return {0, size(), rank(), -1}; }
 };
 
 // RAII bracket of Transport::io_phase.
@@ -458,6 +467,10 @@ class Solver {
   bool own_streams_ = false;
   bool first_cycle_ = false;  // the next launch_overlap is a step() call's first cycle (lead_first)
   hipEvent_t ev_bnd_ = nullptr, ev_comm_ = nullptr, ev_int_ = nullptr;
+  // an edge rank's first-cycle frame-side band (cycle_finish): its own event,
+  // so ev_bnd_ — which receiver-driven transports wait on after post() — keeps
+  // marking only the bands the exchange sends
+  hipEvent_t ev_frame_ = nullptr;
   double* d_work_ = nullptr;   // stats workspace + 6 results
   bool timing_ = false;
   struct PhaseEvents {

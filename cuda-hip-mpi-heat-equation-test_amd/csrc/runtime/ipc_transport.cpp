@@ -31,6 +31,8 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -109,6 +111,7 @@ class IpcTransport final : public Transport {
   }
   void io_phase(bool on) override { io_ += on ? 1 : -1; }
   void graph_launched(hipStream_t stream) override { track(stream, "graph replay"); }
+  FabricInfo fabric_info() override { return {2, size_, rank_, device_}; }
 
   void attach(void* buf0, void* buf1, const SlabLayout& L, DType dt) override {
     if (size_ == 1 && !loop_) return;
@@ -175,9 +178,8 @@ class IpcTransport final : public Transport {
         if (p < 0 || p >= size_) continue;
         HEAT2D_REQUIRE(all[(size_t)p].L.pitch == L.pitch, "IPC transport: slabs of different pitch");
         peer_L_[p > rank_] = all[(size_t)p].L;
-        for (int b = 0; b < 2; ++b)
-          H2D_HIP(hipIpcOpenMemHandle(&peer_buf_[p > rank_][b], all[(size_t)p].buf[b], hipIpcMemLazyEnablePeerAccess));
       }
+      open_peers(all);
     } catch (const std::exception& e) {
       err = e.what();
     }
@@ -260,6 +262,60 @@ class IpcTransport final : public Transport {
   }
 
  private:
+  // hipIpcOpenMemHandle of the neighbours' fields, on a helper thread with a
+  // deadline. Four rank processes sharing one GPU at 32768^2 once stayed
+  // inside the import of a neighbour's 2 GB field for good (profiles/r5/x/):
+  // nothing above this call could bound it. Now a rank whose opens have not
+  // returned within HEAT2D_IPC_ATTACH_TIMEOUT seconds (default 60; an open
+  // takes milliseconds) fails the attach, the collective verdict in attach()
+  // turns that into a failure on EVERY rank, and the caller skips the
+  // transport (bench.py: the next candidate, or a clean exit). The stuck
+  // thread is left behind, detached: it writes only into its own shared
+  // state, never into this object. HEAT2D_IPC_ATTACH_STALL=<rank> makes that
+  // rank's opens hang (tests of the bounded path).
+  void open_peers(const std::vector<IpcCard>& all) {
+    struct Opened {
+      std::mutex mu;
+      std::condition_variable cv;
+      bool done = false;
+      std::string err;
+      void* ptr[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    };
+    auto st = std::make_shared<Opened>();
+    std::vector<std::pair<int, IpcCard>> peers;
+    for (int p : {rank_ - 1, rank_ + 1})
+      if (p >= 0 && p < size_) peers.emplace_back(p > rank_ ? 1 : 0, all[(size_t)p]);
+    const char* sv = std::getenv("HEAT2D_IPC_ATTACH_STALL");
+    const bool stall = sv && *sv && std::atoi(sv) == rank_;
+    const int dev = device_;
+    std::thread([st, peers, dev, stall] {
+      std::string err;
+      void* ptr[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+      try {
+        H2D_HIP(hipSetDevice(dev));
+        while (stall) std::this_thread::sleep_for(std::chrono::seconds(1));
+        for (const auto& pc : peers)
+          for (int b = 0; b < 2; ++b)
+            H2D_HIP(hipIpcOpenMemHandle(&ptr[pc.first][b], pc.second.buf[b], hipIpcMemLazyEnablePeerAccess));
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      std::lock_guard<std::mutex> g(st->mu);
+      std::memcpy(st->ptr, ptr, sizeof(ptr));
+      st->err = err;
+      st->done = true;
+      st->cv.notify_all();
+    }).detach();
+    const char* tv = std::getenv("HEAT2D_IPC_ATTACH_TIMEOUT");
+    const double limit = tv && *tv ? std::atof(tv) : 60.0;
+    std::unique_lock<std::mutex> lk(st->mu);
+    if (!st->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return st->done; }))
+      fail(__FILE__, __LINE__,
+           "IPC transport: hipIpcOpenMemHandle of a neighbour's field did not return within " +
+               std::to_string(limit) + " s on rank " + std::to_string(rank_) + " (HEAT2D_IPC_ATTACH_TIMEOUT)");
+    std::memcpy(peer_buf_, st->ptr, sizeof(peer_buf_));  // (what did open is closed by the destructor)
+    if (!st->err.empty()) fail(__FILE__, __LINE__, st->err);
+  }
   size_t shm_size() const { return (size_t)(64 + 64 * size_ + 4095) / 4096 * 4096; }
   void map_shm(const char* name) {
     shm_bytes_ = shm_size();

@@ -38,11 +38,10 @@
 
 namespace heat2d {
 
-std::vector<int> dp_schedule(int64_t n, int kmax, const std::function<double(int)>& cost, double* total) {
-  HEAT2D_REQUIRE(n >= 1 && kmax >= 1, "dp_schedule needs n >= 1, kmax >= 1");
-  const int K = (int)std::min<int64_t>(kmax, n);
-  std::vector<double> c((size_t)K + 1, -1.0);
-  for (int k = 1; k <= K; ++k) c[(size_t)k] = cost(k);
+namespace {
+
+// The exact DP over m steps: best[m'] for every m' <= m (costs c[1..K], < 0 = unusable).
+std::vector<int> dp_exact(int64_t n, int K, const std::vector<double>& c, double* total) {
   const double inf = std::numeric_limits<double>::infinity();
   // best[m]: least cost of exactly m steps; cyc[m]: its cycle count; take[m]: its first (deepest) depth
   std::vector<double> best((size_t)n + 1, inf);
@@ -71,6 +70,46 @@ std::vector<int> dp_schedule(int64_t n, int kmax, const std::function<double(int
   if (best[(size_t)n] == inf) return {};
   std::vector<int> s;
   for (int64_t m = n; m > 0; m -= take[(size_t)m]) s.push_back(take[(size_t)m]);
+  return s;
+}
+
+}  // namespace
+
+std::vector<int> dp_schedule(int64_t n, int kmax, const std::function<double(int)>& cost, double* total) {
+  HEAT2D_REQUIRE(n >= 1 && kmax >= 1, "dp_schedule needs n >= 1, kmax >= 1");
+  const int K = (int)std::min<int64_t>(kmax, n);
+  std::vector<double> c((size_t)K + 1, -1.0);
+  for (int k = 1; k <= K; ++k) c[(size_t)k] = cost(k);
+  // Long runs (the CLI prepares ntime = 25 000 steps; 10^7 would be 200 MB and
+  // 2.4e8 inner steps per call, and the search calls the DP dozens of times):
+  // with k* the cheapest depth per step, some optimal schedule repeats every
+  // other depth fewer than k* times (k* cycles of depth k cost at least k
+  // cycles of depth k*, same steps), so its other cycles sum to under
+  // K * K * k* steps. The steps above that bound are k* cycles in some optimal
+  // schedule: they are taken as such and only the rest goes through the DP —
+  // the same least cost, in O(K^3 k*) time and memory whatever n.
+  int ks = 0;
+  for (int k = 1; k <= K; ++k) {
+    if (c[(size_t)k] < 0) continue;
+    const double per = c[(size_t)k] / k;
+    const double bper = ks ? c[(size_t)ks] / ks : 0.0;
+    if (ks == 0 || per < bper * (1.0 - 1e-12) || (per <= bper * (1.0 + 1e-12) && k > ks)) ks = k;
+  }
+  const int64_t cap = (int64_t)K * K * std::max(ks, 1);
+  std::vector<int> s;
+  if (ks > 0 && n > cap) {
+    const int64_t j = (n - cap + ks - 1) / ks;
+    double rest = 0.0;
+    s = dp_exact(n - j * ks, K, c, &rest);
+    if (!s.empty() || n - j * ks == 0) {
+      s.insert(s.end(), (size_t)j, ks);
+      if (total) *total = rest + (double)j * c[(size_t)ks];
+    } else {
+      s = dp_exact(n, K, c, total);  // (no schedule of the rest over the known depths: the whole DP)
+    }
+  } else {
+    s = dp_exact(n, K, c, total);
+  }
   std::sort(s.begin(), s.end(), std::greater<int>());
   return s;
 }

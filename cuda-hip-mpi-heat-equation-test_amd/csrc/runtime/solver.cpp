@@ -203,6 +203,7 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     H2D_HIP(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_comm_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_int_, hipEventDisableTiming));
+    H2D_HIP(hipEventCreateWithFlags(&ev_frame_, hipEventDisableTiming));
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
@@ -234,6 +235,7 @@ Solver::~Solver() {
     if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
     if (ev_int_) (void)hipEventDestroy(ev_int_);
+    if (ev_frame_) (void)hipEventDestroy(ev_frame_);
     if (ev_t0_) (void)hipEventDestroy(ev_t0_);
     if (ev_t1_) (void)hipEventDestroy(ev_t1_);
     for (auto* v : {&phase_ev_, &phase_pool_})
@@ -393,7 +395,10 @@ void Solver::cycle_finish() {
     if (pend_frame_ >= 0) {  // the edge rank's frame-side band (launch_overlap), after the exchange
       kern::launch_edge_rect(dtype(), buf_[cur_], dst, L_, split_plan_banded(pend_k_, pend_frame_b_), pend_frame_, cfg_.r,
                              s_comm_, cfg_.arith);
-      H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));  // the next cycle's interior waits for both bands
+      // the next cycle's compute-stream work waits for it (and so for the
+      // exchange ahead of it); ev_bnd_, posted to the transport, is left alone
+      H2D_HIP(hipEventRecord(ev_frame_, s_comm_));
+      H2D_HIP(hipStreamWaitEvent(s_compute_, ev_frame_, 0));
       pend_frame_ = -1;
     }
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));

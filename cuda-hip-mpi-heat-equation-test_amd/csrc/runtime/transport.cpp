@@ -104,6 +104,16 @@ class RcclTransport final : public Transport {
   // output turn is not a hung fabric); exchanges are never issued inside one
   void io_phase(bool on) override { io_ += on ? 1 : -1; }
 
+  FabricInfo fabric_info() override {
+    std::unique_lock<std::timed_mutex> lk(cmu_);
+    live();
+    int n = 0, r = 0, d = -1;
+    H2D_NCCL(ncclCommCount(comm_, &n));
+    H2D_NCCL(ncclCommUserRank(comm_, &r));
+    H2D_NCCL(ncclCommCuDevice(comm_, &d));
+    return {1, n, r, d};
+  }
+
   void check() override {
     if (aborted_) fail_aborted();
     std::unique_lock<std::timed_mutex> lk(cmu_);

@@ -155,6 +155,9 @@ _SIGS = {
     "heat2d_transport_callback": (C.c_int, [EXCHANGE_FN, ALLREDUCE_FN, BARRIER_FN, _P, C.c_int, C.c_int,
                                             C.POINTER(_P)]),
     "heat2d_transport_free": (C.c_int, [_P]),
+    "heat2d_transport_info": (C.c_int, [_P, C.POINTER(C.c_int32)]),
+    "heat2d_device_pci_bus_id": (C.c_int, [C.c_int, C.c_char_p, _I64]),
+    "heat2d_install_crash_handler": (C.c_int, []),
     "heat2d_transport_ipc_loop": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "heat2d_transport_ipc": (C.c_int, [ALLGATHER_FN, ALLREDUCE_FN, BARRIER_FN, _P, C.c_int, C.c_int, C.c_int,
                                        C.POINTER(_P)]),
@@ -256,6 +259,11 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if os.environ.get("HEAT2D_CRASH_BACKTRACE", "1") != "0":
+            # a native backtrace on SIGABRT / SIGSEGV / ... (then the previous
+            # handler, e.g. Python's faulthandler): names the library that
+            # called free() on a glibc heap-check abort
+            L.heat2d_install_crash_handler()
         _lib = L
         return _lib
 
@@ -356,6 +364,25 @@ def rccl_unique_id() -> bytes:
     buf = (C.c_ubyte * 128)()
     call("heat2d_rccl_unique_id", buf)
     return bytes(buf)
+
+
+FABRIC_KINDS = {0: "host", 1: "rccl", 2: "ipc"}
+
+
+def transport_info(handle) -> dict:
+    """What the fabric reports for this rank: kind, nranks, rank, device
+    (RCCL: ncclCommCount / ncclCommUserRank / ncclCommCuDevice)."""
+    out = (C.c_int32 * 4)()
+    call("heat2d_transport_info", handle, out)
+    return {"kind": FABRIC_KINDS.get(int(out[0]), str(out[0])), "nranks": int(out[1]), "rank": int(out[2]),
+            "device": int(out[3])}
+
+
+def pci_bus_id(device: int) -> str:
+    """hipDeviceGetPCIBusId of a device ordinal."""
+    buf = C.create_string_buffer(64)
+    call("heat2d_device_pci_bus_id", int(device), buf, 64)
+    return buf.value.decode()
 
 
 def loaded_path() -> str:

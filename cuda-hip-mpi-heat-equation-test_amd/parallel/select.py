@@ -26,6 +26,7 @@ with plain functions and with gloo ranks (tests/test_select.py).
 """
 from __future__ import annotations
 
+import contextlib
 import traceback
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -66,16 +67,23 @@ def try_collective(fn: Callable[[], object], allreduce_min: Callable[[float], fl
 
 def choose_transport(candidates: Sequence[str], trial: Callable[[str], float],
                      allreduce_min: Callable[[float], float],
-                     allreduce_max: Callable[[float], float]) -> Tuple[Optional[str], Dict[str, dict]]:
-    """Try every candidate transport with ``trial(kind) -> ms`` (it builds the
-    transport and the solver and times the real loop; raising = unusable),
-    reduce each time with MAX over ranks, and return (fastest kind, report).
-    The report holds {"ms": max-over-ranks ms} or {"error": reason} per kind,
-    identical on every rank (a failure anywhere skips the kind everywhere).
-    None if no candidate works."""
+                     allreduce_max: Callable[[float], float],
+                     first_working: bool = False) -> Tuple[Optional[str], Dict[str, dict]]:
+    """Try the candidate transports in order with ``trial(kind) -> ms`` (it
+    builds the transport and the solver and times the real loop; raising =
+    unusable), reduce each time with MAX over ranks, and return (kind, report).
+    ``first_working``: stop at the first candidate that works on every rank
+    (the later ones are fallbacks, never built — bench.py's default "auto":
+    RCCL, and IPC only where RCCL cannot be built); else time them all and
+    keep the fastest ("best"). The report holds {"ms": max-over-ranks ms},
+    {"error": reason} or {"skipped": why} per kind, identical on every rank (a
+    failure anywhere skips the kind everywhere). None if no candidate works."""
     report: Dict[str, dict] = {}
     best, best_ms = None, float("inf")
     for kind in candidates:
+        if first_working and best is not None:
+            report[kind] = {"skipped": f"{best} works on every rank ({kind} is its fallback)"}
+            continue
         ms, why = try_collective(lambda: trial(kind), allreduce_min)
         if why is not None:
             report[kind] = {"error": why}
@@ -88,17 +96,97 @@ def choose_transport(candidates: Sequence[str], trial: Callable[[str], float],
 
 
 def candidate_transports(requested: str, world: int, hip: bool) -> List[str]:
-    """Transports a run may use: one forced kind, or every GPU transport for
-    "auto" (RCCL first: the reference's own model of an MPI-style fabric; IPC
-    second). Single-rank runs have nothing to choose; CPU ranks have one
-    transport (torch.distributed host callbacks), run through the same trial."""
+    """Transports a run may use, in order: one forced kind, or both GPU
+    transports for "auto" / "best" (RCCL first: the reference's own model of
+    an MPI-style fabric; IPC second — with "auto" only as the fallback where
+    RCCL cannot be built, so a node run whose RCCL works never builds the IPC
+    mappings; "best" times both). Single-rank runs have nothing to choose; CPU
+    ranks have one transport (torch.distributed host callbacks), run through
+    the same trial."""
     if world <= 1:
         return []
     if not hip:
         return ["torch-dist"]
-    if requested == "auto":
+    if requested in ("auto", "best"):
         return ["rccl", "ipc"]
     return ["ipc" if requested in ("ipc", "peer") else "rccl"]
+
+
+EXIT_DEADLINE = 124
+
+
+@contextlib.contextmanager
+def deadline(seconds: float, what: str, rank: int = 0, on_expire: Optional[Callable[[str], None]] = None):
+    """Bound a phase that may block inside a native call no other timeout
+    covers (transport construction: RCCL bootstrap, hipIpcOpenMemHandle;
+    solver construction with its collective attach). If the phase has not
+    finished after ``seconds``, every thread's Python stack goes to stderr and
+    the process exits with status 124 (``on_expire(message)`` instead, for
+    tests): the launcher (bench.py's own, or torchrun) then stops the other
+    ranks, so a stuck rank ends the run in bounded time instead of hanging it.
+    Exiting is the only safe end: the blocked thread may hold HIP runtime
+    locks, and a GPU-initialised process is never re-exec'd. ``seconds`` <= 0:
+    unbounded."""
+    if not seconds or seconds <= 0:
+        yield
+        return
+    import faulthandler
+    import os
+    import sys
+    import threading
+    done = threading.Event()
+
+    def watch():
+        if done.wait(seconds):
+            return
+        msg = f"rank {rank}: {what} did not finish within {seconds:g} s (HEAT2D_INIT_TIMEOUT); exiting"
+        if on_expire is not None:
+            on_expire(msg)
+            return
+        sys.stderr.write(f"heat2d: {msg}\n")
+        sys.stderr.flush()
+        faulthandler.dump_traceback(all_threads=True)
+        os._exit(EXIT_DEADLINE)
+
+    t = threading.Thread(target=watch, name="heat2d-deadline", daemon=True)
+    t.start()
+    try:
+        yield
+    finally:
+        done.set()
+
+
+def rank_report(gather: Callable[[dict], List[dict]], *, rank: int, device: Optional[int], transport,
+                rows: int, row0: int, timed_s: float, extra: Optional[dict] = None) -> dict:
+    """Per-rank proof of a multi-rank run, gathered to every rank: what the
+    fabric itself reports (RCCL: ncclCommCount / ncclCommUserRank /
+    ncclCommCuDevice), the rank's device ordinal and PCI bus id, host, slab
+    rows and its own timed seconds. Summarised as {"ranks": [...],
+    "fabric_nranks": n or None (ranks disagree), "distinct_devices": k,
+    "timed_ms": {"min", "max"}} — the reference prints "MPI rank r using GPU
+    d" and "Automatic MPI decomposition: P x 1" (fortran/hip/heat.F90:125,145)."""
+    import socket
+    from ..ops import _native as N
+    me = {"rank": int(rank), "host": socket.gethostname(), "device": device, "rows": int(rows), "row0": int(row0),
+          "timed_ms": round(float(timed_s) * 1e3, 4)}
+    try:
+        me["fabric"] = N.transport_info(transport.handle)
+    except Exception as e:  # noqa: BLE001 - reported, never fatal after the timed run
+        me["fabric"] = {"error": str(e)}
+    if device is not None and device >= 0:
+        try:
+            me["pci_bus_id"] = N.pci_bus_id(device)
+        except Exception as e:  # noqa: BLE001
+            me["pci_bus_id"] = f"error: {e}"
+    if extra:
+        me.update(extra)
+    ranks = sorted(gather(me), key=lambda d: d["rank"])
+    nr = {d["fabric"].get("nranks") for d in ranks}
+    devs = {(d["host"], d.get("pci_bus_id") or d.get("device")) for d in ranks}
+    ms = [d["timed_ms"] for d in ranks]
+    return {"ranks": ranks, "fabric_nranks": nr.pop() if len(nr) == 1 else None,
+            "fabric_kind": ranks[0]["fabric"].get("kind"),
+            "distinct_devices": len(devs), "timed_ms": {"min": min(ms), "max": max(ms)}}
 
 
 def _pow2(r: float) -> bool:
@@ -106,17 +194,32 @@ def _pow2(r: float) -> bool:
     return r > 0 and math.frexp(r)[0] == 0.5
 
 
-def reference_arith(arith: str, r: float) -> Tuple[str, bool]:
-    """(arithmetic of the independent reference run, bitwise?) for a run of
-    ``arith``: the contracted form has its own one-step form (bitwise, any r);
-    the r = 1/4 form equals the reference rounding wherever sum - 4c is exact
-    (the benchmark IC: values in [1, 2]) — checked bitwise against it; the
-    scaled-level form ("fast") is checked within its stated error bound."""
+def reference_checks(arith: str, r: float, sterbenz: bool) -> List[Tuple[str, bool]]:
+    """The independent reference runs a timed field of ``arith`` is checked
+    against, as (run-time compiled one-step form, bitwise?) pairs; the first
+    one is the field check's verdict, the others are reported beside it.
+
+    * exact / fma: their own one-step forms, bitwise (any r, any data);
+    * jacobi (r = 1/4): the JIT's own r * sum form, bitwise (scaling by
+      powers of 4 is exact, so the temporal-blocked scaled levels round like
+      one step per launch), plus the reference rounding ``exact``: bitwise
+      where sum - 4c is exact (``sterbenz``: the reference IC, values in
+      [1, 2]), else within the stated bound (models/reference.fast_error_bound)
+      — on the hot-spot data BASELINE.json names (values in [0, 1]) the two
+      forms round differently and only the bound holds;
+    * fast (scaled levels, any r): the reference rounding, within the bound."""
     if arith == "fma":
-        return "fma", True
+        return [("fma", True)]
     if arith == "fast":
-        return "exact", False
-    return "exact", True
+        return [("exact", False)]
+    if arith == "jacobi":
+        return [("jacobi", True), ("exact", bool(sterbenz))]
+    return [("exact", True)]
+
+
+def reference_arith(arith: str, r: float, sterbenz: bool = True) -> Tuple[str, bool]:
+    """(arithmetic of the primary independent reference run, bitwise?)."""
+    return reference_checks(arith, r, sterbenz)[0]
 
 
 def field_windows(nrows: int, steps: int, row0: int, n_global: int, window: int = 64) -> List[Tuple[int, int, int, int]]:
@@ -140,56 +243,67 @@ def field_windows(nrows: int, steps: int, row0: int, n_global: int, window: int 
 
 def check_timed_field(timed, make_ref: Callable[..., object], steps: int, *, arith: str, r: float, dtype: str,
                       t0_absmax: float, full: bool, amax: Callable[[float], float],
-                      asum: Callable[[float], float], window: int = 64) -> dict:
-    """Check the field a timed run produced against an independent engine.
+                      asum: Callable[[float], float], window: int = 64, sterbenz: bool = True) -> dict:
+    """Check the field a timed run produced against independent engines.
 
     ``timed`` holds IC + ``steps`` steps. ``make_ref(full, rows=None,
-    slab_row0=None, arith=...)`` builds the reference solver from the same IC:
+    slab_row0=None, arith=...)`` builds a reference solver from the same IC:
     full=True — the same rank layout and transport kind as the timed run
     (collective); full=False — a single-rank solver owning global rows
-    [slab_row0, slab_row0 + rows) (see field_windows). The reference runs
+    [slab_row0, slab_row0 + rows) (see field_windows). Each reference runs
     ``steps`` steps one step per launch and the fields are compared on the
     device (HeatSolver.compare); results are reduced over ranks (``amax`` /
-    ``asum``, the same on every rank)."""
-    ref_arith, bitwise = reference_arith(arith, r)
+    ``asum``, the same on every rank). The references are
+    :func:`reference_checks` of ``arith``: the first decides "ok", the others
+    are reported under "vs_<arith>" with their own verdict (``t0_absmax``:
+    max |T| of the IC, for the error bounds; ``sterbenz``: the IC keeps every
+    sum - 4c exact)."""
     import numpy as np
     npdt = np.float64 if dtype == "fp64" else np.float32
-    diff, mism, rows = 0.0, 0.0, 0
-    if full:
-        ref = make_ref(True, arith=ref_arith)
-        try:
-            ref.step(steps)
-            ref.synchronize()
-            res = timed.compare(ref)
-        finally:
-            ref.close()
-        diff, mism, rows = res["max_abs_diff"], float(res["mismatches"]), timed.nrows
-    else:
-        for a, m, g0, nr in field_windows(timed.nrows, steps, timed.row0, timed.problem.n_owned, window):
-            ref = make_ref(False, rows=nr, slab_row0=g0, arith=ref_arith)
+
+    def one(ref_arith: str, bitwise: bool) -> dict:
+        diff, mism, rows = 0.0, 0.0, 0
+        if full:
+            ref = make_ref(True, arith=ref_arith)
             try:
                 ref.step(steps)
                 ref.synchronize()
-                res = timed.compare(ref, r0=a, nrows=m, other_r0=timed.row0 + a - g0)
+                res = timed.compare(ref)
             finally:
                 ref.close()
-            d = res["max_abs_diff"]
-            diff = d if (d != d or diff != diff) else max(diff, d)
-            mism += float(res["mismatches"])
-            rows += m
-    nan = diff != diff
-    diff = amax(float("inf") if nan else diff)
-    mism = asum(mism)
-    rows = int(asum(float(rows)))
-    out = {"mode": "full" if full else "windows", "engine": "jit-" + ref_arith, "steps": int(steps),
-           "rows_checked": rows, "max_abs_diff": diff, "mismatches": int(mism)}
-    if bitwise:
-        out["ok"] = bool(mism == 0 and diff == 0.0)
-    else:
-        from ..models import reference as R
-        bound = R.fast_error_bound(steps, npdt, t0_absmax)
-        out["bound"] = bound
-        out["ok"] = bool(diff <= bound)
+            diff, mism, rows = res["max_abs_diff"], float(res["mismatches"]), timed.nrows
+        else:
+            for a, m, g0, nr in field_windows(timed.nrows, steps, timed.row0, timed.problem.n_owned, window):
+                ref = make_ref(False, rows=nr, slab_row0=g0, arith=ref_arith)
+                try:
+                    ref.step(steps)
+                    ref.synchronize()
+                    res = timed.compare(ref, r0=a, nrows=m, other_r0=timed.row0 + a - g0)
+                finally:
+                    ref.close()
+                d = res["max_abs_diff"]
+                diff = d if (d != d or diff != diff) else max(diff, d)
+                mism += float(res["mismatches"])
+                rows += m
+        nan = diff != diff
+        diff = amax(float("inf") if nan else diff)
+        mism = asum(mism)
+        rows = int(asum(float(rows)))
+        out = {"mode": "full" if full else "windows", "engine": "jit-" + ref_arith, "steps": int(steps),
+               "rows_checked": rows, "max_abs_diff": diff, "mismatches": int(mism)}
+        if bitwise:
+            out["ok"] = bool(mism == 0 and diff == 0.0)
+        else:
+            from ..models import reference as R
+            bound = R.fast_error_bound(steps, npdt, t0_absmax)
+            out["bound"] = bound
+            out["ok"] = bool(diff <= bound)
+        return out
+
+    checks = reference_checks(arith, r, sterbenz)
+    out = one(*checks[0])
+    for ref_arith, bitwise in checks[1:]:
+        out["vs_" + ref_arith] = one(ref_arith, bitwise)
     return out
 
 

@@ -126,6 +126,16 @@ class IcSpec:
             return False
         return min(vals) > 0 and max(vals) <= 2 * min(vals)
 
+    def absmax(self) -> float:
+        """max |T| this IC puts in the field (frame included): the scale of the
+        stated error bounds (models/reference.fast_error_bound). FTCS at
+        r <= 1/4 never exceeds it."""
+        if self.kind == IC_SINE:
+            return abs(self.a)
+        if self.kind == IC_CONST:
+            return max(abs(self.a), abs(self.pad))
+        return max(abs(self.a), abs(self.b), abs(self.pad))
+
     def to_native(self):
         from ..ops import _native as N
         p = N.IcParams()

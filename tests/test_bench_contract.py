@@ -43,6 +43,13 @@ def test_bench_json_line_multi_rank(nproc, dtype):
     fc = d["timed_field_check"]
     assert fc["ok"] is True and fc["mode"] == "full" and fc["mismatches"] == 0 and fc["max_abs_diff"] == 0.0, fc
     assert fc["rows_checked"] == 100 and fc["steps"] == 28
+    # per-rank proof of the decomposition (gathered over the ranks)
+    assert d["fabric"] == {"kind": "host", "nranks": nproc} and d["rccl_nranks"] is None
+    pr = d["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(nproc)) and sum(r["rows"] for r in pr) == 100
+    assert all(r["fabric"]["rank"] == r["rank"] and r["transport"] == "torch-dist" for r in pr)
+    assert d["rank_timed_ms"]["max"] == pytest.approx(d["ms_per_step"] * 24, rel=1e-3)
+    assert d["rank_timed_ms"]["min"] <= d["rank_timed_ms"]["max"]
 
 
 def test_bench_multi_rank_times_the_same_state_as_one_rank():
@@ -162,8 +169,12 @@ def test_bench_auto_transport_falls_back_to_ipc_share_gpu():
     assert four["verified"] is True and four["verify"]["max_abs_diff"] == 0.0, four["verify"]
     # the timed field itself: 4 rank slabs vs the one-step JIT engine on the same layout and transport
     fc = four["timed_field_check"]
-    assert fc["ok"] is True and fc["mode"] == "full" and fc["engine"] == "jit-exact", fc
+    assert fc["ok"] is True and fc["mode"] == "full" and fc["engine"] in ("jit-exact", "jit-jacobi"), fc
     assert fc["mismatches"] == 0 and fc["max_abs_diff"] == 0.0 and fc["rows_checked"] == 8192 and fc["steps"] == 25
+    if fc["engine"] == "jit-jacobi":  # the r = 1/4 form is bitwise the reference rounding on this IC, too
+        assert fc["vs_exact"]["ok"] is True and fc["vs_exact"]["mismatches"] == 0, fc
+    assert four["fabric"] == {"kind": "ipc", "nranks": 4} and len(four["per_rank"]) == 4
+    assert four["distinct_devices"] == 1  # --share-gpu: every rank on the one GPU
     one = run_plain("--gpus", "1", *common)
     assert one["timed_field_check"]["ok"] is True and one["timed_field_check"]["mismatches"] == 0
     assert one["verified"] is True and one["config"]["transport_choice"] is None
@@ -183,6 +194,28 @@ def test_bench_rehearsal_then_verification(transport):
                   "--warmup", "5")
     assert d["config"]["transport"] == f"{transport}-loop" and d["verified"] is True, d
     assert d["halo_bytes"] > 0
+    # what the fabric reports (RCCL: ncclCommCount / ncclCommCuDevice of the 1-rank communicator)
+    assert d["fabric"] == {"kind": transport, "nranks": 1}, d["fabric"]
+    assert d["per_rank"][0]["fabric"]["device"] == 0 and d["per_rank"][0]["pci_bus_id"].count(":") == 2
+    assert d["rccl_nranks"] == (1 if transport == "rccl" else None)
+
+
+@pytest.mark.gpu
+def test_bench_ipc_attach_is_bounded():
+    """An IPC attach that never returns (HEAT2D_IPC_ATTACH_STALL: rank 1's
+    hipIpcOpenMemHandle hangs, as 4 ranks sharing a GPU at 32768^2 once did,
+    profiles/r5/x/) fails the attach after HEAT2D_IPC_ATTACH_TIMEOUT seconds on
+    EVERY rank: with RCCL refused too (ranks sharing a GPU) the run ends
+    promptly with "no transport works", not a hang."""
+    import time
+    env = dict(os.environ, HEAT2D_IPC_ATTACH_STALL="1", HEAT2D_IPC_ATTACH_TIMEOUT="5", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--grid", "2048",
+                        "--steps", "4", "--warmup", "1"], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode != 0 and p.stdout.strip() == "", p.stdout
+    assert "did not return within" in p.stderr and "no transport works on every rank" in p.stderr, p.stderr[-3000:]
+    assert time.time() - t0 < 240
 
 
 @pytest.mark.gpu
@@ -252,6 +285,24 @@ def test_bench_timed_field_check_windows_cpu(nproc):
     fc = d["timed_field_check"]
     assert fc["mode"] == "windows" and fc["ok"] is True and fc["mismatches"] == 0, fc
     assert fc["rows_checked"] == nproc * 3 * 16 and fc["steps"] == 15
+
+
+@pytest.mark.parametrize("ic", ["hotspot", "uniform"])
+def test_bench_hotspot_jacobi_check_cpu(ic):
+    """--ic hotspot (the zero + hot-spot data BASELINE.json names) with the
+    r = 1/4 form: the timed field is checked bitwise against the one-step
+    r * sum form and against the reference rounding — bitwise on the
+    Sterbenz-safe reference IC, within the stated bound on the hot spot
+    (values in [0, 1]: sum - 4c can round)."""
+    d = run_plain("--backend", "cpu", "--gpus", "2", "--grid", "257", "--steps", "40", "--warmup", "3", "--tb", "6",
+                  "--ic", ic, "--verify", "off")
+    assert d["config"]["arith"] == "jacobi (r = 1/4)" and d["config"]["ic"] == ic
+    fc = d["timed_field_check"]
+    assert fc["ok"] is True and fc["engine"] == "cpu-jacobi" and fc["mismatches"] == 0, fc
+    ve = fc["vs_exact"]
+    assert ve["ok"] is True and ve["engine"] == "cpu-exact", ve
+    assert ("bound" in ve) == (ic == "hotspot") and ve["max_abs_diff"] <= ve.get("bound", 0.0)
+    assert ("hot spot" in d["data"]) == (ic == "hotspot")
 
 
 def test_bench_timed_field_check_sigma_fast_cpu():

@@ -100,17 +100,26 @@ def one_gpu_stats():
     return run_bench("--gpus", "1", "--grid", "8192", "--steps", "40", "--warmup", "5", "--check")["field_stats"]
 
 
-@pytest.mark.parametrize("transport", ["rccl", "ipc", "auto"])
+@pytest.mark.parametrize("transport", ["rccl", "ipc", "auto", "best"])
 @pytest.mark.parametrize("P", SIZES)
 def test_bench_multi_gpu_matches_one_gpu(one_gpu_stats, transport, P):
     d = run_bench("--gpus", str(P), "--grid", "8192", "--steps", "40", "--warmup", "5", "--check", "--transport",
                   transport)
     ch = d["config"]["transport_choice"]
     assert ch["requested"] == transport and d["config"]["transport"] == ch["chosen"]
-    if transport != "auto":
+    if transport in ("rccl", "ipc"):
         assert ch["chosen"] == transport
+    elif transport == "auto":  # RCCL works on a node: IPC (its fallback) is never built
+        assert ch["chosen"] == "rccl" and "skipped" in ch["ipc"], ch
     else:
-        assert set(ch) >= {"rccl", "ipc"}
+        assert "ms" in ch["rccl"] and "ms" in ch["ipc"], ch
+    # the decomposition proves itself: what the fabric reports on every rank
+    assert d["fabric"]["nranks"] == P and d["distinct_devices"] == P, d["per_rank"]
+    assert [r["rank"] for r in d["per_rank"]] == list(range(P))
+    assert sum(r["rows"] for r in d["per_rank"]) == 8192
+    if d["config"]["transport"] == "rccl":
+        assert d["rccl_nranks"] == P
+        assert sorted(r["fabric"]["device"] for r in d["per_rank"]) == list(range(P))
     assert d["verified"] is True, d["verify"]
     fc = d["timed_field_check"]
     assert fc["ok"] is True and fc["mode"] == "full" and fc["mismatches"] == 0, fc

@@ -90,3 +90,26 @@ def test_unstable_run_writes_non_finite(tmp_path):
     assert p.returncode == 0, p.stderr[-2000:]
     txt = (tmp_path / "soln00000.dat").read_text()
     assert "Infinity" in txt or "NaN" in txt
+
+
+@pytest.mark.parametrize("how", ["abort", "free"])
+def test_fatal_signal_prints_native_backtrace(how):
+    """A glibc heap-check abort ("free(): invalid pointer") or any fatal
+    signal in a process that loaded the engine prints the native frames (which
+    library called free()) and then Python's faulthandler stacks; the exit
+    status stays the signal's. The round-5 abort left neither."""
+    import sys
+    body = ("import os, faulthandler; faulthandler.enable()\n"
+            "from heat2d.ops import _native as N; N.lib()\n")
+    if how == "abort":
+        body += "os.abort()\n"
+    else:  # free() of a pointer malloc never returned: glibc aborts
+        body += ("import ctypes; libc = ctypes.CDLL('libc.so.6'); buf = ctypes.create_string_buffer(64)\n"
+                 "libc.free(ctypes.cast(ctypes.addressof(buf) + 16, ctypes.c_void_p))\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", body], capture_output=True, text=True, timeout=120, cwd=root)
+    assert p.returncode == -6, (p.returncode, p.stderr[-2000:])
+    assert "heat2d: fatal signal, native backtrace:" in p.stderr, p.stderr[-2000:]
+    assert "Fatal Python error: Aborted" in p.stderr  # the previous handler (faulthandler) ran after ours
+    if how == "free":
+        assert "free()" in p.stderr and "libc.so.6" in p.stderr

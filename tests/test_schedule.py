@@ -116,6 +116,26 @@ def test_dp_large_n_and_unusable_depths(native):
     assert dp(7, 24, lambda k: 1.0 if k in (4,) else -1.0) == ([], -1.0)
 
 
+@pytest.mark.parametrize("curve", ["measured-fp64", "cliff16", "bumpy", "pure-linear", "hbm-bound"])
+@pytest.mark.parametrize("n", [20011, 31000])
+def test_dp_long_runs_stay_exact(native, curve, n):
+    """Above K * K * k* steps the DP takes the surplus as cycles of the
+    cheapest depth per step (some optimal schedule does) and solves only the
+    rest exactly: the same least cost as the full DP."""
+    t = CURVES[curve]
+    s, tot = dp(n, 24, t)
+    assert sum(s) == n and s == sorted(s, reverse=True)
+    assert tot == pytest.approx(brute(n, 24, t), rel=1e-12)
+
+
+def test_dp_ten_million_steps_is_cheap(native):
+    import time
+    t0 = time.perf_counter()
+    s, tot = dp(10_000_000, 24, cliff16)
+    assert time.perf_counter() - t0 < 2.0
+    assert sum(s) == 10_000_000 and s.count(16) > 600_000 and tot > 0
+
+
 def test_dp_ties_fewer_cycles_deeper_first(native):
     s, _ = dp(20, 24, lambda k: 1.0)  # every cycle costs the same: one cycle
     assert s == [20]

@@ -49,7 +49,85 @@ def test_try_collective_cleans_up_on_remote_failure():
     assert obj is None and why == "failed on another rank" and cleaned == ["comm"]
 
 
-@pytest.mark.parametrize("requested,world,hip,expect", [("auto", 8, True, ["rccl", "ipc"]), ("peer", 2, True, ["ipc"]),
+def test_choose_first_working_never_builds_the_fallback():
+    """"auto": RCCL works on every rank, so IPC (its fallback) is never tried."""
+    tried = []
+
+    def trial(kind):
+        tried.append(kind)
+        return 2.0
+    chosen, rep = select.choose_transport(["rccl", "ipc"], trial, ident, ident, first_working=True)
+    assert chosen == "rccl" and tried == ["rccl"] and "skipped" in rep["ipc"] and rep["rccl"] == {"ms": 2.0}
+
+
+def test_choose_first_working_falls_back():
+    def trial(kind):
+        if kind == "rccl":
+            raise RuntimeError("invalid usage (two ranks on one GPU)")
+        return 3.0
+    chosen, rep = select.choose_transport(["rccl", "ipc"], trial, ident, ident, first_working=True)
+    assert chosen == "ipc" and "error" in rep["rccl"] and rep["ipc"] == {"ms": 3.0}
+
+
+def test_deadline_fires_on_a_stuck_phase():
+    import time
+    fired = []
+    with select.deadline(0.2, "RCCL transport construction", rank=3, on_expire=fired.append):
+        time.sleep(0.6)
+    assert len(fired) == 1 and "rank 3: RCCL transport construction did not finish within 0.2 s" in fired[0]
+    fired.clear()
+    with select.deadline(5.0, "quick phase", on_expire=fired.append):
+        pass
+    time.sleep(0.05)
+    assert fired == []
+    with select.deadline(0, "unbounded", on_expire=fired.append):
+        pass
+    assert fired == []
+
+
+def test_deadline_exits_the_process():
+    """Without a test hook the stuck process exits with status 124 and every
+    thread's stack on stderr (the launcher then stops the other ranks)."""
+    code = ("import time; from heat2d.parallel import select\n"
+            "with select.deadline(0.3, 'IPC solver construction', rank=1):\n    time.sleep(30)\n")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       cwd=os.path.dirname(HERE))
+    assert p.returncode == select.EXIT_DEADLINE, p.stderr
+    assert "rank 1: IPC solver construction did not finish" in p.stderr and "time.sleep" not in p.stdout
+    assert "Thread" in p.stderr  # faulthandler's dump of every thread
+
+
+def test_rank_report_summarises_the_ranks():
+    from heat2d.parallel.transport import SelfTransport
+    tr = SelfTransport()
+    try:
+        rows = [(0, 50), (50, 50)]
+        mine = []
+
+        def gather(me):  # two ranks: this one and a fabricated peer on another device
+            other = dict(me, rank=1, row0=rows[1][0], rows=rows[1][1], timed_ms=2.5, device=1,
+                         fabric=dict(me["fabric"], rank=1))
+            mine.append(me)
+            return [other, me]
+        rep = select.rank_report(gather, rank=0, device=None, transport=tr, rows=50, row0=0, timed_s=0.002)
+    finally:
+        tr.close()
+    assert [r["rank"] for r in rep["ranks"]] == [0, 1] and rep["timed_ms"] == {"min": 2.0, "max": 2.5}
+    assert rep["fabric_kind"] == "host" and rep["fabric_nranks"] == 1 and rep["distinct_devices"] == 2
+    assert mine[0]["fabric"] == {"kind": "host", "nranks": 1, "rank": 0, "device": -1}
+
+
+@pytest.mark.parametrize("arith,sterbenz,expect", [
+    ("exact", True, [("exact", True)]), ("fma", False, [("fma", True)]), ("fast", True, [("exact", False)]),
+    ("jacobi", True, [("jacobi", True), ("exact", True)]), ("jacobi", False, [("jacobi", True), ("exact", False)])])
+def test_reference_checks(arith, sterbenz, expect):
+    """The r = 1/4 form is checked bitwise against its own one-step form and
+    against the reference rounding: bitwise only on Sterbenz-safe data."""
+    assert select.reference_checks(arith, 0.25, sterbenz) == expect
+
+
+@pytest.mark.parametrize("requested,world,hip,expect", [("auto", 8, True, ["rccl", "ipc"]), ("best", 8, True, ["rccl", "ipc"]),
+                                                        ("peer", 2, True, ["ipc"]),
                                                         ("rccl", 2, True, ["rccl"]), ("auto", 1, True, []),
                                                         ("auto", 4, False, ["torch-dist"])])
 def test_candidates(requested, world, hip, expect):
