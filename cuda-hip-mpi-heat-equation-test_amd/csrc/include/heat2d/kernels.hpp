@@ -70,6 +70,18 @@ struct TbRect {
 constexpr int kMaxPlanRects = 6;
 constexpr int32_t kPlanDynamic = 2;  // SplitPlan::flags
 constexpr int32_t kPlanLead = 4;     // SplitPlan::flags (valid = 1)
+constexpr int32_t kPlanContinue = 8; // SplitPlan::flags (with kPlanDynamic; interiors over row bands)
+// claim flags of the continued items after the dynamic queue's two counters
+constexpr int64_t kQueueClaims = int64_t(1) << 18;
+// Whether the frame-row band kernel (tb_impl.hpp kVarFrame) keeps 2 waves per
+// SIMD at (dtype, k, arith): then the boundary bands at the global frame rows
+// run on it (frame-column strips on the general kernel) and can lead beside
+// the interior like a middle rank's bands (HEAT2D_FRAME_KERNEL=0: the general
+// kernel for all of them, as before round 6)
+bool frame_ok(DType dt, int k, int arith);
+// Whether the continued-item twin of the interior kernel (dtype, ring, k,
+// arith) exists and keeps the plain kernel's occupancy (tb_impl.hpp kVarCont)
+bool cont_ok(DType dt, int ring, int k, int arith);
 struct SplitPlan {
   int32_t k, ring, valid, nedge;
   TbRect main;
@@ -82,7 +94,11 @@ struct SplitPlan {
   // exchanging slabs): the concurrent order with the band launch issued
   // FIRST — its waves take their slots before the interior's, the interior's
   // last-dispatched waves (its one-item waves) start behind them, and the
-  // exchange follows the bands on the comm stream.
+  // exchange follows the bands on the comm stream. flags & kPlanContinue
+  // (with kPlanDynamic, row bands): continued items — a march that reaches the
+  // top of its band marches on into the band above when no wave has claimed
+  // it (tb_impl.hpp): short bands for a fine dynamic balance without a
+  // priming (or a halo re-read) per band.
   int32_t nrects, flags;
   TbRect rects[kMaxPlanRects];
 };
@@ -109,7 +125,8 @@ bool edges_on_main(const SlabLayout& L, const SplitPlan& p);
 bool edge_rect_on_main(const SlabLayout& L, const SplitPlan& p, int i);
 void launch_edge_rect(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, int i, double r,
                       hipStream_t stream, int arith = 0);
-// queue: 2 device counters (zeroed once) for plans with flags & kPlanDynamic (dynamic items)
+// queue: 2 device counters + kQueueClaims claim flags (zeroed once) for plans with flags &
+// kPlanDynamic (dynamic items) / kPlanContinue (continued items)
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
                   double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr);
 

@@ -32,6 +32,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -179,9 +180,15 @@ class IpcTransport final : public Transport {
         HEAT2D_REQUIRE(all[(size_t)p].L.pitch == L.pitch, "IPC transport: slabs of different pitch");
         peer_L_[p > rank_] = all[(size_t)p].L;
       }
-      open_peers(all);
     } catch (const std::exception& e) {
       err = e.what();
+    }
+    if (err.empty()) {
+      try {
+        open_peers(all);
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
     }
     ok = err.empty() ? 0.0 : 1.0;
     HEAT2D_REQUIRE(ops_.allreduce(ops_.ctx, &ok, 1, 1) == 0, "IPC transport: allreduce callback failed");
@@ -308,8 +315,15 @@ class IpcTransport final : public Transport {
     }).detach();
     const char* tv = std::getenv("HEAT2D_IPC_ATTACH_TIMEOUT");
     const double limit = tv && *tv ? std::atof(tv) : 60.0;
+    const auto t0 = std::chrono::steady_clock::now();
     std::unique_lock<std::mutex> lk(st->mu);
-    if (!st->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return st->done; }))
+    const bool done = st->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return st->done; });
+    if (const char* lv = std::getenv("HEAT2D_IPC_ATTACH_LOG"); lv && std::atoi(lv) != 0) {
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      std::fprintf(stderr, "heat2d ipc: rank %d of %d: %zu neighbour(s) %s after %.1f ms\n", rank_, size_, peers.size(),
+                   done ? "opened" : "NOT opened", ms);
+    }
+    if (!done)
       fail(__FILE__, __LINE__,
            "IPC transport: hipIpcOpenMemHandle of a neighbour's field did not return within " +
                std::to_string(limit) + " s on rank " + std::to_string(rank_) + " (HEAT2D_IPC_ATTACH_TIMEOUT)");

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("cycles", type=int, nargs="?", default=6)
     ap.add_argument("--arith", default="jacobi")
     ap.add_argument("--rows", type=int, default=0)
+    ap.add_argument("--sigma", type=float, default=0.25)
     args = ap.parse_args()
     import torch
     import heat2d
@@ -36,7 +37,7 @@ def main():
     from heat2d.ops import _native as N
 
     torch.cuda.set_device(0)
-    inp = heat2d.InputDat(n=args.n, sigma=0.25, nu=0.05, dom_len=1.0, ntime=args.k, soln=0, nfields=6)
+    inp = heat2d.InputDat(n=args.n, sigma=args.sigma, nu=0.05, dom_len=1.0, ntime=args.k, soln=0, nfields=6)
     prob = heat2d.make_problem(inp, "ghost", "uniform")
     s = HeatSolver(prob, dtype=args.dtype, backend="hip", tb=args.k, device=0, autotune=1, arith=args.arith,
                    rows=args.rows or None)
@@ -61,10 +62,11 @@ def main():
     rows = args.rows or args.n
     ms = dt * 1e3 / args.cycles
     print(json.dumps({"dtype": args.dtype, "n": args.n, "rows": rows, "k": args.k, "cycles": args.cycles,
+                      "arith": args.arith, "sigma": args.sigma,
                       "ms_per_cycle": round(ms, 4), "us_per_level": round(ms * 1e3 / args.k, 2),
                       "gpts": round(rows * args.n * args.k / (ms * 1e-3) / 1e9, 1),
                       "launches_per_cycle": 2 if plan["order"] in ("concurrent", "edge-first", "lead") else 1,
-                      "plan": {k: plan[k] for k in ("order", "ring", "dynamic", "main_bands", "main_items",
+                      "plan": {k: plan[k] for k in ("order", "ring", "dynamic", "continued", "main_bands", "main_items",
                                                     "main_waves", "edge_items", "tuned_ms", "origin")}}),
           flush=True)
     s.close()

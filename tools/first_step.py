@@ -81,7 +81,7 @@ def main():
     s.close()
     tr.close()
     out = {"transport": args.transport, "rows": args.rows, "idle_ms": args.idle_ms, "spin_ms": args.spin_ms,
-           "timers": args.timers, "reps": reps}
+           "timers": args.timers, "hsa_enable_interrupt": os.environ.get("HSA_ENABLE_INTERRUPT"), "reps": reps}
     line = json.dumps(out)
     print(line)
     if args.json:
