@@ -126,9 +126,18 @@ bool edge_rect_on_main(const SlabLayout& L, const SplitPlan& p, int i);
 void launch_edge_rect(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, int i, double r,
                       hipStream_t stream, int arith = 0);
 // queue: 2 device counters + kQueueClaims claim flags (zeroed once) for plans with flags &
-// kPlanDynamic (dynamic items) / kPlanContinue (continued items)
+// kPlanDynamic (dynamic items) / kPlanContinue (continued items). edge_parts
+// (the band part): kEdgeBands | kEdgeCorners — the frame-column strips of the
+// bands at the global frame rows (edge kind 3: the general kernel, a few
+// items) apart from the rest (launch_frame_rects), so a caller can issue them
+// on a stream of their own.
+constexpr int kEdgeBands = 1, kEdgeCorners = 2;
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
-                  double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr);
+                  double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr,
+                  int edge_parts = kEdgeBands | kEdgeCorners);
+// Whether the plan's band part has frame-column corner items apart (the
+// frame-row band kernel is used: bands at the global frame rows and frame_ok)
+bool edges_have_corners(DType dt, const SlabLayout& L, const SplitPlan& p, int arith);
 
 // Initial / boundary condition kinds (covers every IC of the reference
 // variants, see models/presets.py for the mapping).

@@ -688,13 +688,14 @@ namespace {
 // ends (edge kind 3: a few items); the general kernel over all of them where
 // the frame kernel does not keep 2 waves per SIMD (frame_ok).
 void launch_frame_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, const TbRect* R,
-                        int n, double r, hipStream_t stream, int arith) {
+                        int n, double r, hipStream_t stream, int arith, int parts = kEdgeBands | kEdgeCorners) {
   auto items_of = [](const TbRect* q, int m) {
     int64_t it = 0;
     for (int i = 0; i < m; ++i) it += q[i].nb > 0 ? q[i].nb * (q[i].s1 - q[i].s0) : -q[i].nb;
     return it;
   };
   if (!frame_ok(dt, k, arith)) {
+    if (!(parts & kEdgeBands) || n == 0) return;
     const int64_t slots = (int64_t)cu_count() * occupancy(dt, ring, false, k, arith) * 4;
     launch_rects(dt, src, dst, L, k, ring, false, R, n, std::min<int64_t>(items_of(R, n), slots), r, stream, arith);
     return;
@@ -718,12 +719,12 @@ void launch_frame_rects(DType dt, const void* src, void* dst, const SlabLayout& 
     }
   }
   HEAT2D_REQUIRE(nc <= kMaxRects, "too many frame-column rects");
-  if (nc > 0) {  // (first: a few general-kernel waves, issued ahead of the frame kernel's)
+  if (nc > 0 && (parts & kEdgeCorners)) {  // (first: a few general-kernel waves, issued ahead of the frame kernel's)
     const int64_t slots = (int64_t)cu_count() * occupancy(dt, ring, false, k, arith) * 4;
     launch_rects(dt, src, dst, L, k, ring, false, corner, nc, std::min<int64_t>(items_of(corner, nc), slots), r, stream,
                  arith);
   }
-  if (ni > 0) {
+  if (ni > 0 && (parts & kEdgeBands)) {
     const int64_t slots = (int64_t)cu_count() * occupancy_frame(dt, k, arith) * 4;
     launch_rects(dt, src, dst, L, k, 4, false, inner, ni, std::min<int64_t>(items_of(inner, ni), slots), r, stream,
                  arith, nullptr, nullptr, 0, true);
@@ -744,8 +745,12 @@ void launch_edge_rect(DType dt, const void* src, void* dst, const SlabLayout& L,
   launch_rects(dt, src, dst, L, p.k, p.ring, true, &R, 1, std::min<int64_t>(items, slots), r, stream, arith);
 }
 
+bool edges_have_corners(DType dt, const SlabLayout& L, const SplitPlan& p, int arith) {
+  return (p.valid == 1 || p.valid == 3) && !edges_on_main(L, p) && frame_ok(dt, p.k, arith);
+}
+
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
-                  double r, hipStream_t stream, int arith, uint32_t* queue) {
+                  double r, hipStream_t stream, int arith, uint32_t* queue, int edge_parts) {
   // (SplitPlan::flags & kPlanDynamic: the main part takes its items from the
   // dynamic queue; & kPlanContinue: continued items, the queue's band order
   // strided by the items per wave — tb_impl.hpp cont_item)
@@ -767,23 +772,31 @@ void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, con
   if (main_part) {
     launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith, nullptr, q, cstride);
   } else if (edges_on_main(L, p.k, p.edge, p.nedge)) {
-    launch_rects(dt, src, dst, L, p.k, p.ring, true, p.edge, p.nedge, p.edge_waves, r, stream, arith);
+    if (edge_parts & kEdgeBands)
+      launch_rects(dt, src, dst, L, p.k, p.ring, true, p.edge, p.nedge, p.edge_waves, r, stream, arith);
+  } else if (frame_ok(dt, p.k, arith)) {
+    // a band at the global frame rows: ALL bands on the frame-row band kernel
+    // (its edge-kind-1 march is exact on rows clear of the frame too) but
+    // their frame-column strips, which go to the general kernel — two
+    // launches, so a lead-ordered cycle can issue each first on a stream of
+    // its own (Solver::launch_overlap)
+    launch_frame_rects(dt, src, dst, L, p.k, p.ring, p.edge, p.nedge, r, stream, arith, edge_parts);
   } else {
     // bands clear of the global frame rows on the interior kernel, the others
-    // on the frame-row band kernel (launch_frame_rects)
+    // on the general kernel
     TbRect on[4], off[4];
     int n_on = 0, n_off = 0;
     for (int i = 0; i < p.nedge; ++i) {
       if (edges_on_main(L, p.k, &p.edge[i], 1)) on[n_on++] = p.edge[i];
       else off[n_off++] = p.edge[i];
     }
-    if (n_on > 0) {
+    if (n_on > 0 && (edge_parts & kEdgeBands)) {
       int64_t items = 0;
       for (int i = 0; i < n_on; ++i) items += on[i].nb > 0 ? on[i].nb * (on[i].s1 - on[i].s0) : -on[i].nb;
       const int64_t slots = (int64_t)cu_count() * occupancy(dt, p.ring, true, p.k, arith) * 4;
       launch_rects(dt, src, dst, L, p.k, p.ring, true, on, n_on, std::min<int64_t>(items, slots), r, stream, arith);
     }
-    launch_frame_rects(dt, src, dst, L, p.k, p.ring, off, n_off, r, stream, arith);
+    launch_frame_rects(dt, src, dst, L, p.k, p.ring, off, n_off, r, stream, arith, edge_parts);
   }
 }
 

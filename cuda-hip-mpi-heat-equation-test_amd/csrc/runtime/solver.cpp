@@ -199,12 +199,14 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
       // (A high-priority comm stream did not get the band waves dispatched
       // first in steady-state cycles, nor change the small grid: profiles/r4/lead/, r4/m/.)
       H2D_HIP(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+      H2D_HIP(hipStreamCreateWithFlags(&s_side_, hipStreamNonBlocking));
       own_streams_ = true;
     }
     H2D_HIP(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_comm_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_int_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_frame_, hipEventDisableTiming));
+    H2D_HIP(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
@@ -226,6 +228,7 @@ Solver::~Solver() {
     (void)hipSetDevice(cfg_.device);
     if (s_compute_) (void)hipStreamSynchronize(s_compute_);
     if (s_comm_ && s_comm_ != s_compute_) (void)hipStreamSynchronize(s_comm_);
+    if (s_side_) (void)hipStreamSynchronize(s_side_);
     if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
     for (auto& g : sched_graph_) (void)hipGraphExecDestroy(g.second);
     for (auto& b : buf_)
@@ -237,6 +240,7 @@ Solver::~Solver() {
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
     if (ev_int_) (void)hipEventDestroy(ev_int_);
     if (ev_frame_) (void)hipEventDestroy(ev_frame_);
+    if (ev_side_) (void)hipEventDestroy(ev_side_);
     if (ev_t0_) (void)hipEventDestroy(ev_t0_);
     if (ev_t1_) (void)hipEventDestroy(ev_t1_);
     for (auto* v : {&phase_ev_, &phase_pool_})
@@ -245,6 +249,7 @@ Solver::~Solver() {
     if (own_streams_) {
       (void)hipStreamDestroy(s_compute_);
       (void)hipStreamDestroy(s_comm_);
+      if (s_side_) (void)hipStreamDestroy(s_side_);
     }
     (void)hipGetLastError();  // teardown errors must not surface as the next launch's
   } else {
@@ -401,6 +406,11 @@ void Solver::cycle_finish() {
       H2D_HIP(hipEventRecord(ev_frame_, s_comm_));
       H2D_HIP(hipStreamWaitEvent(s_compute_, ev_frame_, 0));
       pend_frame_ = -1;
+    }
+    if (side_pend_) {  // the lead cycle's frame-column corners (launch_overlap): joined into both streams
+      H2D_HIP(hipStreamWaitEvent(s_compute_, ev_side_, 0));
+      H2D_HIP(hipStreamWaitEvent(s_comm_, ev_side_, 0));
+      side_pend_ = false;
     }
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
   }
@@ -1087,8 +1097,20 @@ void Solver::launch_overlap(int k, int64_t B) {
   H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));     // main part c-1
   if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
   if (lead) {
-    // lead: the band launch first (comm stream), then the interior beside it
-    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_, cfg_.arith);
+    // lead: the band launch first (comm stream), then the interior beside it.
+    // Bands at the global frame rows: their frame-column corners (general
+    // kernel, 1 wave per SIMD, a few items) first, on the side stream — on the
+    // comm stream they would hold the frame-row band kernel's launch behind
+    // them until the interior has taken every SIMD (profiles/r6/f/)
+    const bool side = s_side_ && kern::edges_have_corners(dtype(), L_, sp, cfg_.arith);
+    if (side) {
+      for (hipEvent_t e : {ev_int_, ev_bnd_, ev_comm_}) H2D_HIP(hipStreamWaitEvent(s_side_, e, 0));
+      kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_side_, cfg_.arith, nullptr, kern::kEdgeCorners);
+      H2D_HIP(hipEventRecord(ev_side_, s_side_));
+      side_pend_ = true;
+    }
+    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_, cfg_.arith, nullptr,
+                       side ? kern::kEdgeBands : kern::kEdgeBands | kern::kEdgeCorners);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
     kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));
