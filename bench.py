@@ -611,7 +611,7 @@ def main():
     for k, c in sorted(hist.items()):
         pl = s.plan(k) if hip else {"k": k, "valid": 0}
         if hip:
-            plans[str(k)] = {kk: pl[kk] for kk in ("order", "dynamic", "continued", "origin", "ring", "main_bands", "main_waves",
+            plans[str(k)] = {kk: pl[kk] for kk in ("order", "dynamic", "origin", "ring", "main_bands", "main_waves",
                                                     "edge_items", "tuned_ms")}
         traffic += c * plan_hbm_bytes(pl, es, s.nrows, s.ncols)["total"]
     # halo traffic of the timed region: each exchange moves the NEXT cycle's

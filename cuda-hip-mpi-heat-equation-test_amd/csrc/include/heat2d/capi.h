@@ -52,7 +52,7 @@ typedef struct heat2d_split_plan {
   heat2d_rect main;
   heat2d_rect edge[4];
   int64_t main_waves, edge_waves, main_items, edge_items;
-  int32_t nrects, flags;  // flags & 2: dynamic item queue, & 4: lead order, & 8: continued items
+  int32_t nrects, flags;  // flags & 2: dynamic item queue, & 4: lead order
   heat2d_rect rects[6];
 } heat2d_split_plan;
 

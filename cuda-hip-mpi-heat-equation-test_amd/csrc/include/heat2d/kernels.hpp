@@ -70,18 +70,6 @@ struct TbRect {
 constexpr int kMaxPlanRects = 6;
 constexpr int32_t kPlanDynamic = 2;  // SplitPlan::flags
 constexpr int32_t kPlanLead = 4;     // SplitPlan::flags (valid = 1)
-constexpr int32_t kPlanContinue = 8; // SplitPlan::flags (with kPlanDynamic; interiors over row bands)
-// claim flags of the continued items after the dynamic queue's two counters
-constexpr int64_t kQueueClaims = int64_t(1) << 18;
-// Whether the frame-row band kernel (tb_impl.hpp kVarFrame) keeps 2 waves per
-// SIMD at (dtype, k, arith): then the boundary bands at the global frame rows
-// run on it (frame-column strips on the general kernel) and can lead beside
-// the interior like a middle rank's bands (HEAT2D_FRAME_KERNEL=0: the general
-// kernel for all of them, as before round 6)
-bool frame_ok(DType dt, int k, int arith);
-// Whether the continued-item twin of the interior kernel (dtype, ring, k,
-// arith) exists and keeps the plain kernel's occupancy (tb_impl.hpp kVarCont)
-bool cont_ok(DType dt, int ring, int k, int arith);
 struct SplitPlan {
   int32_t k, ring, valid, nedge;
   TbRect main;
@@ -94,11 +82,7 @@ struct SplitPlan {
   // exchanging slabs): the concurrent order with the band launch issued
   // FIRST — its waves take their slots before the interior's, the interior's
   // last-dispatched waves (its one-item waves) start behind them, and the
-  // exchange follows the bands on the comm stream. flags & kPlanContinue
-  // (with kPlanDynamic, row bands): continued items — a march that reaches the
-  // top of its band marches on into the band above when no wave has claimed
-  // it (tb_impl.hpp): short bands for a fine dynamic balance without a
-  // priming (or a halo re-read) per band.
+  // exchange follows the bands on the comm stream.
   int32_t nrects, flags;
   TbRect rects[kMaxPlanRects];
 };
@@ -125,19 +109,9 @@ bool edges_on_main(const SlabLayout& L, const SplitPlan& p);
 bool edge_rect_on_main(const SlabLayout& L, const SplitPlan& p, int i);
 void launch_edge_rect(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, int i, double r,
                       hipStream_t stream, int arith = 0);
-// queue: 2 device counters + kQueueClaims claim flags (zeroed once) for plans with flags &
-// kPlanDynamic (dynamic items) / kPlanContinue (continued items). edge_parts
-// (the band part): kEdgeBands | kEdgeCorners — the frame-column strips of the
-// bands at the global frame rows (edge kind 3: the general kernel, a few
-// items) apart from the rest (launch_frame_rects), so a caller can issue them
-// on a stream of their own.
-constexpr int kEdgeBands = 1, kEdgeCorners = 2;
+// queue: 2 device counters (zeroed once) for plans with flags & kPlanDynamic (dynamic items)
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
-                  double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr,
-                  int edge_parts = kEdgeBands | kEdgeCorners);
-// Whether the plan's band part has frame-column corner items apart (the
-// frame-row band kernel is used: bands at the global frame rows and frame_ok)
-bool edges_have_corners(DType dt, const SlabLayout& L, const SplitPlan& p, int arith);
+                  double r, hipStream_t stream, int arith = 0, uint32_t* queue = nullptr);
 
 // Initial / boundary condition kinds (covers every IC of the reference
 // variants, see models/presets.py for the mapping).

@@ -471,13 +471,6 @@ class Solver {
   // so ev_bnd_ — which receiver-driven transports wait on after post() — keeps
   // marking only the bands the exchange sends
   hipEvent_t ev_frame_ = nullptr;
-  // the frame-column corner items of bands at the global frame rows (edge
-  // kind 3, general kernel), issued on a stream of their own in a lead-ordered
-  // cycle so they neither wait behind nor hold up the band launch on the comm
-  // stream (cycle_finish joins them into both streams)
-  hipStream_t s_side_ = nullptr;
-  hipEvent_t ev_side_ = nullptr;
-  bool side_pend_ = false;
   double* d_work_ = nullptr;   // stats workspace + 6 results
   bool timing_ = false;
   struct PhaseEvents {

@@ -134,24 +134,6 @@ int occupancy(DType dt, int ring, bool main, int k, int arith) {
   });
 }
 
-// resident workgroups per CU of the frame-row band kernel (0: not instantiated)
-int occupancy_frame(DType dt, int k, int arith) {
-  return with_ar(arith, [&](auto ar) {
-    constexpr int AR = decltype(ar)::value;
-    return dt == DType::F32 ? occupancy_blocks_frame<float, AR>(k) : occupancy_blocks_frame<double, AR>(k);
-  });
-}
-
-// resident workgroups per CU of the continued-item interior kernel (0: not instantiated)
-int occupancy_cont(DType dt, int ring, int k, int arith) {
-  return with_ar(arith, [&](auto ar) {
-    constexpr int AR = decltype(ar)::value;
-    if (dt == DType::F32)
-      return ring == 4 ? occupancy_blocks_cont<float, 4, AR>(k) : occupancy_blocks_cont<float, 6, AR>(k);
-    return ring == 4 ? occupancy_blocks_cont<double, 4, AR>(k) : occupancy_blocks_cont<double, 6, AR>(k);
-  });
-}
-
 template <typename T, int AR>
 void dispatch_ar(int ring, bool main, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
                  hipStream_t st) {
@@ -173,20 +155,7 @@ void dispatch_ar(int ring, bool main, int k, unsigned nblocks, const T* s, T* d,
 
 template <typename T>
 void dispatch_t(int ring, bool main, int arith, int k, unsigned nblocks, const T* s, T* d, const TbArgs& a, T r,
-                hipStream_t st, bool frame = false) {
-  if (frame) {  // the frame-row band kernel (ring 4, general rects)
-    with_ar(arith, [&](auto ar) { dispatch_frame<T, decltype(ar)::value>(k, nblocks, s, d, a, r, st); });
-    return;
-  }
-  if (a.cont > 0) {  // continued items: the interior kernels' kVarCont twins
-    HEAT2D_REQUIRE(main && (ring == 4 || ring == 6), "continued items: interior kernels, ring 4 / 6");
-    with_ar(arith, [&](auto ar) {
-      constexpr int AR = decltype(ar)::value;
-      if (ring == 4) dispatch_cont<T, 4, AR>(k, nblocks, s, d, a, r, st);
-      else dispatch_cont<T, 6, AR>(k, nblocks, s, d, a, r, st);
-    });
-    return;
-  }
+                hipStream_t st) {
   with_ar(arith, [&](auto ar) { dispatch_ar<T, decltype(ar)::value>(ring, main, k, nblocks, s, d, a, r, st); });
 }
 
@@ -268,29 +237,11 @@ int64_t choose_bands(int64_t rows, int64_t ns, int64_t simds, int k, int64_t pri
   return best;
 }
 
-}  // namespace
-
-bool frame_ok(DType dt, int k, int arith) {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_FRAME_KERNEL");
-    return !e || std::atoi(e) != 0;
-  }();
-  return on && occupancy_frame(dt, k, arith) >= 2;
-}
-
-bool cont_ok(DType dt, int ring, int k, int arith) {
-  if (!(ring == 4 || ring == 6)) return false;
-  const int c = occupancy_cont(dt, ring, k, arith);
-  return c > 0 && c >= occupancy(dt, ring, true, k, arith);
-}
-
-namespace {
-
 // Launch `rects` (item counts from their nb and strip ranges) on `nwaves` waves.
 // partials != nullptr: the fused-statistics kernel (general, ring 4). Returns the waves launched.
 int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, bool main,
                      const TbRect* rects, int nrect, int64_t nwaves, double r, hipStream_t stream, int arith,
-                     double* partials = nullptr, uint32_t* queue = nullptr, int cont = 0, bool frame = false) {
+                     double* partials = nullptr, uint32_t* queue = nullptr) {
   HEAT2D_REQUIRE(nrect >= 1 && nrect <= (main ? kMainRects : kMaxRects), "bad rect count");
   TbArgs a{};
   a.pitch = L.pitch;
@@ -314,7 +265,7 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   }
   if (q == 0) return 0;
   a.nrect = q;
-  a.cont = 0;
+  a.pad0 = 0;
   a.nitems = items;
   a.nwaves = std::max<int64_t>(1, std::min<int64_t>(nwaves, items));
   a.partials = partials;
@@ -328,20 +279,6 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
   // the dynamic queue only pays with more items than waves (interior and
   // single launches; not the statistics kernel)
   a.queue = (queue && !partials && items > a.nwaves) ? queue : nullptr;
-  // continued items (kPlanContinue): interior kernels over band rects whose
-  // bands (ceil(rows / nb) tall, the last one shorter) are none empty and at
-  // least 2k rows (the march then decides on a continuation in its steady
-  // loop, tb_impl.hpp March::run), within the claim flags' capacity; else the
-  // plain dynamic queue
-  if (cont > 0 && a.queue && main && items <= kQueueClaims && cont_ok(dt, ring, k, arith)) {
-    bool ok = true;
-    for (int i = 0; i < q; ++i) {
-      const TbRectArg& R = a.rect[i];
-      const int64_t rws = R.r1 - R.r0, h = R.nb > 0 ? (rws + R.nb - 1) / R.nb : 0;
-      ok = ok && R.nb > 0 && (R.nb - 1) * h < rws && h >= 2 * (int64_t)k;
-    }
-    if (ok) a.cont = cont;
-  }
   const unsigned nblocks = (unsigned)((a.nwaves + 3) / 4);
   const int64_t o = L.origin();
   if (partials) {
@@ -355,10 +292,10 @@ int64_t launch_rects(DType dt, const void* src, void* dst, const SlabLayout& L, 
     });
   } else if (dt == DType::F32) {
     dispatch_t<float>(ring, main, arith, k, nblocks, static_cast<const float*>(src) + o, static_cast<float*>(dst) + o, a,
-                      (float)r, stream, frame);
+                      (float)r, stream);
   } else {
     dispatch_t<double>(ring, main, arith, k, nblocks, static_cast<const double*>(src) + o, static_cast<double*>(dst) + o,
-                       a, r, stream, frame);
+                       a, r, stream);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(__FILE__, __LINE__, std::string("tb_kernel launch: ") + hipGetErrorString(e));
@@ -681,123 +618,34 @@ bool edge_rect_on_main(const SlabLayout& L, const SplitPlan& p, int i) {
   return i >= 0 && i < p.nedge && edges_on_main(L, p.k, &p.edge[i], 1);
 }
 
-namespace {
-// Boundary-band rects whose marches reach a global frame row: the frame-row
-// band kernel (kVarFrame, 2 waves per SIMD) over their strips clear of the
-// frame columns, the general kernel over the frame-column strips at their two
-// ends (edge kind 3: a few items); the general kernel over all of them where
-// the frame kernel does not keep 2 waves per SIMD (frame_ok).
-void launch_frame_rects(DType dt, const void* src, void* dst, const SlabLayout& L, int k, int ring, const TbRect* R,
-                        int n, double r, hipStream_t stream, int arith, int parts = kEdgeBands | kEdgeCorners) {
-  auto items_of = [](const TbRect* q, int m) {
-    int64_t it = 0;
-    for (int i = 0; i < m; ++i) it += q[i].nb > 0 ? q[i].nb * (q[i].s1 - q[i].s0) : -q[i].nb;
-    return it;
-  };
-  if (!frame_ok(dt, k, arith)) {
-    if (!(parts & kEdgeBands) || n == 0) return;
-    const int64_t slots = (int64_t)cu_count() * occupancy(dt, ring, false, k, arith) * 4;
-    launch_rects(dt, src, dst, L, k, ring, false, R, n, std::min<int64_t>(items_of(R, n), slots), r, stream, arith);
-    return;
-  }
-  // strips clear of the frame columns: [s_lo, s_hi) (the kernel's edge-kind-2 test)
-  const int64_t U = useful_width(dt, k), KA = halo_cols(dt, k), W = 64 * vec_elems(dt);
-  const int64_t s_lo = (KA + U - 1) / U;                     // first strip with c0 = s U - KA >= 0
-  const int64_t num = L.ncols + KA - W;                      // strips s < s_hi have c0 + W <= ncols
-  const int64_t s_hi = num < 0 ? 0 : num / U + 1;
-  TbRect inner[kMaxRects], corner[kMaxRects];
-  int ni = 0, nc = 0;
-  for (int i = 0; i < n; ++i) {
-    HEAT2D_REQUIRE(R[i].nb > 0, "frame-row band rects are row bands");
-    const int64_t a0 = std::max(R[i].s0, s_lo), a1 = std::min(R[i].s1, s_hi);
-    if (a1 > a0) {
-      inner[ni++] = TbRect{R[i].r0, R[i].r1, a0, a1, R[i].nb};
-      if (R[i].s0 < a0) corner[nc++] = TbRect{R[i].r0, R[i].r1, R[i].s0, a0, R[i].nb};
-      if (a1 < R[i].s1) corner[nc++] = TbRect{R[i].r0, R[i].r1, a1, R[i].s1, R[i].nb};
-    } else {
-      corner[nc++] = R[i];
-    }
-  }
-  HEAT2D_REQUIRE(nc <= kMaxRects, "too many frame-column rects");
-  if (nc > 0 && (parts & kEdgeCorners)) {  // (first: a few general-kernel waves, issued ahead of the frame kernel's)
-    const int64_t slots = (int64_t)cu_count() * occupancy(dt, ring, false, k, arith) * 4;
-    launch_rects(dt, src, dst, L, k, ring, false, corner, nc, std::min<int64_t>(items_of(corner, nc), slots), r, stream,
-                 arith);
-  }
-  if (ni > 0 && (parts & kEdgeBands)) {
-    const int64_t slots = (int64_t)cu_count() * occupancy_frame(dt, k, arith) * 4;
-    launch_rects(dt, src, dst, L, k, 4, false, inner, ni, std::min<int64_t>(items_of(inner, ni), slots), r, stream,
-                 arith, nullptr, nullptr, 0, true);
-  }
-}
-}  // namespace
-
 void launch_edge_rect(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, int i, double r,
                       hipStream_t stream, int arith) {
   HEAT2D_REQUIRE(i >= 0 && i < p.nedge, "edge rect index");
   const TbRect& R = p.edge[i];
-  if (!edges_on_main(L, p.k, &R, 1)) {
-    launch_frame_rects(dt, src, dst, L, p.k, p.ring, &R, 1, r, stream, arith);
-    return;
-  }
+  const bool on_main = edges_on_main(L, p.k, &R, 1);
   const int64_t items = R.nb > 0 ? R.nb * (R.s1 - R.s0) : -R.nb;
-  const int64_t slots = (int64_t)cu_count() * occupancy(dt, p.ring, true, p.k, arith) * 4;
-  launch_rects(dt, src, dst, L, p.k, p.ring, true, &R, 1, std::min<int64_t>(items, slots), r, stream, arith);
-}
-
-bool edges_have_corners(DType dt, const SlabLayout& L, const SplitPlan& p, int arith) {
-  return (p.valid == 1 || p.valid == 3) && !edges_on_main(L, p) && frame_ok(dt, p.k, arith);
+  const int64_t slots = (int64_t)cu_count() * occupancy(dt, p.ring, on_main, p.k, arith) * 4;
+  launch_rects(dt, src, dst, L, p.k, p.ring, on_main, &R, 1, std::min<int64_t>(items, slots), r, stream, arith);
 }
 
 void launch_split(DType dt, const void* src, void* dst, const SlabLayout& L, const SplitPlan& p, bool main_part,
-                  double r, hipStream_t stream, int arith, uint32_t* queue, int edge_parts) {
-  // (SplitPlan::flags & kPlanDynamic: the main part takes its items from the
-  // dynamic queue; & kPlanContinue: continued items, the queue's band order
-  // strided by the items per wave — tb_impl.hpp cont_item)
+                  double r, hipStream_t stream, int arith, uint32_t* queue) {
+  // (SplitPlan::flags & kPlanDynamic: the main part takes its items from the dynamic queue)
   uint32_t* q = (p.flags & kPlanDynamic) ? queue : nullptr;
-  const bool cont = (p.flags & kPlanContinue) && p.valid != 2 && p.main.nb > 0 && p.main_waves > 0;
   HEAT2D_REQUIRE(p.valid, "invalid split plan");
-  // the main part: p.main, or its frame-strip-weighted rects (weight_main);
-  // continued items take the one unweighted rect (the queue balances the
-  // frame-column strips' costlier rows)
-  const TbRect* mr = p.nrects > 0 && !cont ? p.rects : &p.main;
-  const int nm = p.nrects > 0 && !cont ? p.nrects : 1;
-  const int64_t mitems = cont ? p.main.nb * (p.main.s1 - p.main.s0) : p.main_items;
-  const int cstride = cont ? (int)std::max<int64_t>(1, (mitems + p.main_waves / 2) / p.main_waves) : 0;
+  // the main part: p.main, or its frame-strip-weighted rects (weight_main)
+  const TbRect* mr = p.nrects > 0 ? p.rects : &p.main;
+  const int nm = p.nrects > 0 ? p.nrects : 1;
   if (p.valid == 2) {  // single general launch over the whole slab (no edge part)
     if (main_part)
       launch_rects(dt, src, dst, L, p.k, p.ring, false, mr, nm, p.main_waves, r, stream, arith, nullptr, q);
     return;
   }
-  if (main_part) {
-    launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith, nullptr, q, cstride);
-  } else if (edges_on_main(L, p.k, p.edge, p.nedge)) {
-    if (edge_parts & kEdgeBands)
-      launch_rects(dt, src, dst, L, p.k, p.ring, true, p.edge, p.nedge, p.edge_waves, r, stream, arith);
-  } else if (frame_ok(dt, p.k, arith)) {
-    // a band at the global frame rows: ALL bands on the frame-row band kernel
-    // (its edge-kind-1 march is exact on rows clear of the frame too) but
-    // their frame-column strips, which go to the general kernel — two
-    // launches, so a lead-ordered cycle can issue each first on a stream of
-    // its own (Solver::launch_overlap)
-    launch_frame_rects(dt, src, dst, L, p.k, p.ring, p.edge, p.nedge, r, stream, arith, edge_parts);
-  } else {
-    // bands clear of the global frame rows on the interior kernel, the others
-    // on the general kernel
-    TbRect on[4], off[4];
-    int n_on = 0, n_off = 0;
-    for (int i = 0; i < p.nedge; ++i) {
-      if (edges_on_main(L, p.k, &p.edge[i], 1)) on[n_on++] = p.edge[i];
-      else off[n_off++] = p.edge[i];
-    }
-    if (n_on > 0 && (edge_parts & kEdgeBands)) {
-      int64_t items = 0;
-      for (int i = 0; i < n_on; ++i) items += on[i].nb > 0 ? on[i].nb * (on[i].s1 - on[i].s0) : -on[i].nb;
-      const int64_t slots = (int64_t)cu_count() * occupancy(dt, p.ring, true, p.k, arith) * 4;
-      launch_rects(dt, src, dst, L, p.k, p.ring, true, on, n_on, std::min<int64_t>(items, slots), r, stream, arith);
-    }
-    launch_frame_rects(dt, src, dst, L, p.k, p.ring, off, n_off, r, stream, arith, edge_parts);
-  }
+  if (main_part)
+    launch_rects(dt, src, dst, L, p.k, p.ring, true, mr, nm, p.main_waves, r, stream, arith, nullptr, q);
+  else
+    launch_rects(dt, src, dst, L, p.k, p.ring, edges_on_main(L, p.k, p.edge, p.nedge), p.edge, p.nedge, p.edge_waves,
+                 r, stream, arith);
 }
 
 }  // namespace kern

@@ -99,10 +99,7 @@ struct TbArgs {
   int64_t nwaves;  // launched waves (grid-stride over items)
   int64_t fixed_lo, fixed_hi;  // local rows outside [fixed_lo, fixed_hi) are Dirichlet
   int32_t nrect;
-  // Continued items (the kVarCont interior kernels, kPlanContinue): the
-  // stride of the queue's band order (> 0). Claim flags, one per item, follow
-  // the two queue counters: queue[2 + item].
-  int32_t cont;
+  int32_t pad0;
   TbRectArg rect[kMaxRects];
   double* partials;   // ST kernels: per-wave statistics, partials[j * nwaves + wave] (kNStatFused = 6 values)
   // Diagnostics (HEAT2D_WAVE_TIMES, kern::wave_times): per launched wave
@@ -296,28 +293,6 @@ constexpr int chain_len() {
   constexpr int c = std::is_same<T, float>::value ? HEAT2D_CHAIN_F32 : HEAT2D_CHAIN_F64;
   return (c <= 0 || c >= K || K < HEAT2D_CHAIN_MIN_K || K > HEAT2D_CHAIN_MAX_K) ? K : c;
 }
-
-// Continued items (kVarCont kernels, SplitPlan::flags & kPlanContinue:
-// interior launches over row bands). A march that reaches the top of its band
-// claims the band above it in the same strip (the next rows of the SAME
-// march) and, when no other wave has claimed it, marches on into it: its level
-// registers are already in the steady state, so that band costs no priming
-// (2k march rows, ~K^2 level-rows of trapezoid) and re-reads no halo rows.
-// Bands can then be short — the fine-grained dynamic balance a thin slab
-// needs (its waves otherwise end a launch up to a whole 500-row item apart,
-// profiles/r5/o/) — without a priming per band. The hook is asked once per
-// body from the first body whose loads would reach past the band's rows (so
-// nothing of the band above has been dropped yet) until it declines; on
-// success it moves the band's lowest output row t0 down. NoExt: no
-// continuation (every other kernel). A separate kernel variant: the hook's
-// loop-variant bounds cost registers (the fp64 K = 20 interior kernel would
-// drop to 1 wave per SIMD), so the plain kernels stay without it and the
-// autotuner uses continued items only where the variant keeps the plain
-// kernel's occupancy (cont_ok()).
-struct NoExt {
-  static constexpr bool on = false;
-  __device__ __forceinline__ bool operator()(int32_t& /*t0*/) const { return false; }
-};
 
 // Cache-policy bits of the march's 16-B row stores: 2 = nt (streaming). The
 // output rows are written once and read by the next pass only, so marking them
@@ -547,8 +522,8 @@ struct March {
   // depths 13..20 although it costs some of them an occupancy level,
   // profiles/r5/i/, r5/j/); the general kernels do not (4-5 % slower for the
   // 1-wave/SIMD fp32 small grid, profiles/priming_skip.md).
-  template <bool PS = false, class Ext = NoExt>
-  __device__ __forceinline__ void run(Ext ext = Ext{}) {
+  template <bool PS = false>
+  __device__ __forceinline__ void run() {
     mload = t0 - K;
     mlo = t0 - Ch::off(K);
     const int32_t mtop = t1 + K - 1;
@@ -569,7 +544,7 @@ struct March {
 #pragma unroll
         for (int e = 0; e < V; ++e) X[p][s][e] = T(0);
     const int32_t iters = mtop - mlo + 1;
-    int32_t bodies = (iters + L - 1) / L;
+    const int32_t bodies = (iters + L - 1) / L;
     // priming bodies (deep levels skipped while not needed), then the steady loop
     const int32_t pb = PS ? min(bodies, (int32_t)((Ch::prime_iters + L - 1) / L)) : 0;
     int32_t m = mtop;
@@ -579,23 +554,8 @@ struct March {
       body_prime(m, b * L, std::make_integer_sequence<int, L>{});
       m -= L;
     }
-    // Ext (continued items): asked at the first body whose lowest load (row
-    // m - L + 3 - RING) lies below mload, then at every body until it declines
-    int32_t dec = Ext::on ? mload + L + RING - 3 : INT32_MIN;
 #pragma unroll 1
     for (; b < bodies; ++b) {
-      if constexpr (Ext::on) {
-        if (m < dec) {
-          if (ext(t0)) {
-            mload = t0 - K;
-            mlo = t0 - Ch::off(K);
-            bodies = (mtop - mlo + L) / L;
-            dec = mload + L + RING - 3;
-          } else {
-            dec = INT32_MIN;
-          }
-        }
-      }
       body(m, std::make_integer_sequence<int, L>{});
       m -= L;
     }
@@ -827,8 +787,8 @@ struct MarchF32 {
   // depths 13..20 although it costs some of them an occupancy level,
   // profiles/r5/i/, r5/j/); the general kernels do not (4-5 % slower for the
   // 1-wave/SIMD fp32 small grid, profiles/priming_skip.md).
-  template <bool PS = false, class Ext = NoExt>
-  __device__ __forceinline__ void run(Ext ext = Ext{}) {  // (Ext: see March::run)
+  template <bool PS = false>
+  __device__ __forceinline__ void run() {
     mload = t0 - K;
     mlo = t0 - Ch::off(K);
     const int32_t mtop = t1 + K - 1;
@@ -843,7 +803,7 @@ struct MarchF32 {
 #pragma unroll
       for (int s = 0; s < KX; ++s) X[p][s] = Row{F2{0.f, 0.f}, F2{0.f, 0.f}};
     const int32_t iters = mtop - mlo + 1;
-    int32_t bodies = (iters + L - 1) / L;
+    const int32_t bodies = (iters + L - 1) / L;
     // priming bodies (deep levels skipped while not needed), then the steady loop
     const int32_t pb = PS ? min(bodies, (int32_t)((Ch::prime_iters + L - 1) / L)) : 0;
     int32_t m = mtop;
@@ -853,23 +813,8 @@ struct MarchF32 {
       body_prime(m, b * L, std::make_integer_sequence<int, L>{});
       m -= L;
     }
-    // Ext (continued items): asked at the first body whose lowest load (row
-    // m - L + 3 - RING) lies below mload, then at every body until it declines
-    int32_t dec = Ext::on ? mload + L + RING - 3 : INT32_MIN;
 #pragma unroll 1
     for (; b < bodies; ++b) {
-      if constexpr (Ext::on) {
-        if (m < dec) {
-          if (ext(t0)) {
-            mload = t0 - K;
-            mlo = t0 - Ch::off(K);
-            bodies = (mtop - mlo + L) / L;
-            dec = mload + L + RING - 3;
-          } else {
-            dec = INT32_MIN;
-          }
-        }
-      }
       body(m, std::make_integer_sequence<int, L>{});
       m -= L;
     }
@@ -887,10 +832,9 @@ template <typename T, int NV>
 constexpr bool kPackedF32 = false;
 #endif
 
-template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, bool PS = false, int CLX = 0,
-          class Ext = NoExt>
+template <typename T, int NV, int K, int EK, int RING, int AR, bool ST = false, bool PS = false, int CLX = 0>
 __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r, int64_t strip, int64_t t0,
-                                      int64_t t1, int lane, StatAcc* acc = nullptr, Ext ext = Ext{}) {
+                                      int64_t t1, int lane, StatAcc* acc = nullptr) {
   using S = TbShape<T, NV, K>;
   constexpr int V = S::V;
   constexpr int ES = (int)sizeof(T);
@@ -951,7 +895,7 @@ __device__ __forceinline__ void march(const T* src, T* dst, const TbArgs& a, T r
     w.run();
     *acc = w.acc;
   } else {
-    w.template run<PS>(ext);
+    w.template run<PS>();
   }
 }
 
@@ -1076,90 +1020,6 @@ __device__ __forceinline__ void queue_exit(const TbArgs& a) {
     __hip_atomic_store(a.queue + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-// The continued-item kernels' exit: as queue_exit, and the last wave out also
-// clears the claim flags (every other wave has left its loop: no claim is
-// pending), so the next launch — or the next replay of a captured one —
-// starts from zeros.
-__device__ __forceinline__ void queue_exit_cont(const TbArgs& a) {
-  uint32_t d = 0;
-  if (lane_id_is0()) d = __hip_atomic_fetch_add(a.queue + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  d = __builtin_amdgcn_readfirstlane(d);
-  if (d + 1u != (uint32_t)a.nwaves) return;
-  for (int64_t i = threadIdx.x & 63; i < a.nitems; i += 64) a.queue[2 + i] = 0u;
-  if (lane_id_is0()) {
-    __hip_atomic_store(a.queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.queue + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// Continued items: the claim flags of a band rect are numbered strip-major
-// (flag = item0 + strip_local * nb + band), so the band above a band is the
-// previous flag, and its bands are cont_rows() tall (the last one shorter),
-// so the band above starts `h` rows earlier — the hook inside the march needs
-// neither a division nor the rect. claim_item: true when this wave got the
-// flag — a band is marched by exactly one wave, whether it took it from the
-// queue or marched into it from the band below.
-__device__ __forceinline__ bool claim_item(const TbArgs& a, int64_t flag) {
-  uint32_t old = 0;
-  if (lane_id_is0()) old = __hip_atomic_exchange(a.queue + 2 + flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return __builtin_amdgcn_readfirstlane(old) == 0u;
-}
-// band height of a continued rect: ceil(rows / nb) (the host checks that no
-// band is empty and each is at least 2k rows: launch_rects)
-__device__ __forceinline__ int64_t cont_rows(const TbRectArg& R) { return (R.r1 - R.r0 + R.nb - 1) / R.nb; }
-// Queue position q -> (flag, strip, output rows). Within a band rect the
-// queue hands out bands in stride order — nb-1, nb-1-s, nb-1-2s, ..., then
-// nb-2, nb-2-s, ... (s = TbArgs::cont) — each band over all strips: the first
-// round of waves starts ~nb/s marches per strip, spaced s bands apart, and
-// each marches on through the bands above its start (in row order: the march
-// runs toward row 0) until it meets a claimed one; the bands nobody has
-// reached are taken from the queue by the waves that end first.
-struct ContItem {
-  int64_t flag, strip, t0, t1, h;
-  int32_t band;  // bands above this one in its strip
-};
-template <int NR>
-__device__ __forceinline__ ContItem cont_item(const TbArgs& a, int64_t q) {
-  TbRectArg R = a.rect[0];
-#pragma unroll
-  for (int i = 1; i < NR; ++i)
-    if (i < a.nrect && q >= a.rect[i].item0) R = a.rect[i];
-  const int64_t ns = R.s1 - R.s0, local = q - R.item0;
-  const int32_t p0 = (int32_t)muldiv(local, 1, ns), sl = (int32_t)(local - (int64_t)p0 * ns);
-  const int32_t nb = (int32_t)R.nb, s = min(a.cont, nb);
-  int32_t p = p0, band = 0;
-  for (int32_t c = 0; c < s; ++c) {  // class c: bands nb-1-c, nb-1-c-s, ...
-    const int32_t n = (nb - c + s - 1) / s;
-    if (p < n) {
-      band = nb - 1 - c - p * s;
-      break;
-    }
-    p -= n;
-  }
-  ContItem g;
-  g.h = cont_rows(R);
-  g.flag = R.item0 + (int64_t)sl * nb + band;
-  g.strip = R.s0 + sl;
-  g.t0 = R.r0 + band * g.h;
-  g.t1 = min(R.r1, g.t0 + g.h);
-  g.band = band;
-  return g;
-}
-// The continuation hook handed to the march (see NoExt).
-struct ContExt {
-  static constexpr bool on = true;
-  const TbArgs& a;
-  int32_t& flag;  // the band being marched
-  int32_t& left;  // bands above it in the strip
-  int32_t h;      // band height
-  __device__ __forceinline__ bool operator()(int32_t& t0) const {
-    if (left == 0 || !claim_item(a, flag - 1)) return false;
-    --flag;
-    --left;
-    t0 -= h;
-    return true;
-  }
-};
 
 // Kernel variants (VAR): 0 plain; 1 fused statistics (StatAcc; general kernel).
 // (A latency-oriented variant for the boundary-band launch — priming skip +
@@ -1168,34 +1028,12 @@ struct ContExt {
 // first items were the bands the exchange sends: one such launch ran 720 us
 // where band launch + interior take 647 (edge-first) or 610 (lead order),
 // profiles/r4/lead/.)
-// kVarCont: continued items (interior kernels); kVarFrame: the frame-row band
-// kernel (ring 4: boundary bands at the global top / bottom rows, frame
-// columns excluded)
-constexpr int kVarPlain = 0, kVarStats = 1, kVarCont = 2, kVarFrame = 3;
-
-// The frame-row band kernel (kVarFrame). A slab at the global frame (the
-// first / last rank; the whole grid at both ends) has a boundary band whose
-// marches reach a Dirichlet row; the interior kernel has no frame-row path, so
-// that band ran on the general kernel, whose four edge kinds cost ~360 VGPRs
-// at depth 20: 1 wave per SIMD, which fits only where a SIMD has no interior
-// wave left — the band ran in the interior's tail and ended 28-49 us after it
-// (profiles/r6/b/). This kernel marches every item as edge kind 1 (frame rows,
-// any row may be one) with one dependency chain and no priming skip: 200
-// VGPRs at fp64 depth 20, 2 waves per SIMD like the interior kernel, so the
-// band can lead beside the interior as a middle rank's bands do. Frame-column
-// strips (edge kind 3 at the band's two ends) stay on the general kernel (two
-// items, launch_frame_rect). (fp32 at K >= 19: its packed march spills under
-// a 2-wave floor, so no floor there — 1 wave per SIMD, frame_ok() false, the
-// general kernel keeps those bands.)
-template <typename T, int NV, int K, int RING, bool MAIN, int AR>
-constexpr int kFrameWaves = (RING == 4 && !MAIN && !(std::is_same<T, float>::value && K >= 19)) ? 2 : 1;
+constexpr int kVarPlain = 0, kVarStats = 1;
 
 template <typename T, int NV, int K, int RING, bool MAIN, int AR, int VAR = kVarPlain>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVarStats ? 1 : VAR == kVarFrame ? kFrameWaves<T, NV, K, RING, MAIN, AR> : kMinWaves<T, NV, K, RING, MAIN, AR>))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVarPlain ? kMinWaves<T, NV, K, RING, MAIN, AR> : 1))) void tb_kernel(const T* __restrict__ src, T* __restrict__ dst, TbArgs a, T r) {
   constexpr bool ST = VAR == kVarStats;
   static_assert(VAR != kVarStats || !MAIN, "the statistics variant uses the general kernel");
-  static_assert(VAR != kVarCont || MAIN, "continued items: interior kernels only");
-  static_assert(VAR != kVarFrame || (!MAIN && RING == 4), "the frame-row band kernel: ring 4, general rects");
   using S = TbShape<T, NV, K>;
   const int lane = threadIdx.x & 63;
   // readfirstlane: make the wave id (and everything derived from it: strip, rows,
@@ -1211,27 +1049,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
   // strips of the same band, so the waves in flight stream whole contiguous
   // rows (HBM page locality) and all march in step.
   StatAcc acc;
-  constexpr int NR = MAIN ? kMainRects : kMaxRects;
-  if constexpr (VAR == kVarCont) {  // continued items over band rects (queue and claim flags required)
-    for (int64_t q = wid; q < a.nitems; q = next_item(a, q)) {
-      const ContItem g = cont_item<NR>(a, q);
-      if (!claim_item(a, g.flag)) continue;  // a march from the band below got there first
-      int32_t flag = (int32_t)g.flag, left = g.band;
-      const ContExt ext{a, flag, left, (int32_t)g.h};
-      if ((g.strip * S::U - S::KA < 0) || (g.strip * S::U - S::KA + S::W > a.ncols))
-        march<T, NV, K, 2, RING, AR, false, true, 0, ContExt>(src, dst, a, r, g.strip, g.t0, g.t1, lane, nullptr, ext);
-      else
-        march<T, NV, K, 0, RING, AR, false, true, 0, ContExt>(src, dst, a, r, g.strip, g.t0, g.t1, lane, nullptr, ext);
-    }
-    queue_exit_cont(a);
-    if (a.wtimes && lane_id_is0()) {
-      a.wtimes[wid * 4 + 1] = wall_clock64();
-      a.wtimes[wid * 4 + 2] = (uint64_t)wid;
-    }
-    return;
-  }
   // one flat loop over the pieces of items wid, wid + nwaves, ... (a nested
   // piece loop around the march costs the deep fp64 kernels registers)
+  constexpr int NR = MAIN ? kMainRects : kMaxRects;
   int64_t it = wid;
   int32_t lin = tb_span<NR>(a, it).lin;
   while (it < a.nitems) {
@@ -1243,9 +1063,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VAR == kVar
     }
     lin += (int32_t)(t1 - t0);
     const int64_t c0 = strip * S::U - S::KA;
-    if constexpr (VAR == kVarFrame) {  // every item as edge kind 1 (no frame columns: host-checked)
-      march<T, NV, K, 1, RING, AR, false, false, K>(src, dst, a, r, strip, t0, t1, lane);
-    } else if constexpr (ST) {
+    if constexpr (ST) {
       const int ek = (((t0 - K < a.fixed_lo) || (t1 + K > a.fixed_hi)) ? 1 : 0) |
                      (((c0 < 0) || (c0 + S::W > a.ncols)) ? 2 : 0);
       switch (ek) {
@@ -1315,18 +1133,6 @@ template <typename T, int RING, bool MAIN, int AR>
 void dispatch(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
 template <typename T, int RING, bool MAIN, int AR>
 int occupancy_blocks(int k);
-// frame-row band kernels (kVarFrame), instantiated beside the ring-4 general
-// kernels in tb_<dtype>_r4_gen*.hip
-template <typename T, int AR>
-void dispatch_frame(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
-template <typename T, int AR>
-int occupancy_blocks_frame(int k);
-// continued-item interior kernels (kVarCont), instantiated beside the plain
-// interior kernels in tb_<dtype>_r<RING>_main*.hip
-template <typename T, int RING, int AR>
-void dispatch_cont(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
-template <typename T, int RING, int AR>
-int occupancy_blocks_cont(int k);
 // fused-statistics kernels: general kernel, ring 4 (tb_<dtype>_stats.hip)
 template <typename T, int AR>
 void dispatch_stats(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, hipStream_t s);
@@ -1356,77 +1162,6 @@ int occupancy_blocks_stats(int k);
   M(T, RING, MAIN, AR, 17) M(T, RING, MAIN, AR, 18) M(T, RING, MAIN, AR, 19) M(T, RING, MAIN, AR, 20)   \
   M(T, RING, MAIN, AR, 21) M(T, RING, MAIN, AR, 22) M(T, RING, MAIN, AR, 23) M(T, RING, MAIN, AR, 24)
 #define H2D_NO_CASES(M, T, RING, MAIN, AR)
-#define H2D_TBC_CASE(T, RING, MAIN, AR, KK)                                                                           \
-  case KK:                                                                                                            \
-    hipLaunchKernelGGL((tb_kernel<T, 1, KK, RING, true, AR, kVarCont>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
-    return;
-#define H2D_OCC_C_CASE(T, RING, MAIN, AR, KK) \
-  case KK:                                    \
-    return blocks_per_cu<T, 1, KK, RING, true, AR, kVarCont>();
-// the continued-item twins of a unit's interior kernels (H2D_TB_CONT_true;
-// general-kernel units: nothing). fp64 K = 17..24 have none: the hook's
-// registers cost those interior kernels their second wave per SIMD (K = 20:
-// 247 -> 257 VGPRs), and 1 wave per SIMD loses more than continued items gain.
-#define H2D_CONT_DEEP_double(DEEP) H2D_NO_CASES
-#define H2D_CONT_DEEP_float(DEEP) DEEP
-#define H2D_TB_CONT_false(T, RING, AR, DEEP)
-#define H2D_TB_CONT_true(T, RING, AR, DEEP)                                                               \
-  template <>                                                                                             \
-  void dispatch_cont<T, RING, AR>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r,    \
-                                  hipStream_t s) {                                                        \
-    switch (k) {                                                                                          \
-      H2D_TB_CASES(H2D_TBC_CASE, T, RING, true, AR)                                                       \
-      DEEP(H2D_TBC_CASE, T, RING, true, AR)                                                               \
-      default:                                                                                            \
-        break;                                                                                            \
-    }                                                                                                     \
-    HEAT2D_REQUIRE(false, "temporal depth not instantiated for the continued-item kernel");               \
-  }                                                                                                       \
-  template <>                                                                                             \
-  int occupancy_blocks_cont<T, RING, AR>(int k) {                                                         \
-    switch (k) {                                                                                          \
-      H2D_TB_CASES(H2D_OCC_C_CASE, T, RING, true, AR)                                                     \
-      DEEP(H2D_OCC_C_CASE, T, RING, true, AR)                                                             \
-      default:                                                                                            \
-        break;                                                                                            \
-    }                                                                                                     \
-    return 0; /* not instantiated */                                                                      \
-  }
-#define H2D_TBF_CASE(T, RING, MAIN, AR, KK)                                                                         \
-  case KK:                                                                                                          \
-    hipLaunchKernelGGL((tb_kernel<T, 1, KK, 4, false, AR, kVarFrame>), dim3(nblocks), dim3(256), 0, s, src, dst, a, r); \
-    return;
-#define H2D_OCC_F_CASE(T, RING, MAIN, AR, KK) \
-  case KK:                                    \
-    return blocks_per_cu<T, 1, KK, 4, false, AR, kVarFrame>();
-// the frame-row band kernels of a ring-4 general unit (H2D_TB_FRAME_false_4;
-// every other unit: nothing)
-#define H2D_TB_FRAME_true_4(T, AR, DEEP)
-#define H2D_TB_FRAME_true_6(T, AR, DEEP)
-#define H2D_TB_FRAME_false_6(T, AR, DEEP)
-#define H2D_TB_FRAME_false_8(T, AR, DEEP)
-#define H2D_TB_FRAME_false_4(T, AR, DEEP)                                                                 \
-  template <>                                                                                             \
-  void dispatch_frame<T, AR>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r,         \
-                             hipStream_t s) {                                                             \
-    switch (k) {                                                                                          \
-      H2D_TB_CASES(H2D_TBF_CASE, T, 4, false, AR)                                                         \
-      DEEP(H2D_TBF_CASE, T, 4, false, AR)                                                                 \
-      default:                                                                                            \
-        break;                                                                                            \
-    }                                                                                                     \
-    HEAT2D_REQUIRE(false, "temporal depth not instantiated for the frame-row band kernel");               \
-  }                                                                                                       \
-  template <>                                                                                             \
-  int occupancy_blocks_frame<T, AR>(int k) {                                                              \
-    switch (k) {                                                                                          \
-      H2D_TB_CASES(H2D_OCC_F_CASE, T, 4, false, AR)                                                       \
-      DEEP(H2D_OCC_F_CASE, T, 4, false, AR)                                                               \
-      default:                                                                                            \
-        break;                                                                                            \
-    }                                                                                                     \
-    return 0; /* not instantiated */                                                                      \
-  }
 #define H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, DEEP)                                                       \
   template <>                                                                                           \
   void dispatch<T, RING, MAIN, AR>(int k, unsigned nblocks, const T* src, T* dst, const TbArgs& a, T r, \
@@ -1448,9 +1183,7 @@ int occupancy_blocks_stats(int k);
         break;                                                                                          \
     }                                                                                                   \
     return 1;                                                                                           \
-  }                                                                                                     \
-  H2D_TB_CONT_##MAIN(T, RING, AR, H2D_CONT_DEEP_##T(DEEP))                                              \
-  H2D_TB_FRAME_##MAIN##_##RING(T, AR, DEEP)
+  }
 #define H2D_TB_UNIT(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_NO_CASES)
 #define H2D_TB_UNIT_F64(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_DEEP)
 #define H2D_TB_UNIT_F32(T, RING, MAIN, AR) H2D_TB_UNIT_IMPL(T, RING, MAIN, AR, H2D_TB_CASES_F32DEEP)

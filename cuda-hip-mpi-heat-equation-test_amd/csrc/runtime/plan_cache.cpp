@@ -143,7 +143,7 @@ bool get_plan(const std::string& ctx, int k, int64_t band, kern::SplitPlan* p, f
   q.nrects = (int32_t)nr;
   q.flags = (int32_t)pr;
   if (!in || q.k != k || q.valid < 1 || q.valid > 3 || q.nedge < 0 || q.nedge > 4 || q.nrects < 0 ||
-      q.nrects > kern::kMaxPlanRects || q.flags < 0 || q.flags > (kern::kPlanDynamic | kern::kPlanLead | kern::kPlanContinue))
+      q.nrects > kern::kMaxPlanRects || q.flags < 0 || q.flags > (kern::kPlanDynamic | kern::kPlanLead))
     return false;
   *p = q;
   *ms = t;

@@ -75,7 +75,7 @@ Footprint solver_footprint(const SolverConfig& cfg, int rank, int nranks) {
   Footprint f{};
   f.field_bytes = 2 * L.elems() * (int64_t)dtype_size((DType)cfg.dtype);
   if (cfg.backend == (int32_t)Backend::Hip)
-    f.work_bytes = (kern::stats_work_elems() + 8) * 8 + 6 * kern::max_stats_waves() * 8 + (2 + kern::kQueueClaims) * 4;
+    f.work_bytes = (kern::stats_work_elems() + 8) * 8 + 6 * kern::max_stats_waves() * 8 + 2 * 4;
   f.total_bytes = f.field_bytes + f.work_bytes;
   return f;
 }
@@ -166,9 +166,8 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     // (solver_footprint() counts exactly these allocations: keep them in step)
     H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_work_), (size_t)(kern::stats_work_elems() + 8) * sizeof(double)));
     H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_part_), (size_t)(6 * kern::max_stats_waves()) * sizeof(double)));
-    // the dynamic queue's two counters + the continued items' claim flags
-    H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_queue_), (size_t)(2 + kern::kQueueClaims) * sizeof(uint32_t)));
-    H2D_HIP(hipMemset(d_queue_, 0, (size_t)(2 + kern::kQueueClaims) * sizeof(uint32_t)));
+    H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_queue_), 2 * sizeof(uint32_t)));
+    H2D_HIP(hipMemset(d_queue_, 0, 2 * sizeof(uint32_t)));
     if (external_stream) {
       s_compute_ = s_comm_ = external_stream;
       cfg_.overlap = 0;
@@ -199,14 +198,12 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
       // (A high-priority comm stream did not get the band waves dispatched
       // first in steady-state cycles, nor change the small grid: profiles/r4/lead/, r4/m/.)
       H2D_HIP(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
-      H2D_HIP(hipStreamCreateWithFlags(&s_side_, hipStreamNonBlocking));
       own_streams_ = true;
     }
     H2D_HIP(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_comm_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_int_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_frame_, hipEventDisableTiming));
-    H2D_HIP(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
@@ -228,7 +225,6 @@ Solver::~Solver() {
     (void)hipSetDevice(cfg_.device);
     if (s_compute_) (void)hipStreamSynchronize(s_compute_);
     if (s_comm_ && s_comm_ != s_compute_) (void)hipStreamSynchronize(s_comm_);
-    if (s_side_) (void)hipStreamSynchronize(s_side_);
     if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
     for (auto& g : sched_graph_) (void)hipGraphExecDestroy(g.second);
     for (auto& b : buf_)
@@ -240,7 +236,6 @@ Solver::~Solver() {
     if (ev_comm_) (void)hipEventDestroy(ev_comm_);
     if (ev_int_) (void)hipEventDestroy(ev_int_);
     if (ev_frame_) (void)hipEventDestroy(ev_frame_);
-    if (ev_side_) (void)hipEventDestroy(ev_side_);
     if (ev_t0_) (void)hipEventDestroy(ev_t0_);
     if (ev_t1_) (void)hipEventDestroy(ev_t1_);
     for (auto* v : {&phase_ev_, &phase_pool_})
@@ -249,7 +244,6 @@ Solver::~Solver() {
     if (own_streams_) {
       (void)hipStreamDestroy(s_compute_);
       (void)hipStreamDestroy(s_comm_);
-      if (s_side_) (void)hipStreamDestroy(s_side_);
     }
     (void)hipGetLastError();  // teardown errors must not surface as the next launch's
   } else {
@@ -407,11 +401,6 @@ void Solver::cycle_finish() {
       H2D_HIP(hipStreamWaitEvent(s_compute_, ev_frame_, 0));
       pend_frame_ = -1;
     }
-    if (side_pend_) {  // the lead cycle's frame-column corners (launch_overlap): joined into both streams
-      H2D_HIP(hipStreamWaitEvent(s_compute_, ev_side_, 0));
-      H2D_HIP(hipStreamWaitEvent(s_comm_, ev_side_, 0));
-      side_pend_ = false;
-    }
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
   }
   roctxRangePop();
@@ -548,11 +537,6 @@ const kern::SplitPlan& Solver::split_plan(int k) {
     // HEAT2D_DYNAMIC=1: the main launch takes its items from the dynamic queue (tests, A/B)
     if (const char* e = std::getenv("HEAT2D_DYNAMIC"); e && std::atoi(e) == 1 && p.valid >= 1 && p.valid <= 3)
       p.flags |= kern::kPlanDynamic;
-    // HEAT2D_CONTINUE=1: continued items on the interior's bands where the
-    // kernel twin exists (with the queue; tests, A/B)
-    if (const char* e = std::getenv("HEAT2D_CONTINUE"); e && std::atoi(e) == 1 && (p.valid == 1 || p.valid == 3) &&
-        p.main.nb > 0 && kern::cont_ok(dtype(), p.ring, k, cfg_.arith))
-      p.flags |= kern::kPlanDynamic | kern::kPlanContinue;
   }
   return p;
 }
@@ -616,21 +600,6 @@ static bool dynamic_candidates() {
   return on;
 }
 
-// Continued-item candidates (HEAT2D_CONTINUE=0 keeps them out of the
-// autotuner; =1 forces them on the interior's bands): every dynamic band plan
-// the screening times is also timed with continued items where the kernel
-// twin keeps the interior kernel's occupancy (kern::cont_ok: fp32, fp64 to
-// K = 16), and so are finer band counts (3x, 4x the default), which continued
-// items make cheap: a march runs on through unclaimed bands without a new
-// priming or halo re-read, and the queue balances at the finer grain.
-static bool continue_candidates() {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT2D_CONTINUE");
-    return dynamic_candidates() && (!e || std::atoi(e) != 0);
-  }();
-  return on;
-}
-
 // The first cycle of a step() call on an exchanging slab runs in the lead
 // order whatever its plan's split order (HEAT2D_LEAD_FIRST=0: the plan's
 // order): issued onto an idle GPU, the band launch gets its wave slots before
@@ -644,13 +613,6 @@ static bool continue_candidates() {
 static bool lead_first() {  // (read per call: tests toggle it within one process)
   const char* e = std::getenv("HEAT2D_LEAD_FIRST");
   return !e || std::atoi(e) != 0;
-}
-// HEAT2D_LEAD_SOLO=1: the lead order for the first cycle of an unexchanging
-// slab too (one rank: the whole grid's frame bands issued before the
-// interior instead of beside it; A/B)
-static bool lead_solo() {
-  const char* e = std::getenv("HEAT2D_LEAD_SOLO");
-  return e && std::atoi(e) != 0;
 }
 
 // smallest steady-state cycle (ms) for which edge-first split plans are tried
@@ -716,7 +678,7 @@ float Solver::time_plan(const kern::SplitPlan& c, int kTimed) {
 static uint64_t plan_env_hash() {
   static const uint64_t h = [] {
     uint64_t v = 1469598103934665603ull;
-    for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_CONTINUE", "HEAT2D_TB_RING",
+    for (const char* name : {"HEAT2D_DYNAMIC", "HEAT2D_TB_RING",
                              "HEAT2D_SPLIT_ORDER", "HEAT2D_SEGMENTS", "HEAT2D_BANDS", "HEAT2D_MAX_WAVES",
                              "HEAT2D_EDGE_BANDS", "HEAT2D_GRAPH_MAX_CYCLE_US"}) {
       const char* e = std::getenv(name);
@@ -764,8 +726,6 @@ bool Solver::cached_split(int k) {
   // (the dynamic queue is off under HEAT2D_DYNAMIC=0; a single launch cannot
   // exchange; the lead order is for exchanging slabs)
   if ((c.flags & kern::kPlanDynamic) && !dynamic_candidates()) return false;
-  if ((c.flags & kern::kPlanContinue) && (!continue_candidates() || !kern::cont_ok(dtype(), c.ring, k, cfg_.arith)))
-    return false;
   if (c.valid == 2 && tr_->exchanges()) return false;
   if ((c.flags & kern::kPlanLead) && (c.valid != 1 || !tr_->exchanges())) return false;
   // HEAT2D_PLAN_CACHE_TRUST=1: no re-time (bench.py --measure-hbm's profiled
@@ -893,10 +853,6 @@ void Solver::autotune_split(int k) {
       kern::SplitPlan d = c;
       d.flags |= kern::kPlanDynamic;
       cands.push_back(d);
-      if (continue_candidates() && c.valid != 2 && c.main.nb > 0 && kern::cont_ok(dtype(), c.ring, k, cfg_.arith)) {
-        d.flags |= kern::kPlanContinue;
-        cands.push_back(d);
-      }
     }
   };
   if (dynamic_candidates() && best.main_items > best.main_waves && best.valid >= 1 && best.valid <= 3) {
@@ -917,15 +873,8 @@ void Solver::autotune_split(int k) {
     // ring 8 (6 rows in flight): fp32 single launches only (stencil_tb.hip ring_ok)
     const std::vector<int> rings = (mode == 2 && dtype() == DType::F32 && k <= 16) ? std::vector<int>{4, 6, 8}
                                                                                      : std::vector<int>{4, 6};
-    // continued items: finer bands too (a march runs on through them)
-    std::vector<double> fs = factors;
-    if (continue_candidates() && mode != 2 && !long_cycles)
-      for (double f : {3.0, 4.0}) fs.push_back(f);
     for (int ring : rings) {
-      for (double f : fs) {
-        // (the finer counts only for continued items)
-        const bool cont_only = f > 2.0;
-        if (cont_only && !kern::cont_ok(dtype(), ring, k, cfg_.arith)) continue;
+      for (double f : factors) {
         const int64_t nb = std::max<int64_t>(1, (int64_t)((mode == 2 ? nb1 : nb0) * f + 0.5));
         if (mode == 1 && ring == best.ring && nb == best.main.nb) continue;
         kern::SplitPlan c = mode == 2 ? kern::plan_single(dtype(), L_, k, compute_cus_, ring, nb, cfg_.arith)
@@ -935,13 +884,6 @@ void Solver::autotune_split(int k) {
         if (mode == 3) c.valid = 3;
         if (mode == 1)  // more items than waves only via explicit band counts above the default
           c.main_waves = std::min<int64_t>(c.main_items, std::max<int64_t>(c.main_waves, best.main_waves));
-        if (cont_only) {
-          if (c.main_items > c.main_waves && dynamic_candidates()) {
-            c.flags |= kern::kPlanDynamic | kern::kPlanContinue;
-            cands.push_back(c);
-          }
-          continue;
-        }
         add(c);
       }
       // segment work items (TbRect nb < 0): the interior cut into equal runs of
@@ -1036,25 +978,20 @@ void Solver::launch_overlap(int k, int64_t B) {
   roctxRangePushA("heat2d.cycle.split");
   PhaseEvents* pe = timing_ ? phase_begin(0) : nullptr;
   pend_pe_ = pe ? (int64_t)phase_ev_.size() - 1 : -1;
-  // (the first cycle leads only where the band launch runs at 2 waves per
-  // SIMD: on the interior kernel (bands clear of the global frame rows), or —
-  // at the global frame (the first / last rank, the whole grid) — on the
-  // frame-row band kernel (kern::frame_ok). Bands on the general kernel, whose
-  // 1-wave/SIMD waves issued first hold the register files of ~750 SIMDs
-  // against the interior, ran 850 us instead of 615 for a one-cycle step
-  // (profiles/r5/ad/). An unexchanging slab (one rank, the whole grid) leads
-  // its first cycle when HEAT2D_LEAD_SOLO=1.)
-  const bool bands_lead = kern::edges_on_main(L_, sp) || kern::frame_ok(dtype(), sp.k, cfg_.arith);
+  // (the first cycle leads only where the band launch runs on the interior
+  // kernel: a slab at the global frame (the first / last rank) bands on the
+  // general kernel, whose 1-wave/SIMD waves issued first hold the register
+  // files of ~750 SIMDs against the interior — 850 us instead of 615 for its
+  // one-cycle step, edge-first 640: profiles/r5/ad/)
   const bool lead = (sp.valid == 1 || sp.valid == 3) &&
                     ((sp.flags & kern::kPlanLead) ||
-                     (first_cycle_ && (tr_->exchanges() || lead_solo()) && lead_first() && bands_lead));
-  // Without the frame-row band kernel, an edge rank's first cycle runs its
-  // two bands apart. The far band (the one the exchange sends, clear of the
-  // global frame) leads on the interior kernel as on a middle rank; the
-  // frame-side band — which no exchange reads — goes on the general kernel
-  // behind the exchange on the comm stream (cycle_finish), into the wave slots
-  // the interior's last round of items leaves free (it ends 28-49 us after
-  // the interior: profiles/r6/b/).
+                     (first_cycle_ && tr_->exchanges() && lead_first() && kern::edges_on_main(L_, sp)));
+  // An edge rank's first cycle: its two bands apart. The far band (the one
+  // the exchange sends, clear of the global frame) leads on the interior
+  // kernel as on a middle rank; the frame-side band — which no exchange
+  // reads — goes on the general kernel behind the exchange on the comm
+  // stream (cycle_finish), into the wave slots the interior's last round of
+  // items leaves free.
   int frame_rect = -1;
   if (!lead && (sp.valid == 1 || sp.valid == 3) && first_cycle_ && tr_->exchanges() && lead_first() &&
       sp.nedge == 2 && kern::edge_rect_on_main(L_, sp, 0) != kern::edge_rect_on_main(L_, sp, 1))
@@ -1097,20 +1034,8 @@ void Solver::launch_overlap(int k, int64_t B) {
   H2D_HIP(hipStreamWaitEvent(s_comm_, ev_int_, 0));     // main part c-1
   if (pe) H2D_HIP(hipEventRecord(pe->ev[2], s_comm_));
   if (lead) {
-    // lead: the band launch first (comm stream), then the interior beside it.
-    // Bands at the global frame rows: their frame-column corners (general
-    // kernel, 1 wave per SIMD, a few items) first, on the side stream — on the
-    // comm stream they would hold the frame-row band kernel's launch behind
-    // them until the interior has taken every SIMD (profiles/r6/f/)
-    const bool side = s_side_ && kern::edges_have_corners(dtype(), L_, sp, cfg_.arith);
-    if (side) {
-      for (hipEvent_t e : {ev_int_, ev_bnd_, ev_comm_}) H2D_HIP(hipStreamWaitEvent(s_side_, e, 0));
-      kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_side_, cfg_.arith, nullptr, kern::kEdgeCorners);
-      H2D_HIP(hipEventRecord(ev_side_, s_side_));
-      side_pend_ = true;
-    }
-    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_, cfg_.arith, nullptr,
-                       side ? kern::kEdgeBands : kern::kEdgeBands | kern::kEdgeCorners);
+    // lead: the band launch first (comm stream), then the interior beside it
+    kern::launch_split(dtype(), src, dst, L_, sp, false, cfg_.r, s_comm_, cfg_.arith);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[0], s_compute_));
     kern::launch_split(dtype(), src, dst, L_, sp, true, cfg_.r, s_compute_, cfg_.arith, d_queue_);
     if (pe) H2D_HIP(hipEventRecord(pe->ev[1], s_compute_));

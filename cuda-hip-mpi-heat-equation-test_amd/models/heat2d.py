@@ -50,14 +50,12 @@ def _plan(h, k: int) -> dict:
     return {"k": p.k, "ring": p.ring, "valid": p.valid,
             "order": ("lead" if p.valid == 1 and p.flags & 4 else
                       {1: "concurrent", 2: "single", 3: "edge-first"}.get(p.valid, "serial")),
-            "dynamic": int((p.flags >> 1) & 1), "continued": int((p.flags >> 3) & 1),
-            "origin": PLAN_ORIGINS.get(org.value, "?"),
+            "dynamic": int((p.flags >> 1) & 1), "origin": PLAN_ORIGINS.get(org.value, "?"),
             "main_bands": p.main.nb, "main_items": p.main_items, "main_waves": p.main_waves,
             "edge_items": p.edge_items, "edge_waves": p.edge_waves, "tuned_ms": ms.value,
             "main_rect": [p.main.r0, p.main.r1, p.main.s0, p.main.s1, p.main.nb],
             "edge_rects": [[e.r0, e.r1, e.s0, e.s1, e.nb] for e in list(p.edge)[:p.nedge]],
-            # the rects launched instead of main_rect: frame-weighted (arith 2;
-            # a continued-item plan launches main_rect itself)
+            # the rects launched instead of main_rect: frame-weighted (arith 2)
             "main_rects": [[e.r0, e.r1, e.s0, e.s1, e.nb] for e in list(p.rects)[:p.nrects]]}
 
 

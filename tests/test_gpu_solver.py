@@ -330,54 +330,6 @@ def test_segment_plans_bitwise(gpu, native, order, nseg, dtype, monkeypatch):
     assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
 
 
-@pytest.mark.parametrize("order,nb,waves", [("concurrent", 9, 0), ("edge-first", 31, 0), ("concurrent", 23, 16),
-                                             ("edge-first", 5, 3)])
-@pytest.mark.parametrize("dtype,tb", [("fp64", 12), ("fp64", 14), ("fp32", 16), ("fp32", 21)])
-def test_continued_item_plans_bitwise(gpu, native, order, nb, waves, dtype, tb, monkeypatch):
-    """Continued items (HEAT2D_CONTINUE=1, the kVarCont interior kernels): a
-    march that reaches the top of its band marches on into the band above when
-    no other wave has claimed it. Forced band counts, few waves (so marches do
-    run on through several bands) and the default persistent grid, both split
-    orders with real loopback exchanges over several cycles (the claim flags
-    must be cleared for the next launch): bitwise the golden."""
-    monkeypatch.setenv("HEAT2D_SPLIT_ORDER", order)
-    monkeypatch.setenv("HEAT2D_CONTINUE", "1")
-    monkeypatch.setenv("HEAT2D_BANDS", str(nb))
-    if waves:
-        monkeypatch.setenv("HEAT2D_MAX_WAVES", str(waves))
-    p = prob(1500, 3 * tb + 2, "ghost", "sine")
-    npdt = np.float64 if dtype == "fp64" else np.float32
-    g = LoopbackGroup(p, 3, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0)
-    g.upload(R.owned(R.initial_field(p, npdt)))
-    g.step(p.ntime)
-    got = g.download()
-    plans = [g.plan(i, tb) for i in range(3)]
-    g.close()
-    for pl in plans:
-        assert pl["continued"] == 1 and pl["dynamic"] == 1 and pl["main_bands"] > 1, pl
-    ref = R.owned(R.ftcs(p, dtype=npdt))
-    assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
-
-
-@pytest.mark.parametrize("dtype,tb", [("fp64", 16), ("fp32", 20)])
-def test_continued_items_graph_and_jacobi_bitwise(gpu, native, dtype, tb, monkeypatch):
-    """Continued items in a replayed hipGraph (the claim flags the last wave
-    clears must be zero again for each replay) on the r = 1/4 (jacobi) form of
-    the reference IC: bitwise its golden."""
-    monkeypatch.setenv("HEAT2D_CONTINUE", "1")
-    monkeypatch.setenv("HEAT2D_BANDS", "12")
-    monkeypatch.setenv("HEAT2D_MAX_WAVES", "64")
-    p = prob(1200, 6 * tb, "ghost", "uniform")
-    npdt = np.float64 if dtype == "fp64" else np.float32
-    s = HeatSolver(p, dtype=dtype, backend="hip", tb=tb, device=0, autotune=0, graph=True, arith="jacobi")
-    s.step(p.ntime)
-    got = s.download()
-    pl = s.plan(tb)
-    s.close()
-    assert pl["continued"] == 1, pl
-    assert np.array_equal(got, R.owned(R.ftcs(p, dtype=npdt, arith="jacobi")))
-
-
 @pytest.mark.parametrize("P", [2, 3])
 def test_loopback_serial_schedule_bitwise(gpu, native, P):
     """overlap=False: one launch per cycle on the compute stream, exchange

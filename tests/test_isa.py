@@ -32,15 +32,10 @@ def tb():
     # main/gen x 4 arith x (ring 4: fp32 K 1..24 + fp64 K 1..24; ring 6: fp32
     # K 1..16 + fp64 K 1..24), the fp32 general ring-8 kernels of single
     # launches (4 arith x K 1..16), plus the fused-statistics variants
-    # (general, ring 4, 4 arith) and the continued-item interior kernels (4
-    # arith x (ring 4: fp32 K 1..24 + fp64 K 1..16; ring 6: fp32 K 1..16 +
-    # fp64 K 1..16))
+    # (general, ring 4, 4 arith)
     assert sum(len(p) == 6 for p in ks) == 8 * (24 + 24) + 8 * (16 + 24) + 4 * 16, len(ks)
     assert sum(len(p) == 7 and p[6] == "stats" for p in ks) == 4 * (24 + 24), len(ks)
-    assert sum(len(p) == 7 and p[6] == "cont" for p in ks) == 4 * ((24 + 16) + (16 + 16)), len(ks)
-    # the frame-row band kernels: ring 4, 4 arith x (fp32 K 1..24 + fp64 K 1..24)
-    assert sum(len(p) == 7 and p[6] == "frame" for p in ks) == 4 * (24 + 24), len(ks)
-    assert len(ks) == 8 * (24 + 24) + 8 * (16 + 24) + 4 * 16 + 4 * (24 + 24) + 4 * (40 + 32) + 4 * 48, len(ks)
+    assert len(ks) == 8 * (24 + 24) + 8 * (16 + 24) + 4 * 16 + 4 * (24 + 24), len(ks)
     return ks
 
 
@@ -72,28 +67,6 @@ def test_deep_fp64_interior_two_waves(tb):
     for k in range(17, 25):  # fp32 K = 17..24: the interior kernel keeps 2 waves/SIMD at ring 4 (floor)
         for ar in (0, 1, 2, 3):
             assert tb[("fp32", 1, k, 4, True, ar)]["waves_per_simd"] >= 2, (k, ar)
-
-
-def test_continued_items_keep_occupancy(tb):
-    """The continued-item twins of the interior kernels the autotuner uses most
-    (fp32 to K = 24 at ring 4; fp64 to K = 16) keep the plain kernel's waves per
-    SIMD (Solver only uses a twin where they match: kern::cont_ok)."""
-    for k in range(1, 25):
-        for ar in (1, 2, 3):
-            assert tb[("fp32", 1, k, 4, True, ar, "cont")]["waves_per_simd"] >= \
-                min(2, tb[("fp32", 1, k, 4, True, ar)]["waves_per_simd"]), (k, ar)
-    assert tb[("fp64", 1, 16, 6, True, 2, "cont")]["waves_per_simd"] == tb[("fp64", 1, 16, 6, True, 2)]["waves_per_simd"]
-
-
-def test_frame_band_kernel_two_waves(tb):
-    """The frame-row band kernel keeps 2 waves per SIMD at every fp64 depth and
-    fp32 to K = 18 (so the boundary bands at the global frame rows can lead
-    beside the interior; the general kernel drops to 1 at fp64 K >= 17)."""
-    for dt, kmax in (("fp64", 24), ("fp32", 18)):
-        for k in range(1, kmax + 1):
-            for ar in (0, 1, 2, 3):
-                f = tb[(dt, 1, k, 4, False, ar, "frame")]
-                assert f["waves_per_simd"] >= 2, (dt, k, ar, f)
 
 
 def test_packed_fp32_compact(tb):

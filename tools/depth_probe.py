@@ -66,7 +66,7 @@ def main():
                       "ms_per_cycle": round(ms, 4), "us_per_level": round(ms * 1e3 / args.k, 2),
                       "gpts": round(rows * args.n * args.k / (ms * 1e-3) / 1e9, 1),
                       "launches_per_cycle": 2 if plan["order"] in ("concurrent", "edge-first", "lead") else 1,
-                      "plan": {k: plan[k] for k in ("order", "ring", "dynamic", "continued", "main_bands", "main_items",
+                      "plan": {k: plan[k] for k in ("order", "ring", "dynamic", "main_bands", "main_items",
                                                     "main_waves", "edge_items", "tuned_ms", "origin")}}),
           flush=True)
     s.close()

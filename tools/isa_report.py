@@ -79,8 +79,8 @@ def tb_params(mangled):
         return None
     p = ("fp64" if m.group(1) == "d" else "fp32", int(m.group(2)), int(m.group(3)), int(m.group(4)),
          m.group(5) == "1", int(m.group(6)))
-    var = m.group(7) or "0"  # kernel variant (tb_impl.hpp): 1 fused statistics, 2 continued items, 3 frame-row bands
-    return p + ({"1": "stats", "2": "cont", "3": "frame"}[var],) if var != "0" else p
+    var = m.group(7) or "0"  # kernel variant (tb_impl.hpp): 1 fused statistics
+    return p + ({"1": "stats"}.get(var, "var" + var),) if var != "0" else p
 
 
 def main():
