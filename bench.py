@@ -175,6 +175,13 @@ def main():
     ap.add_argument("--slab-pos", default="middle", choices=["first", "middle", "last"],
                     help="with --rehearse-comm --rows R: which rank's slab of the grid the rehearsal owns — the "
                          "first / last (the global frame row on one side, rank 0 / N-1) or a middle one")
+    ap.add_argument("--edge-shift", default="auto",
+                    help="rows each edge slab (rank 0 and the last rank, the global frame rows on one side) gives "
+                         "to the middle slabs of a >= 3-rank run: an integer, or auto (default): measured — every "
+                         "rank times its own slab alone (1-rank IPC loop-exchange rehearsal) uniform, then with "
+                         "the estimated shift, and the shift is kept if the slowest slab gets faster "
+                         "(parallel/select.balance_edges; one rank after another with --share-gpu). JSON "
+                         "config.decomposition")
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"],
                     help="cpu: the same harness on the native CPU twin over gloo (CI rehearsal of the "
                          "multi-process path: tests/test_bench_contract.py); not a performance number")
@@ -322,11 +329,13 @@ def main():
             return False
         return kind == "self" or (args.graph == "on" and kind in ("ipc", "ipc-loop"))
 
+    edge_shift = [0]  # the decomposition's edge shift (balance_edges below)
+
     def build(kind, tr):
         return HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb, overlap=not args.no_overlap,
                           graph=uses_graph(kind), tile_rows=args.tile_rows, transport=tr,
                           device=device if hip else None, rows=rows, comm_cus=args.comm_cus, arith=arith,
-                          slab_row0=slab_row0)
+                          slab_row0=slab_row0, edge_shift=edge_shift[0])
 
     own_s = [0.0]  # this rank's own seconds of the last timed run (the JSON's per-rank proof)
 
@@ -384,6 +393,74 @@ def main():
         tr, s, _ = live.pop(kind)
         s.close()
         tr.close()
+
+    from heat2d.ops import _native as N
+    balance_report = None
+    if args.edge_shift != "auto":
+        edge_shift[0] = int(args.edge_shift)
+    elif world >= 3 and hip and not args.rehearse_comm:
+        # Edge-balanced slabs (profiles/r6/b/: an edge
+        # slab's frame-side band runs on the general kernel and ends ~30 us
+        # after the interior at N = 8, so rank 0 and the last rank set the
+        # MAX). Each rank times its own slab alone — a 1-rank IPC loop
+        # exchange of its boundary bands (local device copies, no RCCL or IPC
+        # mapping), the bench's own warmup / prepare / timed step — before any
+        # transport or field of the real run exists.
+        def own_slab_ms(shift):
+            r0, nr = N.decompose(prob.n_owned, world, rank, shift)
+
+            def run():
+                tr_l = make_transport("ipc-loop")
+                try:
+                    s_l = HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb,
+                                     overlap=not args.no_overlap, graph=False, tile_rows=args.tile_rows,
+                                     transport=tr_l, device=device, rows=nr, comm_cus=args.comm_cus, arith=arith,
+                                     slab_row0=r0)
+                    try:
+                        s_l.step(args.warmup)
+                        s_l.synchronize()
+                        s_l.prepare(args.steps)
+                        best = float("inf")
+                        for _ in range(3):
+                            sync()
+                            t0 = time.perf_counter()
+                            s_l.step(args.steps)
+                            s_l.synchronize()
+                            sync()
+                            best = min(best, time.perf_counter() - t0)
+                        return best * 1e3
+                    finally:
+                        s_l.close()
+                finally:
+                    tr_l.close()
+            if not args.share_gpu:
+                return run()
+            # ranks sharing one GPU take turns (their rehearsals would contend)
+            v = float("nan")
+            for r in range(world):
+                if r == rank:
+                    try:
+                        v = run()
+                    except Exception:  # noqa: BLE001 - reported as NaN by balance_edges
+                        import traceback
+                        traceback.print_exc()
+                barrier()
+            return v
+
+        def gather_ms(v):
+            t = torch.zeros(world, dtype=torch.float64)
+            t[rank] = v
+            dist.all_reduce(t)
+            return t.tolist()
+
+        with select.deadline(init_timeout, "edge-balance rehearsal of the slabs", rank):
+            edge_shift[0], balance_report = select.balance_edges(
+                own_slab_ms, gather_ms, lambda d: [N.decompose(prob.n_owned, world, r, d)[1] for r in range(world)],
+                cap=(prob.n_owned // world) // 4)
+        if rank == 0:
+            print(f"bench.py: edge balance: shift {edge_shift[0]} rows: {json.dumps(balance_report)}",
+                  file=sys.stderr, flush=True)
+        barrier()
 
     cands = select.candidate_transports(args.transport, world, hip)
     choice_report = None
@@ -551,7 +628,8 @@ def main():
             try:
                 ref = HeatSolver(prob, dtype=args.dtype, backend=args.backend, transport=tr_ref,
                                  device=device if hip else None, rows=rr, slab_row0=r0, arith=arith,
-                                 engine="jit" if hip else "tb", tb=1, overlap=False, graph=False, autotune=0)
+                                 engine="jit" if hip else "tb", tb=1, overlap=False, graph=False, autotune=0,
+                                 edge_shift=edge_shift[0] if full_run else 0)
             except Exception:
                 tr_ref.close()
                 raise
@@ -684,6 +762,8 @@ def main():
                 "parallelism": f"slab{world}" + (f"-rehearsal-{args.slab_pos}" if args.rehearse_comm and world == 1 else "")
                                + ("-shared-gpu" if args.share_gpu and world > 1 else ""),
                 "transport": tr.name,
+                "decomposition": ({"edge_shift": edge_shift[0], "rows": [d["rows"] for d in proof["ranks"]],
+                                   "balance": balance_report} if world > 1 else None),
                 "transport_choice": (dict(choice_report, chosen=kind, requested=args.transport)
                                      if choice_report is not None else None),
                 "tb_max": tb,

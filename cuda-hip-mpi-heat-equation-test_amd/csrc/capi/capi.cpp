@@ -144,6 +144,14 @@ int heat2d_make_layout(int64_t nrows, int64_t ncols, int64_t halo, int64_t row0,
   });
 }
 
+int heat2d_decompose_shifted(int64_t n, int nranks, int rank, int64_t edge_shift, int64_t* row0, int64_t* nrows) {
+  return guarded([&] {
+    SlabRange r = decompose(n, nranks, rank, edge_shift);
+    *row0 = r.row0;
+    *nrows = r.nrows;
+  });
+}
+
 int heat2d_decompose(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nrows) {
   return guarded([&] {
     SlabRange r = decompose(n, nranks, rank);

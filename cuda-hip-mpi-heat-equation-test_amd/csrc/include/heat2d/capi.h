@@ -33,7 +33,7 @@ typedef struct heat2d_config {
   int64_t tile_rows, halo;
   int32_t comm_cus, autotune;
   int32_t engine, arith; /* arith: 0 reference rounding, 1 contracted fma, 2 jacobi (r = 1/4) */
-  int32_t pad0;
+  int32_t edge_shift; /* rows each edge slab gives the middle ones (common.hpp decompose) */
   int64_t slab_row0, slab_rows_global; /* 1-rank rehearsal of a middle slab (0: the slab is the grid) */
 } heat2d_config;
 
@@ -79,6 +79,8 @@ int heat2d_wave_times(uint64_t* out, int64_t max_waves, int64_t* n);
 int heat2d_make_layout(int64_t nrows, int64_t ncols, int64_t halo, int64_t row0,
                        int64_t nrows_global, heat2d_layout* out);
 int heat2d_decompose(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nrows);
+/* the same with the edge slabs' rows shifted to the middle ones (common.hpp) */
+int heat2d_decompose_shifted(int64_t n, int nranks, int rank, int64_t edge_shift, int64_t* row0, int64_t* nrows);
 /* MAIN + EDGE split of one cycle (the overlapped schedule's two launches) */
 int heat2d_plan_split(int dtype, const heat2d_layout* L, int k, int64_t band, heat2d_split_plan* out);
 int heat2d_plan_tb(int dtype, const heat2d_layout* L, int64_t rb, int64_t re, int k,

@@ -17,6 +17,7 @@ struct Meta {
   int64_t n_owned = 0, n_input = 0;
   std::string convention = "ghost";  // ghost | inclusive
   double sigma = 0, nu = 0, dom_len = 0, r = 0;
+  int64_t edge_shift = 0;  // the writer's decomposition (common.hpp decompose); absent in older saves: 0
   std::string dir;  // read_meta: the directory holding this step's files
 };
 

@@ -15,6 +15,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <stdexcept>
@@ -97,16 +98,33 @@ inline SlabLayout make_layout(int64_t nrows, int64_t ncols, int64_t halo, int64_
 // 1-D slab decomposition of `n` global rows over `nranks` ranks, remainder
 // spread over the first ranks (the reference silently drops n mod P,
 // fortran/hip/heat.F90:147 `nx = n/nblocks(1)`).
+//
+// edge_shift > 0 (nranks >= 3): the two edge slabs (rank 0 and nranks - 1,
+// the global frame rows on one side) each give `edge_shift` rows to the
+// middle ones, spread evenly (remainder to the first middle ranks). An edge
+// slab's cycle costs more per row than a middle one's — its frame-side band
+// runs on the general kernel in the interior's tail (profiles/r6/b/: 40-55 us
+// of a 0.62 ms one-cycle step at N = 8) — and a multi-rank step lasts as long
+// as its slowest rank; bench.py measures the excess and picks the shift
+// (SolverConfig::edge_shift). Clamped to a quarter of the uniform slab.
 struct SlabRange {
   int64_t row0;
   int64_t nrows;
 };
-inline SlabRange decompose(int64_t n, int nranks, int rank) {
+inline int64_t slab_rows(int64_t n, int nranks, int rank, int64_t edge_shift) {
+  const int64_t base = n / nranks, rem = n % nranks;
+  int64_t rows = base + (rank < rem ? 1 : 0);
+  const int64_t e = nranks >= 3 ? std::max<int64_t>(0, std::min<int64_t>(edge_shift, base / 4)) : 0;
+  if (e == 0) return rows;
+  if (rank == 0 || rank == nranks - 1) return rows - e;
+  const int64_t mid = nranks - 2, give = 2 * e;
+  return rows + give / mid + (rank - 1 < give % mid ? 1 : 0);
+}
+inline SlabRange decompose(int64_t n, int nranks, int rank, int64_t edge_shift = 0) {
   HEAT2D_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
-  int64_t base = n / nranks, rem = n % nranks;
-  int64_t nrows = base + (rank < rem ? 1 : 0);
-  int64_t row0 = rank * base + (rank < rem ? rank : rem);
-  return {row0, nrows};
+  int64_t row0 = 0;
+  for (int r = 0; r < rank; ++r) row0 += slab_rows(n, nranks, r, edge_shift);
+  return {row0, slab_rows(n, nranks, rank, edge_shift)};
 }
 
 }  // namespace heat2d

@@ -49,7 +49,7 @@ struct SolverConfig {
   int32_t arith;       // 0: reference arithmetic, every op rounded (bitwise == NumPy golden);
                        // 1: contracted fma(r, sum - 4c, c) (one op fewer per point, kernels.hpp);
                        // 2: r == 1/4 only: r * sum (zero centre weight: 3 adds per point, tb_impl.hpp)
-  int32_t pad0;
+  int32_t edge_shift;  // rows each edge slab gives to the middle ones (decompose(); bench.py measures it)
   // 1-rank rehearsal of a MIDDLE slab (slab_rows_global > 0): this solver owns
   // rows [slab_row0, slab_row0 + n_rows) of a grid of slab_rows_global rows,
   // so its bands are interior bands, as on rank 3 of 8 (0: the slab is the grid)

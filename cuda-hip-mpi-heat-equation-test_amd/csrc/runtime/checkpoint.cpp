@@ -277,6 +277,7 @@ Meta read_meta(const std::string& dir) {
   m.nu = std::atof(json_value(js, "nu").c_str());
   m.dom_len = std::atof(json_value(js, "dom_len").c_str());
   m.r = std::atof(json_value(js, "r").c_str());
+  if (js.find("\"edge_shift\"") != std::string::npos) m.edge_shift = std::atoll(json_value(js, "edge_shift").c_str());
   HEAT2D_REQUIRE(m.nranks >= 1 && m.step >= 0 && m.n_owned >= 1, dir + ": inconsistent meta.json");
   return m;
 }
@@ -291,7 +292,7 @@ void read_rows(const Meta& m, int64_t row0, int64_t nrows, int64_t ncols, int dt
     FILE* f = file.f;
     const NpyInfo info = npy_header(f, path);
     HEAT2D_REQUIRE(info.cols == ncols && info.dtype == dtype, path + ": shape / dtype differ from the run");
-    HEAT2D_REQUIRE(info.rows == decompose(m.n_owned, m.nranks, r).nrows,
+    HEAT2D_REQUIRE(info.rows == decompose(m.n_owned, m.nranks, r, m.edge_shift).nrows,
                    path + ": row count differs from the writer's decomposition");
     const int64_t a = std::max(row0, start), b = std::min(row0 + nrows, start + info.rows);
     if (a < b) {

@@ -66,7 +66,7 @@ SlabLayout solver_layout(const SolverConfig& cfg, int rank, int nranks) {
     HEAT2D_REQUIRE(cfg.slab_row0 >= 0 && cfg.slab_row0 + cfg.n_rows <= cfg.slab_rows_global, "slab outside the grid");
     return make_layout(cfg.n_rows, cfg.n_cols, halo, cfg.slab_row0, cfg.slab_rows_global);
   }
-  const SlabRange sr = decompose(cfg.n_rows, nranks, rank);
+  const SlabRange sr = decompose(cfg.n_rows, nranks, rank, cfg.edge_shift);
   return make_layout(sr.nrows, cfg.n_cols, halo, sr.row0, cfg.n_rows);
 }
 

@@ -108,6 +108,11 @@ class HeatSolver:
             level in the kernels instead of 5); bitwise equal to the CPU twin
             and to models.reference.ftcs(arith="jacobi"), and to "exact"
             wherever sum - 4c is exact (e.g. the reference IC, values in [1, 2]).
+        edge_shift: rows each edge slab (rank 0 and the last rank: the global
+            frame rows on one side) gives to the middle slabs of a >= 3-rank
+            decomposition (common.hpp decompose): an edge slab's cycle costs
+            more per row, and a step lasts as long as the slowest rank;
+            bench.py measures the excess and picks the shift. Same on every rank.
     """
 
     def __init__(self, problem: Problem, *, dtype: str = "fp64", backend: str = "auto", tb: int = 0,
@@ -115,8 +120,9 @@ class HeatSolver:
                  tile_rows: int = 0, halo: int = 0, transport: Optional[T.Transport] = None,
                  device: Optional[int] = None, init: bool = True, rows: Optional[int] = None,
                  comm_cus: int = 0, autotune: int = -1, engine: str = "tb", arith: str = "auto",
-                 slab_row0: Optional[int] = None):
+                 slab_row0: Optional[int] = None, edge_shift: int = 0):
         self.problem = problem
+        self.edge_shift = int(edge_shift)
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]
         self.np_dtype = NP_DTYPES[self.dtype]
@@ -148,6 +154,7 @@ class HeatSolver:
         cfg.halo = halo
         cfg.comm_cus = comm_cus
         cfg.autotune = autotune
+        cfg.edge_shift = self.edge_shift
         if engine not in ("tb", "jit"):
             raise ValueError("engine must be 'tb' (temporal-blocked kernels) or 'jit' (hipRTC, one step per launch)")
         cfg.engine = 1 if engine == "jit" else 0
@@ -404,7 +411,7 @@ class LoopbackGroup:
 
     def __init__(self, problem: Problem, nranks: int, *, dtype: str = "fp64", backend: str = "auto",
                  tb: int = 0, tile_rows: int = 0, device: Optional[int] = None, arith: str = "auto",
-                 overlap: bool = True, autotune: int = -1, comm_cus: int = 0):
+                 overlap: bool = True, autotune: int = -1, comm_cus: int = 0, edge_shift: int = 0):
         self.problem = problem
         self.backend = resolve_backend(backend)
         self.dtype = DTYPES[dtype]
@@ -424,6 +431,7 @@ class LoopbackGroup:
         cfg.device = -1 if device is None else int(device)
         cfg.tile_rows = tile_rows
         cfg.arith = N.ARITH[arith]
+        cfg.edge_shift = int(edge_shift)
         self.nranks = nranks
         h = C.c_void_p()
         N.call("heat2d_group_create", C.byref(cfg), nranks, C.byref(h))
@@ -454,6 +462,15 @@ class LoopbackGroup:
         h = C.c_void_p()
         N.call("heat2d_group_member", self._h, int(i), C.byref(h))
         return h
+
+    def slabs(self) -> list:
+        """(row0, nrows) of every member's slab."""
+        out = []
+        for i in range(self.nranks):
+            L = N.Layout()
+            N.call("heat2d_solver_layout", self._member(i), C.byref(L))
+            out.append((int(L.row0), int(L.nrows)))
+        return out
 
     def plan(self, i: int, k: int) -> dict:
         """Member i's split plan for depth k (as HeatSolver.plan)."""

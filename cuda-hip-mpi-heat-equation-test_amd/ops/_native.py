@@ -80,7 +80,7 @@ class Config(C.Structure):
         ("tile_rows", C.c_int64), ("halo", C.c_int64),
         ("comm_cus", C.c_int32), ("autotune", C.c_int32),
         ("engine", C.c_int32), ("arith", C.c_int32),
-        ("pad0", C.c_int32), ("slab_row0", C.c_int64), ("slab_rows_global", C.c_int64),
+        ("edge_shift", C.c_int32), ("slab_row0", C.c_int64), ("slab_rows_global", C.c_int64),
     ]
 
 
@@ -125,6 +125,7 @@ _SIGS = {
     "heat2d_make_layout": (C.c_int, [_I64, _I64, _I64, _I64, _I64, _LP]),
     "heat2d_parse_input": (C.c_int, [C.c_char_p, C.POINTER(C.c_double)]),
     "heat2d_decompose": (C.c_int, [_I64, C.c_int, C.c_int, C.POINTER(_I64), C.POINTER(_I64)]),
+    "heat2d_decompose_shifted": (C.c_int, [_I64, C.c_int, C.c_int, _I64, C.POINTER(_I64), C.POINTER(_I64)]),
     "heat2d_plan_tb": (C.c_int, [C.c_int, _LP, _I64, _I64, C.c_int, _I64, C.POINTER(TbPlan)]),
     "heat2d_plan_split": (C.c_int, [C.c_int, _LP, C.c_int, _I64, C.POINTER(SplitPlan)]),
     "heat2d_solver_prepare": (C.c_int, [_P, _I64]),
@@ -285,9 +286,14 @@ def make_layout(nrows: int, ncols: int, halo: int, row0: int = 0, nrows_global: 
     return out
 
 
-def decompose(n: int, nranks: int, rank: int) -> tuple[int, int]:
+def decompose(n: int, nranks: int, rank: int, edge_shift: int = 0) -> tuple[int, int]:
+    """(row0, nrows) of `rank`'s slab (common.hpp decompose; edge_shift: rows
+    each edge slab gives the middle ones)."""
     r0, nr = C.c_int64(), C.c_int64()
-    call("heat2d_decompose", n, nranks, rank, C.byref(r0), C.byref(nr))
+    if edge_shift:
+        call("heat2d_decompose_shifted", n, nranks, rank, int(edge_shift), C.byref(r0), C.byref(nr))
+    else:
+        call("heat2d_decompose", n, nranks, rank, C.byref(r0), C.byref(nr))
     return r0.value, nr.value
 
 

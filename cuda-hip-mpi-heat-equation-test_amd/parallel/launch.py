@@ -47,6 +47,9 @@ def build_parser():
     ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma", "jacobi", "fast"],
                     help="exact: reference rounding (bitwise == NumPy golden); fma: contracted update, one op fewer; "
                          "jacobi: r == 1/4 only, r * (S + E + N + W), 3 adds per point")
+    ap.add_argument("--edge-shift", type=int, default=0,
+                    help="rows each edge slab gives to the middle slabs (>= 3 ranks; bench.py measures a good value: "
+                         "its JSON config.decomposition.edge_shift); checkpoints record it")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--ntime", type=int, default=None)
     ap.add_argument("--print-every", type=int, default=0)
@@ -159,7 +162,8 @@ def run(argv=None) -> int:
     def make_solver(tr):
         return HeatSolver(prob, dtype=a.dtype, backend=backend, tb=a.tb, overlap=not a.no_overlap,
                           copy_swap=a.copy_swap, managed=a.managed or var.managed, graph=a.graph, transport=tr,
-                          device=local if backend == "hip" else None, engine=engine, arith=arith)
+                          device=local if backend == "hip" else None, engine=engine, arith=arith,
+                          edge_shift=a.edge_shift)
 
     if world == 1:
         kinds = ["self"]

@@ -15,6 +15,9 @@ So the first run on a node decides by measurement, collectively:
 * :func:`choose_transport` — try each candidate (build + time the real timed
   loop), MAX over ranks per candidate, keep the fastest; a candidate that
   fails anywhere is skipped on every rank (the fallback).
+* :func:`balance_edges` — the edge slabs' rows for >= 3 ranks: each rank
+  times its own slab, and rows move from the two edge slabs (whose frame-side
+  band costs extra) to the middle ones when that lowers the slowest slab.
 * :func:`verify_decomposition` — a small uneven, rough-data problem run with
   the chosen transport and rank layout through the same engine paths
   (autotuned split plans, measured schedule, graphs where the transport
@@ -187,6 +190,74 @@ def rank_report(gather: Callable[[dict], List[dict]], *, rank: int, device: Opti
     return {"ranks": ranks, "fabric_nranks": nr.pop() if len(nr) == 1 else None,
             "fabric_kind": ranks[0]["fabric"].get("kind"),
             "distinct_devices": len(devs), "timed_ms": {"min": min(ms), "max": max(ms)}}
+
+
+def edge_shift_estimate(slab_ms: Sequence[float], rows: Sequence[int], cap: int) -> int:
+    """Rows each edge slab should give to the middle slabs (decompose()'s
+    ``edge_shift``) so the first and last rank finish with the middle ones.
+
+    ``slab_ms[r]`` is rank r's own cycle time on ``rows[r]`` rows. A middle
+    slab costs a = (sum of middle ms) / (sum of middle rows) per row; an edge
+    slab's excess over that rate is E = ms - a * rows (its frame-side band:
+    profiles/r6/b/). Moving d rows from each edge slab to the P - 2 middle
+    ones saves a * d on the edges and costs a * 2d / (P - 2) in the middle,
+    so they meet at d = E / a * (P - 2) / P (rounded, clamped to [0, cap]).
+    The larger of the two edges' excesses sets d. 0 below 3 ranks."""
+    P = len(slab_ms)
+    if P < 3 or len(rows) != P:
+        return 0
+    mid = range(1, P - 1)
+    mid_rows = sum(rows[i] for i in mid)
+    a = sum(slab_ms[i] for i in mid) / mid_rows if mid_rows > 0 else 0.0
+    if not a > 0:
+        return 0
+    excess = max(slab_ms[0] - a * rows[0], slab_ms[-1] - a * rows[-1])
+    d = int(round(excess / a * (P - 2) / P))
+    return max(0, min(d, int(cap)))
+
+
+def balance_edges(measure: Callable[[int], float], gather: Callable[[float], List[float]],
+                  rows_of: Callable[[int], List[int]], cap: int) -> Tuple[int, dict]:
+    """The edge-balanced decomposition of a >= 3-rank run, by measurement.
+
+    ``measure(shift)`` times THIS rank's own slab of the decomposition with
+    that edge shift (bench.py: a 1-rank loop-exchange rehearsal of the slab,
+    the driver's timing) and returns ms; ``gather(v)`` returns every rank's v
+    in rank order; ``rows_of(shift)`` the rows of every rank. Round 1 times
+    the uniform slabs and estimates d (:func:`edge_shift_estimate`); round 2
+    times the shifted slabs, and d is kept only if its slowest slab beats the
+    uniform slowest slab (a node run reports the MAX over ranks). A failure on
+    any rank (measure raising, a non-finite time) keeps 0 on every rank.
+    Collective: every rank calls it with the same ``cap``. Returns (shift,
+    report), identical on every rank."""
+    import math
+
+    def timed(shift: int) -> List[float]:
+        try:
+            v = float(measure(shift))
+        except Exception:  # noqa: BLE001 - reported below through the gathered NaN
+            traceback.print_exc()
+            v = float("nan")
+        return [float(x) for x in gather(v)]
+
+    ms0 = timed(0)
+    report: Dict[str, object] = {"uniform_rows": rows_of(0), "uniform_ms": [round(x, 4) for x in ms0]}
+    if not all(math.isfinite(x) and x > 0 for x in ms0):
+        report["error"] = "a rank's uniform slab rehearsal failed"
+        return 0, report
+    d = edge_shift_estimate(ms0, rows_of(0), cap)
+    report["estimate"] = d
+    if d == 0:
+        return 0, report
+    ms1 = timed(d)
+    report["shifted_rows"] = rows_of(d)
+    report["shifted_ms"] = [round(x, 4) for x in ms1]
+    if not all(math.isfinite(x) and x > 0 for x in ms1):
+        report["error"] = "a rank's shifted slab rehearsal failed"
+        return 0, report
+    keep = max(ms1) < max(ms0)
+    report["kept"] = keep
+    return (d if keep else 0), report
 
 
 def _pow2(r: float) -> bool:

@@ -29,6 +29,8 @@ from typing import Optional
 
 import numpy as np
 
+from ..ops import _native as N
+
 FORMAT = "heat2d-checkpoint-v2"
 FORMATS = (FORMAT, "heat2d-checkpoint-v1")
 
@@ -111,6 +113,7 @@ def save(solver, directory: str, step: Optional[int] = None, extra: Optional[dic
             "n_input": p.n_input,
             "convention": p.convention,
             "sigma": p.sigma, "nu": p.nu, "dom_len": p.dom_len, "r": p.r,
+            "edge_shift": int(getattr(solver, "edge_shift", 0)),
         }
         meta.update(extra or {})
         _write_atomic(os.path.join(sd, "meta.json"), json.dumps(meta, indent=1))
@@ -153,8 +156,8 @@ def load(solver, directory: str) -> dict:
     parts = [np.load(os.path.join(meta["dir"], f"rank{r:05d}.npy"), mmap_mode="r", allow_pickle=False)
              for r in range(meta["nranks"])]
     for r, part in enumerate(parts):
-        base, rem = divmod(meta["n_owned"], meta["nranks"])  # the writer's decomposition (common.hpp)
-        rows = base + (1 if r < rem else 0)
+        # the writer's decomposition (common.hpp decompose)
+        rows = N.decompose(meta["n_owned"], meta["nranks"], r, int(meta.get("edge_shift", 0)))[1]
         if part.shape != (rows, solver.ncols) or part.dtype != solver.np_dtype:
             raise ValueError(f"rank file {r}: {part.shape} {part.dtype}, expected {(rows, solver.ncols)} {want}")
     starts = np.cumsum([0] + [p.shape[0] for p in parts])

@@ -175,6 +175,14 @@ def test_bench_auto_transport_falls_back_to_ipc_share_gpu():
         assert fc["vs_exact"]["ok"] is True and fc["vs_exact"]["mismatches"] == 0, fc
     assert four["fabric"] == {"kind": "ipc", "nranks": 4} and len(four["per_rank"]) == 4
     assert four["distinct_devices"] == 1  # --share-gpu: every rank on the one GPU
+    # the edge-balance rehearsal ran (one rank after another on the shared GPU)
+    # and the run used the shift it kept
+    dec = four["config"]["decomposition"]
+    bal = dec["balance"]
+    assert len(bal["uniform_ms"]) == 4 and min(bal["uniform_ms"]) > 0 and "error" not in bal, bal
+    assert bal["uniform_rows"] == [2048] * 4 and dec["rows"] == [r["rows"] for r in four["per_rank"]]
+    assert dec["rows"][0] == 2048 - dec["edge_shift"] and sum(dec["rows"]) == 8192
+    assert (dec["edge_shift"] > 0) == bool(bal.get("kept")), bal
     one = run_plain("--gpus", "1", *common)
     assert one["timed_field_check"]["ok"] is True and one["timed_field_check"]["mismatches"] == 0
     assert one["verified"] is True and one["config"]["transport_choice"] is None
@@ -285,6 +293,22 @@ def test_bench_timed_field_check_windows_cpu(nproc):
     fc = d["timed_field_check"]
     assert fc["mode"] == "windows" and fc["ok"] is True and fc["mismatches"] == 0, fc
     assert fc["rows_checked"] == nproc * 3 * 16 and fc["steps"] == 15
+
+
+@pytest.mark.parametrize("field_check", ["full", "windows"])
+def test_bench_edge_shift_cpu(field_check):
+    """--edge-shift D: the first and last slab give D rows (clamped to a quarter
+    of a slab) to the middle ones; the timed field is checked against a
+    reference on the same shifted layout (full) or by row windows, and the
+    JSON reports the rows."""
+    d = run_plain("--backend", "cpu", "--gpus", "4", "--grid", "100", "--steps", "12", "--warmup", "3", "--tb", "4",
+                  "--edge-shift", "5", "--field-check", field_check)
+    dec = d["config"]["decomposition"]
+    assert dec["edge_shift"] == 5 and dec["rows"] == [20, 30, 30, 20] and dec["balance"] is None
+    assert [r["rows"] for r in d["per_rank"]] == [20, 30, 30, 20]
+    fc = d["timed_field_check"]
+    assert fc["ok"] is True and fc["mode"] == field_check and fc["mismatches"] == 0, fc
+    assert d["verified"] is True
 
 
 @pytest.mark.parametrize("ic", ["hotspot", "uniform"])

@@ -85,6 +85,25 @@ def test_decompose_uneven(native, n, P):
     assert max(sizes) - min(sizes) <= 1
 
 
+@pytest.mark.parametrize("n,P,shift", [(32768, 8, 235), (32768, 4, 215), (100, 3, 5), (1003, 7, 40), (100, 4, 99),
+                                       (64, 2, 10), (17, 5, 3)])
+def test_decompose_edge_shift(native, n, P, shift):
+    """decompose(n, P, r, edge_shift): the two edge slabs give e = min(shift,
+    (n // P) // 4) rows each to the P - 2 middle ones (the first 2e mod (P - 2)
+    of them one more); contiguous, all n rows; below 3 ranks uniform."""
+    rows = [N.decompose(n, P, r, shift) for r in range(P)]
+    uni = [N.decompose(n, P, r)[1] for r in range(P)]
+    assert sum(nr for _, nr in rows) == n and rows[0][0] == 0
+    for (a0, an), (b0, _) in zip(rows, rows[1:]):
+        assert b0 == a0 + an
+    e = min(shift, (n // P) // 4) if P >= 3 else 0
+    sizes = [nr for _, nr in rows]
+    assert sizes[0] == uni[0] - e and sizes[-1] == uni[-1] - e
+    mid = [s - u for s, u in zip(sizes[1:-1], uni[1:-1])]
+    assert sum(mid) == 2 * e and (not mid or max(mid) - min(mid) <= 1)
+    assert N.decompose(n, P, 0, 0) == N.decompose(n, P, 0)
+
+
 def test_problem_conventions():
     inp = cfg.parse_input_text("100 0.25 0.05 2.0 10")
     g = heat2d.make_problem(inp, "ghost", "uniform")

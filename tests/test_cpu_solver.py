@@ -7,6 +7,7 @@ import pytest
 import heat2d
 from heat2d.models import reference as R
 from heat2d.models.heat2d import HeatSolver, LoopbackGroup
+from heat2d.ops import _native as N
 
 
 def prob(n, steps, conv="ghost", ic="uniform", dom=1.0, sigma=0.25):
@@ -40,6 +41,17 @@ def test_cpu_conventions(native, conv, ic):
 def test_cpu_loopback_bitwise(native, P, tb):
     p = prob(71, 25, "ghost", "uniform")
     g = LoopbackGroup(p, P, dtype="fp64", backend="cpu", tb=tb)
+    g.step(p.ntime)
+    assert np.array_equal(g.download(), R.owned(R.ftcs(p)))
+
+
+@pytest.mark.parametrize("P,shift", [(3, 4), (4, 17), (7, 2), (5, 3)])
+def test_cpu_loopback_edge_shift_bitwise(native, P, shift):
+    """Edge-balanced slabs (thinner first and last slab): the same field, bitwise."""
+    p = prob(71, 25, "ghost", "uniform")
+    g = LoopbackGroup(p, P, dtype="fp64", backend="cpu", tb=3, edge_shift=shift)
+    assert g.slabs() == [N.decompose(71, P, r, shift) for r in range(P)]
+    assert g.slabs()[0][1] < N.decompose(71, P, 0)[1]  # the shift applies
     g.step(p.ntime)
     assert np.array_equal(g.download(), R.owned(R.ftcs(p)))
 

@@ -90,6 +90,23 @@ def test_checkpoint_restart_changes_rank_count(native, tmp_path, p_write, p_read
     assert np.array_equal(T, R.owned(R.ftcs(prob)))
 
 
+def test_checkpoint_edge_shifted_writer(native, tmp_path):
+    """A checkpoint of edge-balanced slabs (--edge-shift) records the shift, and
+    a reader with another rank count (and no shift) cuts its rows right."""
+    (tmp_path / "input.dat").write_text("60 0.25 0.05 1.0 30 1\n")
+    py(tmp_path, "--backend", "cpu", "--ntime", "12", "--checkpoint", "ck", "--output", "none", "--edge-shift", "3",
+       nproc=3)
+    meta = ck_meta(tmp_path / "ck")
+    assert meta["edge_shift"] == 3 and meta["nranks"] == 3
+    name = (tmp_path / "ck" / "latest").read_text().strip()
+    rows = sorted(np.load(f, allow_pickle=False).shape[0] for f in (tmp_path / "ck" / name).glob("*.npy"))
+    assert rows == [17, 17, 26]
+    py(tmp_path, "--backend", "cpu", "--restart", "ck", nproc=2)
+    T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
+
+
 def test_plot_out(native, tmp_path):
     pytest.importorskip("matplotlib")
     (tmp_path / "input.dat").write_text("30 0.25 0.05 2.0 5\n")

@@ -20,6 +20,69 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ident = (lambda v: v)  # noqa: E731  (a 1-rank all-reduce)
 
 
+def test_edge_shift_estimate():
+    # N = 8 slabs of 32768^2 (profiles/r6/b/): edges 668 / 663 us, middles 624 us on 4096 rows
+    ms = [0.668] + [0.624] * 6 + [0.663]
+    rows = [4096] * 8
+    d = select.edge_shift_estimate(ms, rows, cap=1024)
+    a = 0.624 / 4096
+    assert d == round((0.668 - 0.624) / a * 6 / 8) and 200 < d < 300
+    # after the shift the edges and the middles meet (the linear model)
+    assert abs((0.668 - a * d) - (0.624 + a * 2 * d / 6)) < a
+    assert select.edge_shift_estimate(ms, rows, cap=100) == 100  # clamped
+    assert select.edge_shift_estimate([1.0, 1.0, 1.0], [10, 10, 10], cap=5) == 0  # balanced already
+    assert select.edge_shift_estimate([0.9, 1.0, 0.9], [10, 10, 10], cap=5) == 0  # edges faster: never negative
+    assert select.edge_shift_estimate([2.0, 1.0], [10, 10], cap=5) == 0  # 2 ranks: both are edges
+
+
+def _slab_model(P, n, a=1e-3, excess=0.0504):
+    """Rank r's ms on its slab of decompose(n, P, r, shift): a per row, edges + excess."""
+    from heat2d.ops import _native as N
+    state = {}
+
+    def rows_of(shift):
+        return [N.decompose(n, P, r, shift)[1] for r in range(P)]
+
+    def measure(shift):
+        state["shift"] = shift
+        return 0.0  # (every rank's value comes from gather below)
+
+    def gather(_v):
+        rows = rows_of(state["shift"])
+        return [a * rows[r] + (excess if r in (0, P - 1) else 0.0) for r in range(P)]
+    return measure, gather, rows_of
+
+
+def test_balance_edges_keeps_a_faster_shift():
+    measure, gather, rows_of = _slab_model(8, 32768)
+    d, rep = select.balance_edges(measure, gather, rows_of, cap=1024)
+    assert d == rep["estimate"] == 38 and rep["kept"] is True  # 50.4 rows of excess x 6 / 8
+    assert max(rep["shifted_ms"]) < max(rep["uniform_ms"]) and rep["shifted_rows"][0] == 4096 - d
+
+
+def test_balance_edges_rejects_a_slower_shift_and_failures():
+    measure, gather, rows_of = _slab_model(4, 1000)
+    d, rep = select.balance_edges(measure, gather, rows_of, cap=200)
+    assert d == rep["estimate"] > 0  # (the model's shift helps)
+
+    calls = []
+
+    def measure_n(shift):
+        calls.append(shift)
+        return measure(shift)
+
+    def gather_n(v):
+        ms = gather(v)
+        return ms if len(calls) == 1 else [x + 1.0 for x in ms]  # round 2 measured slower
+    d, rep = select.balance_edges(measure_n, gather_n, rows_of, cap=200)
+    assert d == 0 and rep["kept"] is False and rep["estimate"] > 0
+
+    def broken(shift):
+        raise RuntimeError("rehearsal failed")
+    d, rep = select.balance_edges(broken, lambda v: [v] * 4, rows_of, cap=200)
+    assert d == 0 and "failed" in rep["error"]
+
+
 def test_choose_fastest():
     chosen, rep = select.choose_transport(["rccl", "ipc"], lambda k: {"rccl": 2.0, "ipc": 1.5}[k], ident, ident)
     assert chosen == "ipc" and rep == {"rccl": {"ms": 2.0}, "ipc": {"ms": 1.5}}
