@@ -178,10 +178,14 @@ def main():
     ap.add_argument("--edge-shift", default="auto",
                     help="rows each edge slab (rank 0 and the last rank, the global frame rows on one side) gives "
                          "to the middle slabs of a >= 3-rank run: an integer, or auto (default): measured — every "
-                         "rank times its own slab alone (1-rank IPC loop-exchange rehearsal) uniform, then with "
+                         "rank times its own slab alone (1-rank loop-exchange rehearsal: RCCL's, or IPC's where the "
+                         "run falls back to it) uniform, then with "
                          "the estimated shift, and the shift is kept if the slowest slab gets faster "
                          "(parallel/select.balance_edges; one rank after another with --share-gpu). JSON "
                          "config.decomposition")
+    ap.add_argument("--balance-loop", default="auto", choices=["auto", "rccl", "ipc"],
+                    help="--edge-shift auto: the loop exchange of the slab rehearsals (auto: RCCL's when the run "
+                         "tries RCCL first and ranks own their GPUs, else IPC's)")
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"],
                     help="cpu: the same harness on the native CPU twin over gloo (CI rehearsal of the "
                          "multi-process path: tests/test_bench_contract.py); not a performance number")
@@ -402,15 +406,22 @@ def main():
         # Edge-balanced slabs (profiles/r6/b/: an edge
         # slab's frame-side band runs on the general kernel and ends ~30 us
         # after the interior at N = 8, so rank 0 and the last rank set the
-        # MAX). Each rank times its own slab alone — a 1-rank IPC loop
-        # exchange of its boundary bands (local device copies, no RCCL or IPC
-        # mapping), the bench's own warmup / prepare / timed step — before any
-        # transport or field of the real run exists.
+        # MAX). Each rank times its own slab alone — a 1-rank loop exchange
+        # of its boundary bands, the bench's own warmup / prepare / timed
+        # step — before any transport or field of the real run exists. The
+        # loop is the run's own kind of exchange: RCCL's channel kernels share
+        # the CUs with the bands (a 1-rank RCCL communicator per GPU), the IPC
+        # loop is local device copies; their edge excesses differ 2x
+        # (profiles/r6/h/: 41 vs ~80 us at N = 8).
+        first = select.candidate_transports(args.transport, world, hip)[0]
+        loop_kind = ("rccl-loop" if first == "rccl" and not args.share_gpu else "ipc-loop"
+                     ) if args.balance_loop == "auto" else args.balance_loop + "-loop"
+
         def own_slab_ms(shift):
             r0, nr = N.decompose(prob.n_owned, world, rank, shift)
 
             def run():
-                tr_l = make_transport("ipc-loop")
+                tr_l = make_transport(loop_kind)
                 try:
                     s_l = HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb,
                                      overlap=not args.no_overlap, graph=False, tile_rows=args.tile_rows,
@@ -420,8 +431,9 @@ def main():
                         s_l.step(args.warmup)
                         s_l.synchronize()
                         s_l.prepare(args.steps)
+                        s_l.step(args.steps)  # (clocks as in the timed loop)
                         best = float("inf")
-                        for _ in range(3):
+                        for _ in range(5):
                             sync()
                             t0 = time.perf_counter()
                             s_l.step(args.steps)
@@ -457,6 +469,7 @@ def main():
             edge_shift[0], balance_report = select.balance_edges(
                 own_slab_ms, gather_ms, lambda d: [N.decompose(prob.n_owned, world, r, d)[1] for r in range(world)],
                 cap=(prob.n_owned // world) // 4)
+        balance_report["loop"] = loop_kind
         if rank == 0:
             print(f"bench.py: edge balance: shift {edge_shift[0]} rows: {json.dumps(balance_report)}",
                   file=sys.stderr, flush=True)
