@@ -217,19 +217,22 @@ def edge_shift_estimate(slab_ms: Sequence[float], rows: Sequence[int], cap: int)
 
 
 def balance_edges(measure: Callable[[int], float], gather: Callable[[float], List[float]],
-                  rows_of: Callable[[int], List[int]], cap: int) -> Tuple[int, dict]:
+                  rows_of: Callable[[int], List[int]], cap: int, reps: int = 2) -> Tuple[int, dict]:
     """The edge-balanced decomposition of a >= 3-rank run, by measurement.
 
     ``measure(shift)`` times THIS rank's own slab of the decomposition with
     that edge shift (bench.py: a 1-rank loop-exchange rehearsal of the slab,
     the driver's timing) and returns ms; ``gather(v)`` returns every rank's v
-    in rank order; ``rows_of(shift)`` the rows of every rank. Round 1 times
-    the uniform slabs and estimates d (:func:`edge_shift_estimate`); round 2
-    times the shifted slabs, and d is kept only if its slowest slab beats the
-    uniform slowest slab (a node run reports the MAX over ranks). A failure on
-    any rank (measure raising, a non-finite time) keeps 0 on every rank.
-    Collective: every rank calls it with the same ``cap``. Returns (shift,
-    report), identical on every rank."""
+    in rank order; ``rows_of(shift)`` the rows of every rank. The uniform
+    slabs are timed first and d estimated from them
+    (:func:`edge_shift_estimate`); then shifted and uniform slabs alternate
+    until each layout has ``reps`` timings, and every rank keeps its fastest
+    per layout (one slow rehearsal on one rank would otherwise decide). d is
+    kept only if the shifted layout's slowest slab beats the uniform one's (a
+    node run reports the MAX over ranks). A failure on any rank (measure
+    raising, a non-finite time) keeps 0 on every rank. Collective: every rank
+    calls it with the same ``cap`` and ``reps``. Returns (shift, report),
+    identical on every rank."""
     import math
 
     def timed(shift: int) -> List[float]:
@@ -240,21 +243,35 @@ def balance_edges(measure: Callable[[int], float], gather: Callable[[float], Lis
             v = float("nan")
         return [float(x) for x in gather(v)]
 
+    def ok(ms: List[float]) -> bool:
+        return all(math.isfinite(x) and x > 0 for x in ms)
+
     ms0 = timed(0)
     report: Dict[str, object] = {"uniform_rows": rows_of(0), "uniform_ms": [round(x, 4) for x in ms0]}
-    if not all(math.isfinite(x) and x > 0 for x in ms0):
+    if not ok(ms0):
         report["error"] = "a rank's uniform slab rehearsal failed"
         return 0, report
     d = edge_shift_estimate(ms0, rows_of(0), cap)
     report["estimate"] = d
     if d == 0:
         return 0, report
-    ms1 = timed(d)
     report["shifted_rows"] = rows_of(d)
+    ms1 = None
+    for rep in range(max(1, reps)):
+        t1 = timed(d)
+        if not ok(t1):
+            report["error"] = "a rank's shifted slab rehearsal failed"
+            return 0, report
+        ms1 = t1 if ms1 is None else [min(a, b) for a, b in zip(ms1, t1)]
+        if rep + 1 < reps:
+            t0 = timed(0)
+            if not ok(t0):
+                report["error"] = "a rank's uniform slab rehearsal failed"
+                return 0, report
+            ms0 = [min(a, b) for a, b in zip(ms0, t0)]
+    report["uniform_ms"] = [round(x, 4) for x in ms0]
     report["shifted_ms"] = [round(x, 4) for x in ms1]
-    if not all(math.isfinite(x) and x > 0 for x in ms1):
-        report["error"] = "a rank's shifted slab rehearsal failed"
-        return 0, report
+    report["reps"] = max(1, reps)
     keep = max(ms1) < max(ms0)
     report["kept"] = keep
     return (d if keep else 0), report

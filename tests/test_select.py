@@ -60,6 +60,28 @@ def test_balance_edges_keeps_a_faster_shift():
     assert max(rep["shifted_ms"]) < max(rep["uniform_ms"]) and rep["shifted_rows"][0] == 4096 - d
 
 
+def test_balance_edges_repeats_outvote_one_slow_rehearsal():
+    """One slow shifted rehearsal on one rank: with one timing per layout it
+    decides (shift rejected); alternating two per layout, each rank's fastest
+    counts and the shift is kept."""
+    for reps, kept in ((1, False), (2, True)):
+        measure, gather, rows_of = _slab_model(8, 32768)
+        seen = []
+
+        def measure_n(shift):
+            seen.append(shift)
+            return measure(shift)
+
+        def gather_n(v):
+            ms = gather(v)
+            if len(seen) == 2:  # the first shifted round: rank 3 hiccups
+                ms[3] += 0.5
+            return ms
+        d, rep = select.balance_edges(measure_n, gather_n, rows_of, cap=1024, reps=reps)
+        assert rep["kept"] is kept and (d > 0) is kept and rep["reps"] == reps
+        assert seen == ([0, 38] if reps == 1 else [0, 38, 0, 38])
+
+
 def test_balance_edges_rejects_a_slower_shift_and_failures():
     measure, gather, rows_of = _slab_model(4, 1000)
     d, rep = select.balance_edges(measure, gather, rows_of, cap=200)
