@@ -113,3 +113,32 @@ def test_fatal_signal_prints_native_backtrace(how):
     assert "Fatal Python error: Aborted" in p.stderr  # the previous handler (faulthandler) ran after ours
     if how == "free":
         assert "free()" in p.stderr and "libc.so.6" in p.stderr
+
+
+ASAN_DIR = os.path.dirname(ASAN_CLI)
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ASAN_DIR, "python")), reason="make -C csrc asan-python missing")
+def test_bench_multi_rank_cpu_under_asan(tmp_path):
+    """the multi-process `bench.py --backend cpu --check`
+    path (3 gloo ranks started by bench.py itself, transport trials, timed run,
+    field check, verification, checkpoint-free teardown) with every rank under
+    host AddressSanitizer: an interpreter with ASan's runtime linked first,
+    PYTHONMALLOC=malloc (every Python allocation through ASan's allocator) and
+    the instrumented engine (HEAT2D_LIB). No report, a clean exit and the one
+    JSON line. (The GPU path cannot run under this runtime: its HSA
+    interceptors refuse the first device-pool allocation, profiles/r6/d/.)"""
+    import json
+    import sys  # noqa: F401
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=99", PYTHONMALLOC="malloc",
+               HEAT2D_LIB=os.path.join(ASAN_DIR, "libheat2d.so"), OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([os.path.join(ASAN_DIR, "python"), os.path.join(root, "bench.py"), "--backend", "cpu",
+                        "--gpus", "3", "--grid", "100", "--steps", "24", "--warmup", "4", "--tb", "4", "--check",
+                        "--edge-shift", "4"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert "AddressSanitizer" not in p.stderr, p.stderr[-4000:]
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 3 and d["verified"] is True and d["timed_field_check"]["ok"] is True
+    assert d["config"]["decomposition"]["rows"] == [30, 41, 29]  # 34 / 33 / 33, 4 rows from each edge
