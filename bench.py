@@ -181,8 +181,8 @@ def main():
                          "rank times its own slab alone (1-rank loop-exchange rehearsal: RCCL's, or IPC's where the "
                          "run falls back to it) uniform, then with "
                          "the estimated shift, and the shift is kept if the slowest slab gets faster "
-                         "(parallel/select.balance_edges; one rank after another with --share-gpu). JSON "
-                         "config.decomposition")
+                         "(parallel/select.balance_edges; one rank after another with --share-gpu); measure: "
+                         "the same on any backend (the CPU rehearsal of this path). JSON config.decomposition")
     ap.add_argument("--balance-loop", default="auto", choices=["auto", "rccl", "ipc"],
                     help="--edge-shift auto: the loop exchange of the slab rehearsals (auto: RCCL's when the run "
                          "tries RCCL first and ranks own their GPUs, else IPC's)")
@@ -400,9 +400,9 @@ def main():
 
     from heat2d.ops import _native as N
     balance_report = None
-    if args.edge_shift != "auto":
+    if args.edge_shift not in ("auto", "measure"):
         edge_shift[0] = int(args.edge_shift)
-    elif world >= 3 and hip and not args.rehearse_comm:
+    elif world >= 3 and (hip or args.edge_shift == "measure") and not args.rehearse_comm:
         # Edge-balanced slabs (profiles/r6/b/: an edge
         # slab's frame-side band runs on the general kernel and ends ~30 us
         # after the interior at N = 8, so rank 0 and the last rank set the
@@ -413,9 +413,11 @@ def main():
         # the CUs with the bands (a 1-rank RCCL communicator per GPU), the IPC
         # loop is local device copies; their edge excesses differ 2x
         # (profiles/r6/h/: 41 vs ~80 us at N = 8).
+        # (--backend cpu --edge-shift measure: the CI rehearsal of this path,
+        # each rank's slab on the CPU twin without an exchange)
         first = select.candidate_transports(args.transport, world, hip)[0]
-        loop_kind = ("rccl-loop" if first == "rccl" and not args.share_gpu else "ipc-loop"
-                     ) if args.balance_loop == "auto" else args.balance_loop + "-loop"
+        loop_kind = "self" if not hip else (("rccl-loop" if first == "rccl" and not args.share_gpu else "ipc-loop")
+                                            if args.balance_loop == "auto" else args.balance_loop + "-loop")
 
         def own_slab_ms(shift):
             r0, nr = N.decompose(prob.n_owned, world, rank, shift)
@@ -425,8 +427,8 @@ def main():
                 try:
                     s_l = HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb,
                                      overlap=not args.no_overlap, graph=False, tile_rows=args.tile_rows,
-                                     transport=tr_l, device=device, rows=nr, comm_cus=args.comm_cus, arith=arith,
-                                     slab_row0=r0)
+                                     transport=tr_l, device=device if hip else None, rows=nr,
+                                     comm_cus=args.comm_cus, arith=arith, slab_row0=r0)
                     try:
                         s_l.step(args.warmup)
                         s_l.synchronize()

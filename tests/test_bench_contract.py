@@ -311,6 +311,24 @@ def test_bench_edge_shift_cpu(field_check):
     assert d["verified"] is True
 
 
+def test_bench_edge_shift_measured_cpu():
+    """--edge-shift measure on gloo ranks: the path a >= 3-GPU node run takes by
+    default (every rank rehearses its own slab, the shifts are gathered and
+    decided alike on every rank, the real run is built on the kept shift),
+    with the CPU twin's timings; whatever it decides, the run is bitwise."""
+    d = run_bench(4, "--grid", "400", "--steps", "12", "--warmup", "3", "--tb", "4", "--edge-shift", "measure",
+                  port=29574)
+    dec = d["config"]["decomposition"]
+    bal = dec["balance"]
+    assert bal["loop"] == "self" and len(bal["uniform_ms"]) == 4 and min(bal["uniform_ms"]) > 0, bal
+    assert "error" not in bal and bal["uniform_rows"] == [100] * 4
+    assert dec["rows"] == [r["rows"] for r in d["per_rank"]] and sum(dec["rows"]) == 400
+    assert dec["rows"][0] == 100 - dec["edge_shift"] and dec["edge_shift"] <= 25
+    assert (dec["edge_shift"] > 0) == bool(bal.get("kept")), bal
+    fc = d["timed_field_check"]
+    assert fc["ok"] is True and fc["mismatches"] == 0 and d["verified"] is True, fc
+
+
 @pytest.mark.parametrize("ic", ["hotspot", "uniform"])
 def test_bench_hotspot_jacobi_check_cpu(ic):
     """--ic hotspot (the zero + hot-spot data BASELINE.json names) with the
