@@ -78,6 +78,7 @@ struct Args {
   std::string transport = "auto";
   bool share_gpu = false;          // --share-gpu: every rank on device 0 (peer transport; tests / rehearsals)
   int autotune = -1;               // --autotune auto|on|off (SolverConfig::autotune)
+  int edge_shift = 0;              // --edge-shift N: rows each edge slab gives the middle ones (>= 3 ranks)
 };
 
 void usage() {
@@ -88,7 +89,7 @@ void usage() {
       "              [--n N|max] [--ntime N] [--quiet] [--timers] [--engine tb|jit] [--arith auto|exact|fma|jacobi|fast]\n"
       "              [--time-transfers]\n"
       "              [--checkpoint DIR [--checkpoint-every N]] [--restart DIR]\n"
-      "              [--transport auto|rccl|peer] [--share-gpu] [--autotune auto|on|off]\n");
+      "              [--transport auto|rccl|peer] [--share-gpu] [--autotune auto|on|off] [--edge-shift N]\n");
 }
 
 Args parse_args(int argc, char** argv) {
@@ -133,6 +134,13 @@ Args parse_args(int argc, char** argv) {
     else if (s == "--restart") a.restart = need("--restart");
     else if (s == "--transport") a.transport = need("--transport");
     else if (s == "--share-gpu") a.share_gpu = true;
+    else if (s == "--edge-shift") {
+      a.edge_shift = std::atoi(need("--edge-shift").c_str());
+      if (a.edge_shift < 0) {
+        std::fprintf(stderr, "--edge-shift must be >= 0\n");
+        std::exit(2);
+      }
+    }
     else if (s == "--autotune") {
       const std::string v = need("--autotune");
       if (v != "auto" && v != "on" && v != "off") {
@@ -195,6 +203,7 @@ void save_checkpoint(Shared& sh, Solver& s, Transport& tr, int rank, int64_t ste
     m.nu = sh.in.nu;
     m.dom_len = sh.in.dom_len;
     m.r = sh.prob.r;
+    m.edge_shift = a.edge_shift;
     ckpt::write_meta(a.checkpoint, name, m);
   }
   tr.barrier();
@@ -266,6 +275,7 @@ void run_rank(Shared& sh, int rank) {
     // split schedule: the fastest launch plan per depth and a measured cycle schedule
     // (auto: slabs of >= 2^24 points — decided from the thinnest slab, the same on every rank)
     cfg.autotune = a.autotune;
+    cfg.edge_shift = a.edge_shift;
     if (a.engine != "tb" && a.engine != "jit") fail(__FILE__, __LINE__, "--engine must be tb or jit");
     cfg.engine = a.engine == "jit" ? 1 : 0;  // jit: hipRTC kernel rendered for this slab (python/cuda/cuda.py)
     if (a.arith != "exact" && a.arith != "fma" && a.arith != "jacobi" && a.arith != "fast" && a.arith != "auto")

@@ -223,9 +223,10 @@ void write_meta(const std::string& dir, const std::string& name, const Meta& m) 
   std::snprintf(buf, sizeof(buf),
                 "{\n \"format\": \"%s\",\n \"step\": %lld,\n \"nranks\": %d,\n \"dtype\": \"%s\",\n"
                 " \"n_owned\": %lld,\n \"n_input\": %lld,\n \"convention\": \"%s\",\n \"sigma\": %.17g,\n"
-                " \"nu\": %.17g,\n \"dom_len\": %.17g,\n \"r\": %.17g,\n \"writer\": \"heat2d-cli\"\n}\n",
+                " \"nu\": %.17g,\n \"dom_len\": %.17g,\n \"r\": %.17g,\n \"edge_shift\": %lld,\n"
+                " \"writer\": \"heat2d-cli\"\n}\n",
                 kFormat, (long long)m.step, m.nranks, m.dtype == 0 ? "fp32" : "fp64", (long long)m.n_owned,
-                (long long)m.n_input, m.convention.c_str(), m.sigma, m.nu, m.dom_len, m.r);
+                (long long)m.n_input, m.convention.c_str(), m.sigma, m.nu, m.dom_len, m.r, (long long)m.edge_shift);
   write_atomic(join(join(dir, name), "meta.json"), buf);  // + fsync of the step directory (rank files' entries)
   write_atomic(join(dir, "latest"), name + "\n");  // the commit point
   // prune: keep the two newest complete saves, ordered by (step, generation)

@@ -156,6 +156,35 @@ def test_checkpoint_native_cli_interop(native, tmp_path, writer, reader):
     assert np.array_equal(T, R.owned(R.ftcs(prob)))
 
 
+@pytest.mark.parametrize("writer", ["cli", "py"])
+def test_checkpoint_edge_shift_cli_interop(native, tmp_path, writer):
+    """Edge-shifted writers (CLI host-thread ranks or Python gloo ranks, 3 ranks,
+    --edge-shift 4): meta.json records the shift; the other driver resumes
+    with another rank count and a different shift, bitwise."""
+    (tmp_path / "input.dat").write_text("60 0.25 0.05 1.0 30 1\n")
+    cli = [N.CLI_PATH, "--cpu", "--quiet"]
+    if writer == "cli":
+        subprocess.run([*cli, "--gpus", "3", "--edge-shift", "4", "--ntime", "12", "--checkpoint", "ck", "--output",
+                        "none"], cwd=tmp_path, check=True, capture_output=True)
+    else:
+        py(tmp_path, "--backend", "cpu", "--ntime", "12", "--checkpoint", "ck", "--output", "none", "--edge-shift",
+           "4", nproc=3)
+    meta = ck_meta(tmp_path / "ck")
+    assert meta["step"] == 12 and meta["edge_shift"] == 4 and meta["nranks"] == 3
+    name = (tmp_path / "ck" / "latest").read_text().strip()
+    assert sorted(np.load(f, allow_pickle=False).shape[0] for f in (tmp_path / "ck" / name).glob("*.npy")) == \
+        [16, 16, 28]
+    if writer == "cli":
+        py(tmp_path, "--backend", "cpu", "--restart", "ck", "--edge-shift", "2", nproc=4)
+        T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    else:
+        subprocess.run([*cli, "--gpus", "4", "--edge-shift", "3", "--restart", "ck", "--output", "npy"],
+                       cwd=tmp_path, check=True, capture_output=True)
+        T = np.concatenate([np.load(tmp_path / f"soln{r:05d}.npy") for r in range(4)], axis=0)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
+
+
 def test_checkpoint_native_rejects_mismatch(native, tmp_path):
     (tmp_path / "input.dat").write_text("40 0.25 0.05 1.0 10 0\n")
     subprocess.run([N.CLI_PATH, "--cpu", "--quiet", "--checkpoint", "ck"], cwd=tmp_path, check=True,
