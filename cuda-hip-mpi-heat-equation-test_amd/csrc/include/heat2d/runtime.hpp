@@ -108,6 +108,9 @@ class Transport {
   // The solver's two field buffers (allocation bases, layout L): transports
   // that map their peers' fields once (IPC) do it here. Collective.
   virtual void attach(void* /*buf0*/, void* /*buf1*/, const SlabLayout& /*L*/, DType /*dt*/) {}
+  // Bytes to allocate for a field buffer of `bytes` (the solver's two
+  // fields): a transport that exports them to its peers may need more (IPC).
+  virtual size_t field_alloc_bytes(size_t bytes) const { return bytes; }
   // What the fabric itself reports about this rank — the proof that a
   // multi-GPU run really put N ranks on N devices (the reference prints
   // "MPI rank r using GPU d", fortran/hip/heat.F90:125). kind: 0 host / self,

@@ -101,6 +101,17 @@ class IpcTransport final : public Transport {
   int rank() const override { return rank_; }
   int size() const override { return size_; }
   std::string name() const override { return loop_ ? "ipc-loop" : "ipc"; }
+  // A peer's import (hipIpcOpenMemHandle, dmabuf IPC) of a field buffer of
+  // 2^31 <= bytes < 2^32 never returns on this runtime, whatever the rank
+  // count: 2.17 / 2.20 / 2.62 / 2.73 / 2.9 GB fields stalled at N = 2, 3 and 4
+  // rank processes, while 1.1-1.94 GB and 4.31 GB (2^32 + 16 MiB) fields
+  // attach in under 1 ms (profiles/r6/ipc/, r6/c/). Such buffers are
+  // allocated as 2^32 + 16 MiB instead: at most 2 GB more per field, on a
+  // 288 GB device.
+  size_t field_alloc_bytes(size_t bytes) const override {
+    constexpr size_t lo = size_t(1) << 31, safe = (size_t(1) << 32) + (size_t(16) << 20);
+    return (!loop_ && size_ > 1 && bytes >= lo && bytes < safe) ? safe : bytes;
+  }
   bool capturable() const override { return true; }
   bool exchanges() const override { return size_ > 1 || loop_; }
   // (also a device-side timeout or another rank's abort, seen in the shared

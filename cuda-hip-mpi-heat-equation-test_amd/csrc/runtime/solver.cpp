@@ -159,9 +159,10 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
   if (hip_) {
     if (cfg_.device >= 0) H2D_HIP(hipSetDevice(cfg_.device));
     else H2D_HIP(hipGetDevice(&cfg_.device));
+    const size_t alloc = tr_->field_alloc_bytes(bytes);  // (IPC: see IpcTransport::field_alloc_bytes)
     for (int b = 0; b < 2; ++b) {
-      if (cfg_.managed) H2D_HIP(hipMallocManaged(&buf_[b], bytes));
-      else H2D_HIP(hipMalloc(&buf_[b], bytes));
+      if (cfg_.managed) H2D_HIP(hipMallocManaged(&buf_[b], alloc));
+      else H2D_HIP(hipMalloc(&buf_[b], alloc));
     }
     // (solver_footprint() counts exactly these allocations: keep them in step)
     H2D_HIP(hipMalloc(reinterpret_cast<void**>(&d_work_), (size_t)(kern::stats_work_elems() + 8) * sizeof(double)));

@@ -227,6 +227,25 @@ def test_bench_ipc_attach_is_bounded():
 
 
 @pytest.mark.gpu
+def test_bench_ipc_field_in_the_stalling_size_window():
+    """Two rank processes on one GPU at 23170^2 fp64: each field buffer is
+    2.17 GB, inside [2^31, 2^32) bytes, where the runtime's IPC import never
+    returned (profiles/r6/ipc/: every such size stalled, at 2, 3 and 4 ranks).
+    The IPC transport allocates such fields as 2^32 + 16 MiB, and the attach,
+    the timed run and its field check go through (bitwise)."""
+    env = dict(os.environ, HEAT2D_IPC_ATTACH_TIMEOUT="20", HEAT2D_IPC_ATTACH_LOG="1", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--transport",
+                        "ipc", "--grid", "23170", "--steps", "4", "--warmup", "1", "--verify", "off"],
+                       capture_output=True, text=True, timeout=280, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["config"]["transport"] == "ipc" and "NOT opened" not in p.stderr
+    fc = d["timed_field_check"]
+    assert fc["ok"] is True and fc["mismatches"] == 0, fc
+
+
+@pytest.mark.gpu
 def test_bench_plan_cache_second_run(tmp_path):
     """Persistent plan cache: the second identical bench run takes its split
     plans and measured schedule from the cache (each re-validated by one short
