@@ -467,11 +467,13 @@ def main():
             dist.all_reduce(t)
             return t.tolist()
 
+        tb0 = time.perf_counter()
         with select.deadline(init_timeout, "edge-balance rehearsal of the slabs", rank):
             edge_shift[0], balance_report = select.balance_edges(
                 own_slab_ms, gather_ms, lambda d: [N.decompose(prob.n_owned, world, r, d)[1] for r in range(world)],
                 cap=(prob.n_owned // world) // 4)
         balance_report["loop"] = loop_kind
+        balance_report["seconds"] = round(time.perf_counter() - tb0, 2)
         if rank == 0:
             print(f"bench.py: edge balance: shift {edge_shift[0]} rows: {json.dumps(balance_report)}",
                   file=sys.stderr, flush=True)
