@@ -422,31 +422,20 @@ def main():
         def own_slab_ms(shift):
             r0, nr = N.decompose(prob.n_owned, world, rank, shift)
 
-            def run():
+            def make():
                 tr_l = make_transport(loop_kind)
                 try:
                     s_l = HeatSolver(prob, dtype=args.dtype, backend=args.backend, tb=args.tb,
                                      overlap=not args.no_overlap, graph=False, tile_rows=args.tile_rows,
                                      transport=tr_l, device=device if hip else None, rows=nr,
                                      comm_cus=args.comm_cus, arith=arith, slab_row0=r0)
-                    try:
-                        s_l.step(args.warmup)
-                        s_l.synchronize()
-                        s_l.prepare(args.steps)
-                        s_l.step(args.steps)  # (clocks as in the timed loop)
-                        best = float("inf")
-                        for _ in range(5):
-                            sync()
-                            t0 = time.perf_counter()
-                            s_l.step(args.steps)
-                            s_l.synchronize()
-                            sync()
-                            best = min(best, time.perf_counter() - t0)
-                        return best * 1e3
-                    finally:
-                        s_l.close()
-                finally:
+                except Exception:
                     tr_l.close()
+                    raise
+                return s_l, lambda: (s_l.close(), tr_l.close())
+
+            def run():
+                return select.time_own_slab(make, args.steps, args.warmup, sync=sync)
             if not args.share_gpu:
                 return run()
             # ranks sharing one GPU take turns (their rehearsals would contend)

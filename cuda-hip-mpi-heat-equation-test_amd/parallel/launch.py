@@ -47,9 +47,11 @@ def build_parser():
     ap.add_argument("--arith", default="auto", choices=["auto", "exact", "fma", "jacobi", "fast"],
                     help="exact: reference rounding (bitwise == NumPy golden); fma: contracted update, one op fewer; "
                          "jacobi: r == 1/4 only, r * (S + E + N + W), 3 adds per point")
-    ap.add_argument("--edge-shift", type=int, default=0,
-                    help="rows each edge slab gives to the middle slabs (>= 3 ranks; bench.py measures a good value: "
-                         "its JSON config.decomposition.edge_shift); checkpoints record it")
+    ap.add_argument("--edge-shift", default="0",
+                    help="rows each edge slab gives to the middle slabs (>= 3 ranks; checkpoints record it): a "
+                         "number, auto (GPU ranks: measured before the run — every rank times its own slab on a "
+                         "1-rank loop exchange, uniform and shifted, parallel/select.balance_edges, as bench.py "
+                         "does) or measure (the same on any backend)")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--ntime", type=int, default=None)
     ap.add_argument("--print-every", type=int, default=0)
@@ -116,6 +118,66 @@ def _make_solver(kinds, make_transport, make_solver, world):
     raise SystemExit(f"heat2d: no halo transport works on every rank: {errors}")
 
 
+def _measure_edge_shift(prob, a, rank, world, local, backend, first_kind, engine, arith, steps, verbose) -> int:
+    """--edge-shift auto / measure: every rank times its own slab alone — a
+    1-rank loop exchange of the run's kind (RCCL's, IPC's where the run would
+    fall back or ranks share a GPU, none on CPU ranks), one rank after another
+    with --share-gpu — and parallel/select.balance_edges keeps the shift only
+    if the slowest slab gets faster (bench.py runs the same measurement)."""
+    import torch
+    import torch.distributed as dist
+    from heat2d.models.heat2d import HeatSolver
+    from heat2d.ops import _native as N
+    from heat2d.parallel import select
+    from heat2d.parallel import transport as T
+    hip = backend == "hip"
+    loop = (T.RcclLoopTransport if first_kind == "rccl" and not a.share_gpu else T.IpcLoopTransport) if hip \
+        else T.SelfTransport
+    sync = torch.cuda.synchronize if hip else (lambda: None)
+
+    def measure(shift):
+        r0, nr = N.decompose(prob.n_owned, world, rank, shift)
+
+        def make():
+            tr = loop(local) if hip else loop()
+            try:
+                s = HeatSolver(prob, dtype=a.dtype, backend=backend, tb=a.tb, overlap=not a.no_overlap,
+                               transport=tr, device=local if hip else None, rows=nr, slab_row0=r0, engine=engine,
+                               arith=arith)
+            except Exception:
+                tr.close()
+                raise
+            return s, lambda: (s.close(), tr.close())
+
+        if not a.share_gpu:
+            return select.time_own_slab(make, steps, 0, sync=sync)
+        v = float("nan")
+        for r in range(world):  # ranks sharing one GPU take turns
+            if r == rank:
+                try:
+                    v = select.time_own_slab(make, steps, 0, sync=sync)
+                except Exception:  # noqa: BLE001 - a NaN makes every rank keep 0
+                    import traceback
+                    traceback.print_exc()
+            dist.barrier()
+        return v
+
+    def gather(v):
+        t = torch.zeros(world, dtype=torch.float64)
+        t[rank] = v
+        dist.all_reduce(t)
+        return t.tolist()
+
+    shift, rep = select.balance_edges(measure, gather,
+                                      lambda d: [N.decompose(prob.n_owned, world, r, d)[1] for r in range(world)],
+                                      cap=(prob.n_owned // world) // 4)
+    if verbose:
+        print(f" edge balance: shift {shift} rows (estimate {rep.get('estimate')}, slowest slab "
+              f"{max(rep['uniform_ms']):.4f} ms uniform"
+              + (f", {max(rep['shifted_ms']):.4f} ms shifted" if rep.get("shifted_ms") else "") + ")", flush=True)
+    return shift
+
+
 def run(argv=None) -> int:
     a = build_parser().parse_args(argv)
     import heat2d
@@ -159,18 +221,26 @@ def run(argv=None) -> int:
         return {"torch-dist": T.TorchDistTransport, "self": T.SelfTransport,
                 "rccl": lambda: T.RcclTransport(rank, world, local), "peer": lambda: T.IpcTransport(local)}[kind]()
 
-    def make_solver(tr):
-        return HeatSolver(prob, dtype=a.dtype, backend=backend, tb=a.tb, overlap=not a.no_overlap,
-                          copy_swap=a.copy_swap, managed=a.managed or var.managed, graph=a.graph, transport=tr,
-                          device=local if backend == "hip" else None, engine=engine, arith=arith,
-                          edge_shift=a.edge_shift)
-
     if world == 1:
         kinds = ["self"]
     elif backend != "hip":
         kinds = ["torch-dist"]
     else:
         kinds = {"auto": ["rccl", "peer"], "rccl": ["rccl"], "peer": ["peer"]}[a.transport]
+
+    edge_shift = 0
+    if a.edge_shift not in ("auto", "measure"):
+        edge_shift = int(a.edge_shift)
+    elif world >= 3 and (backend == "hip" or a.edge_shift == "measure") and engine == "tb":
+        edge_shift = _measure_edge_shift(prob, a, rank, world, local, backend, kinds[0], engine, arith,
+                                         min(nsteps, 48), root and not a.quiet)
+
+    def make_solver(tr):
+        return HeatSolver(prob, dtype=a.dtype, backend=backend, tb=a.tb, overlap=not a.no_overlap,
+                          copy_swap=a.copy_swap, managed=a.managed or var.managed, graph=a.graph, transport=tr,
+                          device=local if backend == "hip" else None, engine=engine, arith=arith,
+                          edge_shift=edge_shift)
+
     tr, s, kind, fallback = _make_solver(kinds, make_transport, make_solver, world)
     if fallback and root and not a.quiet:
         print(f"heat2d: halo transport {kind} ({'; '.join(f'{k} failed: {v}' for k, v in fallback.items())})",

@@ -216,6 +216,34 @@ def edge_shift_estimate(slab_ms: Sequence[float], rows: Sequence[int], cap: int)
     return max(0, min(d, int(cap)))
 
 
+def time_own_slab(make: Callable[[], Tuple[object, Callable[[], None]]], steps: int, warmup: int,
+                  sync: Callable[[], None] = lambda: None, reps: int = 5) -> float:
+    """ms of one ``step(steps)`` of a rehearsal solver: ``make()`` returns
+    (solver, cleanup) — this rank's slab on a 1-rank loop exchange (or none) —
+    then ``warmup`` steps, ``prepare(steps)``, one untimed ``step(steps)``
+    (clocks as in a timed loop) and the fastest of ``reps`` timed ones. The
+    per-rank measurement :func:`balance_edges` gathers."""
+    import time
+    s, cleanup = make()
+    try:
+        if warmup > 0:
+            s.step(warmup)
+        s.synchronize()
+        s.prepare(steps)
+        s.step(steps)
+        best = float("inf")
+        for _ in range(max(1, reps)):
+            sync()
+            t0 = time.perf_counter()
+            s.step(steps)
+            s.synchronize()
+            sync()
+            best = min(best, time.perf_counter() - t0)
+        return best * 1e3
+    finally:
+        cleanup()
+
+
 def balance_edges(measure: Callable[[int], float], gather: Callable[[float], List[float]],
                   rows_of: Callable[[int], List[int]], cap: int, reps: int = 2) -> Tuple[int, dict]:
     """The edge-balanced decomposition of a >= 3-rank run, by measurement.

@@ -156,6 +156,18 @@ def test_checkpoint_native_cli_interop(native, tmp_path, writer, reader):
     assert np.array_equal(T, R.owned(R.ftcs(prob)))
 
 
+def test_torchrun_edge_shift_measured(native, tmp_path):
+    """`python -m heat2d --edge-shift measure` on 4 gloo ranks: every rank
+    rehearses its own slab (CPU twin), the shift is decided alike on every
+    rank, and whatever it is the merged field is bitwise the golden one."""
+    (tmp_path / "input.dat").write_text("200 0.25 0.05 1.0 30 1\n")
+    out = py(tmp_path, "--backend", "cpu", "--tb", "4", "--edge-shift", "measure", nproc=4)
+    assert " edge balance: shift " in out, out[-2000:]
+    T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
+
+
 @pytest.mark.parametrize("writer", ["cli", "py"])
 def test_checkpoint_edge_shift_cli_interop(native, tmp_path, writer):
     """Edge-shifted writers (CLI host-thread ranks or Python gloo ranks, 3 ranks,
@@ -380,3 +392,17 @@ def test_checkpoint_legacy_generation_names(native, tmp_path, writer):
     s = HeatSolver(prob, dtype="fp64", backend="cpu", tb=3)
     checkpoint.load(s, str(ck))
     assert np.array_equal(s.download(), R.owned(R.ftcs(prob)))
+
+
+@pytest.mark.gpu
+def test_torchrun_edge_shift_auto_share_gpu(native, gpu, tmp_path):
+    """`python -m heat2d --edge-shift auto --share-gpu` under torchrun: 3 GPU
+    rank processes take turns timing their own slabs (1-rank IPC loop), agree
+    on the shift, run over the peer (hipIpc) transport — bitwise the golden."""
+    (tmp_path / "input.dat").write_text("1200 0.25 0.05 1.0 40 1\n")
+    out = py(tmp_path, "--backend", "hip", "--share-gpu", "--arith", "exact", "--edge-shift", "auto", nproc=3,
+             timeout=600)
+    assert " edge balance: shift " in out, out[-2000:]
+    T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
