@@ -189,13 +189,14 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"],
                     help="cpu: the same harness on the native CPU twin over gloo (CI rehearsal of the "
                          "multi-process path: tests/test_bench_contract.py); not a performance number")
-    ap.add_argument("--transport", default="auto", choices=["auto", "best", "rccl", "ipc", "peer"],
+    ap.add_argument("--transport", default="auto", choices=["auto", "best", "rccl", "ipc", "peer", "host"],
                     help="halo exchange between rank processes: rccl (RCCL send/recv over xGMI), ipc (alias peer: "
                          "no RCCL, the neighbours' fields mapped through hipIpc handles, halos pulled by device "
                          "copies ordered by stream-side counters; capturable into hipGraphs), auto (default): RCCL, "
                          "and IPC only where RCCL cannot be built on every rank (a transport that fails to "
                          "initialise on any rank is skipped on every rank), or best: build both, time the real "
-                         "timed loop with each (MAX over ranks) and keep the faster")
+                         "timed loop with each (MAX over ranks) and keep the faster; host: halos staged through "
+                         "pinned host memory over torch.distributed (gloo), auto's last resort")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank on GPU 0: the exact multi-process path on a 1-GPU box (RCCL refuses two ranks "
                          "on one GPU, so auto falls back to ipc); a correctness / overhead rehearsal, not a node "

@@ -62,11 +62,12 @@ def build_parser():
     ap.add_argument("--checkpoint-every", type=int, default=0)
     ap.add_argument("--restart", default=None)
     ap.add_argument("--quiet", action="store_true")
-    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "peer"],
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "peer", "host"],
                     help="halo exchange between GPU rank processes: rccl (RCCL send/recv), peer (hipIpc "
                          "mappings of the neighbours' fields, stream-ordered by host-shared counters), or auto "
                          "(default): rccl if its communicator and solver build on every rank, else peer on every "
-                         "rank; host collectives over gloo")
+                         "rank, else host; host: halos staged through pinned host memory over torch.distributed "
+                         "(gloo); host collectives over gloo")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank on GPU 0 (--transport peer or auto): the multi-process path on one GPU")
     return ap
@@ -226,7 +227,10 @@ def run(argv=None) -> int:
     elif backend != "hip":
         kinds = ["torch-dist"]
     else:
-        kinds = {"auto": ["rccl", "peer"], "rccl": ["rccl"], "peer": ["peer"]}[a.transport]
+        # auto ends with the host-staged exchange (pinned staging + gloo): the
+        # run still completes where neither RCCL nor the IPC mappings attach
+        kinds = {"auto": ["rccl", "peer", "torch-dist"], "rccl": ["rccl"], "peer": ["peer"],
+                 "host": ["torch-dist"]}[a.transport]
 
     edge_shift = 0
     if a.edge_shift not in ("auto", "measure"):

@@ -103,15 +103,22 @@ def candidate_transports(requested: str, world: int, hip: bool) -> List[str]:
     transports for "auto" / "best" (RCCL first: the reference's own model of
     an MPI-style fabric; IPC second — with "auto" only as the fallback where
     RCCL cannot be built, so a node run whose RCCL works never builds the IPC
-    mappings; "best" times both). Single-rank runs have nothing to choose; CPU
-    ranks have one transport (torch.distributed host callbacks), run through
-    the same trial."""
+    mappings; "best" times both). "auto" ends with the host-staged
+    torch.distributed exchange (pinned staging + gloo send/recv, the
+    reference's own MPI path): slow, but a node where neither RCCL nor the IPC
+    mappings attach still runs and reports. Single-rank runs have nothing to
+    choose; CPU ranks have one transport (torch.distributed host callbacks),
+    run through the same trial."""
     if world <= 1:
         return []
     if not hip:
         return ["torch-dist"]
-    if requested in ("auto", "best"):
+    if requested == "auto":
+        return ["rccl", "ipc", "torch-dist"]
+    if requested == "best":
         return ["rccl", "ipc"]
+    if requested == "host":
+        return ["torch-dist"]
     return ["ipc" if requested in ("ipc", "peer") else "rccl"]
 
 

@@ -209,21 +209,34 @@ def test_bench_rehearsal_then_verification(transport):
 
 
 @pytest.mark.gpu
-def test_bench_ipc_attach_is_bounded():
+@pytest.mark.parametrize("transport", ["ipc", "auto"])
+def test_bench_ipc_attach_is_bounded(transport):
     """An IPC attach that never returns (HEAT2D_IPC_ATTACH_STALL: rank 1's
     hipIpcOpenMemHandle hangs, as 4 ranks sharing a GPU at 32768^2 once did,
-    profiles/r5/x/) fails the attach after HEAT2D_IPC_ATTACH_TIMEOUT seconds on
-    EVERY rank: with RCCL refused too (ranks sharing a GPU) the run ends
-    promptly with "no transport works", not a hang."""
+    profiles/r6/ipc/) fails the attach after HEAT2D_IPC_ATTACH_TIMEOUT seconds
+    on EVERY rank. Forced IPC: the run ends promptly with "no transport
+    works", not a hang. auto (RCCL refused too: ranks sharing a GPU): the run
+    goes on over its last resort, the host-staged torch.distributed exchange,
+    and its decomposition still verifies bitwise."""
     import time
     env = dict(os.environ, HEAT2D_IPC_ATTACH_STALL="1", HEAT2D_IPC_ATTACH_TIMEOUT="5", OMP_NUM_THREADS="1")
     env.pop("WORLD_SIZE", None)
     t0 = time.time()
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--grid", "2048",
-                        "--steps", "4", "--warmup", "1"], capture_output=True, text=True, timeout=300, env=env)
-    assert p.returncode != 0 and p.stdout.strip() == "", p.stdout
-    assert "did not return within" in p.stderr and "no transport works on every rank" in p.stderr, p.stderr[-3000:]
+                        "--steps", "4", "--warmup", "1", "--transport", transport, "--edge-shift", "0"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert "did not return within" in p.stderr, p.stderr[-3000:]
     assert time.time() - t0 < 240
+    if transport == "ipc":
+        assert p.returncode != 0 and p.stdout.strip() == "", p.stdout
+        assert "no transport works on every rank" in p.stderr, p.stderr[-3000:]
+        return
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    ch = d["config"]["transport_choice"]
+    assert d["config"]["transport"] == "torch-dist" and ch["chosen"] == "torch-dist", ch
+    assert "error" in ch["rccl"] and "error" in ch["ipc"] and ch["torch-dist"]["ms"] > 0, ch
+    assert d["verified"] is True and d["timed_field_check"]["ok"] is True, (d["verify"], d["timed_field_check"])
 
 
 @pytest.mark.gpu

@@ -211,7 +211,9 @@ def test_reference_checks(arith, sterbenz, expect):
     assert select.reference_checks(arith, 0.25, sterbenz) == expect
 
 
-@pytest.mark.parametrize("requested,world,hip,expect", [("auto", 8, True, ["rccl", "ipc"]), ("best", 8, True, ["rccl", "ipc"]),
+@pytest.mark.parametrize("requested,world,hip,expect", [("auto", 8, True, ["rccl", "ipc", "torch-dist"]),
+                                                        ("best", 8, True, ["rccl", "ipc"]),
+                                                        ("host", 2, True, ["torch-dist"]),
                                                         ("peer", 2, True, ["ipc"]),
                                                         ("rccl", 2, True, ["rccl"]), ("auto", 1, True, []),
                                                         ("auto", 4, False, ["torch-dist"])])
