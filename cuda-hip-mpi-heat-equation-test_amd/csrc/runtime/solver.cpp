@@ -1112,8 +1112,15 @@ void Solver::ensure_pair_graph() {
   const bool ovl = cfg_.overlap != 0;
   if (ovl) (void)split_plan(K);  // plan / autotune (synchronising) before any capture
   if (!graph_exec_ || graph_k_ != K) {
-    if (graph_exec_) H2D_HIP(hipGraphExecDestroy(graph_exec_));
+    if (graph_exec_) {
+      hipGraphExec_t old = graph_exec_;
+      graph_exec_ = nullptr;  // (a failure below must not leave the destructor a destroyed exec)
+      H2D_HIP(hipGraphExecDestroy(old));
+    }
     hipGraph_t g = nullptr;
+    // the capture's fork / join events live until the graph is instantiated
+    // and destroyed (not destroyed while a capture graph may still name them)
+    hipEvent_t fork = nullptr, join = nullptr;
     const int saved = cur_, saved_ghost = ghost_, saved_last = last_k_;
     const int64_t saved_steps = steps_, saved_hist = hist_[K], saved_halo = halo_rows_;
     ghost_ = (int)band_;  // replays start after step()'s top-up
@@ -1132,7 +1139,6 @@ void Solver::ensure_pair_graph() {
       // Cross-cycle overlap inside the graph is kept; at graph boundaries the
       // launches serialise (the next graph's first cycle needs this one's
       // second anyway, except the exchange, which then is not hidden).
-      hipEvent_t fork = nullptr, join = nullptr;
       H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
       H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
       H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
@@ -1151,8 +1157,6 @@ void Solver::ensure_pair_graph() {
       H2D_HIP(hipEventRecord(join, s_comm_));
       H2D_HIP(hipStreamWaitEvent(s_compute_, join, 0));
       H2D_HIP(hipStreamEndCapture(s_compute_, &g));
-      H2D_HIP(hipEventDestroy(fork));
-      H2D_HIP(hipEventDestroy(join));
     }
     cur_ = saved;
     steps_ = saved_steps;
@@ -1165,6 +1169,8 @@ void Solver::ensure_pair_graph() {
     if (!g) H2D_HIP(hipStreamEndCapture(s_compute_, &g));
     H2D_HIP(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
     H2D_HIP(hipGraphDestroy(g));
+    for (hipEvent_t e : {fork, join})
+      if (e) H2D_HIP(hipEventDestroy(e));
     H2D_HIP(hipGraphUpload(graph_exec_, s_compute_));  // (not in the first timed launch)
     graph_k_ = K;
     if (ovl) {  // the events were recorded inside the capture only: re-establish them
@@ -1539,8 +1545,6 @@ void Solver::capture_schedule(int64_t n) {
   H2D_HIP(hipEventRecord(join, s_comm_));
   H2D_HIP(hipStreamWaitEvent(s_compute_, join, 0));
   H2D_HIP(hipStreamEndCapture(s_compute_, &g));
-  H2D_HIP(hipEventDestroy(fork));
-  H2D_HIP(hipEventDestroy(join));
   cur_ = saved;
   steps_ = saved_steps;
   ghost_ = saved_ghost;
@@ -1552,11 +1556,15 @@ void Solver::capture_schedule(int64_t n) {
   hipGraphExec_t ge = nullptr;
   H2D_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   H2D_HIP(hipGraphDestroy(g));
+  H2D_HIP(hipEventDestroy(fork));  // (after the graph that was captured with them)
+  H2D_HIP(hipEventDestroy(join));
   // upload it now (prepare), not in the first launch — the timed step(n):
   // small grid 5568 vs 5548, headline 4777 vs 4760 (medians, interleaved,
   // profiles/r4/gu/)
   H2D_HIP(hipGraphUpload(ge, s_compute_));
-  sched_graph_[{n, cur_}] = ge;
+  hipGraphExec_t& slot = sched_graph_[{n, cur_}];
+  if (slot) H2D_HIP(hipGraphExecDestroy(slot));  // a re-captured schedule replaces its old graph
+  slot = ge;
   // the events were recorded inside the capture only: re-establish them
   H2D_HIP(hipEventRecord(ev_int_, s_compute_));
   H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));

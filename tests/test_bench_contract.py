@@ -21,7 +21,7 @@ def run_bench(nproc, *args, port):
            "--gpus", str(nproc), "--backend", "cpu", *args]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode == 0, failure_text(p.stderr)
     lines = [l for l in p.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, p.stdout
     return json.loads(lines[0])
@@ -87,7 +87,7 @@ def test_bench_launches_ranks_itself():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--backend", "cpu", "--gpus", "4", "--grid",
                         "100", "--steps", "8", "--warmup", "2", "--tb", "4"], capture_output=True, text=True,
                        timeout=600, env=env)
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode == 0, failure_text(p.stderr)
     lines = [l for l in p.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, p.stdout
     d = json.loads(lines[0])
@@ -106,12 +106,23 @@ def test_bench_refuses_missing_gpus():
     assert "GPU(s) visible" in p.stderr
 
 
+def failure_text(err: str) -> str:
+    """A failed run's stderr for the assertion message: the native backtrace
+    of a fatal signal in full (the crash handler's frames, which name the
+    library and offset that called free() — the Python tail alone cut them
+    off), then the tail."""
+    mark = "heat2d: fatal signal, native backtrace:"
+    i = err.find(mark)
+    head = err[max(0, i - 600):i + 6000] + "\n...\n" if i >= 0 else ""
+    return head + err[-3000:]
+
+
 def run_plain(*args, timeout=600):
     env = dict(os.environ, OMP_NUM_THREADS="1")
     env.pop("WORLD_SIZE", None)
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
                        timeout=timeout, env=env)
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode == 0, failure_text(p.stderr)
     lines = [l for l in p.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, p.stdout
     return json.loads(lines[0])
@@ -231,7 +242,7 @@ def test_bench_ipc_attach_is_bounded(transport):
         assert p.returncode != 0 and p.stdout.strip() == "", p.stdout
         assert "no transport works on every rank" in p.stderr, p.stderr[-3000:]
         return
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode == 0, failure_text(p.stderr)
     d = json.loads(p.stdout.strip().splitlines()[-1])
     ch = d["config"]["transport_choice"]
     assert d["config"]["transport"] == "torch-dist" and ch["chosen"] == "torch-dist", ch
@@ -251,7 +262,7 @@ def test_bench_ipc_field_in_the_stalling_size_window():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--transport",
                         "ipc", "--grid", "23170", "--steps", "4", "--warmup", "1", "--verify", "off"],
                        capture_output=True, text=True, timeout=280, env=env)
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode == 0, failure_text(p.stderr)
     d = json.loads(p.stdout.strip().splitlines()[-1])
     assert d["config"]["transport"] == "ipc" and "NOT opened" not in p.stderr
     fc = d["timed_field_check"]
