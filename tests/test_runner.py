@@ -343,6 +343,22 @@ def test_torchrun_auto_transport_falls_back_share_gpu(native, gpu, tmp_path):
 
 
 @pytest.mark.gpu
+def test_torchrun_host_transport_share_gpu(native, gpu, tmp_path):
+    """`python -m heat2d --transport host` under torchrun: GPU ranks whose halos
+    go device -> pinned host -> gloo send/recv -> device (the reference's
+    host-staged MPI swap, fortran/hip/heat.F90:196-230; auto's last resort
+    after RCCL and IPC), uneven slabs — bitwise == the NumPy golden."""
+    (tmp_path / "input.dat").write_text("301 0.25 0.05 1.0 29 1\n")
+    py(tmp_path, "--backend", "hip", "--transport", "host", "--share-gpu", "--arith", "exact", "--json", "m.json",
+       nproc=3)
+    d = json.loads((tmp_path / "m.json").read_text())
+    assert d["transport"] == "torch-dist", d
+    T = np.concatenate([io.read_xyz(f)[2] for f in io.rank_files(str(tmp_path))], axis=0)
+    prob = heat2d.make_problem(heat2d.read_input(str(tmp_path / "input.dat")), "ghost", "uniform")
+    assert np.array_equal(T, R.owned(R.ftcs(prob)))
+
+
+@pytest.mark.gpu
 def test_torchrun_peer_transport_share_gpu_checkpoint(native, gpu, tmp_path):
     """`python -m heat2d --transport peer --share-gpu` under torchrun: rank
     processes on one GPU, halos over hipIpc mappings; a 3-rank run checkpoints
