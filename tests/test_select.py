@@ -154,6 +154,23 @@ def test_choose_first_working_falls_back():
     assert chosen == "ipc" and "error" in rep["rccl"] and rep["ipc"] == {"ms": 3.0}
 
 
+def test_choose_auto_reaches_the_host_transport():
+    """auto's whole chain on a node where neither RCCL nor the IPC mappings
+    attach: both fail on every rank alike and the host-staged exchange runs."""
+    tried = []
+
+    def trial(kind):
+        tried.append(kind)
+        if kind != "torch-dist":
+            raise RuntimeError(f"{kind} cannot attach")
+        return 9.0
+    cands = select.candidate_transports("auto", 8, True)
+    chosen, rep = select.choose_transport(cands, trial, ident, ident, first_working=True)
+    assert chosen == "torch-dist" and tried == ["rccl", "ipc", "torch-dist"]
+    assert "cannot attach" in rep["rccl"]["error"] and "cannot attach" in rep["ipc"]["error"]
+    assert rep["torch-dist"] == {"ms": 9.0}
+
+
 def test_deadline_fires_on_a_stuck_phase():
     import time
     fired = []
