@@ -474,6 +474,10 @@ class Solver {
   // so ev_bnd_ — which receiver-driven transports wait on after post() — keeps
   // marking only the bands the exchange sends
   hipEvent_t ev_frame_ = nullptr;
+  // fork / join of every stream capture (pair graph, measured schedules,
+  // schedule trials): created once and destroyed after the streams, so no
+  // event a capture recorded is freed while a stream may still name it
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   double* d_work_ = nullptr;   // stats workspace + 6 results
   bool timing_ = false;
   struct PhaseEvents {

@@ -205,6 +205,8 @@ Solver::Solver(const SolverConfig& cfg, std::shared_ptr<Transport> tr, hipStream
     H2D_HIP(hipEventCreateWithFlags(&ev_comm_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_int_, hipEventDisableTiming));
     H2D_HIP(hipEventCreateWithFlags(&ev_frame_, hipEventDisableTiming));
+    H2D_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    H2D_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     H2D_HIP(hipEventRecord(ev_comm_, s_comm_));
     H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
     H2D_HIP(hipEventRecord(ev_int_, s_compute_));
@@ -233,19 +235,16 @@ Solver::~Solver() {
     if (d_work_) (void)hipFree(d_work_);
     if (d_part_) (void)hipFree(d_part_);
     if (d_queue_) (void)hipFree(d_queue_);
-    if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
-    if (ev_comm_) (void)hipEventDestroy(ev_comm_);
-    if (ev_int_) (void)hipEventDestroy(ev_int_);
-    if (ev_frame_) (void)hipEventDestroy(ev_frame_);
-    if (ev_t0_) (void)hipEventDestroy(ev_t0_);
-    if (ev_t1_) (void)hipEventDestroy(ev_t1_);
-    for (auto* v : {&phase_ev_, &phase_pool_})
-      for (auto& pe : *v)
-        for (auto& e : pe.ev) (void)hipEventDestroy(e);
+    // the streams go before the events recorded on them (captures included)
     if (own_streams_) {
       (void)hipStreamDestroy(s_compute_);
       (void)hipStreamDestroy(s_comm_);
     }
+    for (hipEvent_t e : {ev_bnd_, ev_comm_, ev_int_, ev_frame_, ev_fork_, ev_join_, ev_t0_, ev_t1_})
+      if (e) (void)hipEventDestroy(e);
+    for (auto* v : {&phase_ev_, &phase_pool_})
+      for (auto& pe : *v)
+        for (auto& e : pe.ev) (void)hipEventDestroy(e);
     (void)hipGetLastError();  // teardown errors must not surface as the next launch's
   } else {
     for (auto& b : buf_) std::free(b);
@@ -1118,9 +1117,7 @@ void Solver::ensure_pair_graph() {
       H2D_HIP(hipGraphExecDestroy(old));
     }
     hipGraph_t g = nullptr;
-    // the capture's fork / join events live until the graph is instantiated
-    // and destroyed (not destroyed while a capture graph may still name them)
-    hipEvent_t fork = nullptr, join = nullptr;
+    const hipEvent_t fork = ev_fork_, join = ev_join_;  // (the solver's own: see runtime.hpp)
     const int saved = cur_, saved_ghost = ghost_, saved_last = last_k_;
     const int64_t saved_steps = steps_, saved_hist = hist_[K], saved_halo = halo_rows_;
     ghost_ = (int)band_;  // replays start after step()'s top-up
@@ -1139,8 +1136,6 @@ void Solver::ensure_pair_graph() {
       // Cross-cycle overlap inside the graph is kept; at graph boundaries the
       // launches serialise (the next graph's first cycle needs this one's
       // second anyway, except the exchange, which then is not hidden).
-      H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-      H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
       H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
       H2D_HIP(hipEventRecord(fork, s_compute_));
       H2D_HIP(hipStreamWaitEvent(s_comm_, fork, 0));
@@ -1169,8 +1164,6 @@ void Solver::ensure_pair_graph() {
     if (!g) H2D_HIP(hipStreamEndCapture(s_compute_, &g));
     H2D_HIP(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
     H2D_HIP(hipGraphDestroy(g));
-    for (hipEvent_t e : {fork, join})
-      if (e) H2D_HIP(hipEventDestroy(e));
     H2D_HIP(hipGraphUpload(graph_exec_, s_compute_));  // (not in the first timed launch)
     graph_k_ = K;
     if (ovl) {  // the events were recorded inside the capture only: re-establish them
@@ -1435,9 +1428,8 @@ float Solver::time_trial_eager(const std::vector<int>& sc, int reps) {
 float Solver::time_trial_schedule(const std::vector<int>& sc, int reps) {
   for (int k : sc) (void)split_plan(k);
   synchronize();
-  hipEvent_t fork = nullptr, join = nullptr, e0 = nullptr, e1 = nullptr;
-  H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-  H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  const hipEvent_t fork = ev_fork_, join = ev_join_;  // (the solver's own: see runtime.hpp)
+  hipEvent_t e0 = nullptr, e1 = nullptr;  // (recorded outside the capture)
   H2D_HIP(hipEventCreate(&e0));
   H2D_HIP(hipEventCreate(&e1));
   hipGraph_t g = nullptr;
@@ -1465,7 +1457,7 @@ float Solver::time_trial_schedule(const std::vector<int>& sc, int reps) {
     ms = std::min(ms, t);
   }
   H2D_HIP(hipGraphExecDestroy(ge));
-  for (hipEvent_t e : {fork, join, e0, e1}) H2D_HIP(hipEventDestroy(e));
+  for (hipEvent_t e : {e0, e1}) H2D_HIP(hipEventDestroy(e));
   // the events were recorded inside the capture only: re-establish them
   H2D_HIP(hipEventRecord(ev_int_, s_compute_));
   H2D_HIP(hipEventRecord(ev_bnd_, s_comm_));
@@ -1525,9 +1517,7 @@ void Solver::capture_schedule(int64_t n) {
   int64_t saved_hist[kMaxTB + 1];
   std::copy(hist_, hist_ + kMaxTB + 1, saved_hist);
   first_cycle_ = false;  // captured cycles keep their plans' order, whatever ran before
-  hipEvent_t fork = nullptr, join = nullptr;
-  H2D_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-  H2D_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  const hipEvent_t fork = ev_fork_, join = ev_join_;  // (the solver's own: see runtime.hpp)
   hipGraph_t g = nullptr;
   H2D_HIP(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
   H2D_HIP(hipEventRecord(fork, s_compute_));
@@ -1556,8 +1546,6 @@ void Solver::capture_schedule(int64_t n) {
   hipGraphExec_t ge = nullptr;
   H2D_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   H2D_HIP(hipGraphDestroy(g));
-  H2D_HIP(hipEventDestroy(fork));  // (after the graph that was captured with them)
-  H2D_HIP(hipEventDestroy(join));
   // upload it now (prepare), not in the first launch — the timed step(n):
   // small grid 5568 vs 5548, headline 4777 vs 4760 (medians, interleaved,
   // profiles/r4/gu/)
