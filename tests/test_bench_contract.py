@@ -9,6 +9,7 @@ import subprocess
 import sys
 
 import pytest
+from diag import failure_text
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
@@ -104,17 +105,6 @@ def test_bench_refuses_missing_gpus():
                        capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode != 0 and p.stdout.strip() == ""
     assert "GPU(s) visible" in p.stderr
-
-
-def failure_text(err: str) -> str:
-    """A failed run's stderr for the assertion message: the native backtrace
-    of a fatal signal in full (the crash handler's frames, which name the
-    library and offset that called free() — the Python tail alone cut them
-    off), then the tail."""
-    mark = "heat2d: fatal signal, native backtrace:"
-    i = err.find(mark)
-    head = err[max(0, i - 600):i + 6000] + "\n...\n" if i >= 0 else ""
-    return head + err[-3000:]
 
 
 def run_plain(*args, timeout=600):

@@ -8,6 +8,7 @@ import sys
 
 import numpy as np
 import pytest
+from diag import failure_text
 
 import heat2d
 from heat2d.models import reference as R
@@ -31,7 +32,7 @@ def py(cwd, *args, nproc=1, timeout=300):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(nproc), "--master-addr",
                "127.0.0.1", "--master-port", str(port()), "-m", "heat2d", *args]
     out = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
-    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert out.returncode == 0, out.stdout[-3000:] + failure_text(out.stderr)
     return out.stdout
 
 
